@@ -1,0 +1,166 @@
+"""Headline benchmark: rows/sec of `map_blocks` MatMul(512x512)+Relu over a
+10M-row float32[512] DataFrame (BASELINE.json config 3, the north-star metric
+"rows/sec map_blocks MatMul on 10M-row DF at 1/2/4/8 MI355X").
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+The 10M rows are split over the ranks (strong scaling: total work fixed),
+4 partitions per rank. Data is synthetic (random normal) and the weights are
+random-init; both are generated outside the timed region.
+
+One step = one full `map_blocks` pass, materialised: every partition's
+float32[512] input is read from the DataFrame's page-locked host memory,
+staged to HBM, multiplied by W (one fused MFMA GEMM+ReLU kernel per chunk)
+and the float32[512] output column is written back to page-locked host
+memory (PCIe traffic both ways is inside the timed region).
+
+`--mode device` additionally times the same pass on a DataFrame cached in
+HBM (`cache_on_device()`, outputs stay in HBM) and reports it as an extra
+field; the headline `value` is always the host-resident pass.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as torch_dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+BASELINE_VALUE = None  # the reference publishes no number
+TOTAL_ROWS = 10_000_000
+DIM = 512
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=TOTAL_ROWS)
+    ap.add_argument("--parts-per-gpu", type=int, default=4)
+    ap.add_argument("--mode", choices=["host", "device", "both"], default="both")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import tensorframes_amd as tfs
+    from tensorframes_amd import tf
+    from tensorframes_amd.frame.block import Block
+    from tensorframes_amd.frame.types import ArrayType, FloatType, StructField, StructType
+    from tensorframes_amd.parallel import dist
+
+    dist.init()
+    rank, world = dist.rank(), dist.world_size()
+    assert torch.cuda.is_available(), "bench.py needs a GPU"
+    dev = torch.device("cuda", dist.local_rank() % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+
+    nparts = world * args.parts_per_gpu
+    schema = StructType([StructField("x", ArrayType(FloatType(), False), False)])
+
+    # ---- synthetic data, generated on the GPU and staged into pinned host memory (untimed)
+    from tensorframes_amd._native import _C
+
+    def make(p):
+        a, b = (p * args.rows) // nparts, ((p + 1) * args.rows) // nparts
+        host = _C.empty_pinned([b - a, DIM], torch.float32)
+        gen = torch.Generator(device=dev).manual_seed(1000 + p)
+        step = 1 << 20
+        for s in range(0, b - a, step):
+            e = min(b - a, s + step)
+            host[s:e].copy_(torch.randn((e - s, DIM), device=dev, generator=gen))
+        return Block(b - a, {"x": host})
+
+    base = tfs.generate(schema, nparts, make).cache()
+    blocks = base.local_blocks()  # materialise the synthetic frame once (untimed)
+
+    g = torch.Generator().manual_seed(7)
+    w = (torch.randn((DIM, DIM), generator=g) / np.sqrt(DIM)).numpy().astype(np.float32)
+    with tf.Graph().as_default():
+        x = tfs.block(base, "x")
+        y = tf.nn.relu(tf.matmul(x, tf.constant(w)), name="y")
+
+    def step_host():
+        out = tfs.map_blocks(y, base, trim=True)
+        return out.local_blocks()
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist.is_distributed():
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce_(t, "Max")
+            dt = float(t.item())
+        return dt, res
+
+    results = {}
+    dt, res = timed(step_host, args.steps, args.warmup)
+    # correctness spot check on a few rows of the first local partition
+    pid = min(res)
+    xin = blocks[pid].columns["x"][:64].double()
+    ref = torch.clamp_min(xin @ torch.as_tensor(w).double(), 0)
+    err = (res[pid].columns["y"][:64].double() - ref).abs().max().item()
+    assert err < 1e-3, f"wrong result: max abs err {err}"
+    results["host"] = dt
+
+    dev_rows_per_s = None
+    if args.mode in ("device", "both"):
+        base_dev = base.cache_on_device(dev)
+
+        def step_dev():
+            return tfs.map_blocks(y, base_dev, trim=True).local_blocks()
+        ddt, _ = timed(step_dev, args.steps, args.warmup)
+        dev_rows_per_s = args.rows * args.steps / ddt
+        results["device"] = ddt
+        del base_dev
+
+    ms = results["host"] / args.steps * 1e3
+    value = args.rows * args.steps / results["host"]
+    if rank == 0:
+        out = {
+            "metric": "rows/sec map_blocks MatMul on 10M-row DF at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
+            "dtype": "fp32",
+            "data": "synthetic (random normal float32[512] rows in page-locked host memory; random-init W)",
+            "config": {
+                "model": "map_blocks relu(matmul(x[?,512], W[512,512])) float32",
+                "global_batch": args.rows,
+                "seq_len": DIM,
+                "parallelism": f"dp{world}",
+                "partitions": nparts,
+                "rows": args.rows,
+            },
+            "device_resident_rows_per_sec": dev_rows_per_s,
+            "device_resident_ms_per_step": None if dev_rows_per_s is None else results["device"] / args.steps * 1e3,
+            "gemm_tflops_device_resident": None if dev_rows_per_s is None else dev_rows_per_s * 2 * DIM * DIM / 1e12,
+            "max_abs_err": err,
+        }
+        print(json.dumps(out))
+    dist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,228 @@
+// pybind11 module `tensorframes_amd._C`: graph import/analysis, the executor,
+// pinned host memory. Replaces the Py4J + JNI bridges of the reference
+// (reference: src/main/scala/org/tensorframes/impl/PythonInterface.scala:21-180).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "ir/graph.h"
+#include "kernels/kernels.h"
+#include "runtime/executor.h"
+
+namespace py = pybind11;
+using namespace tfa;
+
+namespace {
+
+py::object shape_to_py(const Shape& s) {
+  if (s.unknown_rank) return py::none();
+  py::list l;
+  for (auto d : s.dims) l.append(d);
+  return l;
+}
+
+Shape shape_from_py(const py::object& o) {
+  if (o.is_none()) return Shape::unknown();
+  std::vector<int64_t> d;
+  for (auto v : o) d.push_back(v.is_none() ? -1 : v.cast<int64_t>());
+  return Shape(d);
+}
+
+const char* row_name(RowClass r) {
+  switch (r) {
+    case RowClass::CONST: return "const";
+    case RowClass::ROW: return "row";
+    default: return "mixed";
+  }
+}
+
+// {name: (dtype_enum, dims|None)} -> TensorInfo map
+std::map<std::string, TensorInfo> infos_from_py(const py::dict& d) {
+  std::map<std::string, TensorInfo> m;
+  for (auto kv : d) {
+    auto t = kv.second.cast<py::tuple>();
+    TensorInfo ti;
+    ti.dtype = static_cast<DType>(t[0].cast<int>());
+    ti.shape = shape_from_py(t[1]);
+    m[kv.first.cast<std::string>()] = ti;
+  }
+  return m;
+}
+
+py::list infos_to_py(const std::vector<TensorInfo>& v) {
+  py::list l;
+  for (auto& ti : v) {
+    py::dict d;
+    d["dtype"] = static_cast<int>(ti.dtype);
+    d["shape"] = shape_to_py(ti.shape);
+    d["row"] = row_name(ti.row);
+    d["const"] = ti.value.has_value();
+    l.append(d);
+  }
+  return l;
+}
+
+// Static inference over every node of a graph (used by the DSL for
+// get_shape()). Nodes that fail inference report an error string.
+py::dict infer_all(const std::string& bytes) {
+  auto g = Graph::from_bytes(bytes);
+  std::vector<TensorRef> all;
+  for (size_t i = 0; i < g->nodes().size(); ++i) all.push_back({static_cast<int>(i), 0});
+  auto order = g->closure(all);
+  Graph::Infos infos = g->infer(order, {}, false);
+  py::dict out;
+  for (size_t i = 0; i < g->nodes().size(); ++i) out[py::str(g->node(i).name)] = infos_to_py(infos[i]);
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "tensorframes_amd native runtime (GraphDef executor + HIP/CDNA4 kernels)";
+
+  py::register_exception<GraphError>(m, "GraphError", PyExc_ValueError);
+
+  py::class_<Graph, std::shared_ptr<Graph>>(m, "Graph")
+      .def(py::init([](py::bytes b) { return Graph::from_bytes(std::string(b)); }))
+      .def("node_names",
+           [](const Graph& g) {
+             std::vector<std::string> v;
+             for (auto& n : g.nodes()) v.push_back(n.name);
+             return v;
+           })
+      .def("node_ops",
+           [](const Graph& g) {
+             std::vector<std::string> v;
+             for (auto& n : g.nodes()) v.push_back(n.op);
+             return v;
+           })
+      .def("node_inputs",
+           [](const Graph& g, const std::string& name) {
+             int i = g.find(name);
+             TFA_CHECK(i >= 0, "no node named '", name, "'");
+             return g.def().nodes[i].inputs;
+           })
+      .def("placeholders",
+           [](const Graph& g) {
+             std::vector<std::string> v;
+             for (int i : g.placeholders()) v.push_back(g.node(i).name);
+             return v;
+           })
+      .def("zero_input_nodes",
+           [](const Graph& g) {
+             std::vector<std::string> v;
+             for (auto& n : g.nodes())
+               if (n.inputs.empty() && n.control.empty()) v.push_back(n.name);
+             return v;
+           })
+      .def("has_node", [](const Graph& g, const std::string& n) { return g.find(n) >= 0; })
+      .def("serialize", [](const Graph& g) { return py::bytes(serialize_graphdef(g.def())); })
+      .def("__len__", [](const Graph& g) { return g.nodes().size(); });
+
+  py::class_<Program, std::shared_ptr<Program>>(m, "Program")
+      .def(py::init([](std::shared_ptr<Graph> g, std::vector<std::string> fetches,
+                       std::vector<std::string> feeds) {
+             return std::make_shared<Program>(g, fetches, feeds);
+           }),
+           py::arg("graph"), py::arg("fetches"), py::arg("feeds"))
+      .def_property_readonly("fetch_names", &Program::fetch_names)
+      .def_property_readonly("feed_names", &Program::feed_names)
+      .def("row_separable",
+           [](const Program& p, py::dict hints) { return p.row_separable(infos_from_py(hints)); })
+      .def("monoids",
+           [](const Program& p) {
+             py::list l;
+             for (auto& mi : p.monoids()) l.append(py::make_tuple(mi.fetch, mi.placeholder, mi.op));
+             return l;
+           })
+      .def("run", &Program::run, py::call_guard<py::gil_scoped_release>())
+      .def("run_chunked", &Program::run_chunked, py::arg("seg_inputs"), py::arg("seg_outputs"),
+           py::arg("chunk_rows"), py::arg("device"), py::arg("depth") = 3,
+           py::call_guard<py::gil_scoped_release>())
+      .def("describe", &Program::describe_plan)
+      .def("reset_stats", &Program::reset_stats)
+      .def("stats", [](const Program& p) {
+        ExecStats s = p.stats();
+        py::dict d;
+        d["runs"] = s.runs;
+        d["kernels"] = s.kernels;
+        d["plans_built"] = s.plans_built;
+        d["h2d_bytes"] = s.h2d_bytes;
+        d["d2h_bytes"] = s.d2h_bytes;
+        d["chunks"] = s.chunks;
+        d["wall_ms"] = s.wall_ms;
+        return d;
+      });
+
+  m.def("analyze_fetches",
+        [](std::shared_ptr<Graph> g, std::vector<std::string> fetches, std::vector<std::string> feeds,
+           py::dict hints) {
+          Program p(g, fetches, feeds);
+          Graph::Infos infos = p.analyze(infos_from_py(hints));
+          py::dict out;
+          // per fetch and per feed: info of output 0 (or the indexed output)
+          for (auto& f : fetches) {
+            TensorRef r = g->resolve(f);
+            out[py::str(f)] = infos_to_py({infos[r.node][r.index]})[0];
+          }
+          for (auto& f : feeds) {
+            TensorRef r = g->resolve(f);
+            out[py::str(f)] = infos_to_py({infos[r.node][r.index]})[0];
+          }
+          return out;
+        });
+  m.def("infer_all", &infer_all);
+  m.def("registered_ops", [] { return OpRegistry::get().names(); });
+  m.def("roundtrip_graphdef",
+        [](py::bytes b) { return py::bytes(serialize_graphdef(parse_graphdef(std::string(b)))); });
+  m.def("decode_tensor_proto", [](py::bytes b) {
+    HostTensor t = parse_tensor_proto(std::string(b));
+    if (t.dtype == DType::STRING) {
+      py::list l;
+      for (auto& s : t.strings) l.append(py::bytes(s));
+      return py::object(l);
+    }
+    return py::cast(host_tensor_to_at(t));
+  });
+  // Segmented reduction over rows sorted by segment (CSR offsets, int64):
+  // the groupBy/aggregate monoid fast path. Device tensors run the HIP
+  // kernel; host tensors the ATen reference.
+  m.def("segment_reduce", [](const std::string& op, const at::Tensor& x, const at::Tensor& offsets) {
+    TFA_CHECK(x.dim() >= 1, "segment_reduce needs rank >= 1");
+    TFA_CHECK(offsets.scalar_type() == at::kLong && offsets.dim() == 1, "offsets must be int64[nseg+1]");
+    int64_t nseg = offsets.size(0) - 1;
+    std::vector<int64_t> osz = x.sizes().vec();
+    osz[0] = nseg;
+    k::RedOp rop = op == "Sum" ? k::RedOp::SUM : op == "Min" ? k::RedOp::MIN : op == "Max" ? k::RedOp::MAX
+                 : op == "Prod" ? k::RedOp::PROD : op == "Mean" ? k::RedOp::MEAN : k::RedOp::ALL;
+    TFA_CHECK(rop != k::RedOp::ALL, "segment_reduce: unsupported op ", op);
+    if (!x.is_cuda()) {
+      at::Tensor off = offsets.to(at::kCPU);
+      const int64_t* o = off.data_ptr<int64_t>();
+      std::vector<at::Tensor> parts;
+      for (int64_t s = 0; s < nseg; ++s) {
+        at::Tensor seg = x.narrow(0, o[s], o[s + 1] - o[s]);
+        switch (rop) {
+          case k::RedOp::SUM: parts.push_back(seg.sum(0, false, x.scalar_type())); break;
+          case k::RedOp::MIN: parts.push_back(std::get<0>(seg.min(0))); break;
+          case k::RedOp::MAX: parts.push_back(std::get<0>(seg.max(0))); break;
+          case k::RedOp::PROD: parts.push_back(seg.prod(0, false, x.scalar_type())); break;
+          default: parts.push_back(seg.to(at::kDouble).mean(0).to(x.scalar_type()));
+        }
+      }
+      return nseg ? at::stack(parts, 0) : at::empty(osz, x.options());
+    }
+    c10::hip::HIPGuard guard(x.device().index());
+    at::Tensor xc = x.contiguous();
+    at::Tensor out = at::empty(osz, xc.options());
+    int64_t inner = nseg ? out.numel() / nseg : 0;
+    if (out.numel())
+      k::segment_reduce_csr(rop, from_scalar_type(xc.scalar_type()), xc.data_ptr(),
+                            offsets.contiguous().data_ptr<int64_t>(), out.data_ptr(), nseg, inner,
+                            c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    return out;
+  });
+  m.def("empty_pinned", &empty_pinned);
+  m.def("pin_host_tensor", &pin_host_tensor);
+  m.def("unpin_host_tensor", &unpin_host_tensor);
+}

@@ -1,0 +1,374 @@
+// Graph import, edge resolution, closure and static inference / constant folding.
+#include "graph.h"
+
+#include <algorithm>
+#include <set>
+
+namespace tfa {
+
+OpRegistry& OpRegistry::get() {
+  static OpRegistry* r = [] {
+    auto* reg = new OpRegistry();
+    register_array_ops(*reg);
+    register_math_ops(*reg);
+    register_nn_ops(*reg);
+    return reg;
+  }();
+  return *r;
+}
+
+std::vector<std::string> OpRegistry::names() const {
+  std::vector<std::string> v;
+  for (auto& kv : ops_) v.push_back(kv.first);
+  std::sort(v.begin(), v.end());
+  return v;
+}
+
+// ------------------------------------------------------------------ attrs
+static const AttrValue& need_attr(const Node& n, const std::string& k) {
+  const AttrValue* a = n.def->find_attr(k);
+  TFA_CHECK(a, "node '", n.name, "' (", n.op, ") is missing attribute '", k, "'");
+  return *a;
+}
+
+int64_t Node::attr_i(const std::string& k, std::optional<int64_t> d) const {
+  const AttrValue* a = def->find_attr(k);
+  if (!a) {
+    TFA_CHECK(d.has_value(), "node '", name, "' (", op, ") is missing attribute '", k, "'");
+    return *d;
+  }
+  return a->i;
+}
+float Node::attr_f(const std::string& k, std::optional<float> d) const {
+  const AttrValue* a = def->find_attr(k);
+  if (!a) {
+    TFA_CHECK(d.has_value(), "node '", name, "' (", op, ") is missing attribute '", k, "'");
+    return *d;
+  }
+  return a->f;
+}
+bool Node::attr_b(const std::string& k, std::optional<bool> d) const {
+  const AttrValue* a = def->find_attr(k);
+  if (!a) {
+    TFA_CHECK(d.has_value(), "node '", name, "' (", op, ") is missing attribute '", k, "'");
+    return *d;
+  }
+  return a->b;
+}
+DType Node::attr_type(const std::string& k, std::optional<DType> d) const {
+  const AttrValue* a = def->find_attr(k);
+  if (!a) {
+    TFA_CHECK(d.has_value(), "node '", name, "' (", op, ") is missing attribute '", k, "'");
+    return *d;
+  }
+  return a->type;
+}
+std::string Node::attr_s(const std::string& k, std::optional<std::string> d) const {
+  const AttrValue* a = def->find_attr(k);
+  if (!a) {
+    TFA_CHECK(d.has_value(), "node '", name, "' (", op, ") is missing attribute '", k, "'");
+    return *d;
+  }
+  return a->s;
+}
+Shape Node::attr_shape(const std::string& k) const { return need_attr(*this, k).shape; }
+std::vector<int64_t> Node::attr_ilist(const std::string& k, std::vector<int64_t> d) const {
+  const AttrValue* a = def->find_attr(k);
+  if (!a || !a->list) return d;
+  return a->list->i;
+}
+const HostTensor& Node::attr_tensor(const std::string& k) const {
+  const AttrValue& a = need_attr(*this, k);
+  TFA_CHECK(a.tensor, "attribute '", k, "' of node '", name, "' is not a tensor");
+  return *a.tensor;
+}
+
+// ------------------------------------------------------------------ dtype helpers
+at::ScalarType to_scalar_type(DType d) {
+  switch (d) {
+    case DType::F32: return at::kFloat;
+    case DType::F64: return at::kDouble;
+    case DType::I32: return at::kInt;
+    case DType::I64: return at::kLong;
+    case DType::U8: return at::kByte;
+    case DType::I8: return at::kChar;
+    case DType::I16: return at::kShort;
+    case DType::BOOL: return at::kBool;
+    case DType::F16: return at::kHalf;
+    case DType::BF16: return at::kBFloat16;
+    default: TFA_CHECK(false, "dtype ", dtype_name(d), " has no tensor representation");
+  }
+  return at::kFloat;
+}
+
+DType from_scalar_type(at::ScalarType s) {
+  switch (s) {
+    case at::kFloat: return DType::F32;
+    case at::kDouble: return DType::F64;
+    case at::kInt: return DType::I32;
+    case at::kLong: return DType::I64;
+    case at::kByte: return DType::U8;
+    case at::kChar: return DType::I8;
+    case at::kShort: return DType::I16;
+    case at::kBool: return DType::BOOL;
+    case at::kHalf: return DType::F16;
+    case at::kBFloat16: return DType::BF16;
+    default: TFA_CHECK(false, "unsupported tensor scalar type ", c10::toString(s));
+  }
+  return DType::INVALID;
+}
+
+at::Tensor host_tensor_to_at(const HostTensor& t) {
+  auto dims = dims_or_throw(t.shape, "constant");
+  at::Tensor out = at::empty(dims, at::TensorOptions().dtype(to_scalar_type(t.dtype)));
+  if (!t.bytes.empty()) std::memcpy(out.data_ptr(), t.bytes.data(), t.bytes.size());
+  return out;
+}
+
+std::vector<int64_t> to_int_vector(const at::Tensor& t) {
+  at::Tensor c = t.to(at::kCPU).to(at::kLong).contiguous().reshape({-1});
+  const int64_t* p = c.data_ptr<int64_t>();
+  return std::vector<int64_t>(p, p + c.numel());
+}
+
+Shape shape_of(const at::Tensor& t) { return Shape(t.sizes().vec()); }
+
+std::vector<int64_t> dims_or_throw(const Shape& s, const char* what) {
+  TFA_CHECK(s.fully_known(), "shape of ", what, " must be fully known, got ", s.str());
+  return s.dims;
+}
+
+Shape broadcast_shapes(const Shape& a, const Shape& b) {
+  if (a.unknown_rank || b.unknown_rank) return Shape::unknown();
+  const Shape& hi = a.dims.size() >= b.dims.size() ? a : b;
+  const Shape& lo = a.dims.size() >= b.dims.size() ? b : a;
+  size_t off = hi.dims.size() - lo.dims.size();
+  std::vector<int64_t> out(hi.dims.begin(), hi.dims.end());
+  for (size_t i = 0; i < lo.dims.size(); ++i) {
+    int64_t d1 = hi.dims[off + i], d2 = lo.dims[i];
+    int64_t r;
+    if (d1 == d2) r = d1;
+    else if (d1 == 1) r = d2;
+    else if (d2 == 1) r = d1;
+    else if (d1 < 0) r = d2;   // unknown vs known (>1)
+    else if (d2 < 0) r = d1;
+    else {
+      TFA_CHECK(false, "Incompatible shapes: ", a.str(), " ", b.str());
+      r = -1;
+    }
+    out[off + i] = r;
+  }
+  return Shape(out);
+}
+
+// ------------------------------------------------------------------ ctx helpers
+std::optional<std::vector<int64_t>> InferCtx::ivalue(int i) const {
+  const TensorInfo& t = input(i);
+  if (!t.value) return std::nullopt;
+  return to_int_vector(*t.value);
+}
+
+std::optional<double> InferCtx::scalar_value(int i) const {
+  const TensorInfo& t = input(i);
+  if (!t.value || t.value->numel() != 1) return std::nullopt;
+  return t.value->to(at::kDouble).item<double>();
+}
+
+bool InferCtx::all_const() const {
+  for (auto* t : in)
+    if (t->row != RowClass::CONST) return false;
+  return true;
+}
+
+void InferCtx::rows_default() {
+  RowClass r = all_const() ? RowClass::CONST : RowClass::MIXED;
+  for (auto& o : out) o.row = r;
+}
+
+void InferCtx::rows_like(int i) {
+  for (auto& o : out) o.row = input(i).row;
+}
+
+void InferCtx::rows_elementwise() {
+  if (all_const()) {
+    for (auto& o : out) o.row = RowClass::CONST;
+    return;
+  }
+  int out_rank = out.at(0).shape.rank();
+  RowClass r = RowClass::ROW;
+  if (out_rank < 1) r = RowClass::MIXED;
+  for (auto* t : in) {
+    if (r == RowClass::MIXED) break;
+    if (t->row == RowClass::MIXED) {
+      r = RowClass::MIXED;
+    } else if (t->row == RowClass::ROW) {
+      if (t->shape.rank() != out_rank) r = RowClass::MIXED;
+    } else {  // CONST operand: must not carry a row dim
+      int rk = t->shape.rank();
+      if (rk < 0) r = RowClass::MIXED;
+      else if (rk == out_rank && t->shape.dims[0] != 1) r = RowClass::MIXED;
+    }
+  }
+  for (auto& o : out) o.row = r;
+}
+
+at::TensorOptions ExecCtx::options(int i) const { return in.at(i).options(); }
+
+std::vector<int64_t> ExecCtx::host_ivalue(int i) const {
+  const TensorInfo* t = in_info->at(i);
+  if (t->value) return to_int_vector(*t->value);
+  return to_int_vector(in.at(i));  // data-dependent: device->host sync
+}
+
+at::Tensor ExecCtx::alloc_out(int i) {
+  const TensorInfo& oi = out_info->at(i);
+  auto dims = dims_or_throw(oi.shape, "output");
+  at::TensorOptions opt = at::TensorOptions().dtype(to_scalar_type(oi.dtype));
+  if (!in.empty() && in[0].defined()) opt = opt.device(in[0].device());
+  else if (gpu) opt = opt.device(at::kCUDA);
+  return at::empty(dims, opt);
+}
+
+// ------------------------------------------------------------------ Graph
+static std::pair<std::string, int> split_tensor_name(const std::string& s) {
+  auto pos = s.rfind(':');
+  if (pos == std::string::npos) return {s, 0};
+  std::string idx = s.substr(pos + 1);
+  if (idx.empty() || !std::all_of(idx.begin(), idx.end(), ::isdigit)) return {s, 0};
+  return {s.substr(0, pos), std::stoi(idx)};
+}
+
+Graph::Graph(GraphDef def) : def_(std::move(def)) {
+  const OpRegistry& reg = OpRegistry::get();
+  nodes_.resize(def_.nodes.size());
+  for (size_t i = 0; i < def_.nodes.size(); ++i) {
+    const NodeDef& nd = def_.nodes[i];
+    TFA_CHECK(!nd.name.empty(), "GraphDef node ", i, " has no name");
+    TFA_CHECK(!by_name_.count(nd.name), "duplicate node name '", nd.name, "' in GraphDef");
+    by_name_[nd.name] = static_cast<int>(i);
+    Node& n = nodes_[i];
+    n.name = nd.name;
+    n.op = nd.op;
+    n.def = &nd;
+  }
+  for (size_t i = 0; i < def_.nodes.size(); ++i) {
+    const NodeDef& nd = def_.nodes[i];
+    Node& n = nodes_[i];
+    for (const std::string& in : nd.inputs) {
+      if (!in.empty() && in[0] == '^') {
+        int j = find(in.substr(1));
+        TFA_CHECK(j >= 0, "node '", n.name, "': unknown control input '", in, "'");
+        n.control.push_back(j);
+      } else {
+        n.inputs.push_back(resolve(in));
+      }
+    }
+    const OpDef* od = reg.find(n.op);
+    n.num_outputs = od ? od->num_outputs(n) : 1;
+  }
+}
+
+std::shared_ptr<Graph> Graph::from_bytes(const std::string& bytes) {
+  return std::make_shared<Graph>(parse_graphdef(bytes));
+}
+
+TensorRef Graph::resolve(const std::string& name) const {
+  auto [base, idx] = split_tensor_name(name);
+  int n = find(base);
+  if (n < 0) n = find(name);  // names that legitimately contain ':'
+  TFA_CHECK(n >= 0, "Graph has no node named '", base, "'");
+  return TensorRef{n, idx};
+}
+
+std::vector<int> Graph::closure(const std::vector<TensorRef>& fetches) const {
+  std::vector<int> order;
+  std::vector<int> state(nodes_.size(), 0);  // 0 new, 1 visiting, 2 done
+  std::vector<std::pair<int, size_t>> stack;
+  for (auto& f : fetches) {
+    if (state[f.node]) continue;
+    stack.push_back({f.node, 0});
+    state[f.node] = 1;
+    while (!stack.empty()) {
+      auto& [n, k] = stack.back();
+      const Node& nd = nodes_[n];
+      size_t total = nd.inputs.size() + nd.control.size();
+      if (k < total) {
+        int dep = k < nd.inputs.size() ? nd.inputs[k].node : nd.control[k - nd.inputs.size()];
+        ++k;
+        if (state[dep] == 1) TFA_CHECK(false, "cycle in graph at node '", nodes_[dep].name, "'");
+        if (state[dep] == 0) {
+          state[dep] = 1;
+          stack.push_back({dep, 0});
+        }
+      } else {
+        state[n] = 2;
+        order.push_back(n);
+        stack.pop_back();
+      }
+    }
+  }
+  return order;
+}
+
+std::vector<int> Graph::placeholders() const {
+  std::vector<int> v;
+  for (size_t i = 0; i < nodes_.size(); ++i)
+    if ((nodes_[i].op == "Placeholder" || nodes_[i].op == "PlaceholderV2") && nodes_[i].inputs.empty())
+      v.push_back(static_cast<int>(i));
+  return v;
+}
+
+static constexpr int64_t kFoldLimit = int64_t(1) << 22;  // elements
+
+Graph::Infos Graph::infer(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds,
+                          bool concrete) const {
+  const OpRegistry& reg = OpRegistry::get();
+  Infos infos(nodes_.size());
+  for (int ni : order) {
+    const Node& n = nodes_[ni];
+    auto fit = feeds.find(ni);
+    if (fit != feeds.end()) {
+      infos[ni] = {fit->second};
+      infos[ni][0].row = fit->second.row;
+      continue;
+    }
+    const OpDef* od = reg.find(n.op);
+    TFA_CHECK(od, "Op type not registered '", n.op, "' (node '", n.name,
+              "'): tensorframes_amd has no kernel for it");
+    InferCtx ctx{n, {}, std::vector<TensorInfo>(n.num_outputs), concrete};
+    for (auto& r : n.inputs) {
+      TFA_CHECK(r.index < static_cast<int>(infos[r.node].size()), "node '", n.name,
+                "' reads output ", r.index, " of '", nodes_[r.node].name, "' which has only ",
+                infos[r.node].size(), " outputs");
+      ctx.in.push_back(&infos[r.node][r.index]);
+    }
+    try {
+      od->infer(ctx);
+    } catch (const GraphError& e) {
+      throw GraphError(str_cat("while inferring shapes of node '", n.name, "' (", n.op, "): ", e.what()));
+    }
+    if (od->rows) od->rows(ctx);
+    else ctx.rows_default();
+    // constant folding: every input statically known
+    bool foldable = !od->stateful && n.op != "Placeholder" && n.op != "PlaceholderV2";
+    for (auto* t : ctx.in)
+      if (!t->value) foldable = false;
+    for (auto& o : ctx.out)
+      if (o.value || !o.shape.fully_known() || o.shape.num_elements() > kFoldLimit ||
+          o.dtype == DType::STRING)
+        foldable = false;
+    if (foldable && !ctx.in.empty() && od->compute) {
+      ExecCtx ex{n, {}, {}, &ctx.out, &ctx.in, false, nullptr};
+      for (auto* t : ctx.in) ex.in.push_back(*t->value);
+      ex.out.resize(ctx.out.size());
+      od->compute(ex);
+      for (size_t k = 0; k < ctx.out.size(); ++k) ctx.out[k].value = ex.out[k].contiguous();
+    }
+    for (auto& o : ctx.out)
+      if (o.value) o.row = RowClass::CONST;
+    infos[ni] = std::move(ctx.out);
+  }
+  return infos;
+}
+
+}  // namespace tfa

@@ -1,0 +1,48 @@
+// Helpers shared by the op registrations (ops_array.cpp, ops_math.cpp, ops_nn.cpp).
+//
+// Every op has one compute function that runs on CPU tensors through ATen
+// (the oracle / constant-folding path) and on device tensors through the
+// tensorframes_amd HIP kernels (kernels/kernels.h). There is no ATen fallback
+// on the device path: an unsupported device case raises.
+#pragma once
+
+#include <ATen/ATen.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../kernels/kernels.h"
+#include "graph.h"
+
+namespace tfa {
+
+inline hipStream_t stream_of(const ExecCtx& c) { return static_cast<hipStream_t>(c.stream); }
+inline DType dt_of(const at::Tensor& t) { return from_scalar_type(t.scalar_type()); }
+
+inline int64_t norm_axis(int64_t a, int64_t rank, const char* what = "axis") {
+  int64_t r = a < 0 ? a + rank : a;
+  TFA_CHECK(r >= 0 && r < std::max<int64_t>(rank, 1), what, " ", a, " out of range for rank ", rank);
+  return r;
+}
+
+// Copy an arbitrarily strided device view into another (same sizes). Device only.
+void gpu_copy(const at::Tensor& src, const at::Tensor& dst, hipStream_t s);
+// Contiguous copy of a (view) tensor on its device (ATen on CPU, our kernel on GPU).
+at::Tensor materialize(const ExecCtx& c, const at::Tensor& view);
+// Device-side broadcast descriptor for operands already expanded to `out` sizes.
+k::Bcast make_bcast(const std::vector<int64_t>& out, const at::Tensor& a, const at::Tensor& b,
+                    const at::Tensor* c = nullptr);
+
+inline void require_gpu_dtype(const at::Tensor& t, std::initializer_list<at::ScalarType> ok,
+                              const char* op) {
+  for (auto s : ok)
+    if (t.scalar_type() == s) return;
+  TFA_CHECK(false, op, ": dtype ", c10::toString(t.scalar_type()), " is not supported on the GPU path");
+}
+
+// Common infer: same dtype/shape as input i.
+inline void infer_like(InferCtx& c, int i = 0) {
+  c.set(0, c.input(i).dtype, c.input(i).shape);
+}
+
+}  // namespace tfa

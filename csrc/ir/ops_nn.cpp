@@ -1,0 +1,347 @@
+// NN ops: BiasAdd, Softmax, Conv2D, pooling, FusedBatchNorm (inference), TopKV2.
+//
+// These are the ops of the CNN-scoring workloads (frozen VGG / Inception
+// GraphDefs; reference: src/main/python/tensorframes_snippets/read_image.py:56-118).
+// Layout is TF's default NHWC.
+#include <cmath>
+#include <limits>
+
+#include "ops_common.h"
+
+namespace tfa {
+
+void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, bool tb,
+              const at::Tensor* bias, int act, at::Tensor& out);
+
+namespace {
+
+bool nchw(const Node& n) { return n.attr_s("data_format", std::string("NHWC")) == "NCHW"; }
+
+void window_out(int64_t in, int64_t k, int64_t s, int64_t d, bool same, int64_t& out,
+                int64_t& pad_before, int64_t& pad_after) {
+  int64_t eff = (k - 1) * d + 1;
+  if (in < 0) { out = -1; pad_before = pad_after = 0; return; }
+  if (same) {
+    out = (in + s - 1) / s;
+    int64_t total = std::max<int64_t>((out - 1) * s + eff - in, 0);
+    pad_before = total / 2;
+    pad_after = total - pad_before;
+  } else {
+    out = in >= eff ? (in - eff) / s + 1 : 0;
+    pad_before = pad_after = 0;
+  }
+}
+
+bool is_same(const Node& n) {
+  std::string p = n.attr_s("padding");
+  TFA_CHECK(p == "SAME" || p == "VALID", n.op, ": unsupported padding '", p, "'");
+  return p == "SAME";
+}
+
+struct Conv2DGeom {
+  int64_t N, H, W, C, KH, KW, OC, OH, OW, sh, sw, dh, dw, pt, pb, pl, pr;
+};
+
+Conv2DGeom conv_geom(const Node& n, const std::vector<int64_t>& x, const std::vector<int64_t>& w) {
+  TFA_CHECK(!nchw(n), n.op, ": only data_format NHWC is supported");
+  auto st = n.attr_ilist("strides", {1, 1, 1, 1});
+  auto dl = n.attr_ilist("dilations", {1, 1, 1, 1});
+  TFA_CHECK(st.size() == 4 && st[0] == 1 && st[3] == 1, n.op, ": strides must be [1,sh,sw,1]");
+  Conv2DGeom g;
+  g.N = x[0]; g.H = x[1]; g.W = x[2]; g.C = x[3];
+  g.KH = w[0]; g.KW = w[1]; g.OC = w[3];
+  TFA_CHECK(w[2] == g.C || g.C < 0 || w[2] < 0, n.op, ": filter in-channels ", w[2], " != input channels ", g.C);
+  g.sh = st[1]; g.sw = st[2];
+  g.dh = dl.size() == 4 ? dl[1] : 1;
+  g.dw = dl.size() == 4 ? dl[2] : 1;
+  bool same = is_same(n);
+  window_out(g.H, g.KH, g.sh, g.dh, same, g.OH, g.pt, g.pb);
+  window_out(g.W, g.KW, g.sw, g.dw, same, g.OW, g.pl, g.pr);
+  return g;
+}
+
+struct PoolGeom {
+  int64_t N, H, W, C, KH, KW, sh, sw, OH, OW, pt, pb, pl, pr;
+};
+
+PoolGeom pool_geom(const Node& n, const std::vector<int64_t>& x) {
+  TFA_CHECK(!nchw(n), n.op, ": only data_format NHWC is supported");
+  auto ks = n.attr_ilist("ksize");
+  auto st = n.attr_ilist("strides");
+  TFA_CHECK(ks.size() == 4 && ks[0] == 1 && ks[3] == 1, n.op, ": ksize must be [1,kh,kw,1]");
+  TFA_CHECK(st.size() == 4 && st[0] == 1 && st[3] == 1, n.op, ": strides must be [1,sh,sw,1]");
+  PoolGeom g;
+  g.N = x[0]; g.H = x[1]; g.W = x[2]; g.C = x[3];
+  g.KH = ks[1]; g.KW = ks[2]; g.sh = st[1]; g.sw = st[2];
+  bool same = is_same(n);
+  window_out(g.H, g.KH, g.sh, 1, same, g.OH, g.pt, g.pb);
+  window_out(g.W, g.KW, g.sw, 1, same, g.OW, g.pl, g.pr);
+  return g;
+}
+
+void rows_batch(InferCtx& c) {
+  // NHWC ops are row-local over N when their parameters are constant
+  if (c.all_const()) { for (auto& o : c.out) o.row = RowClass::CONST; return; }
+  bool ok = c.input(0).row == RowClass::ROW;
+  for (size_t i = 1; i < c.in.size(); ++i) ok = ok && c.in[i]->row == RowClass::CONST;
+  for (auto& o : c.out) o.row = ok ? RowClass::ROW : RowClass::MIXED;
+}
+
+}  // namespace
+
+// shared with the planner's fused conv epilogue
+void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
+                int act, at::Tensor& out) {
+  Conv2DGeom g = conv_geom(c.node, x0.sizes().vec(), w0.sizes().vec());
+  if (!c.gpu) {
+    at::Tensor x = x0.permute({0, 3, 1, 2});
+    x = at::constant_pad_nd(x, {g.pl, g.pr, g.pt, g.pb}, 0);
+    at::Tensor w = w0.permute({3, 2, 0, 1});
+    std::vector<int64_t> stride{g.sh, g.sw}, pad{0, 0}, dil{g.dh, g.dw};
+    at::Tensor y = at::conv2d(x, w, c10::optional<at::Tensor>(), at::IntArrayRef(stride),
+                              at::IntArrayRef(pad), at::IntArrayRef(dil), 1);
+    y = y.permute({0, 2, 3, 1});
+    if (bias) y = y + *bias;
+    if (act == 1) y = at::clamp_min(y, 0);
+    if (act == 2) y = at::clamp(y, 0, 6);
+    out = y.contiguous();
+    return;
+  }
+  require_gpu_dtype(x0, {at::kFloat}, "Conv2D");
+  at::Tensor x = materialize(c, x0), w = materialize(c, w0);
+  if (out.numel() == 0) return;
+  k::ConvArgs a;
+  a.N = g.N; a.H = g.H; a.W = g.W; a.C = g.C;
+  a.KH = g.KH; a.KW = g.KW; a.OC = g.OC; a.OH = g.OH; a.OW = g.OW;
+  a.sh = g.sh; a.sw = g.sw; a.dh = g.dh; a.dw = g.dw; a.pad_t = g.pt; a.pad_l = g.pl;
+  a.x = x.data_ptr(); a.w = w.data_ptr(); a.y = out.data_ptr();
+  a.bias = bias ? bias->data_ptr() : nullptr;
+  a.act = act;
+  k::conv2d_nhwc(DType::F32, a, stream_of(c));
+}
+
+void register_nn_ops(OpRegistry& r) {
+  // ---- BiasAdd
+  OpDef bias;
+  bias.infer = [](InferCtx& c) {
+    const TensorInfo& x = c.input(0);
+    const TensorInfo& b = c.input(1);
+    TFA_CHECK(x.dtype == b.dtype, "BiasAdd: dtype mismatch");
+    TFA_CHECK(b.shape.rank() == 1 || b.shape.unknown_rank, "BiasAdd: bias must be a vector");
+    c.set(0, x.dtype, x.shape);
+  };
+  bias.rows = [](InferCtx& c) { c.rows_elementwise(); };
+  bias.compute = [](ExecCtx& c) {
+    at::Tensor x = c.input(0), b = c.input(1);
+    bool cf = nchw(c.node);
+    at::Tensor bb = b;
+    if (cf && x.dim() > 2) {
+      std::vector<int64_t> s(x.dim(), 1);
+      s[1] = b.size(0);
+      bb = b.reshape(s);
+    }
+    if (!c.gpu) { c.out[0] = (x + bb).contiguous(); return; }
+    require_gpu_dtype(x, {at::kFloat, at::kDouble, at::kInt, at::kLong}, "BiasAdd");
+    at::Tensor xc = materialize(c, x), bc = materialize(c, bb);
+    c.out[0] = c.alloc_out(0);
+    int64_t n = xc.numel();
+    if (!n) return;
+    if (!cf || x.dim() <= 2) {
+      TFA_CHECK(bc.numel() == x.size(-1), "BiasAdd: bias length ", bc.numel(), " != last dim ", x.size(-1));
+      k::binary(k::BinOp::ADD, dt_of(xc), xc.data_ptr(), bc.data_ptr(), c.out[0].data_ptr(), n, 3,
+                x.size(-1), nullptr, stream_of(c));
+    } else {
+      k::Bcast bcd = make_bcast(x.sizes().vec(), xc, bc);
+      k::binary(k::BinOp::ADD, dt_of(xc), xc.data_ptr(), bc.data_ptr(), c.out[0].data_ptr(), n, 4,
+                1, &bcd, stream_of(c));
+    }
+  };
+  r.add("BiasAdd", bias);
+  r.add("BiasAddV1", bias);
+
+  // ---- Softmax / LogSoftmax (last axis)
+  auto make_softmax = [](bool log) {
+    OpDef d;
+    d.infer = [](InferCtx& c) { infer_like(c); };
+    d.rows = [](InferCtx& c) {
+      c.rows_like(0);
+      if (c.out[0].row == RowClass::ROW && c.input(0).shape.rank() < 2) c.out[0].row = RowClass::MIXED;
+    };
+    d.compute = [log](ExecCtx& c) {
+      at::Tensor x = c.input(0);
+      if (!c.gpu) { c.out[0] = (log ? at::log_softmax(x, -1) : at::softmax(x, -1)).contiguous(); return; }
+      require_gpu_dtype(x, {at::kFloat, at::kDouble}, "Softmax");
+      at::Tensor xc = materialize(c, x);
+      c.out[0] = c.alloc_out(0);
+      int64_t cols = xc.dim() ? xc.size(-1) : 1;
+      if (xc.numel()) k::softmax(dt_of(xc), log, xc.data_ptr(), c.out[0].data_ptr(), xc.numel() / cols, cols, stream_of(c));
+    };
+    return d;
+  };
+  r.add("Softmax", make_softmax(false));
+  r.add("LogSoftmax", make_softmax(true));
+
+  // ---- Conv2D
+  OpDef conv;
+  conv.infer = [](InferCtx& c) {
+    const TensorInfo& x = c.input(0);
+    const TensorInfo& w = c.input(1);
+    TFA_CHECK(x.dtype == w.dtype, "Conv2D: dtype mismatch");
+    if (x.shape.unknown_rank || w.shape.unknown_rank) {
+      c.set(0, x.dtype, Shape({-1, -1, -1, -1}));
+      return;
+    }
+    TFA_CHECK(x.shape.rank() == 4 && w.shape.rank() == 4, "Conv2D needs rank-4 input and filter");
+    Conv2DGeom g = conv_geom(c.node, x.shape.dims, w.shape.dims);
+    c.set(0, x.dtype, Shape({g.N, g.OH, g.OW, g.OC}));
+  };
+  conv.rows = rows_batch;
+  conv.compute = [](ExecCtx& c) {
+    at::Tensor out = c.gpu ? c.alloc_out(0) : at::Tensor();
+    run_conv2d(c, c.input(0), c.input(1), nullptr, 0, out);
+    c.out[0] = out;
+  };
+  r.add("Conv2D", conv);
+
+  // ---- MaxPool / AvgPool
+  auto make_pool = [](bool is_max) {
+    OpDef d;
+    d.infer = [](InferCtx& c) {
+      const TensorInfo& x = c.input(0);
+      if (x.shape.unknown_rank) { c.set(0, x.dtype, Shape({-1, -1, -1, -1})); return; }
+      TFA_CHECK(x.shape.rank() == 4, c.node.op, " needs a rank-4 input");
+      PoolGeom g = pool_geom(c.node, x.shape.dims);
+      c.set(0, x.dtype, Shape({g.N, g.OH, g.OW, g.C}));
+    };
+    d.rows = rows_batch;
+    d.compute = [is_max](ExecCtx& c) {
+      at::Tensor x = c.input(0);
+      PoolGeom g = pool_geom(c.node, x.sizes().vec());
+      if (!c.gpu) {
+        at::Tensor xn = x.permute({0, 3, 1, 2});
+        at::Tensor y;
+        if (is_max) {
+          double lo = -std::numeric_limits<double>::infinity();
+          at::Tensor xp = at::constant_pad_nd(xn, {g.pl, g.pr, g.pt, g.pb}, lo);
+          y = at::max_pool2d(xp, {g.KH, g.KW}, {g.sh, g.sw});
+        } else {
+          at::Tensor xp = at::constant_pad_nd(xn, {g.pl, g.pr, g.pt, g.pb}, 0);
+          at::Tensor ones = at::constant_pad_nd(at::ones_like(xn.narrow(1, 0, 1)), {g.pl, g.pr, g.pt, g.pb}, 0);
+          at::Tensor s = at::avg_pool2d(xp, {g.KH, g.KW}, {g.sh, g.sw});
+          at::Tensor cnt = at::avg_pool2d(ones, {g.KH, g.KW}, {g.sh, g.sw});
+          y = s / cnt;
+        }
+        c.out[0] = y.permute({0, 2, 3, 1}).contiguous();
+        return;
+      }
+      require_gpu_dtype(x, {at::kFloat}, c.node.op.c_str());
+      at::Tensor xc = materialize(c, x);
+      c.out[0] = c.alloc_out(0);
+      if (!c.out[0].numel()) return;
+      k::PoolArgs a;
+      a.N = g.N; a.H = g.H; a.W = g.W; a.C = g.C; a.OH = g.OH; a.OW = g.OW;
+      a.KH = g.KH; a.KW = g.KW; a.sh = g.sh; a.sw = g.sw; a.pad_t = g.pt; a.pad_l = g.pl;
+      a.is_max = is_max;
+      a.x = xc.data_ptr();
+      a.y = c.out[0].data_ptr();
+      k::pool2d_nhwc(DType::F32, a, stream_of(c));
+    };
+    return d;
+  };
+  r.add("MaxPool", make_pool(true));
+  r.add("AvgPool", make_pool(false));
+
+  // ---- FusedBatchNorm (inference): y = x*s + b with s = scale/sqrt(var+eps)
+  auto make_bn = [](int nout) {
+    OpDef d;
+    d.num_outputs = [nout](const Node&) { return nout; };
+    d.host_inputs = {1, 2, 3, 4};
+    d.infer = [](InferCtx& c) {
+      TFA_CHECK(!c.node.attr_b("is_training", true) || true, "");
+      infer_like(c);
+      for (size_t i = 1; i < c.out.size(); ++i) c.set(static_cast<int>(i), c.input(1).dtype, c.input(1).shape);
+    };
+    d.rows = rows_batch;
+    d.compute = [](ExecCtx& c) {
+      TFA_CHECK(!c.node.attr_b("is_training", true), c.node.op,
+                ": only inference mode (is_training=false) is supported");
+      TFA_CHECK(!nchw(c.node), c.node.op, ": only NHWC is supported");
+      float eps = c.node.attr_f("epsilon", 1e-4f);
+      auto host = [&](int i) {
+        const TensorInfo* t = c.in_info->at(i);
+        return (t->value ? *t->value : c.input(i).to(at::kCPU)).to(at::kDouble);
+      };
+      at::Tensor scale = host(1), offset = host(2), mean = host(3), var = host(4);
+      at::Tensor s = scale * at::rsqrt(var + eps);
+      at::Tensor b = offset - mean * s;
+      at::Tensor x = c.input(0);
+      for (size_t i = 1; i < c.out.size(); ++i) c.out[i] = c.input(std::min<int>(static_cast<int>(i) + 2, 4));
+      if (!c.gpu) {
+        c.out[0] = (x * s.to(x.scalar_type()) + b.to(x.scalar_type())).contiguous();
+        return;
+      }
+      require_gpu_dtype(x, {at::kFloat, at::kDouble}, c.node.op.c_str());
+      at::Tensor xc = materialize(c, x);
+      at::Tensor sd = s.to(xc.scalar_type()).to(xc.device(), true);
+      at::Tensor bd = b.to(xc.scalar_type()).to(xc.device(), true);
+      c.out[0] = c.alloc_out(0);
+      if (xc.numel())
+        k::channel_affine(dt_of(xc), xc.data_ptr(), sd.data_ptr(), bd.data_ptr(), c.out[0].data_ptr(),
+                          xc.numel(), xc.size(-1), 0, stream_of(c));
+    };
+    return d;
+  };
+  r.add("FusedBatchNorm", make_bn(5));
+  r.add("FusedBatchNormV2", make_bn(5));
+  r.add("FusedBatchNormV3", make_bn(6));
+
+  // ---- TopKV2 (input, k) -> values, indices(int32)
+  OpDef topk;
+  topk.num_outputs = [](const Node&) { return 2; };
+  topk.host_inputs = {1};
+  topk.infer = [](InferCtx& c) {
+    const TensorInfo& x = c.input(0);
+    auto kv = c.ivalue(1);
+    if (x.shape.unknown_rank) {
+      c.set(0, x.dtype, Shape::unknown());
+      c.set(1, DType::I32, Shape::unknown());
+      return;
+    }
+    std::vector<int64_t> d = x.shape.dims;
+    TFA_CHECK(!d.empty(), "TopKV2 needs rank >= 1");
+    int64_t kk = kv ? (*kv)[0] : -1;
+    TFA_CHECK(kk < 0 || d.back() < 0 || kk <= d.back(), "TopKV2: k=", kk, " > last dim ", d.back());
+    d.back() = kk;
+    c.set(0, x.dtype, Shape(d));
+    c.set(1, DType::I32, Shape(d));
+  };
+  topk.rows = [](InferCtx& c) {
+    c.rows_default();
+    if (c.input(0).row == RowClass::ROW && c.input(0).shape.rank() >= 2 && c.input(1).row == RowClass::CONST)
+      for (auto& o : c.out) o.row = RowClass::ROW;
+  };
+  topk.compute = [](ExecCtx& c) {
+    at::Tensor x = c.input(0);
+    int64_t kk = c.host_ivalue(1)[0];
+    if (!c.gpu) {
+      auto res = at::topk(x, kk, -1, true, true);
+      // TF breaks ties by lower index first; ATen's stable sort gives the same
+      auto srt = at::sort(x, /*stable=*/true, -1, /*descending=*/true);
+      c.out[0] = std::get<0>(srt).narrow(-1, 0, kk).contiguous();
+      c.out[1] = std::get<1>(srt).narrow(-1, 0, kk).to(at::kInt).contiguous();
+      (void)res;
+      return;
+    }
+    require_gpu_dtype(x, {at::kFloat, at::kDouble, at::kInt, at::kLong}, "TopKV2");
+    at::Tensor xc = materialize(c, x);
+    c.out[0] = c.alloc_out(0);
+    c.out[1] = c.alloc_out(1);
+    int64_t cols = xc.size(-1);
+    if (c.out[0].numel())
+      k::topk(dt_of(xc), xc.data_ptr(), c.out[0].data_ptr(), c.out[1].data_ptr<int32_t>(),
+              xc.numel() / cols, cols, static_cast<int>(kk), stream_of(c));
+  };
+  r.add("TopKV2", topk);
+}
+
+}  // namespace tfa

@@ -1,0 +1,55 @@
+// Device-side helpers shared by the tensorframes_amd HIP kernels (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "kernels.h"
+
+namespace tfa {
+namespace k {
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+// Memory-bound grid sizing: enough blocks to fill 256 CUs several times over,
+// grid-stride for the rest.
+inline int ew_grid(int64_t work_items, int block = 256, int max_blocks = 256 * 8) {
+  int64_t b = (work_items + block - 1) / block;
+  if (b < 1) b = 1;
+  if (b > max_blocks) b = max_blocks;
+  return static_cast<int>(b);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Broadcast index math: linear output index -> operand offset.
+__device__ __forceinline__ int64_t bcast_offset(int64_t i, int rank, const int64_t* dims,
+                                                const int64_t* strides) {
+  int64_t off = 0;
+  for (int d = rank - 1; d >= 0; --d) {
+    int64_t q = i / dims[d];
+    int64_t r = i - q * dims[d];
+    off += r * strides[d];
+    i = q;
+  }
+  return off;
+}
+
+}  // namespace k
+}  // namespace tfa
+
+#define TFA_LAUNCH_CHECK(what)                                                        \
+  do {                                                                                \
+    hipError_t _e = hipGetLastError();                                                \
+    if (_e != hipSuccess) {                                                           \
+      throw ::tfa::GraphError(::tfa::str_cat("HIP launch of ", what, " failed: ",     \
+                                             hipGetErrorString(_e)));                 \
+    }                                                                                 \
+  } while (0)

@@ -1,0 +1,125 @@
+// Host-side launch API of the tensorframes_amd HIP kernel library (gfx950 / CDNA4).
+//
+// These functions are torch-free: raw device pointers + hipStream_t. Each one
+// checks the shapes it is handed against what its grid assumes before it
+// launches (a bad launch can fault the whole node).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../common.h"
+
+namespace tfa {
+namespace k {
+
+constexpr int kMaxRank = 8;
+
+void check_launch(const char* what);
+
+// ------------------------------------------------------------ elementwise
+enum class BinOp : int {
+  ADD, SUB, MUL, DIV, FLOORDIV, FLOORMOD, TRUNCMOD, MAX, MIN, POW, SQDIFF,
+  EQ, NE, LT, LE, GT, GE, LAND, LOR, ATAN2, DIVNONAN,
+};
+enum class UnOp : int {
+  NEG, ABS, SQUARE, SQRT, RSQRT, EXP, LOG, LOG1P, EXPM1, RECIP, RELU, RELU6, ELU, SELU,
+  SIGMOID, TANH, SOFTPLUS, SOFTSIGN, FLOOR, CEIL, ROUND, SIGN, SIN, COS, TAN, NOT, IDENTITY,
+  ERF, ISNAN, ISINF, ISFINITE,
+};
+
+// Broadcast descriptor: output dims and per-operand element strides (0 on broadcast dims).
+struct Bcast {
+  int rank = 0;
+  int64_t dims[kMaxRank];
+  int64_t sa[kMaxRank];
+  int64_t sb[kMaxRank];
+  int64_t sc[kMaxRank];  // third operand (Select)
+};
+
+// out = op(a, b). mode: 0 same-shape contiguous, 1 b scalar, 2 a scalar,
+// 3 row-broadcast (b is [inner], a is [n/inner, inner]), 4 general broadcast.
+void binary(BinOp op, DType dt, const void* a, const void* b, void* out, int64_t n, int mode,
+            int64_t inner, const Bcast* bc, hipStream_t s);
+// out_dtype is BOOL for comparisons/logical ops.
+void unary(UnOp op, DType dt, const void* x, void* y, int64_t n, hipStream_t s);
+void cast(DType from, DType to, const void* x, void* y, int64_t n, hipStream_t s);
+void select(DType dt, const void* cond, const void* a, const void* b, void* out, int64_t n,
+            const Bcast& bc, hipStream_t s);
+void fill(DType dt, void* out, int64_t n, double value, hipStream_t s);
+void range(DType dt, void* out, int64_t n, double start, double delta, hipStream_t s);
+
+
+// ------------------------------------------------------------ reductions
+enum class RedOp : int { SUM, PROD, MIN, MAX, MEAN, ALL, ANY };
+// x viewed as [outer, r, inner] -> y [outer, inner]. workspace: see reduce_workspace_bytes.
+size_t reduce_workspace_bytes(DType dt, int64_t outer, int64_t r, int64_t inner);
+void reduce(RedOp op, DType dt, const void* x, void* y, int64_t outer, int64_t r, int64_t inner,
+            void* workspace, hipStream_t s);
+// arg-reduce over r of [outer, r, inner]; out int32 or int64
+void argreduce(bool is_min, DType dt, DType out_dt, const void* x, void* y, int64_t outer,
+               int64_t r, int64_t inner, hipStream_t s);
+// softmax / log-softmax over the last dim of [rows, cols]
+void softmax(DType dt, bool log, const void* x, void* y, int64_t rows, int64_t cols, hipStream_t s);
+// top-k along the last dim of [rows, cols]: values (dt) + indices (int32), sorted descending
+void topk(DType dt, const void* x, void* vals, int32_t* idx, int64_t rows, int64_t cols, int k,
+          hipStream_t s);
+// segmented reductions: rows of x [n, inner] with segment ids (sorted or not) into [nseg, inner]
+size_t unsorted_segment_workspace_bytes(RedOp op, DType dt, int64_t n, int64_t inner, int64_t nseg);
+void unsorted_segment_reduce(RedOp op, DType dt, DType idt, const void* x, const void* ids,
+                             void* y, int64_t n, int64_t inner, int64_t nseg, void* workspace,
+                             hipStream_t s);
+// segmented reduce with CSR offsets over contiguous rows (deterministic)
+void segment_reduce_csr(RedOp op, DType dt, const void* x, const int64_t* offsets, void* y,
+                        int64_t nseg, int64_t inner, hipStream_t s);
+
+// ------------------------------------------------------------ data movement
+// dst[idx] = src[idx] over `dims`, both operands addressed by element strides
+// (src strides may be 0 or negative; pointers already include the offsets).
+void strided_copy(int64_t elem_size, int rank, const int64_t* dims, const void* src,
+                  const int64_t* src_strides, void* dst, const int64_t* dst_strides,
+                  hipStream_t s);
+// Gather rows: out[o, j, i] = params[o, idx[j], i]
+void gather(int64_t elem_size, DType idt, const void* params, const void* idx, void* out,
+            int64_t outer, int64_t axis_dim, int64_t nidx, int64_t inner, hipStream_t s);
+void one_hot(DType dt, DType idt, const void* idx, void* out, int64_t n, int64_t depth,
+             double on, double off, hipStream_t s);
+
+// ------------------------------------------------------------ GEMM (MFMA)
+// C[b] = op(A[b]) @ op(B[b]) (+ bias[N]) (relu); row-major, leading dims in elements.
+struct GemmArgs {
+  int64_t M, N, K;
+  const void* A; int64_t lda; int64_t strideA;
+  const void* B; int64_t ldb; int64_t strideB;
+  void* C; int64_t ldc; int64_t strideC;
+  bool ta, tb;
+  const void* bias;  // nullable, length N
+  int act;           // 0 none, 1 relu, 2 relu6
+  int64_t batch;
+};
+void gemm(DType dt, const GemmArgs& g, hipStream_t s);
+
+// ------------------------------------------------------------ conv / pool (NHWC)
+struct ConvArgs {
+  int64_t N, H, W, C;       // input
+  int64_t KH, KW, OC;       // filter [KH, KW, C, OC]
+  int64_t OH, OW;
+  int64_t sh, sw, dh, dw;
+  int64_t pad_t, pad_l;
+  const void* x; const void* w; void* y;
+  const void* bias; int act;
+};
+void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s);
+struct PoolArgs {
+  int64_t N, H, W, C, OH, OW, KH, KW, sh, sw, pad_t, pad_l;
+  bool is_max;
+  const void* x; void* y;
+};
+void pool2d_nhwc(DType dt, const PoolArgs& a, hipStream_t s);
+// y = x * scale[c] + shift[c] (+relu), channel = last dim
+void channel_affine(DType dt, const void* x, const void* scale, const void* shift, void* y,
+                    int64_t n, int64_t C, int act, hipStream_t s);
+
+}  // namespace k
+}  // namespace tfa

@@ -1,0 +1,669 @@
+// Reductions for gfx950: Sum/Prod/Min/Max/Mean/All/Any over [outer, r, inner],
+// arg-min/max, row softmax, row top-k, segment reductions.
+//
+// All float sums accumulate in f64 and every multi-block reduction goes
+// through a fixed-order partial-slab pass (no float atomics), so results are
+// bitwise reproducible run to run.
+#include <cfloat>
+#include <climits>
+#include <cmath>
+
+#include "hip_common.h"
+
+namespace tfa {
+namespace k {
+
+namespace {
+
+template <typename T> struct AccT { using type = double; };
+template <> struct AccT<int32_t> { using type = int64_t; };
+template <> struct AccT<int64_t> { using type = int64_t; };
+template <> struct AccT<uint8_t> { using type = int64_t; };
+
+template <typename A>
+__device__ __forceinline__ A big_pos() {
+  if constexpr (std::is_floating_point<A>::value) return INFINITY;
+  else return LLONG_MAX;
+}
+template <typename A>
+__device__ __forceinline__ A big_neg() {
+  if constexpr (std::is_floating_point<A>::value) return -INFINITY;
+  else return LLONG_MIN;
+}
+
+template <int OP, typename A>
+__device__ __forceinline__ A ident() {
+  if constexpr (OP == (int)RedOp::SUM || OP == (int)RedOp::MEAN || OP == (int)RedOp::ANY) return A(0);
+  else if constexpr (OP == (int)RedOp::PROD || OP == (int)RedOp::ALL) return A(1);
+  else if constexpr (OP == (int)RedOp::MIN) return big_pos<A>();
+  else return big_neg<A>();
+}
+
+template <int OP, typename A>
+__device__ __forceinline__ A combine(A a, A b) {
+  if constexpr (OP == (int)RedOp::SUM || OP == (int)RedOp::MEAN) return a + b;
+  else if constexpr (OP == (int)RedOp::PROD) return a * b;
+  else if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::ALL) return b < a ? b : a;
+  else return b > a ? b : a;
+}
+
+template <int OP, typename A>
+__device__ __forceinline__ A wave_reduce(A v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = combine<OP, A>(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+template <int OP, typename T, typename A>
+__device__ __forceinline__ T finish(A v, int64_t count) {
+  if constexpr (OP == (int)RedOp::MEAN) {
+    if constexpr (std::is_floating_point<A>::value) return T(v / A(count));
+    else return T(v / count);  // truncating, like TF integer Mean
+  } else {
+    return T(v);
+  }
+}
+
+// ---- row reduce (inner == 1): one wave per row
+template <typename T, int OP, int VEC>
+__global__ __launch_bounds__(256) void row_reduce_wave(const T* __restrict__ x, T* __restrict__ y,
+                                                       int64_t outer, int64_t r) {
+  using A = typename AccT<T>::type;
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < outer; row += waves) {
+    const T* p = x + row * r;
+    A acc = ident<OP, A>();
+    if (VEC > 1) {
+      int64_t nv = r / VEC;
+      for (int64_t i = lane; i < nv; i += 64) {
+        struct alignas(sizeof(T) * VEC) V { T v[VEC]; } v = reinterpret_cast<const V*>(p)[i];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc = combine<OP, A>(acc, A(v.v[j]));
+      }
+      for (int64_t i = nv * VEC + lane; i < r; i += 64) acc = combine<OP, A>(acc, A(p[i]));
+    } else {
+      for (int64_t i = lane; i < r; i += 64) acc = combine<OP, A>(acc, A(p[i]));
+    }
+    acc = wave_reduce<OP, A>(acc);
+    if (lane == 0) y[row] = finish<OP, T, A>(acc, r);
+  }
+}
+
+// ---- column-style reduce over [outer, r, inner]; grid = (col_blocks, outer, S)
+// Each thread owns one column and a contiguous slice of r. S > 1 writes
+// partials part[s][outer][inner] (accumulator type), combined by col_final.
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void col_reduce(const T* __restrict__ x, T* __restrict__ y,
+                                                  typename AccT<T>::type* __restrict__ part,
+                                                  int64_t outer, int64_t r, int64_t inner,
+                                                  int64_t rows_per_split) {
+  using A = typename AccT<T>::type;
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t o = blockIdx.y;
+  const int64_t s = blockIdx.z;
+  if (col >= inner) return;
+  const int64_t r0 = s * rows_per_split;
+  const int64_t r1 = min(r, r0 + rows_per_split);
+  const T* p = x + (o * r) * inner + col;
+  A acc0 = ident<OP, A>(), acc1 = ident<OP, A>(), acc2 = ident<OP, A>(), acc3 = ident<OP, A>();
+  int64_t i = r0;
+  for (; i + 4 <= r1; i += 4) {  // 4 independent chains keep 4 loads in flight
+    acc0 = combine<OP, A>(acc0, A(p[(i + 0) * inner]));
+    acc1 = combine<OP, A>(acc1, A(p[(i + 1) * inner]));
+    acc2 = combine<OP, A>(acc2, A(p[(i + 2) * inner]));
+    acc3 = combine<OP, A>(acc3, A(p[(i + 3) * inner]));
+  }
+  for (; i < r1; ++i) acc0 = combine<OP, A>(acc0, A(p[i * inner]));
+  A acc = combine<OP, A>(combine<OP, A>(acc0, acc1), combine<OP, A>(acc2, acc3));
+  if (part == nullptr) y[o * inner + col] = finish<OP, T, A>(acc, r);
+  else part[(s * outer + o) * inner + col] = acc;
+}
+
+// Vectorised variant: each thread owns VEC adjacent columns (16-byte loads).
+template <typename T, int OP, int VEC>
+__global__ __launch_bounds__(256) void col_reduce_vec(const T* __restrict__ x, T* __restrict__ y,
+                                                      typename AccT<T>::type* __restrict__ part,
+                                                      int64_t outer, int64_t r, int64_t inner,
+                                                      int64_t rows_per_split) {
+  using A = typename AccT<T>::type;
+  struct alignas(sizeof(T) * VEC) V { T v[VEC]; };
+  const int64_t cg = (int64_t)blockIdx.x * 256 + threadIdx.x;  // column group
+  const int64_t o = blockIdx.y;
+  const int64_t s = blockIdx.z;
+  if (cg * VEC >= inner) return;
+  const int64_t r0 = s * rows_per_split;
+  const int64_t r1 = min(r, r0 + rows_per_split);
+  const V* p = reinterpret_cast<const V*>(x + (o * r) * inner) + cg;
+  const int64_t rs = inner / VEC;  // row stride in vectors
+  A acc[2][VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[0][j] = acc[1][j] = ident<OP, A>();
+  int64_t i = r0;
+  for (; i + 2 <= r1; i += 2) {
+    V v0 = p[(i + 0) * rs];
+    V v1 = p[(i + 1) * rs];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      acc[0][j] = combine<OP, A>(acc[0][j], A(v0.v[j]));
+      acc[1][j] = combine<OP, A>(acc[1][j], A(v1.v[j]));
+    }
+  }
+  for (; i < r1; ++i) {
+    V v0 = p[i * rs];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[0][j] = combine<OP, A>(acc[0][j], A(v0.v[j]));
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    A a = combine<OP, A>(acc[0][j], acc[1][j]);
+    int64_t col = cg * VEC + j;
+    if (part == nullptr) y[o * inner + col] = finish<OP, T, A>(a, r);
+    else part[(s * outer + o) * inner + col] = a;
+  }
+}
+
+// ---- few long rows (inner == 1): grid = (S, outer), each block folds a
+// contiguous slice of its row with all 256 threads, partial -> part[s][outer].
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void row_split(const T* __restrict__ x,
+                                                 typename AccT<T>::type* __restrict__ part,
+                                                 int64_t outer, int64_t r, int64_t per_split) {
+  using A = typename AccT<T>::type;
+  __shared__ A red[4];
+  const int64_t s = blockIdx.x, o = blockIdx.y;
+  const int64_t r0 = s * per_split, r1 = min(r, r0 + per_split);
+  const T* p = x + o * r;
+  A acc = ident<OP, A>();
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) acc = combine<OP, A>(acc, A(p[i]));
+  acc = wave_reduce<OP, A>(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    A t = combine<OP, A>(combine<OP, A>(red[0], red[1]), combine<OP, A>(red[2], red[3]));
+    part[s * outer + o] = t;
+  }
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void col_final(const typename AccT<T>::type* __restrict__ part,
+                                                 T* __restrict__ y, int64_t n, int64_t S, int64_t r) {
+  using A = typename AccT<T>::type;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    A acc = ident<OP, A>();
+    for (int64_t s = 0; s < S; ++s) acc = combine<OP, A>(acc, part[s * n + i]);
+    y[i] = finish<OP, T, A>(acc, r);
+  }
+}
+
+struct RedPlan {
+  bool row_wave;
+  int64_t S;             // r splits (col path)
+  int64_t col_blocks;
+  int vec;
+};
+
+template <typename T>
+RedPlan plan_reduce(int64_t outer, int64_t r, int64_t inner) {
+  RedPlan p{};
+  constexpr int VEC = 16 / sizeof(T) > 0 ? 16 / sizeof(T) : 1;
+  if (inner == 1 && (outer >= 1024 || r <= 4096)) {
+    p.row_wave = true;
+    return p;
+  }
+  p.row_wave = false;
+  if (inner == 1) {  // few long rows: split each row over S blocks
+    p.vec = 1;
+    p.col_blocks = 0;
+    int64_t S = std::max<int64_t>(1, 2048 / std::max<int64_t>(outer, 1));
+    p.S = std::min<int64_t>(std::min<int64_t>(S, std::max<int64_t>(1, r / 1024)), 65535);
+    return p;
+  }
+  p.vec = (inner % VEC == 0) ? VEC : 1;
+  int64_t cols = (inner + p.vec - 1) / p.vec;
+  p.col_blocks = (cols + 255) / 256;
+  int64_t blocks = p.col_blocks * outer;
+  int64_t target = 2048;
+  int64_t S = blocks >= target ? 1 : (target + blocks - 1) / blocks;
+  int64_t max_s = std::max<int64_t>(1, r / 64);
+  p.S = std::min<int64_t>(std::min<int64_t>(S, max_s), 65535);
+  return p;
+}
+
+template <typename T, int OP>
+void reduce_typed(const void* xv, void* yv, int64_t outer, int64_t r, int64_t inner, void* ws,
+                  hipStream_t s) {
+  using A = typename AccT<T>::type;
+  const T* x = static_cast<const T*>(xv);
+  T* y = static_cast<T*>(yv);
+  RedPlan p = plan_reduce<T>(outer, r, inner);
+  if (p.row_wave) {
+    constexpr int VEC = 16 / sizeof(T);
+    bool vec = (r % VEC == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+    int grid = (int)std::min<int64_t>((outer + 3) / 4, 4096);
+    if (vec) hipLaunchKernelGGL((row_reduce_wave<T, OP, VEC>), dim3(grid), dim3(256), 0, s, x, y, outer, r);
+    else hipLaunchKernelGGL((row_reduce_wave<T, OP, 1>), dim3(grid), dim3(256), 0, s, x, y, outer, r);
+    return;
+  }
+  int64_t rows_per_split = (r + p.S - 1) / p.S;
+  int64_t S = (r + rows_per_split - 1) / rows_per_split;
+  if (inner == 1) {
+    TFA_CHECK(ws != nullptr || S == 1, "reduce: missing workspace");
+    TFA_CHECK(outer <= 65535, "reduce: outer dim ", outer, " too large for the split-row path");
+    A* part2 = static_cast<A*>(ws);
+    if (S == 1) {
+      hipLaunchKernelGGL((row_reduce_wave<T, OP, 1>), dim3((unsigned)((outer + 3) / 4)), dim3(256), 0, s, x, y, outer, r);
+      return;
+    }
+    hipLaunchKernelGGL((row_split<T, OP>), dim3((unsigned)S, (unsigned)outer), dim3(256), 0, s, x, part2, outer, r,
+                       rows_per_split);
+    hipLaunchKernelGGL((col_final<T, OP>), dim3(ew_grid(outer)), dim3(256), 0, s, part2, y, outer, S, r);
+    return;
+  }
+  TFA_CHECK(outer <= 65535, "reduce: outer dim ", outer, " too large for the column path");
+  A* part = S > 1 ? static_cast<A*>(ws) : nullptr;
+  TFA_CHECK(S == 1 || ws != nullptr, "reduce: missing workspace");
+  dim3 grid((unsigned)p.col_blocks, (unsigned)outer, (unsigned)S);
+  bool vec_ok = p.vec > 1 && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  if (vec_ok) {
+    constexpr int VEC = 16 / sizeof(T);
+    hipLaunchKernelGGL((col_reduce_vec<T, OP, VEC>), grid, dim3(256), 0, s, x, y, part, outer, r, inner,
+                       rows_per_split);
+  } else {
+    dim3 g2((unsigned)((inner + 255) / 256), (unsigned)outer, (unsigned)S);
+    hipLaunchKernelGGL((col_reduce<T, OP>), g2, dim3(256), 0, s, x, y, part, outer, r, inner, rows_per_split);
+  }
+  if (S > 1) {
+    int64_t n = outer * inner;
+    hipLaunchKernelGGL((col_final<T, OP>), dim3(ew_grid(n)), dim3(256), 0, s, part, y, n, S, r);
+  }
+}
+
+template <typename T>
+void reduce_dispatch_op(RedOp op, const void* x, void* y, int64_t outer, int64_t r, int64_t inner,
+                        void* ws, hipStream_t s) {
+  switch (op) {
+    case RedOp::SUM: reduce_typed<T, (int)RedOp::SUM>(x, y, outer, r, inner, ws, s); break;
+    case RedOp::PROD: reduce_typed<T, (int)RedOp::PROD>(x, y, outer, r, inner, ws, s); break;
+    case RedOp::MIN: reduce_typed<T, (int)RedOp::MIN>(x, y, outer, r, inner, ws, s); break;
+    case RedOp::MAX: reduce_typed<T, (int)RedOp::MAX>(x, y, outer, r, inner, ws, s); break;
+    case RedOp::MEAN: reduce_typed<T, (int)RedOp::MEAN>(x, y, outer, r, inner, ws, s); break;
+    default: TFA_CHECK(false, "reduce: op needs bool input");
+  }
+}
+
+// ---- arg reduce
+template <typename T, typename O, bool MIN>
+__global__ __launch_bounds__(256) void argreduce_row(const T* __restrict__ x, O* __restrict__ y,
+                                                     int64_t outer, int64_t r) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < outer; row += waves) {
+    const T* p = x + row * r;
+    T best = p[0];
+    int64_t bi = 0;
+    for (int64_t i = lane; i < r; i += 64) {
+      T v = p[i];
+      bool better = MIN ? (v < best || (v == best && i < bi)) : (v > best || (v == best && i < bi));
+      if (better) { best = v; bi = i; }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      T ov = __shfl_xor(best, off, 64);
+      int64_t oi = __shfl_xor(bi, off, 64);
+      bool better = MIN ? (ov < best || (ov == best && oi < bi)) : (ov > best || (ov == best && oi < bi));
+      if (better) { best = ov; bi = oi; }
+    }
+    if (lane == 0) y[row] = (O)bi;
+  }
+}
+
+template <typename T, typename O, bool MIN>
+__global__ __launch_bounds__(256) void argreduce_col(const T* __restrict__ x, O* __restrict__ y,
+                                                     int64_t outer, int64_t r, int64_t inner) {
+  const int64_t n = outer * inner;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+    int64_t o = t / inner, c = t % inner;
+    const T* p = x + o * r * inner + c;
+    T best = p[0];
+    int64_t bi = 0;
+    for (int64_t i = 1; i < r; ++i) {
+      T v = p[i * inner];
+      if (MIN ? v < best : v > best) { best = v; bi = i; }
+    }
+    y[t] = (O)bi;
+  }
+}
+
+template <typename T, typename O>
+void argreduce_typed(bool is_min, const void* xv, void* yv, int64_t outer, int64_t r, int64_t inner,
+                     hipStream_t s) {
+  const T* x = static_cast<const T*>(xv);
+  O* y = static_cast<O*>(yv);
+  if (inner == 1) {
+    int grid = (int)std::min<int64_t>((outer + 3) / 4, 4096);
+    if (is_min) hipLaunchKernelGGL((argreduce_row<T, O, true>), dim3(grid), dim3(256), 0, s, x, y, outer, r);
+    else hipLaunchKernelGGL((argreduce_row<T, O, false>), dim3(grid), dim3(256), 0, s, x, y, outer, r);
+  } else {
+    int64_t n = outer * inner;
+    if (is_min) hipLaunchKernelGGL((argreduce_col<T, O, true>), dim3(ew_grid(n)), dim3(256), 0, s, x, y, outer, r, inner);
+    else hipLaunchKernelGGL((argreduce_col<T, O, false>), dim3(ew_grid(n)), dim3(256), 0, s, x, y, outer, r, inner);
+  }
+}
+
+// ---- softmax (wave per row, 3 passes over an L2-resident row)
+template <typename T, bool LOG>
+__global__ __launch_bounds__(256) void softmax_rows(const T* __restrict__ x, T* __restrict__ y,
+                                                    int64_t rows, int64_t cols) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += waves) {
+    const T* p = x + row * cols;
+    T* q = y + row * cols;
+    T m = -INFINITY;
+    for (int64_t i = lane; i < cols; i += 64) m = p[i] > m ? p[i] : m;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      T o = __shfl_xor(m, off, 64);
+      m = o > m ? o : m;
+    }
+    T sum = 0;
+    for (int64_t i = lane; i < cols; i += 64) sum += exp(p[i] - m);
+    sum = wave_sum(sum);
+    if (LOG) {
+      T ls = log(sum);
+      for (int64_t i = lane; i < cols; i += 64) q[i] = p[i] - m - ls;
+    } else {
+      T inv = T(1) / sum;
+      for (int64_t i = lane; i < cols; i += 64) q[i] = exp(p[i] - m) * inv;
+    }
+  }
+}
+
+// ---- top-k: wave per row, k selection rounds ordered (value desc, index asc)
+template <typename T>
+__global__ __launch_bounds__(256) void topk_rows(const T* __restrict__ x, T* __restrict__ vals,
+                                                 int32_t* __restrict__ idx, int64_t rows, int64_t cols,
+                                                 int kk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += waves) {
+    const T* p = x + row * cols;
+    T pv = 0;
+    int64_t pi = -1;
+    for (int j = 0; j < kk; ++j) {
+      bool have = false;
+      T bv = 0;
+      int64_t bi = INT64_MAX;
+      for (int64_t i = lane; i < cols; i += 64) {
+        T v = p[i];
+        // eligible: strictly after the previous pick in (value desc, index asc) order
+        bool elig = pi < 0 || v < pv || (v == pv && i > pi);
+        if (elig && (!have || v > bv || (v == bv && i < bi))) {
+          have = true;
+          bv = v;
+          bi = i;
+        }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        T ov = __shfl_xor(bv, off, 64);
+        int64_t oi = __shfl_xor(bi, off, 64);
+        int oh = __shfl_xor((int)have, off, 64);
+        if (oh && (!have || ov > bv || (ov == bv && oi < bi))) {
+          have = true;
+          bv = ov;
+          bi = oi;
+        }
+      }
+      pv = bv;
+      pi = bi;
+      if (lane == 0) {
+        vals[row * kk + j] = bv;
+        idx[row * kk + j] = (int32_t)bi;
+      }
+    }
+  }
+}
+
+// ---- unsorted segment reduce, deterministic LDS-private path.
+// grid = (B row-blocks, col tiles); blockDim = TILE (one thread per column);
+// each block folds its rows in order into LDS acc[seg][col], writes its slab.
+template <typename T, typename I, int OP>
+__global__ __launch_bounds__(256) void useg_private(const T* __restrict__ x, const I* __restrict__ ids,
+                                                    typename AccT<T>::type* __restrict__ part,
+                                                    int64_t n, int64_t inner, int64_t nseg,
+                                                    int64_t rows_per_block) {
+  using A = typename AccT<T>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  A* acc = reinterpret_cast<A*>(smem);
+  const int tile = blockDim.x;
+  const int64_t col = (int64_t)blockIdx.y * tile + threadIdx.x;
+  for (int64_t sgi = 0; sgi < nseg; ++sgi) acc[sgi * tile + threadIdx.x] = ident<OP, A>();
+  const int64_t r0 = blockIdx.x * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  if (col < inner) {
+    for (int64_t i = r0; i < r1; ++i) {
+      int64_t sg = (int64_t)ids[i];
+      if (sg < 0 || sg >= nseg) continue;
+      A* a = &acc[sg * tile + threadIdx.x];
+      *a = combine<OP, A>(*a, A(x[i * inner + col]));
+    }
+    for (int64_t sgi = 0; sgi < nseg; ++sgi)
+      part[((int64_t)blockIdx.x * nseg + sgi) * inner + col] = acc[sgi * tile + threadIdx.x];
+  }
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void useg_final(const typename AccT<T>::type* __restrict__ part,
+                                                  T* __restrict__ y, int64_t m, int64_t B) {
+  using A = typename AccT<T>::type;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    A acc = ident<OP, A>();
+    for (int64_t b = 0; b < B; ++b) acc = combine<OP, A>(acc, part[b * m + i]);
+    if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
+      // TF: empty segments get the type's lowest (max) / highest (min) value
+      if (acc == ident<OP, A>()) {
+        if constexpr (std::is_floating_point<T>::value)
+          acc = OP == (int)RedOp::MAX ? A(-std::numeric_limits<T>::max()) : A(std::numeric_limits<T>::max());
+        else
+          acc = OP == (int)RedOp::MAX ? A(std::numeric_limits<T>::lowest()) : A(std::numeric_limits<T>::max());
+      }
+    }
+    y[i] = T(acc);
+  }
+}
+
+// ---- CSR segment reduce over sorted rows: grid = (nseg, col tiles)
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void seg_csr(const T* __restrict__ x, const int64_t* __restrict__ off,
+                                               T* __restrict__ y, int64_t nseg, int64_t inner) {
+  using A = typename AccT<T>::type;
+  const int64_t sg = blockIdx.x;
+  const int64_t col = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+  if (col >= inner) return;
+  A acc = ident<OP, A>();
+  for (int64_t i = off[sg]; i < off[sg + 1]; ++i) acc = combine<OP, A>(acc, A(x[i * inner + col]));
+  y[sg * inner + col] = finish<OP, T, A>(acc, off[sg + 1] - off[sg]);
+}
+
+constexpr int64_t kUsegTile = 256;
+constexpr int64_t kUsegLds = 64 * 1024;
+
+int64_t useg_tile(int64_t inner) {
+  int64_t t = ((inner + 63) / 64) * 64;
+  return std::min<int64_t>(t, kUsegTile);
+}
+
+int64_t useg_blocks(int64_t n) { return std::max<int64_t>(1, std::min<int64_t>(1024, (n + 127) / 128)); }
+
+}  // namespace
+
+// ====================================================================== host API
+size_t reduce_workspace_bytes(DType dt, int64_t outer, int64_t r, int64_t inner) {
+  int64_t S = 1;
+  switch (dt) {
+    case DType::F32: { auto p = plan_reduce<float>(outer, r, inner); S = p.row_wave ? 1 : p.S; break; }
+    case DType::F64: { auto p = plan_reduce<double>(outer, r, inner); S = p.row_wave ? 1 : p.S; break; }
+    case DType::I32: { auto p = plan_reduce<int32_t>(outer, r, inner); S = p.row_wave ? 1 : p.S; break; }
+    case DType::I64: { auto p = plan_reduce<int64_t>(outer, r, inner); S = p.row_wave ? 1 : p.S; break; }
+    case DType::BOOL: { auto p = plan_reduce<uint8_t>(outer, r, inner); S = p.row_wave ? 1 : p.S; break; }
+    default: return 0;
+  }
+  if (S <= 1) return 0;
+  return static_cast<size_t>(S) * outer * inner * 8;  // accumulators are 8 bytes
+}
+
+void reduce(RedOp op, DType dt, const void* x, void* y, int64_t outer, int64_t r, int64_t inner,
+            void* workspace, hipStream_t s) {
+  if (outer * inner <= 0) return;
+  TFA_CHECK(r > 0, "reduce: empty reduction handled by caller");
+  switch (dt) {
+    case DType::F32: reduce_dispatch_op<float>(op, x, y, outer, r, inner, workspace, s); break;
+    case DType::F64: reduce_dispatch_op<double>(op, x, y, outer, r, inner, workspace, s); break;
+    case DType::I32: reduce_dispatch_op<int32_t>(op, x, y, outer, r, inner, workspace, s); break;
+    case DType::I64: reduce_dispatch_op<int64_t>(op, x, y, outer, r, inner, workspace, s); break;
+    case DType::BOOL:
+      if (op == RedOp::ALL) reduce_typed<uint8_t, (int)RedOp::ALL>(x, y, outer, r, inner, workspace, s);
+      else if (op == RedOp::ANY) reduce_typed<uint8_t, (int)RedOp::ANY>(x, y, outer, r, inner, workspace, s);
+      else TFA_CHECK(false, "reduce: only All/Any on bool");
+      break;
+    default: TFA_CHECK(false, "reduce: dtype ", dtype_name(dt), " not supported");
+  }
+  TFA_LAUNCH_CHECK("reduce");
+}
+
+void argreduce(bool is_min, DType dt, DType out_dt, const void* x, void* y, int64_t outer, int64_t r,
+               int64_t inner, hipStream_t s) {
+  if (outer * inner <= 0) return;
+  TFA_CHECK(r > 0, "argreduce over an empty axis");
+  TFA_CHECK(out_dt == DType::I32 || out_dt == DType::I64, "argreduce: output must be int32/int64");
+  bool o64 = out_dt == DType::I64;
+  switch (dt) {
+    case DType::F32: o64 ? argreduce_typed<float, int64_t>(is_min, x, y, outer, r, inner, s) : argreduce_typed<float, int32_t>(is_min, x, y, outer, r, inner, s); break;
+    case DType::F64: o64 ? argreduce_typed<double, int64_t>(is_min, x, y, outer, r, inner, s) : argreduce_typed<double, int32_t>(is_min, x, y, outer, r, inner, s); break;
+    case DType::I32: o64 ? argreduce_typed<int32_t, int64_t>(is_min, x, y, outer, r, inner, s) : argreduce_typed<int32_t, int32_t>(is_min, x, y, outer, r, inner, s); break;
+    case DType::I64: o64 ? argreduce_typed<int64_t, int64_t>(is_min, x, y, outer, r, inner, s) : argreduce_typed<int64_t, int32_t>(is_min, x, y, outer, r, inner, s); break;
+    default: TFA_CHECK(false, "argreduce: dtype ", dtype_name(dt), " not supported");
+  }
+  TFA_LAUNCH_CHECK("argreduce");
+}
+
+void softmax(DType dt, bool log, const void* x, void* y, int64_t rows, int64_t cols, hipStream_t s) {
+  if (rows * cols <= 0) return;
+  int grid = (int)std::min<int64_t>((rows + 3) / 4, 8192);
+  if (dt == DType::F32) {
+    if (log) hipLaunchKernelGGL((softmax_rows<float, true>), dim3(grid), dim3(256), 0, s, (const float*)x, (float*)y, rows, cols);
+    else hipLaunchKernelGGL((softmax_rows<float, false>), dim3(grid), dim3(256), 0, s, (const float*)x, (float*)y, rows, cols);
+  } else if (dt == DType::F64) {
+    if (log) hipLaunchKernelGGL((softmax_rows<double, true>), dim3(grid), dim3(256), 0, s, (const double*)x, (double*)y, rows, cols);
+    else hipLaunchKernelGGL((softmax_rows<double, false>), dim3(grid), dim3(256), 0, s, (const double*)x, (double*)y, rows, cols);
+  } else {
+    TFA_CHECK(false, "softmax: float types only");
+  }
+  TFA_LAUNCH_CHECK("softmax");
+}
+
+void topk(DType dt, const void* x, void* vals, int32_t* idx, int64_t rows, int64_t cols, int kk,
+          hipStream_t s) {
+  if (rows <= 0 || kk <= 0) return;
+  TFA_CHECK(kk <= cols, "topk: k > cols");
+  int grid = (int)std::min<int64_t>((rows + 3) / 4, 8192);
+  switch (dt) {
+    case DType::F32: hipLaunchKernelGGL((topk_rows<float>), dim3(grid), dim3(256), 0, s, (const float*)x, (float*)vals, idx, rows, cols, kk); break;
+    case DType::F64: hipLaunchKernelGGL((topk_rows<double>), dim3(grid), dim3(256), 0, s, (const double*)x, (double*)vals, idx, rows, cols, kk); break;
+    case DType::I32: hipLaunchKernelGGL((topk_rows<int32_t>), dim3(grid), dim3(256), 0, s, (const int32_t*)x, (int32_t*)vals, idx, rows, cols, kk); break;
+    case DType::I64: hipLaunchKernelGGL((topk_rows<int64_t>), dim3(grid), dim3(256), 0, s, (const int64_t*)x, (int64_t*)vals, idx, rows, cols, kk); break;
+    default: TFA_CHECK(false, "topk: dtype not supported");
+  }
+  TFA_LAUNCH_CHECK("topk");
+}
+
+size_t unsorted_segment_workspace_bytes(RedOp, DType, int64_t n, int64_t inner, int64_t nseg) {
+  return static_cast<size_t>(useg_blocks(n)) * nseg * inner * 8;
+}
+
+template <typename T, typename I, int OP>
+static void useg_typed(const void* x, const void* ids, void* y, int64_t n, int64_t inner, int64_t nseg,
+                       void* ws, hipStream_t s) {
+  using A = typename AccT<T>::type;
+  int64_t tile = useg_tile(inner);
+  size_t lds = static_cast<size_t>(nseg * tile * sizeof(A));
+  TFA_CHECK(lds <= kUsegLds, "unsorted segment reduce: ", nseg, " segments x ", tile,
+            " columns exceed the LDS budget");
+  int64_t B = useg_blocks(n);
+  int64_t rpb = (n + B - 1) / B;
+  dim3 grid((unsigned)B, (unsigned)((inner + tile - 1) / tile));
+  hipLaunchKernelGGL((useg_private<T, I, OP>), grid, dim3((unsigned)tile), lds, s, (const T*)x, (const I*)ids,
+                     (A*)ws, n, inner, nseg, rpb);
+  int64_t m = nseg * inner;
+  hipLaunchKernelGGL((useg_final<T, OP>), dim3(ew_grid(m)), dim3(256), 0, s, (const A*)ws, (T*)y, m, B);
+}
+
+template <typename T, typename I>
+static void useg_op(RedOp op, const void* x, const void* ids, void* y, int64_t n, int64_t inner,
+                    int64_t nseg, void* ws, hipStream_t s) {
+  switch (op) {
+    case RedOp::SUM: useg_typed<T, I, (int)RedOp::SUM>(x, ids, y, n, inner, nseg, ws, s); break;
+    case RedOp::PROD: useg_typed<T, I, (int)RedOp::PROD>(x, ids, y, n, inner, nseg, ws, s); break;
+    case RedOp::MIN: useg_typed<T, I, (int)RedOp::MIN>(x, ids, y, n, inner, nseg, ws, s); break;
+    case RedOp::MAX: useg_typed<T, I, (int)RedOp::MAX>(x, ids, y, n, inner, nseg, ws, s); break;
+    default: TFA_CHECK(false, "unsorted segment reduce: unsupported op");
+  }
+}
+
+void unsorted_segment_reduce(RedOp op, DType dt, DType idt, const void* x, const void* ids, void* y,
+                             int64_t n, int64_t inner, int64_t nseg, void* workspace, hipStream_t s) {
+  if (nseg * inner <= 0) return;
+  if (n == 0) {
+    double v = (op == RedOp::PROD) ? 1.0 : 0.0;
+    fill(dt, y, nseg * inner, v, s);
+    return;
+  }
+  TFA_CHECK(workspace != nullptr, "unsorted segment reduce: missing workspace");
+  TFA_CHECK(idt == DType::I32 || idt == DType::I64, "segment ids must be int32/int64");
+  bool i64 = idt == DType::I64;
+  switch (dt) {
+    case DType::F32: i64 ? useg_op<float, int64_t>(op, x, ids, y, n, inner, nseg, workspace, s) : useg_op<float, int32_t>(op, x, ids, y, n, inner, nseg, workspace, s); break;
+    case DType::F64: i64 ? useg_op<double, int64_t>(op, x, ids, y, n, inner, nseg, workspace, s) : useg_op<double, int32_t>(op, x, ids, y, n, inner, nseg, workspace, s); break;
+    case DType::I32: i64 ? useg_op<int32_t, int64_t>(op, x, ids, y, n, inner, nseg, workspace, s) : useg_op<int32_t, int32_t>(op, x, ids, y, n, inner, nseg, workspace, s); break;
+    case DType::I64: i64 ? useg_op<int64_t, int64_t>(op, x, ids, y, n, inner, nseg, workspace, s) : useg_op<int64_t, int32_t>(op, x, ids, y, n, inner, nseg, workspace, s); break;
+    default: TFA_CHECK(false, "unsorted segment reduce: dtype not supported");
+  }
+  TFA_LAUNCH_CHECK("unsorted_segment_reduce");
+}
+
+template <typename T>
+static void seg_csr_op(RedOp op, const void* x, const int64_t* off, void* y, int64_t nseg, int64_t inner,
+                       hipStream_t s) {
+  dim3 grid((unsigned)nseg, (unsigned)((inner + 255) / 256));
+  unsigned bs = (unsigned)std::min<int64_t>(256, ((inner + 63) / 64) * 64);
+  switch (op) {
+    case RedOp::SUM: hipLaunchKernelGGL((seg_csr<T, (int)RedOp::SUM>), grid, dim3(bs), 0, s, (const T*)x, off, (T*)y, nseg, inner); break;
+    case RedOp::PROD: hipLaunchKernelGGL((seg_csr<T, (int)RedOp::PROD>), grid, dim3(bs), 0, s, (const T*)x, off, (T*)y, nseg, inner); break;
+    case RedOp::MIN: hipLaunchKernelGGL((seg_csr<T, (int)RedOp::MIN>), grid, dim3(bs), 0, s, (const T*)x, off, (T*)y, nseg, inner); break;
+    case RedOp::MAX: hipLaunchKernelGGL((seg_csr<T, (int)RedOp::MAX>), grid, dim3(bs), 0, s, (const T*)x, off, (T*)y, nseg, inner); break;
+    case RedOp::MEAN: hipLaunchKernelGGL((seg_csr<T, (int)RedOp::MEAN>), grid, dim3(bs), 0, s, (const T*)x, off, (T*)y, nseg, inner); break;
+    default: TFA_CHECK(false, "segment reduce: unsupported op");
+  }
+}
+
+void segment_reduce_csr(RedOp op, DType dt, const void* x, const int64_t* offsets, void* y, int64_t nseg,
+                        int64_t inner, hipStream_t s) {
+  if (nseg * inner <= 0) return;
+  TFA_CHECK(nseg <= 0x7fffffff, "segment reduce: too many segments");
+  switch (dt) {
+    case DType::F32: seg_csr_op<float>(op, x, offsets, y, nseg, inner, s); break;
+    case DType::F64: seg_csr_op<double>(op, x, offsets, y, nseg, inner, s); break;
+    case DType::I32: seg_csr_op<int32_t>(op, x, offsets, y, nseg, inner, s); break;
+    case DType::I64: seg_csr_op<int64_t>(op, x, offsets, y, nseg, inner, s); break;
+    default: TFA_CHECK(false, "segment reduce: dtype not supported");
+  }
+  TFA_LAUNCH_CHECK("segment_reduce_csr");
+}
+
+}  // namespace k
+}  // namespace tfa

@@ -1,0 +1,589 @@
+// Planner + executor (see executor.h).
+#include "executor.h"
+
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+#include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <set>
+#include <sstream>
+
+#include "../ir/ops_common.h"
+
+namespace tfa {
+
+void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, bool tb,
+              const at::Tensor* bias, int act, at::Tensor& out);
+void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
+                int act, at::Tensor& out);
+
+namespace {
+
+#define HIP_OK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    TFA_CHECK(_e == hipSuccess, "HIP error ", hipGetErrorString(_e), " at ", #expr); \
+  } while (0)
+
+bool debug_sync() {
+  static bool v = [] {
+    const char* e = std::getenv("TFA_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+struct RangeGuard {
+  explicit RangeGuard(const std::string& name) { roctxRangePushA(name.c_str()); }
+  ~RangeGuard() { roctxRangePop(); }
+};
+
+std::string strip0(const std::string& s) {
+  if (s.size() > 2 && s.compare(s.size() - 2, 2, ":0") == 0) return s.substr(0, s.size() - 2);
+  return s;
+}
+
+}  // namespace
+
+struct Program::Step {
+  enum Kind { OP, GEMM, CONV } kind = OP;
+  int node = -1;         // node whose op runs (for GEMM/CONV: the MatMul/Conv2D node)
+  int out_node = -1;     // node whose outputs this step produces
+  std::vector<int> in_slots;
+  std::vector<int> out_slots;
+  std::vector<TensorInfo> out_info;
+  std::vector<const TensorInfo*> in_info;
+  int bias_slot = -1;
+  int act = 0;
+  std::vector<int> release;  // slots dropped after the step
+};
+
+struct Program::Plan {
+  Graph::Infos infos;
+  std::vector<Step> steps;
+  int nslots = 0;
+  std::vector<int> feed_slots;
+  std::vector<std::pair<int, TensorRef>> const_slots;  // slot <- constant value of ref
+  std::vector<int> fetch_slots;
+  std::map<int, std::map<int, at::Tensor>> dev_consts;  // device index -> slot -> tensor
+  int fused = 0;
+};
+
+Program::Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetches,
+                 const std::vector<std::string>& feeds)
+    : g_(std::move(g)) {
+  TFA_CHECK(!fetches.empty(), "no fetches given");
+  std::set<std::string> seen;
+  for (auto& f : fetches) {
+    fetches_.push_back(g_->resolve(f));
+    fetch_names_.push_back(strip0(f));
+  }
+  std::set<int> cut;
+  for (auto& f : feeds) {
+    TensorRef r = g_->resolve(f);
+    TFA_CHECK(r.index == 0, "can only feed output 0 of node '", f, "'");
+    feed_nodes_.push_back(r.node);
+    feed_names_.push_back(strip0(f));
+    cut.insert(r.node);
+  }
+  // closure with feed nodes as cut points
+  std::vector<int> state(g_->nodes().size(), 0);
+  std::vector<std::pair<int, size_t>> stack;
+  for (auto& f : fetches_) {
+    if (state[f.node]) continue;
+    stack.push_back({f.node, 0});
+    state[f.node] = 1;
+    while (!stack.empty()) {
+      auto& [n, k] = stack.back();
+      const Node& nd = g_->node(n);
+      size_t total = cut.count(n) ? 0 : nd.inputs.size() + nd.control.size();
+      if (k < total) {
+        int dep = k < nd.inputs.size() ? nd.inputs[k].node : nd.control[k - nd.inputs.size()];
+        ++k;
+        TFA_CHECK(state[dep] != 1, "cycle in graph at node '", g_->node(dep).name, "'");
+        if (state[dep] == 0) {
+          state[dep] = 1;
+          stack.push_back({dep, 0});
+        }
+      } else {
+        state[n] = 2;
+        order_.push_back(n);
+        stack.pop_back();
+      }
+    }
+  }
+  // every placeholder reached must be fed
+  for (int n : order_) {
+    const Node& nd = g_->node(n);
+    if ((nd.op == "Placeholder" || nd.op == "PlaceholderV2") && !cut.count(n))
+      TFA_CHECK(false, "placeholder '", nd.name, "' is needed by the fetches but is not fed");
+  }
+}
+
+Graph::Infos Program::analyze(const std::map<std::string, TensorInfo>& feed_infos) const {
+  std::map<int, TensorInfo> feeds;
+  for (size_t i = 0; i < feed_nodes_.size(); ++i) {
+    auto it = feed_infos.find(feed_names_[i]);
+    if (it != feed_infos.end()) {
+      TensorInfo ti = it->second;
+      ti.row = RowClass::ROW;
+      feeds[feed_nodes_[i]] = ti;
+    } else {
+      const Node& nd = g_->node(feed_nodes_[i]);
+      if (nd.op != "Placeholder" && nd.op != "PlaceholderV2") {
+        TensorInfo ti;
+        ti.row = RowClass::ROW;
+        feeds[feed_nodes_[i]] = ti;
+      }
+    }
+  }
+  return g_->infer(order_, feeds, false);
+}
+
+bool Program::row_separable(const std::map<std::string, TensorInfo>& feed_infos) const {
+  Graph::Infos infos = analyze(feed_infos);
+  for (auto& f : fetches_)
+    if (infos[f.node][f.index].row != RowClass::ROW) return false;
+  return true;
+}
+
+std::vector<MonoidInfo> Program::monoids() const {
+  std::vector<MonoidInfo> out;
+  for (size_t i = 0; i < fetches_.size(); ++i) {
+    const Node& n = g_->node(fetches_[i].node);
+    if (!(n.op == "Sum" || n.op == "Min" || n.op == "Max" || n.op == "Prod")) return {};
+    if (n.inputs.size() != 2) return {};
+    const Node& src = g_->node(n.inputs[0].node);
+    if (!(src.op == "Placeholder" || src.op == "PlaceholderV2")) return {};
+    const Node& ax = g_->node(n.inputs[1].node);
+    if (ax.op != "Const") return {};
+    at::Tensor v = host_tensor_to_at(ax.attr_tensor("value"));
+    auto axes = to_int_vector(v);
+    if (axes.size() != 1 || axes[0] != 0) return {};
+    bool keep = n.has_attr("keep_dims") ? n.attr_b("keep_dims") : n.attr_b("keepdims", false);
+    if (keep) return {};
+    out.push_back({fetch_names_[i], src.name, n.op});
+  }
+  return out;
+}
+
+static std::string plan_key(const std::vector<at::Tensor>& inputs) {
+  std::ostringstream os;
+  for (auto& t : inputs) {
+    os << static_cast<int>(t.scalar_type()) << ':' << (t.is_cuda() ? 1 : 0) << '[';
+    for (auto d : t.sizes()) os << d << ',';
+    os << ']';
+  }
+  return os.str();
+}
+
+std::shared_ptr<Program::Plan> Program::plan_for(const std::vector<at::Tensor>& inputs) {
+  TFA_CHECK(inputs.size() == feed_nodes_.size(), "expected ", feed_nodes_.size(), " inputs, got ",
+            inputs.size());
+  std::string key = plan_key(inputs);
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = plans_.find(key);
+  if (it != plans_.end()) return it->second;
+  auto p = build_plan(inputs);
+  plans_[key] = p;
+  stats_.plans_built++;
+  return p;
+}
+
+std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>& inputs) {
+  auto p = std::make_shared<Plan>();
+  std::map<int, TensorInfo> feeds;
+  for (size_t i = 0; i < inputs.size(); ++i) {
+    TensorInfo ti;
+    ti.dtype = from_scalar_type(inputs[i].scalar_type());
+    ti.shape = shape_of(inputs[i]);
+    ti.row = RowClass::ROW;
+    const Node& nd = g_->node(feed_nodes_[i]);
+    if (nd.op == "Placeholder" || nd.op == "PlaceholderV2") {
+      DType want = nd.attr_type("dtype");
+      TFA_CHECK(want == ti.dtype, "placeholder '", nd.name, "' has dtype ", dtype_name(want),
+                " but was fed ", dtype_name(ti.dtype), " (no implicit casting)");
+      if (const AttrValue* a = nd.def->find_attr("shape")) {
+        if (a->kind == AttrValue::SHAPE && !a->shape.unknown_rank) {
+          const Shape& s = a->shape;
+          bool ok = s.rank() == ti.shape.rank();
+          for (int d = 0; ok && d < s.rank(); ++d) ok = s.dims[d] < 0 || s.dims[d] == ti.shape.dims[d];
+          TFA_CHECK(ok, "placeholder '", nd.name, "' has shape ", s.str(), " but was fed ", ti.shape.str());
+        }
+      }
+    }
+    feeds[feed_nodes_[i]] = ti;
+  }
+  p->infos = g_->infer(order_, feeds, true);
+  const Graph::Infos& infos = p->infos;
+
+  // slots
+  std::map<TensorRef, int> slot_of;
+  auto new_slot = [&]() { return p->nslots++; };
+  std::set<int> feed_set(feed_nodes_.begin(), feed_nodes_.end());
+  for (size_t i = 0; i < feed_nodes_.size(); ++i) {
+    int s = new_slot();
+    slot_of[{feed_nodes_[i], 0}] = s;
+    p->feed_slots.push_back(s);
+  }
+  auto is_const = [&](const TensorRef& r) { return static_cast<bool>(infos[r.node][r.index].value); };
+  auto slot_for = [&](const TensorRef& r) -> int {
+    auto it = slot_of.find(r);
+    if (it != slot_of.end()) return it->second;
+    TFA_CHECK(is_const(r), "internal: tensor '", g_->node(r.node).name, ":", r.index, "' has no producer");
+    int s = new_slot();
+    slot_of[r] = s;
+    p->const_slots.push_back({s, r});
+    return s;
+  };
+
+  // consumer counts (runtime consumers + fetches)
+  std::map<TensorRef, int> uses;
+  std::set<TensorRef> fetched(fetches_.begin(), fetches_.end());
+  std::vector<int> runtime;
+  for (int n : order_) {
+    if (feed_set.count(n)) continue;
+    const Node& nd = g_->node(n);
+    bool all_const = true;
+    for (auto& o : infos[n]) all_const = all_const && (o.value.has_value() || o.dtype == DType::STRING);
+    if (all_const || nd.num_outputs == 0) continue;
+    runtime.push_back(n);
+    for (auto& r : nd.inputs) uses[r]++;
+  }
+  for (auto& f : fetches_) uses[f]++;
+
+  std::map<int, int> consumer;  // node -> its single runtime consumer node (if exactly one use)
+  for (int n : runtime)
+    for (auto& r : g_->node(n).inputs)
+      if (uses[r] == 1) consumer[r.node] = n;
+
+  const OpRegistry& reg = OpRegistry::get();
+  std::set<int> absorbed;
+  for (int n : runtime) {
+    if (absorbed.count(n)) continue;
+    const Node& nd = g_->node(n);
+    Step st;
+    st.node = n;
+    st.out_node = n;
+    // ---- fusion: MatMul/Conv2D -> (BiasAdd | Add const-vector) -> (Relu | Relu6)
+    bool gemm = nd.op == "MatMul" &&
+                (infos[n][0].dtype == DType::F32 || infos[n][0].dtype == DType::F64);
+    bool conv = nd.op == "Conv2D" && infos[n][0].dtype == DType::F32;
+    if (gemm || conv) {
+      st.kind = gemm ? Step::GEMM : Step::CONV;
+      int cur = n;
+      TensorRef cur_ref{n, 0};
+      int64_t ncols = infos[n][0].shape.dims.back();
+      auto single = [&](int node) -> int {
+        TensorRef r{node, 0};
+        if (fetched.count(r) || uses[r] != 1 || !consumer.count(node)) return -1;
+        return consumer[node];
+      };
+      int c1 = single(cur);
+      if (c1 >= 0) {
+        const Node& cn = g_->node(c1);
+        int other = -1;
+        if (cn.op == "BiasAdd" && cn.inputs[0] == cur_ref &&
+            cn.attr_s("data_format", std::string("NHWC")) != "NCHW")
+          other = 1;
+        else if ((cn.op == "Add" || cn.op == "AddV2") && cn.inputs.size() == 2)
+          other = cn.inputs[0] == cur_ref ? 1 : (cn.inputs[1] == cur_ref ? 0 : -1);
+        if (other >= 0) {
+          const TensorRef& br = cn.inputs[other];
+          const TensorInfo& bi = infos[br.node][br.index];
+          bool ok = bi.shape.rank() == 1 && bi.shape.dims[0] == ncols && bi.dtype == infos[n][0].dtype &&
+                    infos[c1][0].shape == infos[n][0].shape;
+          if (ok) {
+            st.bias_slot = -2 - static_cast<int>(br.node);  // resolved below
+            st.bias_slot = slot_for(br);
+            absorbed.insert(c1);
+            cur = c1;
+            cur_ref = {c1, 0};
+          }
+        }
+      }
+      int c2 = single(cur);
+      if (c2 >= 0) {
+        const Node& cn = g_->node(c2);
+        if ((cn.op == "Relu" || cn.op == "Relu6") && cn.inputs[0] == cur_ref) {
+          st.act = cn.op == "Relu" ? 1 : 2;
+          absorbed.insert(c2);
+          cur = c2;
+        }
+      }
+      st.out_node = cur;
+      if (cur != n) p->fused++;
+    }
+    const OpDef* od = reg.find(nd.op);
+    TFA_CHECK(od && od->compute, "op '", nd.op, "' has no compute function");
+    for (auto& r : nd.inputs) {
+      st.in_slots.push_back(slot_for(r));
+      st.in_info.push_back(&infos[r.node][r.index]);
+    }
+    st.out_info = infos[st.out_node];
+    for (size_t k = 0; k < infos[st.out_node].size(); ++k) {
+      int s = new_slot();
+      slot_of[{st.out_node, static_cast<int>(k)}] = s;
+      st.out_slots.push_back(s);
+    }
+    p->steps.push_back(std::move(st));
+  }
+  for (auto& f : fetches_) p->fetch_slots.push_back(slot_for(f));
+
+  // liveness: release each slot after its last reading step (fetches/consts are kept)
+  std::vector<int> last(p->nslots, -1);
+  for (size_t i = 0; i < p->steps.size(); ++i) {
+    for (int s : p->steps[i].in_slots) last[s] = static_cast<int>(i);
+    if (p->steps[i].bias_slot >= 0) last[p->steps[i].bias_slot] = static_cast<int>(i);
+  }
+  std::set<int> keep(p->fetch_slots.begin(), p->fetch_slots.end());
+  for (auto& cs : p->const_slots) keep.insert(cs.first);
+  for (int s = 0; s < p->nslots; ++s)
+    if (last[s] >= 0 && !keep.count(s)) p->steps[last[s]].release.push_back(s);
+  return p;
+}
+
+at::Tensor Program::device_const(Plan& p, int slot, const at::Device& dev) {
+  int di = dev.is_cuda() ? dev.index() : -1;
+  auto& m = p.dev_consts[di];
+  auto it = m.find(slot);
+  if (it != m.end()) return it->second;
+  TensorRef r{};
+  for (auto& cs : p.const_slots)
+    if (cs.first == slot) r = cs.second;
+  const at::Tensor& v = *p.infos[r.node][r.index].value;
+  at::Tensor t = dev.is_cuda() ? v.contiguous().to(dev, /*non_blocking=*/false) : v.contiguous();
+  m[slot] = t;
+  return t;
+}
+
+std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream) {
+  const OpRegistry& reg = OpRegistry::get();
+  at::Device dev = inputs.empty() ? at::Device(at::kCPU) : inputs[0].device();
+  bool gpu = dev.is_cuda();
+  for (auto& t : inputs)
+    TFA_CHECK(t.device() == dev, "all inputs must live on the same device");
+  std::vector<at::Tensor> slots(p.nslots);
+  for (size_t i = 0; i < inputs.size(); ++i) slots[p.feed_slots[i]] = inputs[i].contiguous();
+  for (auto& cs : p.const_slots) slots[cs.first] = device_const(p, cs.first, dev);
+  for (auto& st : p.steps) {
+    const Node& nd = g_->node(st.node);
+    ExecCtx c{nd, {}, {}, &st.out_info, &st.in_info, gpu, stream};
+    for (int s : st.in_slots) c.in.push_back(slots[s]);
+    c.out.resize(st.out_info.size());
+    {
+      std::unique_ptr<RangeGuard> rg;
+      if (gpu) rg = std::make_unique<RangeGuard>(nd.op + ":" + nd.name);
+      try {
+        if (st.kind == Step::OP) {
+          reg.find(nd.op)->compute(c);
+        } else {
+          at::Tensor out = gpu ? c.alloc_out(0) : at::Tensor();
+          at::Tensor bias;
+          if (st.bias_slot >= 0) bias = slots[st.bias_slot];
+          const at::Tensor* bp = st.bias_slot >= 0 ? &bias : nullptr;
+          if (st.kind == Step::GEMM)
+            run_gemm(c, c.in[0], c.in[1], nd.attr_b("transpose_a", false), nd.attr_b("transpose_b", false), bp, st.act, out);
+          else
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out);
+          c.out[0] = out;
+        }
+      } catch (const GraphError& e) {
+        throw GraphError(str_cat("while executing node '", nd.name, "' (", nd.op, "): ", e.what()));
+      }
+    }
+    if (gpu && debug_sync()) {
+      HIP_OK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+      HIP_OK(hipGetLastError());
+    }
+    for (size_t k = 0; k < st.out_slots.size(); ++k) {
+      at::Tensor& o = c.out[k];
+      TFA_CHECK(o.defined(), "internal: node '", nd.name, "' produced no output ", k);
+      const Shape& want = st.out_info[k].shape;
+      TFA_CHECK(want.fully_known() && o.sizes().vec() == want.dims, "internal: node '", nd.name,
+                "' produced shape ", shape_of(o).str(), " but inference said ", want.str());
+      slots[st.out_slots[k]] = o;
+    }
+    for (int s : st.release) slots[s] = at::Tensor();
+    stats_.kernels++;
+  }
+  std::vector<at::Tensor> outs;
+  for (int s : p.fetch_slots) outs.push_back(slots[s]);
+  return outs;
+}
+
+std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
+  auto p = plan_for(inputs);
+  bool gpu = !inputs.empty() && inputs[0].is_cuda();
+  void* stream = nullptr;
+  std::optional<c10::hip::HIPGuard> guard;
+  if (gpu) {
+    guard.emplace(inputs[0].device().index());
+    stream = c10::hip::getCurrentHIPStream(inputs[0].device().index()).stream();
+  }
+  auto outs = execute(*p, inputs, stream);
+  stats_.runs++;
+  return outs;
+}
+
+void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
+                          const std::vector<std::vector<at::Tensor>>& seg_outputs,
+                          int64_t chunk_rows, int device, int depth) {
+  TFA_CHECK(seg_inputs.size() == seg_outputs.size(), "segments mismatch");
+  TFA_CHECK(chunk_rows > 0, "chunk_rows must be > 0");
+  depth = std::max(2, std::min(depth, 4));
+  c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+  at::Device dev(at::kCUDA, static_cast<c10::DeviceIndex>(device));
+  auto compute = c10::hip::getCurrentHIPStream(device);
+  auto h2d = c10::hip::getStreamFromPool(false, device);
+  auto d2h = c10::hip::getStreamFromPool(false, device);
+  auto t0 = std::chrono::steady_clock::now();
+
+  struct Chunk {
+    size_t seg;
+    int64_t start, rows;
+  };
+  std::vector<Chunk> chunks;
+  for (size_t s = 0; s < seg_inputs.size(); ++s) {
+    TFA_CHECK(seg_inputs[s].size() == feed_nodes_.size(), "segment ", s, ": expected ",
+              feed_nodes_.size(), " inputs");
+    TFA_CHECK(seg_outputs[s].size() == fetches_.size(), "segment ", s, ": expected ",
+              fetches_.size(), " outputs");
+    int64_t rows = seg_inputs[s].empty() ? 0 : seg_inputs[s][0].size(0);
+    for (auto& t : seg_inputs[s]) {
+      TFA_CHECK(t.size(0) == rows, "segment inputs disagree on rows");
+      TFA_CHECK(!t.is_cuda() && t.is_contiguous(), "run_chunked inputs must be contiguous host tensors");
+    }
+    for (auto& t : seg_outputs[s])
+      TFA_CHECK(!t.is_cuda() && t.is_contiguous() && t.size(0) == rows,
+                "run_chunked outputs must be contiguous host tensors with ", rows, " rows");
+    for (int64_t st = 0; st < rows; st += chunk_rows) chunks.push_back({s, st, std::min(chunk_rows, rows - st)});
+  }
+  if (chunks.empty()) return;
+
+  // device input ring
+  size_t nin = feed_nodes_.size();
+  std::vector<std::vector<at::Tensor>> ring(depth);
+  for (int d = 0; d < depth; ++d)
+    for (size_t i = 0; i < nin; ++i) {
+      auto sz = seg_inputs[0][i].sizes().vec();
+      sz[0] = chunk_rows;
+      ring[d].push_back(at::empty(sz, seg_inputs[0][i].options().device(dev).pinned_memory(false)));
+    }
+  std::vector<hipEvent_t> ev_h2d(depth), ev_comp(depth), ev_d2h(depth);
+  for (int d = 0; d < depth; ++d) {
+    HIP_OK(hipEventCreateWithFlags(&ev_h2d[d], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_comp[d], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_d2h[d], hipEventDisableTiming));
+  }
+  std::vector<bool> used(depth, false);
+  int64_t h2d_bytes = 0, d2h_bytes = 0;
+  for (size_t ci = 0; ci < chunks.size(); ++ci) {
+    const Chunk& ch = chunks[ci];
+    int slot = static_cast<int>(ci % depth);
+    // H2D: wait until the compute (and any D2H of outputs aliasing the ring) of this slot finished
+    if (used[slot]) {
+      HIP_OK(hipStreamWaitEvent(h2d.stream(), ev_comp[slot], 0));
+      HIP_OK(hipStreamWaitEvent(h2d.stream(), ev_d2h[slot], 0));
+    }
+    std::vector<at::Tensor> dev_in;
+    for (size_t i = 0; i < nin; ++i) {
+      const at::Tensor& src = seg_inputs[ch.seg][i];
+      int64_t row_bytes = src.numel() / std::max<int64_t>(src.size(0), 1) * src.element_size();
+      at::Tensor dst = ring[slot][i].narrow(0, 0, ch.rows);
+      const char* sp = static_cast<const char*>(src.data_ptr()) + ch.start * row_bytes;
+      if (ch.rows * row_bytes)
+        HIP_OK(hipMemcpyAsync(dst.data_ptr(), sp, ch.rows * row_bytes, hipMemcpyHostToDevice, h2d.stream()));
+      h2d_bytes += ch.rows * row_bytes;
+      dev_in.push_back(dst);
+    }
+    HIP_OK(hipEventRecord(ev_h2d[slot], h2d.stream()));
+    // compute
+    HIP_OK(hipStreamWaitEvent(compute.stream(), ev_h2d[slot], 0));
+    std::vector<at::Tensor> outs;
+    {
+      RangeGuard rg("chunk_compute");
+      auto p = plan_for(dev_in);
+      outs = execute(*p, dev_in, compute.stream());
+    }
+    HIP_OK(hipEventRecord(ev_comp[slot], compute.stream()));
+    // D2H
+    HIP_OK(hipStreamWaitEvent(d2h.stream(), ev_comp[slot], 0));
+    for (size_t j = 0; j < outs.size(); ++j) {
+      at::Tensor o = outs[j];
+      const at::Tensor& dst = seg_outputs[ch.seg][j];
+      int64_t row_bytes = dst.numel() / std::max<int64_t>(dst.size(0), 1) * dst.element_size();
+      TFA_CHECK(o.size(0) == ch.rows && o.numel() * o.element_size() == ch.rows * row_bytes,
+                "fetch '", fetch_names_[j], "' produced ", o.size(0), " rows for a chunk of ", ch.rows);
+      if (!o.is_cuda()) o = o.to(dev);  // constant fetch
+      char* dp = static_cast<char*>(dst.data_ptr()) + ch.start * row_bytes;
+      if (ch.rows * row_bytes)
+        HIP_OK(hipMemcpyAsync(dp, o.data_ptr(), ch.rows * row_bytes, hipMemcpyDeviceToHost, d2h.stream()));
+      c10::hip::HIPCachingAllocator::recordStream(o.storage().data_ptr(), d2h);
+      d2h_bytes += ch.rows * row_bytes;
+    }
+    HIP_OK(hipEventRecord(ev_d2h[slot], d2h.stream()));
+    used[slot] = true;
+    stats_.chunks++;
+  }
+  HIP_OK(hipStreamSynchronize(h2d.stream()));
+  HIP_OK(hipStreamSynchronize(compute.stream()));
+  HIP_OK(hipStreamSynchronize(d2h.stream()));
+  for (int d = 0; d < depth; ++d) {
+    hipEventDestroy(ev_h2d[d]);
+    hipEventDestroy(ev_comp[d]);
+    hipEventDestroy(ev_d2h[d]);
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  stats_.runs++;
+  stats_.h2d_bytes += h2d_bytes;
+  stats_.d2h_bytes += d2h_bytes;
+  stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+}
+
+ExecStats Program::stats() const { return stats_; }
+void Program::reset_stats() { stats_ = ExecStats(); }
+
+std::string Program::describe_plan(const std::vector<at::Tensor>& inputs) {
+  auto p = plan_for(inputs);
+  std::ostringstream os;
+  os << "plan: " << p->steps.size() << " steps, " << p->const_slots.size() << " constants, "
+     << p->fused << " fused epilogues\n";
+  for (auto& st : p->steps) {
+    const Node& nd = g_->node(st.node);
+    os << "  " << (st.kind == Step::GEMM ? "GEMM" : st.kind == Step::CONV ? "CONV" : "OP  ") << ' '
+       << nd.op << ' ' << nd.name;
+    if (st.out_node != st.node) os << " -> " << g_->node(st.out_node).name;
+    if (st.bias_slot >= 0) os << " +bias";
+    if (st.act) os << (st.act == 1 ? " +relu" : " +relu6");
+    os << ' ' << st.out_info[0].shape.str() << '\n';
+  }
+  return os.str();
+}
+
+// ------------------------------------------------------------------ pinned memory
+at::Tensor empty_pinned(const std::vector<int64_t>& sizes, at::ScalarType dt) {
+  int64_t n = 1;
+  for (auto s : sizes) n *= s;
+  size_t bytes = static_cast<size_t>(std::max<int64_t>(n, 1)) * c10::elementSize(dt);
+  void* p = nullptr;
+  HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+  return at::from_blob(p, sizes, [](void* q) { hipHostFree(q); }, at::TensorOptions().dtype(dt));
+}
+
+void pin_host_tensor(const at::Tensor& t) {
+  TFA_CHECK(!t.is_cuda(), "pin_host_tensor needs a host tensor");
+  size_t bytes = t.numel() * t.element_size();
+  if (!bytes) return;
+  HIP_OK(hipHostRegister(t.data_ptr(), bytes, hipHostRegisterDefault));
+}
+
+void unpin_host_tensor(const at::Tensor& t) {
+  if (t.numel()) hipHostUnregister(t.data_ptr());
+}
+
+}  // namespace tfa

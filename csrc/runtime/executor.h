@@ -1,0 +1,92 @@
+// Program = a graph pruned to (fetches, feeds) + a cache of concrete plans.
+//
+// Replaces the per-partition `withSession { runner.feed(..).fetch(..).run() }`
+// of the reference (reference: src/main/scala/org/tensorframes/impl/DebugRowOps.scala:766-803,900-917).
+// A plan is specialised to concrete feed shapes: shapes are inferred, every
+// shape-only subgraph is folded on the host, MatMul/Conv2D + BiasAdd + Relu
+// chains are fused into one kernel, and intermediate buffers are released at
+// their last use (the HIP caching allocator then reuses them).
+#pragma once
+
+#include <ATen/ATen.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../ir/graph.h"
+
+namespace tfa {
+
+struct MonoidInfo {
+  std::string fetch;
+  std::string placeholder;
+  std::string op;  // Sum / Min / Max / Prod
+};
+
+struct ExecStats {
+  int64_t runs = 0;
+  int64_t kernels = 0;
+  int64_t plans_built = 0;
+  int64_t h2d_bytes = 0;
+  int64_t d2h_bytes = 0;
+  int64_t chunks = 0;
+  double h2d_ms = 0, compute_ms = 0, d2h_ms = 0, wall_ms = 0;
+};
+
+class Program {
+ public:
+  Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetches,
+          const std::vector<std::string>& feeds);
+
+  const std::vector<std::string>& fetch_names() const { return fetch_names_; }
+  const std::vector<std::string>& feed_names() const { return feed_names_; }
+
+  // Static analysis with optional hints (dtype/shape per feed).
+  Graph::Infos analyze(const std::map<std::string, TensorInfo>& feed_infos) const;
+  // Can the graph be evaluated on row chunks of the block independently?
+  bool row_separable(const std::map<std::string, TensorInfo>& feed_infos) const;
+  // Per-fetch monoid reduction `fetch = Op(placeholder, axis 0)` (empty if not all are).
+  std::vector<MonoidInfo> monoids() const;
+
+  // Run on concrete inputs (all on one device: CPU or a GPU). Returns the fetches.
+  std::vector<at::Tensor> run(const std::vector<at::Tensor>& inputs);
+
+  // Pipelined host->device->host execution over row chunks of several segments.
+  // seg_inputs[s][i]: pinned host tensor for feed i of segment s (leading dim = rows).
+  // seg_outputs[s][j]: preallocated pinned host tensor for fetch j.
+  void run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
+                   const std::vector<std::vector<at::Tensor>>& seg_outputs, int64_t chunk_rows,
+                   int device, int depth);
+
+  ExecStats stats() const;
+  void reset_stats();
+  std::string describe_plan(const std::vector<at::Tensor>& inputs);
+
+ private:
+  struct Step;
+  struct Plan;
+  std::shared_ptr<Plan> plan_for(const std::vector<at::Tensor>& inputs);
+  std::shared_ptr<Plan> build_plan(const std::vector<at::Tensor>& inputs);
+  std::vector<at::Tensor> execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream);
+  at::Tensor device_const(Plan& p, int slot, const at::Device& dev);
+
+  std::shared_ptr<Graph> g_;
+  std::vector<std::string> fetch_names_, feed_names_;
+  std::vector<TensorRef> fetches_;
+  std::vector<int> feed_nodes_;
+  std::vector<int> order_;
+  std::mutex mu_;
+  std::map<std::string, std::shared_ptr<Plan>> plans_;
+  ExecStats stats_;
+};
+
+// pinned host memory (hipHostMalloc, exact size; freed with hipHostFree)
+at::Tensor empty_pinned(const std::vector<int64_t>& sizes, at::ScalarType dt);
+// page-lock an existing host tensor's memory in place (hipHostRegister)
+void pin_host_tensor(const at::Tensor& t);
+void unpin_host_tensor(const at::Tensor& t);
+
+}  // namespace tfa

@@ -1,0 +1,33 @@
+#!/bin/bash
+# GPU-box driver: runs named steps under their own time limits; stops at the
+# first step that faults the GPU, aborts, segfaults or times out.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() {
+  local name=$1; shift
+  local secs=$1; shift
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if grep -qiE "memory access fault|illegal address|hipErrorIllegal|HSA_STATUS_ERROR|core dumped" "gpurun_out/$name.log"; then
+    echo "GPU fault in $name: stopping"; exit 99
+  fi
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"smoke tests bench"}
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 1200 python -m pytest tests -m gpu -x -q ;;
+    kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -x -q ;;
+    bench) run bench 900 python bench.py --steps ${BENCH_STEPS:-5} --warmup ${BENCH_WARMUP:-2} ${BENCH_ARGS:-} ;;
+    benchsmall) run benchsmall 600 python bench.py --steps 3 --warmup 1 --rows 1000000 ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --mode host ${BENCH_ARGS:-} ;;
+  esac
+done
+echo "all steps done"

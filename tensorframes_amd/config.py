@@ -1,0 +1,49 @@
+"""Runtime configuration (one dataclass, `TFA_*` environment overrides).
+
+The reference has no flag system (configuration is spread over Spark conf,
+sbt properties and a hard-coded UDAF buffer size; reference:
+src/main/scala/org/tensorframes/impl/DebugRowOps.scala:573)."""
+from __future__ import annotations
+
+import dataclasses
+import os
+
+
+def _env(name, default, cast):
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    if cast is bool:
+        return v.lower() in ("1", "true", "yes", "on")
+    return cast(v)
+
+
+@dataclasses.dataclass
+class Config:
+    # "auto" (GPU when present), "cpu", "cuda"
+    device: str = dataclasses.field(default_factory=lambda: _env("TFA_DEVICE", "auto", str))
+    # target bytes of one input column per pipelined chunk (host->device->host)
+    chunk_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_CHUNK_BYTES", 128 << 20, int))
+    # ring depth of the copy/compute pipeline
+    pipeline_depth: int = dataclasses.field(default_factory=lambda: _env("TFA_PIPELINE_DEPTH", 3, int))
+    # partitions smaller than this run in one shot (no chunking)
+    min_chunked_rows: int = dataclasses.field(default_factory=lambda: _env("TFA_MIN_CHUNKED_ROWS", 65536, int))
+    # allocate map_blocks outputs in page-locked host memory (DMA target)
+    pinned_outputs: bool = dataclasses.field(default_factory=lambda: _env("TFA_PINNED_OUTPUTS", True, bool))
+    pinned_min_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_PINNED_MIN_BYTES", 1 << 20, int))
+    # map_rows: cells at least this large run on the GPU, smaller ones on the host executor
+    map_rows_gpu_min_elems: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_GPU_MIN", 16384, int))
+    # synchronise + check after every kernel (debugging)
+    debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
+
+
+config = Config()
+
+
+def set_config(**kw):
+    for k, v in kw.items():
+        if not hasattr(config, k):
+            raise AttributeError(f"unknown config key {k}")
+        setattr(config, k, v)
+    if "debug_sync" in kw:
+        os.environ["TFA_DEBUG_SYNC"] = "1" if kw["debug_sync"] else "0"

@@ -1,0 +1,840 @@
+"""TensorFrames operators: map_blocks, map_rows, reduce_blocks, reduce_rows,
+aggregate, analyze, print_schema, block, row.
+
+Public signatures and return conventions are the reference's
+(reference: src/main/python/tensorframes/core.py:138-366); validation rules and
+error messages follow its Scala engine (reference:
+src/main/scala/org/tensorframes/impl/DebugRowOps.scala:53-346,396-592).
+Execution is native: a cached `Program` per graph (C++ planner/executor with
+HIP/gfx950 kernels), partitions pinned to ranks, cross-partition reductions
+as RCCL collectives.
+"""
+from __future__ import annotations
+
+import os
+import zlib
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import engine
+from ._native import _C
+from .config import config
+from .frame.block import (Block, ObjectColumn, RaggedColumn, build_column, column_tf_dtype,
+                          column_values, concat_blocks, is_dense)
+from .frame.column_info import ColumnInformation, SparkTFColInfo, explain_schema
+from .frame.dataframe import DataFrame, GroupedData, _Derived, _Materialized, _sort_key
+from .frame.types import (NumericType, Row, StructField, StructType, sql_type_for_tf)
+from .graph import dsl
+from .graph import proto as P
+from .parallel import dist
+from .utils import dtypes as D
+from .utils.logging import logger, metrics
+from .utils.shape import UNKNOWN, Shape
+
+__all__ = ["reduce_rows", "map_rows", "reduce_blocks", "map_blocks", "analyze", "print_schema",
+           "aggregate", "block", "row"]
+
+
+class TensorFramesError(ValueError):
+    """Validation error raised before any data is touched."""
+
+
+def _check(cond: bool, msg: str):
+    if not cond:
+        raise TensorFramesError(msg)
+
+
+# ------------------------------------------------------------------ graph specs
+@dataclass
+class GraphSpec:
+    graph_bytes: bytes
+    fetch_names: List[str]           # column names (":0" stripped)
+    fetch_refs: List[str]            # tensor names as given to the runtime
+    hints: Dict[str, Shape]          # shape hints (fetches, zero-input nodes)
+    dsl_fetches: Optional[list] = None
+
+
+def _strip(name: str) -> str:
+    return name[:-2] if name.endswith(":0") else name
+
+
+def _graph_bytes(graph) -> bytes:
+    if isinstance(graph, (bytes, bytearray)):
+        return bytes(graph)
+    if isinstance(graph, dsl.Graph):
+        return graph.serialize()
+    if isinstance(graph, P.GraphDef):
+        return P.serialize_graphdef(graph)
+    if isinstance(graph, str) and os.path.exists(graph):
+        with open(graph, "rb") as f:
+            return f.read()
+    if hasattr(graph, "SerializeToString"):
+        return graph.SerializeToString()
+    raise TypeError(f"cannot interpret {type(graph).__name__} as a graph")
+
+
+def _resolve(fetches, graph=None, shape_hints: Optional[Dict[str, Any]] = None) -> GraphSpec:
+    fl = list(fetches) if isinstance(fetches, (list, tuple)) else [fetches]
+    _check(len(fl) > 0, "no fetches given")
+    hints: Dict[str, Shape] = {}
+    dsl_fetches = None
+    if graph is None:
+        g = None
+        names = []
+        for f in fl:
+            if isinstance(f, dsl.Tensor):
+                g = g or f.graph
+                if f.graph is not g:
+                    raise TypeError(f"Fetch {f} belongs to another graph")
+                names.append(f.name)
+            elif isinstance(f, dsl.Operation):
+                g = g or f.graph
+                names.append(f.outputs[0].name)
+            elif isinstance(f, str):
+                names.append(f)
+            else:
+                raise TypeError(f"Fetch argument {f!r} has invalid type {type(f).__name__}, "
+                                f"must be a string or Tensor.")
+        g = g or dsl.get_default_graph()
+        for n in names:
+            try:
+                g.as_graph_element(n if ":" in n else n + ":0")
+            except (KeyError, ValueError) as e:
+                raise ValueError(f"Fetch argument {n!r} cannot be interpreted as a Tensor. ({e})")
+        gbytes = g.serialize()
+        dsl_fetches = [g.get_tensor_by_name(n if ":" in n else n + ":0") for n in names]
+    else:
+        gbytes = _graph_bytes(graph)
+        names = [f.name if isinstance(f, dsl.Tensor) else str(f) for f in fl]
+    cols = [_strip(n).split(":")[0] for n in names]
+    if len(set(cols)) != len(cols):
+        raise ValueError(f"Could not infer a list of unique names for the columns: {names}")
+    for k, v in (shape_hints or {}).items():
+        hints[_strip(k)] = v if isinstance(v, Shape) else Shape([UNKNOWN if d is None else d for d in v])
+    return GraphSpec(gbytes, cols, names, hints, dsl_fetches)
+
+
+@dataclass
+class NodeSummary:
+    """reference: GraphNodeSummary (src/main/scala/org/tensorframes/impl/TensorFlowOps.scala:163-169)."""
+
+    name: str
+    is_placeholder: bool
+    is_input: bool
+    is_output: bool
+    tf_dtype: int
+    shape: Shape
+
+    @property
+    def sql_type(self) -> NumericType:
+        return sql_type_for_tf(self.tf_dtype)
+
+
+def analyze_graph(spec: GraphSpec) -> Dict[str, NodeSummary]:
+    """Inputs = every zero-input Placeholder of the graph, outputs = the fetches;
+    a shape hint overrides the inferred shape (reference: TensorFlowOps.scala:101-141)."""
+    g = engine.native_graph(spec.graph_bytes)
+    inputs = list(g.placeholders())
+    infos = _C.analyze_fetches(g, spec.fetch_refs, inputs, {})
+    out: Dict[str, NodeSummary] = {}
+    for ph in inputs:
+        i = infos[ph]
+        shape = spec.hints.get(ph) or (Shape(i["shape"]) if i["shape"] is not None else None)
+        out[ph] = NodeSummary(ph, True, True, False, i["dtype"], shape)
+    for ref, col in zip(spec.fetch_refs, spec.fetch_names):
+        i = infos[ref]
+        shape = spec.hints.get(col) or (Shape(i["shape"]) if i["shape"] is not None else None)
+        if col in out:
+            s = out[col]
+            out[col] = NodeSummary(col, s.is_placeholder, True, True, s.tf_dtype, s.shape)
+        else:
+            out[col] = NodeSummary(col, False, False, True, i["dtype"], shape)
+    return out
+
+
+def _sql_type_or_error(s: NodeSummary) -> NumericType:
+    try:
+        return s.sql_type
+    except TypeError:
+        raise TensorFramesError(f"Output '{s.name}' has dtype {D.dtype_name(s.tf_dtype)}, which "
+                                f"cannot be stored in a DataFrame column (double, float, int32, int64)")
+
+
+def _col_info(field: StructField) -> SparkTFColInfo:
+    stf = ColumnInformation(field).stf
+    _check(stf is not None,
+           f"Data column {field.name} has not been analyzed yet, cannot run TF on this dataframe")
+    return stf
+
+
+def _shape_str(s: Optional[Shape]) -> str:
+    return "<unknown>" if s is None else str(s)
+
+
+# ------------------------------------------------------------------ helpers
+def _dense_inputs(block: Block, cols: Sequence[str], op: str) -> List[torch.Tensor]:
+    ins = []
+    for c in cols:
+        col = block.columns[c]
+        if not is_dense(col):
+            raise TensorFramesError(
+                f"{op}: column '{c}' has cells of different shapes (or non-numeric values) in one "
+                f"block; use map_rows for variable-sized rows")
+        ins.append(col)
+    return ins
+
+
+def _empty_output(shape: Optional[Shape], tf_dtype: int) -> torch.Tensor:
+    cell = [0 if d == UNKNOWN else d for d in (shape.dims[1:] if shape is not None and shape.num_dims else [])]
+    return torch.empty([0] + cell, dtype=D.torch_dtype(tf_dtype))
+
+
+def _concrete_output_shapes(spec_bytes: bytes, fetch_refs, feed_names, inputs) -> List[tuple]:
+    g = engine.native_graph(spec_bytes)
+    hints = {n: (D.as_dtype(t.dtype).enum, list(t.shape)) for n, t in zip(feed_names, inputs)}
+    infos = _C.analyze_fetches(g, list(fetch_refs), list(feed_names), hints)
+    return [infos[r]["shape"] for r in fetch_refs]
+
+
+# ------------------------------------------------------------------ map_blocks
+def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Optional[Dict[str, str]] = None,
+               graph=None, shape_hints=None) -> DataFrame:
+    """Transforms a DataFrame block by block (one partition = one block).
+
+    Placeholders are bound to the columns of the same name (or through
+    `feed_dict`: placeholder -> column). Output columns, sorted by name, come
+    before the input columns; with ``trim=True`` only the outputs are kept and
+    the number of rows may differ from the input (reference:
+    src/main/python/tensorframes/core.py:213-253; DebugRowOps.scala:305-393).
+    """
+    spec = _resolve(fetches, graph, shape_hints)
+    summary = analyze_graph(spec)
+    inputs = [s for s in summary.values() if s.is_input]
+    outputs = sorted([s for s in summary.values() if s.is_output], key=lambda s: s.name)
+    fields = {f.name: f for f in dframe.schema.fields}
+    cols = ", ".join(dframe.schema.names)
+    feed_dict = dict(feed_dict or {})
+    binding: Dict[str, str] = {}
+    for inp in inputs:
+        cname = feed_dict.get(inp.name, inp.name)
+        _check(cname in fields, f"Graph input {inp.name} found, but no column to match it. "
+                                f"Dataframe columns: {cols}")
+        f = fields[cname]
+        stf = _col_info(f)
+        _check(stf.tf_dtype == inp.tf_dtype,
+               f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data type "
+               f"of the column ({sql_type_for_tf(inp.tf_dtype) if inp.tf_dtype in (1, 2, 3, 9) else D.dtype_name(inp.tf_dtype)})")
+        _check(inp.shape is None or stf.shape.check_more_precise_than(inp.shape),
+               f"The data column '{f.name}' has shape {stf.shape} (not compatible) with shape "
+               f"{_shape_str(inp.shape)} requested by the TF graph")
+        _check(inp.is_placeholder, f"Invalid type for input node {inp.name}. It has to be a placeholder")
+        binding[inp.name] = cname
+    out_fields = []
+    for out in outputs:
+        _check(trim or out.name not in fields,
+               f"TF graph has an output node called '{out.name}', but this column already exists. "
+               f"Input columns: {cols}")
+        st = _sql_type_or_error(out)
+        shape = out.shape if out.shape is not None and out.shape.num_dims > 0 else Shape(UNKNOWN)
+        out_fields.append(ColumnInformation.struct_field(out.name, st.tf_dtype, shape))
+    out_schema = StructType(out_fields + ([] if trim else list(dframe.schema.fields)))
+
+    feed_names = [i.name for i in inputs]
+    feed_cols = [binding[n] for n in feed_names]
+    # fetches in output-column order
+    ref_of = dict(zip(spec.fetch_names, spec.fetch_refs))
+    fetch_refs = [ref_of[o.name] for o in outputs]
+    prog = engine.program(spec.graph_bytes, fetch_refs, feed_names)
+    hints = {n: (summary[n].tf_dtype, list(_col_info(fields[c]).shape.dims)) for n, c in zip(feed_names, feed_cols)}
+    separable = bool(feed_names) and prog.row_separable(hints)
+    out_meta = [(o.name, o.tf_dtype, o.shape) for o in outputs]
+
+    def compute(blocks: Dict[int, Block]) -> Dict[int, Block]:
+        res: Dict[int, Block] = {}
+        host_jobs = []
+        for pid in sorted(blocks):
+            b = blocks[pid]
+            if b.nrows == 0:
+                cols_out = {n: _empty_output(s, dt) for n, dt, s in out_meta}
+                if not trim:
+                    cols_out.update(b.columns)
+                res[pid] = Block(0, cols_out)
+                continue
+            ins = _dense_inputs(b, feed_cols, "map_blocks")
+            on_device = bool(ins) and all(t.is_cuda for t in ins)
+            if on_device or not engine.gpu_available() or not ins:
+                outs = engine.run_program(prog, ins, ins[0].device if on_device else None)
+                if not on_device and any(o.is_cuda for o in outs):
+                    outs = [o.cpu() for o in outs]
+                res[pid] = _assemble(b, outs, out_meta, trim)
+            else:
+                host_jobs.append((pid, b, ins))
+        if host_jobs:
+            _run_host_jobs(host_jobs, res)
+        metrics.add("map_blocks_rows", sum(b.nrows for b in blocks.values()))
+        return res
+
+    def _run_host_jobs(jobs, res):
+        big = [j for j in jobs if separable and j[1].nrows >= config.min_chunked_rows]
+        small = [j for j in jobs if j not in big]
+        if big:
+            specs = []
+            for pid, b, ins in big:
+                shapes = _concrete_output_shapes(spec.graph_bytes, fetch_refs, feed_names, ins)
+                specs.append([(tuple(s), D.torch_dtype(dt)) for s, (_, dt, _) in zip(shapes, out_meta)])
+            outs_all = engine.run_segments_pipelined(prog, [j[2] for j in big], specs)
+            for (pid, b, _), outs in zip(big, outs_all):
+                res[pid] = _assemble(b, outs, out_meta, trim)
+        for pid, b, ins in small:
+            outs = engine.run_block_host(prog, ins, False)
+            res[pid] = _assemble(b, outs, out_meta, trim)
+
+    return DataFrame(out_schema, _Derived(dframe, compute), dframe.num_partitions)
+
+
+def _assemble(b: Block, outs: List[torch.Tensor], out_meta, trim: bool) -> Block:
+    cols = {}
+    nrows = None
+    for (name, dt, _), o in zip(out_meta, outs):
+        if o.dim() == 0:
+            o = o.reshape(1)
+        n = o.shape[0]
+        if nrows is None:
+            nrows = n
+        elif n != nrows:
+            raise TensorFramesError(
+                f"The graph produced outputs with different numbers of rows ({nrows} and {n} for '{name}')")
+        cols[name] = o
+    nrows = b.nrows if nrows is None else nrows
+    if not trim:
+        _check(nrows == b.nrows,
+               f"map_blocks: the graph produced {nrows} rows for a block of {b.nrows} rows; every "
+               f"output must keep the number of rows (use trim=True to change it)")
+        cols.update(b.columns)
+    return Block(nrows, cols)
+
+
+# ------------------------------------------------------------------ map_rows
+def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = None, graph=None,
+             shape_hints=None) -> DataFrame:
+    """Transforms a DataFrame row by row (reference: core.py:175-211; DebugRowOps.scala:396-477).
+
+    Placeholders have the shape of one cell; `feed_dict` maps placeholder ->
+    column (defaults to the placeholder's own name). Cells whose first dim is
+    unknown may vary in length from row to row."""
+    spec = _resolve(fetches, graph, shape_hints)
+    summary = analyze_graph(spec)
+    inputs = [s for s in summary.values() if s.is_input]
+    outputs = sorted([s for s in summary.values() if s.is_output], key=lambda s: s.name)
+    fields = {f.name: f for f in dframe.schema.fields}
+    cols = ", ".join(dframe.schema.names)
+    feed_dict = dict(feed_dict or {})
+    binding = {}
+    for inp in inputs:
+        cname = feed_dict.get(inp.name, inp.name)
+        _check(cname in fields, f"Graph input {inp.name} found, but no column to match it. "
+                                f"Dataframe columns: {cols}")
+        f = fields[cname]
+        stf = _col_info(f)
+        _check(stf.tf_dtype == inp.tf_dtype,
+               f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data type "
+               f"of the column ({D.dtype_name(inp.tf_dtype)})")
+        cell = stf.shape.tail()
+        _check(inp.shape is None or cell.check_more_precise_than(inp.shape),
+               f"The data column '{f.name}' has shape {stf.shape} (not compatible) with shape "
+               f"{_shape_str(inp.shape)} requested by the TF graph")
+        _check(inp.is_placeholder, f"Invalid type for input node {inp.name}. It has to be a placeholder")
+        binding[inp.name] = cname
+    out_fields = []
+    for out in outputs:
+        _check(out.name not in fields, f"TF graph has an output node called '{out.name}', but this "
+                                       f"column already exists. Input columns: {cols}")
+        st = _sql_type_or_error(out)
+        cell = out.shape if out.shape is not None else Shape()
+        out_fields.append(ColumnInformation.struct_field(out.name, st.tf_dtype, cell.prepend(UNKNOWN)))
+    out_schema = StructType(out_fields + list(dframe.schema.fields))
+    feed_names = [i.name for i in inputs]
+    feed_cols = [binding[n] for n in feed_names]
+    ref_of = dict(zip(spec.fetch_names, spec.fetch_refs))
+    fetch_refs = [ref_of[o.name] for o in outputs]
+    prog = engine.program(spec.graph_bytes, fetch_refs, feed_names)
+    out_meta = [(o.name, o.tf_dtype, o.shape) for o in outputs]
+
+    def compute(blocks):
+        res = {}
+        for pid in sorted(blocks):
+            b = blocks[pid]
+            per_out: List[List[torch.Tensor]] = [[] for _ in outputs]
+            cell_views = [_cells(b.columns[c]) for c in feed_cols]
+            dev = _rows_device(cell_views)
+            for i in range(b.nrows):
+                ins = [cv[i] for cv in cell_views]
+                outs = engine.run_program(prog, ins, dev)
+                for j, o in enumerate(outs):
+                    per_out[j].append(o.cpu() if o.is_cuda else o)
+            cols_out = {}
+            for (name, dt, shp), vals in zip(out_meta, per_out):
+                cols_out[name] = _stack_cells(vals, dt, shp)
+            cols_out.update(b.columns)
+            res[pid] = Block(b.nrows, cols_out)
+        metrics.add("map_rows_rows", sum(b.nrows for b in blocks.values()))
+        return res
+
+    return DataFrame(out_schema, _Derived(dframe, compute), dframe.num_partitions)
+
+
+def _cells(col) -> List[torch.Tensor]:
+    if is_dense(col):
+        return list(col.unbind(0)) if col.shape[0] else []
+    if isinstance(col, RaggedColumn):
+        return [torch.from_numpy(np.asarray(c, order="C")) for c in col.cells]
+    raise TensorFramesError("map_rows: only numeric columns can be fed to a graph")
+
+
+def _rows_device(cell_views) -> torch.device:
+    """Small cells run on the host executor (per-row kernel launches would
+    dominate); large cells (images, long vectors) run on the GPU."""
+    if not engine.gpu_available():
+        return torch.device("cpu")
+    if cell_views and cell_views[0] and cell_views[0][0].is_cuda:
+        return cell_views[0][0].device
+    biggest = max((cv[0].numel() for cv in cell_views if cv), default=0)
+    return engine.compute_device() if biggest >= config.map_rows_gpu_min_elems else torch.device("cpu")
+
+
+def _stack_cells(vals: List[torch.Tensor], tf_dtype: int, shape: Optional[Shape]):
+    if not vals:
+        return _empty_output(shape.prepend(UNKNOWN) if shape is not None else None, tf_dtype)
+    shapes = {tuple(v.shape) for v in vals}
+    if len(shapes) == 1:
+        return torch.stack(vals, 0)
+    return RaggedColumn([v.numpy() for v in vals], tf_dtype)
+
+
+# ------------------------------------------------------------------ reductions
+def _unpack(values: Dict[str, np.ndarray], spec: GraphSpec, summary: Dict[str, NodeSummary]):
+    """numpy for rank>0 fetches, python scalars otherwise; a bare value for one
+    fetch (reference: src/main/python/tensorframes/core.py:90-104)."""
+    res = []
+    for name in spec.fetch_names:
+        v = values[name]
+        v = np.asarray(v)
+        res.append(v if v.ndim > 0 else v.item())
+    return res[0] if len(res) == 1 else res
+
+
+_MONOID_PAIR_OPS = {"Add": "Sum", "AddV2": "Sum", "Mul": "Prod", "Minimum": "Min", "Maximum": "Max"}
+
+
+def _pair_monoid(spec: GraphSpec, names: List[str]) -> Optional[Dict[str, str]]:
+    """For reduce_rows: {X: reduction} if every fetch is X = op(X_1, X_2) for a monoid op."""
+    g = P.parse_graphdef(spec.graph_bytes)
+    by = {n.name: n for n in g.node}
+    out = {}
+    for x in names:
+        n = by.get(x)
+        if n is None or n.op not in _MONOID_PAIR_OPS or len(n.input) != 2:
+            return None
+        ins = sorted(i.split(":")[0] for i in n.input)
+        if ins != sorted([f"{x}_1", f"{x}_2"]):
+            return None
+        out[x] = _MONOID_PAIR_OPS[n.op]
+    return out
+
+
+def _reducer_program(op: str, tf_dtype: int, cell_rank: int):
+    """Native program `y = op(x, axis=0)` (used for monoid fast paths)."""
+    g = dsl.Graph()
+    with g.as_default():
+        x = dsl.placeholder(D.DType(tf_dtype), shape=[None] + [None] * cell_rank, name="x")
+        fn = {"Sum": dsl.reduce_sum, "Min": dsl.reduce_min, "Max": dsl.reduce_max, "Prod": dsl.reduce_prod}[op]
+        fn(x, axis=[0], name="y")
+    return engine.program(g.serialize(), ["y"], ["x"])
+
+
+def _monoid_reduce(op: str, t: torch.Tensor, dev: Optional[torch.device] = None) -> torch.Tensor:
+    prog = _reducer_program(op, D.as_dtype(t.dtype).enum, t.dim() - 1)
+    return engine.run_program(prog, [t], dev)[0]
+
+
+def _combine_across(partials: List[torch.Tensor], op: str) -> torch.Tensor:
+    """Monoid combine of per-partition partial cells: locally with the native
+    reduction, then across ranks with one all-reduce (RCCL for device tensors)."""
+    dev = engine.compute_device()
+    if partials:
+        local = _monoid_reduce(op, torch.stack([p.to(dev) for p in partials], 0), dev)
+        has = 1
+    else:
+        local, has = None, 0
+    if dist.is_distributed():
+        counts = dist.all_gather_object((has, None if local is None else (tuple(local.shape), str(local.dtype))))
+        if not any(c[0] for c in counts):
+            raise TensorFramesError("Cannot reduce an empty DataFrame")
+        shape, dt = next(c[1] for c in counts if c[0])
+        if local is None:  # identity element for ranks without data
+            local = _identity(op, shape, getattr(torch, dt.split(".")[-1]), dev)
+        with metrics.timer("allreduce"):
+            local = dist.all_reduce_(local.contiguous(), op)
+    elif local is None:
+        raise TensorFramesError("Cannot reduce an empty DataFrame")
+    return local
+
+
+def _identity(op: str, shape, dtype, dev) -> torch.Tensor:
+    if op == "Sum":
+        return torch.zeros(shape, dtype=dtype, device=dev)
+    if op == "Prod":
+        return torch.ones(shape, dtype=dtype, device=dev)
+    info = torch.finfo(dtype) if dtype.is_floating_point else torch.iinfo(dtype)
+    return torch.full(shape, info.max if op == "Min" else info.min, dtype=dtype, device=dev)
+
+
+def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
+    """Reduces blocks to one value per fetch. For each fetch `x` the graph
+    reads a placeholder `x_input` holding a block of column `x`; the graph is
+    applied to every partition and then to the stack of partial results, so it
+    must be associative (reference: core.py:255-291; DebugRowOps.scala:80-170,503-526).
+    Sum/Min/Max/Prod over axis 0 take the native reduction + RCCL all-reduce path."""
+    spec = _resolve(fetches, graph, shape_hints)
+    summary = analyze_graph(spec)
+    out_names, in_names = _reduce_blocks_schema(dframe.schema, summary)
+    prog = engine.program(spec.graph_bytes, [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names],
+                          in_names)
+    monoid = {m[0]: m[2] for m in prog.monoids()}  # fetch -> op
+    uniform = monoid if set(monoid) == set(out_names) else None
+
+    partials: List[List[torch.Tensor]] = [[] for _ in out_names]
+    cols = [n for n in out_names]
+    for pid, b in sorted(dframe.local_blocks().items()):
+        if b.nrows == 0:
+            continue
+        ins = _dense_inputs(b, cols, "reduce_blocks")
+        on_device = all(t.is_cuda for t in ins)
+        outs = engine.run_program(prog, ins, ins[0].device if on_device else None)
+        for j, o in enumerate(outs):
+            partials[j].append(o)
+
+    if uniform:
+        # partials reduced on device, then one all-reduce per fetch over RCCL
+        results = {name: _combine_across(partials[j], uniform[name]).cpu().numpy()
+                   for j, name in enumerate(out_names)}
+    else:
+        # generic associative graph: gather every partition's partial row and
+        # run the graph once on the stacked [P, ...] block
+        rows = [[partials[k][i].cpu() for k in range(len(out_names))] for i in range(len(partials[0]))]
+        allp = [x for chunk in dist.all_gather_object(rows) for x in chunk]
+        _check(len(allp) > 0, "Cannot reduce an empty DataFrame")
+        stacks = [torch.stack([r[k] for r in allp], 0) for k in range(len(out_names))]
+        outs = engine.run_program(prog, stacks)
+        results = {n: o.cpu().numpy() for n, o in zip(out_names, outs)}
+    metrics.add("reduce_blocks_calls")
+    return _unpack(results, spec, summary)
+
+
+def _reduce_blocks_schema(schema: StructType, summary: Dict[str, NodeSummary]) -> Tuple[List[str], List[str]]:
+    fields = {f.name: f for f in schema.fields}
+    field_list = ", ".join(sorted(fields))
+    outputs = {n: s for n, s in summary.items() if s.is_output}
+    inputs = {n: s for n, s in summary.items() if s.is_input}
+    out_list = ", ".join(sorted(outputs))
+    missing = sorted(set(outputs) - set(fields))
+    _check(not missing, f"Based on the TF graph, some inputs are missing: {', '.join(missing)}. "
+                        f"Dataframe columns: {field_list}; Outputs: {out_list}")
+    expected = {o + "_input" for o in outputs}
+    extra = sorted(set(inputs) - expected)
+    _check(not extra, f"Extra graph inputs have been found: {', '.join(extra)}. Dataframe columns: {field_list}")
+    missing_in = sorted(expected - set(inputs))
+    _check(not missing_in, f"Some inputs are missing in the graph: {', '.join(missing_in)}. "
+                           f"Dataframe columns: {field_list}")
+    order = [f.name for f in schema.fields if f.name in outputs]
+    for name in order:
+        f = fields[name]
+        stf = _col_info(f)
+        out = outputs[name]
+        _check(stf.tf_dtype == out.tf_dtype,
+               f"Output '{name}' has type {D.dtype_name(out.tf_dtype)} but the column type is {stf.dataType}")
+        cell = stf.shape.tail()
+        _check(out.shape is None or out.shape.check_more_precise_than(cell),
+               f"Output '{name}' has shape {_shape_str(out.shape)}, not compatible with the shape of "
+               f"field elements {cell}")
+        in_stf_shape = cell.prepend(UNKNOWN)
+        inp = inputs[name + "_input"]
+        _check(inp.shape is None or in_stf_shape.check_more_precise_than(inp.shape),
+               f"The data column '{name}' has shape {in_stf_shape}, not compatible with shape "
+               f"{_shape_str(inp.shape)} requested by the TF graph")
+        _check(stf.tf_dtype == inp.tf_dtype,
+               f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data type "
+               f"of the column ({D.dtype_name(inp.tf_dtype)})")
+    return order, [n + "_input" for n in order]
+
+
+def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
+    """Pairwise reduction of rows: for each column `x` the graph reads `x_1`,
+    `x_2` (two cells) and produces `x`; every column must be reduced
+    (reference: core.py:138-173; DebugRowOps.scala:172-262,479-501).
+    `x = x_1 (+|*|min|max) x_2` graphs run as one native block reduction per
+    partition + an RCCL all-reduce."""
+    spec = _resolve(fetches, graph, shape_hints)
+    summary = analyze_graph(spec)
+    names = _reduce_rows_schema(dframe.schema, summary)
+    prog = engine.program(spec.graph_bytes, [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in names],
+                          [n + "_1" for n in names] + [n + "_2" for n in names])
+    monoid = _pair_monoid(spec, names)
+    results: Dict[str, np.ndarray] = {}
+    if monoid is not None:
+        partials: Dict[str, List[torch.Tensor]] = {n: [] for n in names}
+        for pid, b in sorted(dframe.local_blocks().items()):
+            if b.nrows == 0:
+                continue
+            for n in names:
+                col = b.columns[n]
+                if is_dense(col):
+                    partials[n].append(_monoid_reduce(monoid[n], col))
+                else:
+                    partials[n].append(_fold_rows(prog, names, [_cells(b.columns[m]) for m in names])[names.index(n)])
+        for n in names:
+            results[n] = _combine_across(partials[n], monoid[n]).cpu().numpy()
+        return _unpack(results, spec, summary)
+    # generic: sequential fold per partition, then fold the partials
+    partials_rows = []
+    for pid, b in sorted(dframe.local_blocks().items()):
+        if b.nrows == 0:
+            continue
+        partials_rows.append([t.cpu() for t in _fold_rows(prog, names, [_cells(b.columns[n]) for n in names])])
+    allp = [x for chunk in dist.all_gather_object(partials_rows) for x in chunk]
+    _check(len(allp) > 0, "Cannot reduce an empty DataFrame")
+    acc = allp[0]
+    for r in allp[1:]:
+        acc = engine.run_program(prog, list(acc) + list(r), torch.device("cpu"))
+    return _unpack({n: a.cpu().numpy() for n, a in zip(names, acc)}, spec, summary)
+
+
+def _fold_rows(prog, names, cells_per_col) -> List[torch.Tensor]:
+    n = len(cells_per_col[0])
+    acc = [cv[0] for cv in cells_per_col]
+    dev = torch.device("cpu")
+    for i in range(1, n):
+        acc = engine.run_program(prog, list(acc) + [cv[i] for cv in cells_per_col], dev)
+    return acc
+
+
+def _reduce_rows_schema(schema: StructType, summary: Dict[str, NodeSummary]) -> List[str]:
+    fields = {f.name: f for f in schema.fields}
+    field_list = ", ".join(sorted(fields))
+    outputs = {n: s for n, s in summary.items() if s.is_output}
+    inputs = {n: s for n, s in summary.items() if s.is_input}
+    out_list = ", ".join(sorted(outputs))
+    extra = sorted(set(outputs) - set(fields))
+    _check(not extra, f"Some extra outputs were found in the reducer: {', '.join(extra)}. "
+                      f"Dataframe columns: {field_list}; Outputs: {out_list}")
+    missing = sorted(set(fields) - set(outputs))
+    _check(not missing, f"Some outputs are missing in the reducer: {', '.join(missing)}. "
+                        f"Dataframe columns: {field_list}; Outputs: {out_list}")
+    expected = {f + s for f in fields for s in ("_1", "_2")}
+    extra_in = sorted(set(inputs) - expected)
+    _check(not extra_in, f"Extra graph inputs have been found: {', '.join(extra_in)}. "
+                         f"Dataframe columns: {field_list}")
+    missing_in = sorted(expected - set(inputs))
+    _check(not missing_in, f"Some inputs are missing in th graph: {', '.join(missing_in)}. "
+                           f"Dataframe columns: {field_list}")
+    for name, f in fields.items():
+        stf = _col_info(f)
+        out = outputs[name]
+        _check(stf.tf_dtype == out.tf_dtype,
+               f"Output '{name}' has type {D.dtype_name(out.tf_dtype)} but the column type is {stf.dataType}")
+        cell = stf.shape.tail()
+        _check(out.shape is None or out.shape.check_more_precise_than(cell),
+               f"Output '{name}' has shape {_shape_str(out.shape)}, not compatible with the shapes"
+               f"of field elements {cell}")
+        for suffix in ("_1", "_2"):
+            inp = inputs[name + suffix]
+            _check(inp.shape is None or cell.check_more_precise_than(inp.shape),
+                   f"The data column '{name}' has shape {stf.shape} (not compatible) with shape "
+                   f"{_shape_str(inp.shape)} requested by the TF graph")
+            _check(stf.tf_dtype == inp.tf_dtype,
+                   f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data "
+                   f"type of the column ({D.dtype_name(inp.tf_dtype)})")
+    return [f.name for f in schema.fields]
+
+
+# ------------------------------------------------------------------ aggregate
+def _stable_hash(key: tuple) -> int:
+    return zlib.crc32(repr(key).encode())
+
+
+def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) -> DataFrame:
+    """Algebraic aggregation over `df.groupBy(keys)`: the reduce_blocks graph
+    contract applied per key. Output = key columns ++ fetched columns, one row
+    per key (reference: core.py:319-336; DebugRowOps.scala:547-695).
+
+    Rows are hash-partitioned by key across ranks (all-to-all), sorted by key
+    on each rank, and Sum/Min/Max/Prod graphs run as one native segmented
+    reduction over all keys; other graphs run once per key."""
+    df = grouped_data.df
+    keys = grouped_data.keys
+    spec = _resolve(fetches, graph, shape_hints)
+    summary = analyze_graph(spec)
+    out_names, in_names = _reduce_blocks_schema(df.schema, summary)
+    prog = engine.program(spec.graph_bytes, [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names],
+                          in_names)
+    monoid = {m[0]: m[2] for m in prog.monoids()}
+    uniform = set(monoid) == set(out_names)
+    all_cols = keys + out_names
+
+    def compute(blocks):
+        # 1. shuffle (key -> owner rank)
+        w = dist.world_size()
+        send = [[] for _ in range(w)]
+        for pid, b in sorted(blocks.items()):
+            if b.nrows == 0:
+                continue
+            kv = [column_values(b.columns[k]) for k in keys]
+            ktuples = list(zip(*kv))
+            dest = np.array([_stable_hash(t) % w for t in ktuples], dtype=np.int64) if w > 1 else np.zeros(len(ktuples), np.int64)
+            host = b.select(all_cols).to(torch.device("cpu"))
+            for r in range(w):
+                idx = np.nonzero(dest == r)[0]
+                if len(idx):
+                    send[r].append(host.take(idx.tolist()))
+        recv = dist.all_to_all_objects(send)
+        mine = [blk for lst in recv for blk in lst]
+        if not mine:
+            return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, w))}
+        full = concat_blocks(mine, all_cols)
+        # 2. group ids, rows sorted by key
+        kv = [column_values(full.columns[k]) for k in keys]
+        ktuples = list(zip(*kv))
+        uniq = sorted(set(ktuples), key=_sort_key)
+        gid = {k: i for i, k in enumerate(uniq)}
+        codes = np.array([gid[k] for k in ktuples], dtype=np.int64)
+        order = np.argsort(codes, kind="stable")
+        counts = np.bincount(codes, minlength=len(uniq))
+        offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        sorted_blk = full.take(order.tolist())
+        out_cols: Dict[str, Any] = {}
+        for i, k in enumerate(keys):
+            out_cols[k] = build_column([u[i] for u in uniq], _tf_of_field(df.schema[k]))
+        if uniform and all(is_dense(sorted_blk.columns[n]) for n in out_names):
+            for n in out_names:
+                out_cols[n] = _segment_reduce(monoid[n], sorted_blk.columns[n], offsets)
+        else:
+            per = {n: [] for n in out_names}
+            for g in range(len(uniq)):
+                seg = sorted_blk.slice(int(offsets[g]), int(offsets[g + 1]))
+                ins = _dense_inputs(seg, out_names, "aggregate")
+                outs = engine.run_program(prog, ins)
+                for n, o in zip(out_names, outs):
+                    per[n].append(o.cpu())
+            for n in out_names:
+                out_cols[n] = torch.stack(per[n], 0)
+        return {dist.rank(): Block(len(uniq), out_cols)}
+
+    out_fields = [df.schema[k] for k in keys]
+    for n in out_names:
+        o = summary[n]
+        shape = (o.shape if o.shape is not None else Shape()).prepend(UNKNOWN)
+        out_fields.append(ColumnInformation.struct_field(n, o.tf_dtype, shape))
+    return DataFrame(StructType(out_fields), _Derived(df, compute), max(1, dist.world_size()))
+
+
+def _tf_of_field(f: StructField) -> Optional[int]:
+    from .frame.types import scalar_type_of
+    s = scalar_type_of(f.dataType)
+    return s.tf_dtype if isinstance(s, NumericType) else None
+
+
+def _empty_agg_cols(df, keys, out_names):
+    cols = {k: ObjectColumn([]) for k in keys}
+    for n in out_names:
+        stf = _col_info(df.schema[n])
+        cols[n] = _empty_output(stf.shape, stf.tf_dtype)
+    return cols
+
+
+def _segment_reduce(op: str, col: torch.Tensor, offsets: np.ndarray) -> torch.Tensor:
+    dev = engine.compute_device()
+    x = col.to(dev) if col.device != dev else col
+    off = torch.from_numpy(offsets).to(dev)
+    y = _C.segment_reduce(op, x.contiguous(), off)
+    return y.cpu() if not col.is_cuda else y
+
+
+# ------------------------------------------------------------------ analyze / schema
+def analyze(dframe: DataFrame) -> DataFrame:
+    """Scans the data and records every numeric column's block shape in the
+    schema metadata: the lead dim is the partition size when all non-empty
+    partitions agree (else unknown), cell dims that vary become unknown
+    (reference: src/main/scala/org/tensorframes/ExperimentalOperations.scala:35-157)."""
+    local = {}
+    for pid, b in dframe.local_blocks().items():
+        if b.nrows == 0:
+            continue
+        shapes = {}
+        for f in dframe.schema.fields:
+            col = b.columns[f.name]
+            if is_dense(col):
+                shapes[f.name] = list(col.shape)
+            elif isinstance(col, RaggedColumn):
+                cell = None
+                for c in col.cells:
+                    s = Shape(tuple(c.shape))
+                    cell = s if cell is None else (cell.merge(s) or Shape(tuple([UNKNOWN] * max(cell.num_dims, s.num_dims))))
+                shapes[f.name] = [b.nrows] + list(cell.dims)
+        local[pid] = shapes
+    merged: Dict[str, Optional[Shape]] = {}
+    for chunk in dist.all_gather_object(local):
+        for pid, shapes in chunk.items():
+            for name, dims in shapes.items():
+                s = Shape(dims)
+                if name not in merged:
+                    merged[name] = s
+                elif merged[name] is not None:
+                    merged[name] = merged[name].merge(s)
+    fields = []
+    for f in dframe.schema.fields:
+        ci = ColumnInformation(f)
+        if f.name in merged and merged[f.name] is not None and ci.stf is not None:
+            fields.append(ColumnInformation.with_info(f, SparkTFColInfo(merged[f.name], ci.stf.dataType)).merged())
+        else:
+            fields.append(f)
+    return dframe.with_schema(StructType(fields))
+
+
+def print_schema(dframe: DataFrame):
+    """Prints the schema with the tensor metadata (reference: DebugRowOps.scala:528-545)."""
+    print(explain_schema(dframe.schema), end="")
+
+
+def explain(dframe: DataFrame) -> str:
+    return explain_schema(dframe.schema)
+
+
+def block(df: DataFrame, col_name: str, tf_name: Optional[str] = None):
+    """Placeholder for blocks of column `col_name` (lead dim always unknown)
+    (reference: src/main/python/tensorframes/core.py:338-351,368-391)."""
+    return _auto_placeholder(df, col_name, tf_name, is_block=True)
+
+
+def row(df: DataFrame, col_name: str, tf_name: Optional[str] = None):
+    """Placeholder for one cell of column `col_name` (reference: core.py:353-366)."""
+    return _auto_placeholder(df, col_name, tf_name, is_block=False)
+
+
+def _auto_placeholder(df: DataFrame, col_name: str, tf_name: Optional[str], is_block: bool):
+    if col_name not in df.schema:
+        raise TensorFramesError(f"Could not find column with name {col_name}; available columns: "
+                                f"{', '.join(df.columns)}")
+    f = df.schema[col_name]
+    stf = ColumnInformation(f).stf
+    if stf is None:
+        raise TensorFramesError(f"The datatype of column '{col_name}' could not be understood by "
+                                f"tensorframes: {f.dataType}")
+    shape = [None if d == UNKNOWN else d for d in stf.shape.dims]
+    if is_block:
+        shape[0] = None
+    else:
+        shape = shape[1:]
+    return dsl.placeholder(D.DType(stf.tf_dtype), shape=shape, name=tf_name or col_name)

@@ -1,0 +1,175 @@
+"""Execution engine: compiled programs, device placement, host<->device staging.
+
+One `Program` (native: csrc/runtime/executor.*) per (graph, fetches, feeds)
+is cached and shared by every partition and every call, so a graph is parsed,
+shape-inferred and planned once and its constants are uploaded to HBM once —
+the reference instead imports the GraphDef into a fresh TF session per
+partition (reference: src/main/scala/org/tensorframes/impl/DebugRowOps.scala:766-803,
+src/main/scala/org/tensorframes/impl/TensorFlowOps.scala:76-95).
+
+Block execution on a GPU:
+  * device-resident blocks run in place;
+  * large host blocks of a row-separable graph stream through a pipelined
+    chunk loop (pinned host -> HBM on a copy stream, kernels on the compute
+    stream, HBM -> pinned host on a second copy stream);
+  * anything else: one H2D, run, one D2H.
+"""
+from __future__ import annotations
+
+import hashlib
+import threading
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ._native import _C
+from .config import config
+from .parallel import dist
+from .utils import dtypes as D
+from .utils.logging import logger, metrics
+
+_graph_cache: "OrderedDict[str, object]" = OrderedDict()
+_prog_cache: "OrderedDict[tuple, object]" = OrderedDict()
+_lock = threading.Lock()
+_MAX_CACHE = 64
+
+
+def _key(graph_bytes: bytes) -> str:
+    return hashlib.sha1(graph_bytes).hexdigest()
+
+
+def native_graph(graph_bytes: bytes):
+    k = _key(graph_bytes)
+    with _lock:
+        g = _graph_cache.get(k)
+        if g is None:
+            g = _C.Graph(graph_bytes)
+            _graph_cache[k] = g
+            while len(_graph_cache) > _MAX_CACHE:
+                _graph_cache.popitem(last=False)
+        return g
+
+
+def program(graph_bytes: bytes, fetches: Sequence[str], feeds: Sequence[str]):
+    k = (_key(graph_bytes), tuple(fetches), tuple(feeds))
+    with _lock:
+        p = _prog_cache.get(k)
+        if p is not None:
+            _prog_cache.move_to_end(k)
+            return p
+    g = native_graph(graph_bytes)
+    p = _C.Program(g, list(fetches), list(feeds))
+    with _lock:
+        _prog_cache[k] = p
+        while len(_prog_cache) > _MAX_CACHE:
+            _prog_cache.popitem(last=False)
+    return p
+
+
+# ------------------------------------------------------------------ devices
+def gpu_available() -> bool:
+    return config.device != "cpu" and torch.cuda.is_available()
+
+
+def compute_device() -> torch.device:
+    if gpu_available():
+        n = torch.cuda.device_count()
+        return torch.device("cuda", dist.local_rank() % max(n, 1))
+    if config.device == "cuda":
+        raise RuntimeError("TFA_DEVICE=cuda but no GPU is visible")
+    return torch.device("cpu")
+
+
+def to_device(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    if t.device == dev:
+        return t
+    return t.to(dev, non_blocking=t.is_pinned())
+
+
+def empty_host(shape, dtype: torch.dtype, pinned: bool) -> torch.Tensor:
+    nbytes = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+    if pinned and gpu_available() and nbytes >= config.pinned_min_bytes:
+        return _C.empty_pinned(list(shape), dtype)
+    return torch.empty(tuple(shape), dtype=dtype)
+
+
+def pin(t: torch.Tensor) -> torch.Tensor:
+    """Page-lock a host tensor for DMA (copy into pinned memory)."""
+    if not gpu_available() or t.is_cuda or t.is_pinned():
+        return t
+    out = _C.empty_pinned(list(t.shape), t.dtype)
+    out.copy_(t)
+    return out
+
+
+# ------------------------------------------------------------------ execution
+def run_program(prog, inputs: List[torch.Tensor], dev: Optional[torch.device] = None) -> List[torch.Tensor]:
+    """Run on one device; inputs are moved there if needed. Outputs stay on `dev`."""
+    dev = dev or compute_device()
+    ins = [to_device(t.contiguous(), dev) for t in inputs]
+    if dev.type == "cuda":
+        with torch.cuda.device(dev):
+            return list(prog.run(ins))
+    return list(prog.run(ins))
+
+
+def run_block_host(prog, inputs: List[torch.Tensor], separable: bool,
+                   out_specs: Optional[List[Tuple[tuple, torch.dtype]]] = None) -> List[torch.Tensor]:
+    """Host-resident block -> host-resident outputs, on the compute device."""
+    dev = compute_device()
+    rows = inputs[0].shape[0] if inputs else 0
+    if dev.type != "cuda":
+        return [o.contiguous() for o in prog.run([t.contiguous() for t in inputs])]
+    if separable and out_specs is not None and rows >= config.min_chunked_rows:
+        return run_segments_pipelined(prog, [inputs], [out_specs])[0]
+    outs = run_program(prog, inputs, dev)
+    res = []
+    for o in outs:
+        h = empty_host(tuple(o.shape), o.dtype, config.pinned_outputs)
+        h.copy_(o, non_blocking=h.is_pinned())
+        res.append(h)
+    torch.cuda.current_stream(dev).synchronize()
+    metrics.add("d2h_bytes", sum(o.numel() * o.element_size() for o in outs))
+    return res
+
+
+def chunk_rows_for(inputs: List[torch.Tensor]) -> int:
+    row_bytes = max((t[0].numel() * t.element_size() if t.shape[0] else 1) for t in inputs) if inputs else 1
+    return max(1024, int(config.chunk_bytes // max(row_bytes, 1)))
+
+
+def run_segments_pipelined(prog, segments: List[List[torch.Tensor]],
+                           out_specs: List[List[Tuple[tuple, torch.dtype]]]) -> List[List[torch.Tensor]]:
+    """Pipelined H2D/compute/D2H over row chunks of several host segments.
+
+    out_specs[s][j] = (full output shape, dtype) of fetch j for segment s.
+    """
+    dev = compute_device()
+    segs = [[pin(t.contiguous()) for t in seg] for seg in segments]
+    outs = [[empty_host(shape, dt, True) for (shape, dt) in spec] for spec in out_specs]
+    chunk = chunk_rows_for(segs[0]) if segs and segs[0] else 1 << 16
+    with metrics.timer("pipelined"):
+        prog.run_chunked(segs, outs, chunk, dev.index or 0, config.pipeline_depth)
+    st = prog.stats()
+    metrics.add("chunks", st["chunks"])
+    return outs
+
+
+def run_graph(graph_bytes: bytes, fetch_names: Sequence[str], feeds: Dict[str, object],
+              device=None) -> List[np.ndarray]:
+    """Evaluate fetches of a serialized graph on numpy/torch feeds (tf.Session.run)."""
+    names = [str(n) for n in feeds]
+    prog = program(graph_bytes, list(fetch_names), names)
+    ins = []
+    for n in names:
+        v = feeds[n]
+        ins.append(v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v, order="C")))
+    dev = torch.device(device) if device is not None else compute_device()
+    outs = run_program(prog, ins, dev)
+    res = []
+    for o in outs:
+        a = o.cpu().numpy()
+        res.append(a[()] if a.ndim == 0 else a)
+    return res

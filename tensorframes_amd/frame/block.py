@@ -1,0 +1,208 @@
+"""Columnar partition storage.
+
+A `Block` is one partition: a row count plus one column store per field.
+Numeric columns whose cells share one shape are stored densely as a single
+tensor ``[rows, *cell]`` (host memory, optionally page-locked for DMA, or
+device memory when the frame is cached on the GPU). This replaces the
+reference's boxed ``Row`` <-> ``java.nio`` buffer loops
+(reference: src/main/scala/org/tensorframes/impl/DataOps.scala:20-81,
+src/main/scala/org/tensorframes/impl/TFDataOps.scala:27-204): the tensor IS the block.
+Ragged numeric columns keep one array per cell; other columns (strings,
+binary, ...) are Python lists.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..utils import dtypes as D
+from ..utils.shape import UNKNOWN, Shape
+
+
+class RaggedColumn:
+    """Numeric column whose cells have different shapes (one array per row)."""
+
+    __slots__ = ("cells", "tf_dtype")
+
+    def __init__(self, cells: List[np.ndarray], tf_dtype: int):
+        self.cells = cells
+        self.tf_dtype = tf_dtype
+
+    def __len__(self):
+        return len(self.cells)
+
+    def take(self, idx) -> "RaggedColumn":
+        return RaggedColumn([self.cells[i] for i in idx], self.tf_dtype)
+
+    def slice(self, a, b) -> "RaggedColumn":
+        return RaggedColumn(self.cells[a:b], self.tf_dtype)
+
+
+class ObjectColumn:
+    """Non-tensor column (strings, bytes, arbitrary Python values)."""
+
+    __slots__ = ("values",)
+
+    def __init__(self, values: List[Any]):
+        self.values = list(values)
+
+    def __len__(self):
+        return len(self.values)
+
+    def take(self, idx) -> "ObjectColumn":
+        return ObjectColumn([self.values[i] for i in idx])
+
+    def slice(self, a, b) -> "ObjectColumn":
+        return ObjectColumn(self.values[a:b])
+
+
+Column = Any  # torch.Tensor | RaggedColumn | ObjectColumn
+
+
+@dataclass
+class Block:
+    nrows: int
+    columns: Dict[str, Column] = field(default_factory=dict)
+
+    def column(self, name: str) -> Column:
+        return self.columns[name]
+
+    def select(self, names: Sequence[str]) -> "Block":
+        return Block(self.nrows, {n: self.columns[n] for n in names})
+
+    def slice(self, a: int, b: int) -> "Block":
+        return Block(b - a, {n: col_slice(c, a, b) for n, c in self.columns.items()})
+
+    def take(self, idx) -> "Block":
+        return Block(len(idx), {n: col_take(c, idx) for n, c in self.columns.items()})
+
+    def to(self, device) -> "Block":
+        return Block(self.nrows, {n: (c.to(device) if isinstance(c, torch.Tensor) else c)
+                                  for n, c in self.columns.items()})
+
+
+def is_dense(col: Column) -> bool:
+    return isinstance(col, torch.Tensor)
+
+
+def col_slice(col: Column, a: int, b: int) -> Column:
+    if isinstance(col, torch.Tensor):
+        return col[a:b]
+    return col.slice(a, b)
+
+
+def col_take(col: Column, idx) -> Column:
+    if isinstance(col, torch.Tensor):
+        t = torch.as_tensor(np.asarray(idx, dtype=np.int64), device=col.device)
+        return col.index_select(0, t)
+    return col.take(list(idx))
+
+
+def col_len(col: Column) -> int:
+    return col.shape[0] if isinstance(col, torch.Tensor) else len(col)
+
+
+def concat_columns(cols: List[Column]) -> Column:
+    if all(isinstance(c, torch.Tensor) for c in cols):
+        shapes = {tuple(c.shape[1:]) for c in cols}
+        if len(shapes) == 1:
+            return torch.cat([c.cpu() for c in cols], 0) if len(cols) > 1 else cols[0]
+        cells = [np.asarray(x) for c in cols for x in c.cpu().numpy()]
+        return RaggedColumn(cells, D.as_dtype(cols[0].dtype).enum)
+    if all(isinstance(c, (torch.Tensor, RaggedColumn)) for c in cols):
+        cells, dt = [], None
+        for c in cols:
+            if isinstance(c, torch.Tensor):
+                dt = D.as_dtype(c.dtype).enum
+                cells.extend(np.asarray(x) for x in c.cpu().numpy())
+            else:
+                dt = c.tf_dtype
+                cells.extend(c.cells)
+        return RaggedColumn(cells, dt)
+    vals = []
+    for c in cols:
+        vals.extend(column_values(c))
+    return ObjectColumn(vals)
+
+
+def concat_blocks(blocks: List[Block], names: Sequence[str]) -> Block:
+    if not blocks:
+        return Block(0, {})
+    n = sum(b.nrows for b in blocks)
+    return Block(n, {nm: concat_columns([b.columns[nm] for b in blocks]) for nm in names})
+
+
+# ------------------------------------------------------------------ conversion
+
+def _cell_shape(v) -> Optional[tuple]:
+    """Shape of a nested-list / ndarray cell, None if ragged inside."""
+    if isinstance(v, np.ndarray):
+        return tuple(v.shape)
+    if isinstance(v, (list, tuple)):
+        if len(v) == 0:
+            return (0,)
+        subs = [_cell_shape(x) for x in v]
+        if any(s is None for s in subs) or len(set(subs)) != 1:
+            return None
+        return (len(v),) + subs[0]
+    return ()
+
+
+def build_column(values: List[Any], tf_dtype: Optional[int]) -> Column:
+    """Values of one column of one partition -> column store."""
+    if tf_dtype is None or tf_dtype == D.DT_STRING:
+        return ObjectColumn(values)
+    npdt = D.numpy_dtype(tf_dtype)
+    if len(values) == 0:
+        return torch.empty((0,), dtype=D.torch_dtype(tf_dtype))
+    shapes = {_cell_shape(v) for v in values}
+    if None not in shapes and len(shapes) == 1:
+        arr = np.asarray(values, dtype=npdt)
+        return torch.from_numpy(np.asarray(arr, order="C"))
+    return RaggedColumn([np.asarray(v, dtype=npdt) for v in values], tf_dtype)
+
+
+def column_values(col: Column) -> List[Any]:
+    """Column -> Python values (Spark-like: scalars, nested lists, str, bytes)."""
+    if isinstance(col, torch.Tensor):
+        t = col.detach()
+        if t.device.type != "cpu":
+            t = t.cpu()
+        return t.numpy().tolist()
+    if isinstance(col, RaggedColumn):
+        return [c.tolist() for c in col.cells]
+    return list(col.values)
+
+
+def column_cell(col: Column, i: int):
+    if isinstance(col, torch.Tensor):
+        v = col[i]
+        return v.item() if v.dim() == 0 else v.cpu().numpy().tolist()
+    if isinstance(col, RaggedColumn):
+        return col.cells[i].tolist()
+    return col.values[i]
+
+
+def column_cell_shape(col: Column, i: int) -> Optional[Shape]:
+    if isinstance(col, torch.Tensor):
+        return Shape(tuple(col.shape[1:]))
+    if isinstance(col, RaggedColumn):
+        return Shape(tuple(col.cells[i].shape))
+    return None
+
+
+def column_tf_dtype(col: Column) -> Optional[int]:
+    if isinstance(col, torch.Tensor):
+        return D.as_dtype(col.dtype).enum
+    if isinstance(col, RaggedColumn):
+        return col.tf_dtype
+    return None
+
+
+def dense_block_shape(col: Column) -> Optional[Shape]:
+    if isinstance(col, torch.Tensor):
+        return Shape(tuple(col.shape))
+    return None

@@ -1,0 +1,498 @@
+"""A partitioned, lazily evaluated columnar DataFrame (the Spark substrate).
+
+TensorFrames runs on Spark DataFrames (reference: README.md:3-9); Spark is not
+available here, so this module provides the subset of DataFrame behaviour the
+TensorFrames operators rely on (reference: SURVEY.md §2.4):
+
+* a schema of `StructField`s whose metadata carries tensor shape/type info;
+* an ordered list of partitions; operators are lazy and run when an action
+  (`collect`, `count`, `first`, ...) forces them;
+* `groupBy(...)` for keyed aggregation, `repartition`, `cache`/`persist`;
+* SPMD distribution: under torch.distributed every rank holds the partitions
+  ``p % world_size == rank``; actions gather results to every rank.
+
+Dense numeric columns are stored as one tensor per partition (see block.py),
+which can live in page-locked host memory (DMA source/target) or, after
+`cache_on_device()`, in HBM.
+"""
+from __future__ import annotations
+
+import math
+import numbers
+from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from ..parallel import dist
+from ..utils import dtypes as D
+from .block import (Block, ObjectColumn, RaggedColumn, build_column, column_values, concat_blocks,
+                    is_dense)
+from .column_info import ColumnInformation, DataFrameInfo, explain_schema
+from .types import (ArrayType, BinaryType, BooleanType, DataType, DoubleType, FloatType, IntegerType,
+                    LongType, NumericType, Row, StringType, StructField, StructType, scalar_type_of)
+
+
+# ------------------------------------------------------------------ sources
+class _Source:
+    def compute(self) -> Dict[int, Block]:
+        raise NotImplementedError
+
+
+class _Materialized(_Source):
+    def __init__(self, blocks: Dict[int, Block]):
+        self._blocks = blocks
+
+    def compute(self):
+        return self._blocks
+
+
+class _Generated(_Source):
+    def __init__(self, num_partitions: int, fn: Callable[[int], Block]):
+        self._n = num_partitions
+        self._fn = fn
+
+    def compute(self):
+        return {p: self._fn(p) for p in dist.local_partitions(self._n)}
+
+
+class _Derived(_Source):
+    def __init__(self, parent: "DataFrame", fn: Callable[[Dict[int, Block]], Dict[int, Block]]):
+        self._parent = parent
+        self._fn = fn
+
+    def compute(self):
+        return self._fn(self._parent._blocks())
+
+
+# ------------------------------------------------------------------ DataFrame
+class DataFrame:
+    def __init__(self, schema: StructType, source: _Source, num_partitions: int):
+        self._schema = schema
+        self._source = source
+        self._nparts = num_partitions
+        self._persist = False
+        self._cached: Optional[Dict[int, Block]] = None
+
+    # -- metadata
+    @property
+    def schema(self) -> StructType:
+        return self._schema
+
+    @property
+    def columns(self) -> List[str]:
+        return self._schema.names
+
+    @property
+    def dtypes(self):
+        return [(f.name, f.dataType.simpleString()) for f in self._schema.fields]
+
+    @property
+    def num_partitions(self) -> int:
+        return self._nparts
+
+    def getNumPartitions(self) -> int:  # noqa: N802
+        return self._nparts
+
+    @property
+    def rdd(self):
+        return self  # `df.rdd.getNumPartitions()` compatibility
+
+    def __repr__(self):
+        return "DataFrame[" + ", ".join(f"{n}: {t}" for n, t in self.dtypes) + "]"
+
+    def printSchema(self):  # noqa: N802
+        print(explain_schema(self._schema), end="")
+
+    def explain_tensors(self) -> str:
+        """`DataFrame[double[?,2], ...]` (reference: src/main/scala/org/tensorframes/DataFrameInfo.scala:10-17)."""
+        return DataFrameInfo.get(self._schema).explain()
+
+    explainTensors = explain_tensors  # noqa: N815
+
+    # -- evaluation
+    def _blocks(self) -> Dict[int, Block]:
+        if self._cached is not None:
+            return self._cached
+        b = self._source.compute()
+        if self._persist:
+            self._cached = b
+        return b
+
+    def cache(self) -> "DataFrame":
+        self._persist = True
+        return self
+
+    def persist(self, *_args) -> "DataFrame":
+        return self.cache()
+
+    def unpersist(self) -> "DataFrame":
+        self._persist = False
+        self._cached = None
+        return self
+
+    def cache_on_device(self, device=None) -> "DataFrame":
+        """Device-resident copy: dense columns moved to HBM once, reused by every
+        following operator (iterative workloads do not re-cross PCIe)."""
+        from ..engine import compute_device
+        dev = torch.device(device) if device is not None else compute_device()
+        blocks = {p: b.to(dev) for p, b in self._blocks().items()}
+        df = DataFrame(self._schema, _Materialized(blocks), self._nparts)
+        df._persist = True
+        df._cached = blocks
+        return df
+
+    def to_host(self) -> "DataFrame":
+        blocks = {p: b.to(torch.device("cpu")) for p, b in self._blocks().items()}
+        return DataFrame(self._schema, _Materialized(blocks), self._nparts)
+
+    def local_blocks(self) -> Dict[int, Block]:
+        return self._blocks()
+
+    # -- actions
+    def _local_rows(self) -> List[tuple]:
+        out = []
+        names = self._schema.names
+        for pid in sorted(self._blocks()):
+            b = self._blocks()[pid]
+            cols = [column_values(b.columns[n]) for n in names]
+            out.append((pid, [Row.from_fields(names, vals) for vals in zip(*cols)] if cols else
+                        [Row.from_fields([], []) for _ in range(b.nrows)]))
+        return out
+
+    def collect(self) -> List[Row]:
+        parts = []
+        for chunk in dist.all_gather_object(self._local_rows()):
+            parts.extend(chunk)
+        parts.sort(key=lambda x: x[0])
+        return [r for _, rows in parts for r in rows]
+
+    def count(self) -> int:
+        n = sum(b.nrows for b in self._blocks().values())
+        return sum(dist.all_gather_object(n))
+
+    def first(self) -> Optional[Row]:
+        rows = self.take(1)
+        return rows[0] if rows else None
+
+    head = first
+
+    def take(self, n: int) -> List[Row]:
+        return self.collect()[:n]
+
+    def show(self, n: int = 20):
+        rows = self.take(n)
+        print(" | ".join(self.columns))
+        for r in rows:
+            print(" | ".join(str(v) for v in r))
+
+    def toPandas(self):  # noqa: N802
+        import pandas as pd
+        rows = self.collect()
+        return pd.DataFrame([list(r) for r in rows], columns=self.columns)
+
+    def to_numpy(self, column: str) -> np.ndarray:
+        """All rows of a dense column as one array (gathered on every rank)."""
+        local = []
+        for pid in sorted(self._blocks()):
+            c = self._blocks()[pid].columns[column]
+            local.append((pid, c.detach().cpu().numpy() if is_dense(c) else np.asarray(column_values(c), dtype=object)))
+        parts = [x for chunk in dist.all_gather_object(local) for x in chunk]
+        parts.sort(key=lambda x: x[0])
+        arrs = [a for _, a in parts if len(a)]
+        return np.concatenate(arrs, 0) if arrs else np.zeros((0,))
+
+    # -- transformations
+    def select(self, *cols) -> "DataFrame":
+        names = [c for cs in cols for c in (cs if isinstance(cs, (list, tuple)) else [cs])]
+        for n in names:
+            if n not in self._schema:
+                raise ValueError(f"Column {n} not found in {self.columns}")
+        schema = StructType([self._schema[n] for n in names])
+        return DataFrame(schema, _Derived(self, lambda bs: {p: b.select(names) for p, b in bs.items()}),
+                         self._nparts)
+
+    def drop(self, *names) -> "DataFrame":
+        return self.select([n for n in self.columns if n not in names])
+
+    def withColumnRenamed(self, existing: str, new: str) -> "DataFrame":  # noqa: N802
+        fields = [f.copy(name=new) if f.name == existing else f for f in self._schema.fields]
+
+        def fn(bs):
+            return {p: Block(b.nrows, {(new if k == existing else k): v for k, v in b.columns.items()})
+                    for p, b in bs.items()}
+        return DataFrame(StructType(fields), _Derived(self, fn), self._nparts)
+
+    def with_schema(self, schema: StructType) -> "DataFrame":
+        """Same data, new schema (used by `analyze` to attach metadata)."""
+        df = DataFrame(schema, _Derived(self, lambda bs: bs), self._nparts)
+        return df
+
+    def repartition(self, n: int) -> "DataFrame":
+        names = self.columns
+
+        def fn(bs):
+            allb = []
+            for chunk in dist.all_gather_object([(p, b.to(torch.device("cpu"))) for p, b in sorted(bs.items())]):
+                allb.extend(chunk)
+            allb.sort(key=lambda x: x[0])
+            full = concat_blocks([b for _, b in allb], names)
+            return {p: full.slice(*_bounds(full.nrows, n, p)) for p in dist.local_partitions(n)}
+        return DataFrame(self._schema, _Derived(self, fn), n)
+
+    def coalesce(self, n: int) -> "DataFrame":
+        return self.repartition(min(n, self._nparts))
+
+    def groupBy(self, *cols) -> "GroupedData":  # noqa: N802
+        names = [c for cs in cols for c in (cs if isinstance(cs, (list, tuple)) else [cs])]
+        for n in names:
+            if n not in self._schema:
+                raise ValueError(f"groupBy: column {n} not found in {self.columns}")
+        return GroupedData(self, names)
+
+    groupby = groupBy
+
+    # -- TensorFrames method forms (reference: src/main/scala/org/tensorframes/dsl/Implicits.scala:25-116)
+    def map_blocks(self, fetches, trim: bool = False, **kw) -> "DataFrame":
+        from .. import core
+        return core.map_blocks(fetches, self, trim=trim, **kw)
+
+    mapBlocks = map_blocks  # noqa: N815
+
+    def map_blocks_trimmed(self, fetches, **kw) -> "DataFrame":
+        from .. import core
+        return core.map_blocks(fetches, self, trim=True, **kw)
+
+    mapBlocksTrimmed = map_blocks_trimmed  # noqa: N815
+
+    def map_rows(self, fetches, feed_dict=None, **kw) -> "DataFrame":
+        from .. import core
+        return core.map_rows(fetches, self, feed_dict=feed_dict, **kw)
+
+    mapRows = map_rows  # noqa: N815
+
+    def reduce_blocks(self, fetches, **kw):
+        from .. import core
+        return core.reduce_blocks(fetches, self, **kw)
+
+    reduceBlocks = reduce_blocks  # noqa: N815
+
+    def reduce_rows(self, fetches, **kw):
+        from .. import core
+        return core.reduce_rows(fetches, self, **kw)
+
+    reduceRows = reduce_rows  # noqa: N815
+
+    def analyze(self) -> "DataFrame":
+        from .. import core
+        return core.analyze(self)
+
+    def block(self, col_name: str, tf_name: Optional[str] = None):
+        from .. import core
+        return core.block(self, col_name, tf_name)
+
+    def row(self, col_name: str, tf_name: Optional[str] = None):
+        from .. import core
+        return core.row(self, col_name, tf_name)
+
+
+class GroupedData:
+    def __init__(self, df: DataFrame, keys: List[str]):
+        self.df = df
+        self.keys = keys
+
+    def aggregate(self, fetches, **kw) -> DataFrame:
+        from .. import core
+        return core.aggregate(fetches, self, **kw)
+
+    def count(self) -> DataFrame:
+        rows = self.df.select(self.keys).collect()
+        counts: Dict[tuple, int] = {}
+        for r in rows:
+            counts[tuple(r)] = counts.get(tuple(r), 0) + 1
+        keys = sorted(counts, key=_sort_key)
+        data = [Row.from_fields(self.keys + ["count"], list(k) + [counts[k]]) for k in keys]
+        fields = [self.df.schema[k] for k in self.keys] + [StructField("count", LongType(), False)]
+        return create_dataframe(data, StructType(fields))
+
+
+def _sort_key(k):
+    return tuple((0, v) if isinstance(v, numbers.Number) else (1, str(v)) for v in k)
+
+
+# ------------------------------------------------------------------ construction
+def _bounds(n: int, parts: int, p: int):
+    """Row range of partition p when n rows are sliced evenly (Spark parallelize)."""
+    return (p * n) // parts, ((p + 1) * n) // parts
+
+
+def _infer_type(v) -> Optional[DataType]:
+    if v is None:
+        return None
+    if isinstance(v, (bool, np.bool_)):
+        return BooleanType()
+    if isinstance(v, np.generic):
+        return {np.dtype(np.float64): DoubleType(), np.dtype(np.float32): FloatType(),
+                np.dtype(np.int32): IntegerType(), np.dtype(np.int64): LongType()}.get(v.dtype, DoubleType())
+    if isinstance(v, float):
+        return DoubleType()
+    if isinstance(v, int):
+        return LongType()
+    if isinstance(v, str):
+        return StringType()
+    if isinstance(v, (bytes, bytearray)):
+        return BinaryType()
+    if isinstance(v, np.ndarray):
+        t = _infer_type(v.reshape(-1)[0]) if v.size else DoubleType()
+        for _ in range(v.ndim):
+            t = ArrayType(t, False)
+        return t
+    if isinstance(v, (list, tuple)):
+        inner = None
+        for x in v:
+            inner = _infer_type(x)
+            if inner is not None:
+                break
+        return ArrayType(inner or DoubleType(), False)
+    raise TypeError(f"cannot infer a column type for value {v!r} of type {type(v).__name__}")
+
+
+def _tf_of(dt: DataType) -> Optional[int]:
+    s = scalar_type_of(dt)
+    return s.tf_dtype if isinstance(s, NumericType) else None
+
+
+def _normalize_rows(data: Sequence[Any], names: Optional[List[str]]):
+    rows = list(data)
+    if not rows:
+        return [], names or []
+    r0 = rows[0]
+    if isinstance(r0, Row) and r0.__fields__:
+        names = names or list(r0.__fields__)
+        return [tuple(r) for r in rows], names
+    if isinstance(r0, dict):
+        names = names or list(r0.keys())
+        return [tuple(r[n] for n in names) for r in rows], names
+    if isinstance(r0, (tuple, list, Row)):
+        names = names or [f"_{i + 1}" for i in range(len(r0))]
+        return [tuple(r) for r in rows], names
+    names = names or ["value"]
+    return [(r,) for r in rows], names
+
+
+def create_dataframe(data, schema=None, num_partitions: Optional[int] = None) -> DataFrame:
+    """Build a DataFrame from local data (rows, dicts, tuples, scalars, or a
+    dict of column arrays). `schema`: a StructType, a list of column names, or None."""
+    nparts = num_partitions or max(1, dist.world_size())
+    if isinstance(data, dict):
+        return from_columns(data, num_partitions=nparts, schema=schema if isinstance(schema, StructType) else None)
+    try:
+        import pandas as pd
+        if isinstance(data, pd.DataFrame):
+            return from_columns({c: data[c].to_numpy() if data[c].dtype != object else list(data[c])
+                                 for c in data.columns}, num_partitions=nparts)
+    except ImportError:  # pragma: no cover
+        pass
+    names = schema if isinstance(schema, (list, tuple)) else None
+    rows, names = _normalize_rows(data, list(names) if names else None)
+    if isinstance(schema, StructType):
+        st = schema
+        names = st.names
+    else:
+        fields = []
+        for i, n in enumerate(names):
+            t = None
+            for r in rows:
+                t = _infer_type(r[i])
+                if t is not None:
+                    break
+            if t is None:
+                t = StringType()
+            fields.append(StructField(n, t, True))
+        st = StructType(fields)
+    for r in rows:
+        if len(r) != len(names):
+            raise ValueError(f"row {r} has {len(r)} values, schema has {len(names)} columns")
+    blocks = {}
+    n = len(rows)
+    for p in dist.local_partitions(nparts):
+        a, b = _bounds(n, nparts, p)
+        cols = {}
+        for i, f in enumerate(st.fields):
+            vals = [r[i] for r in rows[a:b]]
+            if any(v is None for v in vals):
+                raise ValueError(f"column '{f.name}' contains null values; tensorframes_amd requires "
+                                 f"non-null columns (the reference silently accepted them)")
+            cols[f.name] = build_column(vals, _tf_of(f.dataType))
+        blocks[p] = Block(b - a, cols)
+    return DataFrame(st, _Materialized(blocks), nparts)
+
+
+createDataFrame = create_dataframe  # noqa: N816
+
+
+def _field_for_array(name: str, arr) -> StructField:
+    if isinstance(arr, torch.Tensor):
+        tf = D.as_dtype(arr.dtype).enum
+        ndim = arr.dim()
+    else:
+        arr = np.asarray(arr)
+        if arr.dtype.kind in ("U", "S", "O"):
+            return StructField(name, StringType() if arr.dtype.kind != "S" else BinaryType(), False)
+        tf = D.as_dtype(arr.dtype).enum
+        ndim = arr.ndim
+    from .types import nested_array, sql_type_for_tf
+    return StructField(name, nested_array(sql_type_for_tf(tf), ndim - 1), False)
+
+
+def from_columns(columns: Dict[str, Any], num_partitions: Optional[int] = None,
+                 schema: Optional[StructType] = None, pinned: bool = False) -> DataFrame:
+    """DataFrame from whole-column arrays ``{name: array[rows, *cell]}`` (zero-copy
+    for contiguous numpy/torch inputs; `pinned=True` page-locks dense columns)."""
+    nparts = num_partitions or max(1, dist.world_size())
+    cols = {}
+    n = None
+    for k, v in columns.items():
+        if isinstance(v, torch.Tensor):
+            t = v
+        else:
+            a = np.asarray(v)
+            t = torch.from_numpy(np.asarray(a, order="C")) if a.dtype.kind not in ("U", "S", "O") else list(v)
+        ln = t.shape[0] if isinstance(t, torch.Tensor) else len(t)
+        if n is None:
+            n = ln
+        elif ln != n:
+            raise ValueError(f"column {k} has {ln} rows, expected {n}")
+        cols[k] = t
+    n = n or 0
+    st = schema or StructType([_field_for_array(k, v) for k, v in cols.items()])
+    blocks = {}
+    for p in dist.local_partitions(nparts):
+        a, b = _bounds(n, nparts, p)
+        bc = {}
+        for k, t in cols.items():
+            if isinstance(t, torch.Tensor):
+                s = t[a:b]
+                if pinned:
+                    from ..engine import pin
+                    s = pin(s)
+                bc[k] = s
+            else:
+                bc[k] = ObjectColumn(t[a:b])
+        blocks[p] = Block(b - a, bc)
+    return DataFrame(st, _Materialized(blocks), nparts)
+
+
+def generate(schema: StructType, num_partitions: int, fn: Callable[[int], Block]) -> DataFrame:
+    """Lazily generated partitions (synthetic data sets larger than host RAM are
+    produced partition by partition, only on the owning rank)."""
+    return DataFrame(schema, _Generated(num_partitions, fn), num_partitions)
+
+
+def range_(n: int, num_partitions: Optional[int] = None, name: str = "id") -> DataFrame:
+    nparts = num_partitions or max(1, dist.world_size())
+
+    def fn(p):
+        a, b = _bounds(n, nparts, p)
+        return Block(b - a, {name: torch.arange(a, b, dtype=torch.int64)})
+    return generate(StructType([StructField(name, LongType(), False)]), nparts, fn)

@@ -1,0 +1,1156 @@
+"""TF-1.x-compatible graph builder (no TensorFlow needed).
+
+Emits GraphDefs with the same op names, attributes and node-naming rules as
+TF 1.x Python, so code written against ``tf.placeholder`` / ``tf.add`` /
+``tf.reduce_sum`` ... for the reference works by swapping the import:
+
+    from tensorframes_amd import tf
+    with tf.Graph().as_default():
+        x = tf.placeholder(tf.double, shape=[None], name="x")
+        z = tf.add(x, 3, name="z")
+
+Naming follows TF: a name is made unique per graph with ``_1``, ``_2`` ...
+suffixes, and non-tensor op arguments become ``Const`` nodes named
+``<op>/<arg>`` (e.g. ``Fill/dims``, ``z/y``), matching the golden NodeDefs the
+reference's DSL is tested against (reference: src/test/scala/org/tensorframes/dsl/BasicSuite.scala:12-33,
+src/main/scala/org/tensorframes/dsl/Paths.scala:13-56). Graph contexts are per
+thread (the reference's DSL path state was a global, reference: Paths.scala:10).
+
+Static shapes come from the native runtime's shape inference
+(csrc/ir/*: one implementation shared with the executor).
+"""
+from __future__ import annotations
+
+import builtins as _builtins
+import contextlib
+import threading
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from ..utils import dtypes as D
+from ..utils.dtypes import (DType, as_dtype, bfloat16, bool_, double, float16, float32, float64,  # noqa: F401
+                            int8, int16, int32, int64, string, uint8)
+from . import proto as P
+
+bool = bool_  # noqa: A001  (tf.bool)
+
+
+# ------------------------------------------------------------------ shapes
+class Dimension:
+    def __init__(self, v: Optional[int]):
+        self.value = v
+
+    def __eq__(self, o):
+        ov = o.value if isinstance(o, Dimension) else o
+        return self.value == ov
+
+    def __int__(self):
+        return self.value
+
+    def __index__(self):
+        return self.value
+
+    def __repr__(self):
+        return f"Dimension({self.value})"
+
+
+class TensorShape:
+    def __init__(self, dims: Optional[Sequence[Optional[int]]]):
+        self._dims = None if dims is None else [None if (d is None or d < 0) else int(d) for d in dims]
+
+    @property
+    def ndims(self) -> Optional[int]:
+        return None if self._dims is None else len(self._dims)
+
+    @property
+    def dims(self):
+        return None if self._dims is None else [Dimension(d) for d in self._dims]
+
+    def as_list(self) -> List[Optional[int]]:
+        if self._dims is None:
+            raise ValueError("as_list() is not defined on an unknown TensorShape.")
+        return list(self._dims)
+
+    def is_fully_defined(self) -> bool:
+        return self._dims is not None and all(d is not None for d in self._dims)
+
+    def __len__(self):
+        return len(self._dims or [])
+
+    def __getitem__(self, i):
+        return self._dims[i]
+
+    def __iter__(self):
+        return iter(self._dims or [])
+
+    def __eq__(self, o):
+        if isinstance(o, TensorShape):
+            return self._dims == o._dims
+        if isinstance(o, (list, tuple)):
+            return self._dims == list(o)
+        return NotImplemented
+
+    def __repr__(self):
+        if self._dims is None:
+            return "TensorShape(None)"
+        return "TensorShape([" + ", ".join("Dimension(None)" if d is None else f"Dimension({d})"
+                                           for d in self._dims) + "])"
+
+
+# ------------------------------------------------------------------ graph
+class Graph:
+    def __init__(self):
+        self._nodes: List[P.NodeDef] = []
+        self._ops: Dict[str, "Operation"] = {}
+        self._names_in_use: Dict[str, int] = {}
+        self._scope: List[str] = []
+        self._infer_cache: Tuple[int, Dict[str, Any]] = (-1, {})
+        self._lock = threading.Lock()
+
+    # -- context
+    @contextlib.contextmanager
+    def as_default(self):
+        _stack().append(self)
+        try:
+            yield self
+        finally:
+            _stack().pop()
+
+    @contextlib.contextmanager
+    def name_scope(self, name: str):
+        if name is None or name == "":
+            yield ""
+            return
+        if name.endswith("/"):
+            scope = name[:-1]
+        else:
+            scope = self.unique_name(name)
+        old = self._scope
+        self._scope = scope.split("/") if scope else []
+        try:
+            yield scope + "/"
+        finally:
+            self._scope = old
+
+    def unique_name(self, name: str, mark_as_used: bool = True) -> str:
+        full = "/".join(self._scope + [name]) if self._scope else name
+        key = full.lower()
+        i = self._names_in_use.get(key, 0)
+        if mark_as_used:
+            self._names_in_use[key] = i + 1
+        if i > 0:
+            base = full
+            while True:
+                cand = f"{base}_{i}"
+                if cand.lower() not in self._names_in_use:
+                    full = cand
+                    if mark_as_used:
+                        self._names_in_use[cand.lower()] = 1
+                    break
+                i += 1
+        return full
+
+    # -- nodes
+    def _add(self, node: P.NodeDef, n_out: int, out_dtypes: List[DType]) -> "Operation":
+        with self._lock:
+            if node.name in self._ops:
+                raise ValueError(f"Duplicate node name in graph: '{node.name}'")
+            self._nodes.append(node)
+            op = Operation(self, node, n_out, out_dtypes)
+            self._ops[node.name] = op
+            return op
+
+    def get_operations(self) -> List["Operation"]:
+        return [self._ops[n.name] for n in self._nodes]
+
+    def get_operation_by_name(self, name: str) -> "Operation":
+        if name not in self._ops:
+            raise KeyError(f"The name '{name}' refers to an Operation not in the graph.")
+        return self._ops[name]
+
+    def get_tensor_by_name(self, name: str) -> "Tensor":
+        base, _, idx = name.partition(":")
+        op = self.get_operation_by_name(base)
+        return op.outputs[int(idx or 0)]
+
+    def as_graph_element(self, obj, allow_tensor=True, allow_operation=True):
+        if isinstance(obj, Tensor):
+            if obj.graph is not self:
+                raise ValueError(f"Tensor {obj} is not an element of this graph.")
+            return obj
+        if isinstance(obj, Operation):
+            return obj
+        if isinstance(obj, str):
+            if ":" in obj:
+                return self.get_tensor_by_name(obj)
+            return self.get_operation_by_name(obj)
+        raise TypeError(f"Can not convert a {type(obj).__name__} into a graph element.")
+
+    def as_graph_def(self, add_shapes: bool = False) -> P.GraphDef:
+        g = P.GraphDef(list(self._nodes), producer=24)
+        if add_shapes:
+            shapes = self._inferred()
+            nodes = []
+            for n in self._nodes:
+                m = P.NodeDef(n.name, n.op, n.input, dict(n.attr), n.device)
+                outs = shapes.get(n.name)
+                if outs:
+                    m.attr["_output_shapes"] = P.AttrValue.shapelist([o["shape"] for o in outs])
+                nodes.append(m)
+            g = P.GraphDef(nodes, producer=24)
+        return g
+
+    def serialize(self) -> bytes:
+        return P.serialize_graphdef(self.as_graph_def())
+
+    def _inferred(self) -> Dict[str, Any]:
+        n = len(self._nodes)
+        if self._infer_cache[0] != n:
+            from .._native import _C
+            res = _C.infer_all(self.serialize())
+            self._infer_cache = (n, res)
+        return self._infer_cache[1]
+
+    def finalize(self):
+        pass
+
+    def __enter__(self):
+        self._ctx = self.as_default()
+        return self._ctx.__enter__()
+
+    def __exit__(self, *a):
+        return self._ctx.__exit__(*a)
+
+
+_tls = threading.local()
+_global_default = [Graph()]
+
+
+def _stack() -> List[Graph]:
+    if not hasattr(_tls, "stack"):
+        _tls.stack = []
+    return _tls.stack
+
+
+def get_default_graph() -> Graph:
+    st = _stack()
+    return st[-1] if st else _global_default[0]
+
+
+def reset_default_graph():
+    _global_default[0] = Graph()
+
+
+@contextlib.contextmanager
+def name_scope(name: str):
+    with get_default_graph().name_scope(name) as s:
+        yield s
+
+
+# reference-DSL spellings (reference: src/main/scala/org/tensorframes/dsl/package.scala:31-35)
+scope = name_scope
+
+
+@contextlib.contextmanager
+def with_graph():
+    with Graph().as_default() as g:
+        yield g
+
+
+class Operation:
+    def __init__(self, graph: Graph, node: P.NodeDef, n_out: int, out_dtypes: List[DType]):
+        self.graph = graph
+        self.node_def = node
+        self.outputs = [Tensor(self, i, out_dtypes[i] if i < len(out_dtypes) else None)
+                        for i in _builtins.range(n_out)]
+
+    @property
+    def name(self) -> str:
+        return self.node_def.name
+
+    @property
+    def type(self) -> str:
+        return self.node_def.op
+
+    @property
+    def inputs(self) -> List["Tensor"]:
+        out = []
+        for i in self.node_def.input:
+            if not i.startswith("^"):
+                out.append(self.graph.get_tensor_by_name(i if ":" in i else i + ":0"))
+        return out
+
+    def get_attr(self, name):
+        a = self.node_def.attr[name]
+        if a.kind == "type":
+            return DType(a.value)
+        if a.kind == "shape":
+            return None if a.value.unknown_rank else a.value.dims
+        return a.value
+
+    def __repr__(self):
+        return f"<tf.Operation '{self.name}' type={self.type}>"
+
+
+class Tensor:
+    def __init__(self, op: Operation, value_index: int, dtype: Optional[DType]):
+        self.op = op
+        self.value_index = value_index
+        self._dtype = dtype
+
+    @property
+    def graph(self) -> Graph:
+        return self.op.graph
+
+    @property
+    def name(self) -> str:
+        return f"{self.op.name}:{self.value_index}"
+
+    @property
+    def dtype(self) -> DType:
+        if self._dtype is None:
+            info = self.graph._inferred()[self.op.name][self.value_index]
+            self._dtype = DType(info["dtype"])
+        return self._dtype
+
+    def get_shape(self) -> TensorShape:
+        info = self.graph._inferred()[self.op.name][self.value_index]
+        return TensorShape(info["shape"])
+
+    @property
+    def shape(self) -> TensorShape:
+        return self.get_shape()
+
+    # -- operators (implicit constant lifting; reference: src/main/scala/org/tensorframes/dsl/Implicits.scala:121-123)
+    def __add__(self, o):
+        return add(self, o)
+
+    def __radd__(self, o):
+        return add(o, self)
+
+    def __sub__(self, o):
+        return subtract(self, o)
+
+    def __rsub__(self, o):
+        return subtract(o, self)
+
+    def __mul__(self, o):
+        return multiply(self, o)
+
+    def __rmul__(self, o):
+        return multiply(o, self)
+
+    def __truediv__(self, o):
+        return truediv(self, o)
+
+    def __rtruediv__(self, o):
+        return truediv(o, self)
+
+    def __div__(self, o):
+        return div(self, o)
+
+    def __floordiv__(self, o):
+        return floordiv(self, o)
+
+    def __mod__(self, o):
+        return mod(self, o)
+
+    def __pow__(self, o):
+        return pow(self, o)
+
+    def __neg__(self):
+        return negative(self)
+
+    def __abs__(self):
+        return abs(self)
+
+    def __matmul__(self, o):
+        return matmul(self, o)
+
+    def __lt__(self, o):
+        return less(self, o)
+
+    def __le__(self, o):
+        return less_equal(self, o)
+
+    def __gt__(self, o):
+        return greater(self, o)
+
+    def __ge__(self, o):
+        return greater_equal(self, o)
+
+    def __and__(self, o):
+        return logical_and(self, o)
+
+    def __or__(self, o):
+        return logical_or(self, o)
+
+    def __invert__(self):
+        return logical_not(self)
+
+    def __getitem__(self, item):
+        return _slice_helper(self, item)
+
+    def __hash__(self):
+        return id(self)
+
+    def __eq__(self, o):  # TF-1.x semantics: identity
+        return self is o
+
+    def eval(self, feed_dict=None, session=None):
+        s = session or Session(self.graph)
+        return s.run(self, feed_dict)
+
+    def __repr__(self):
+        try:
+            shp = self.get_shape()
+        except Exception:  # noqa: BLE001 (repr must not fail)
+            shp = "?"
+        return f"<tf.Tensor '{self.name}' shape={shp} dtype={self.dtype.name}>"
+
+
+# ------------------------------------------------------------------ core builders
+def _const_node(graph: Graph, value, dtype: Optional[DType], name: str, shape=None) -> Tensor:
+    arr, dt = _to_numpy(value, dtype)
+    if shape is not None:
+        shape = [int(s) for s in shape]
+        if arr.size == 1:
+            arr = np.full(shape, arr.reshape(-1)[0], dtype=arr.dtype)
+        else:
+            arr = arr.reshape(shape)
+    tp = P.TensorProto.from_numpy(arr, dt.enum)
+    node = P.NodeDef(name, "Const", [], {"dtype": P.AttrValue.type(dt), "value": P.AttrValue.tensor(tp)})
+    return graph._add(node, 1, [dt]).outputs[0]
+
+
+def _to_numpy(value, dtype: Optional[DType]) -> Tuple[np.ndarray, DType]:
+    if isinstance(value, Tensor):
+        raise TypeError("expected a python / numpy value")
+    if dtype is not None:
+        dtype = as_dtype(dtype)
+        if dtype.enum == D.DT_STRING:
+            return np.array(value, dtype=object), dtype
+        return np.asarray(value, dtype=dtype.as_numpy_dtype), dtype
+    arr = np.asarray(value)
+    if arr.dtype.kind in ("U", "S", "O"):
+        return np.array(value, dtype=object), string
+    if arr.dtype == np.float64 and not isinstance(value, np.ndarray):
+        return arr.astype(np.float32), float32  # TF default for python floats
+    if arr.dtype == np.int64 and not isinstance(value, np.ndarray):
+        return arr.astype(np.int32), int32  # TF default for python ints
+    return arr, as_dtype(arr.dtype)
+
+
+def convert_to_tensor(value, dtype=None, name=None) -> Tensor:
+    if isinstance(value, Tensor):
+        if dtype is not None and as_dtype(dtype) != value.dtype:
+            raise TypeError(f"Tensor conversion requested dtype {as_dtype(dtype).name} for Tensor "
+                            f"with dtype {value.dtype.name}: {value!r}")
+        return value
+    g = get_default_graph()
+    return _const_node(g, value, dtype, g.unique_name(name or "Const"))
+
+
+def _graph_of(values) -> Graph:
+    for v in values:
+        if isinstance(v, Tensor):
+            return v.graph
+        if isinstance(v, (list, tuple)):
+            for w in v:
+                if isinstance(w, Tensor):
+                    return w.graph
+    return get_default_graph()
+
+
+def _op(op_type: str, inputs: List[Tuple[str, Any]], attrs: Dict[str, P.AttrValue],
+        name: Optional[str], n_out: int = 1, out_dtypes: Optional[List[DType]] = None,
+        dtype_hint: Optional[DType] = None, list_inputs: Sequence[str] = ()) -> Operation:
+    """Create an op: open its name scope, lift python values to `<op>/<arg>` Consts."""
+    g = _graph_of([v for _, v in inputs])
+    with g.as_default():
+        op_name = g.unique_name(name or op_type)
+        names: List[str] = []
+        g_scope = g._scope
+        g._scope = op_name.split("/")
+        try:
+            for arg, v in inputs:
+                vals = v if arg in list_inputs else [v]
+                for j, item in enumerate(vals):
+                    if isinstance(item, Tensor):
+                        t = item
+                    else:
+                        nm = arg if arg not in list_inputs else (f"{arg}_{j}" if j else arg)
+                        t = _const_node(g, item, dtype_hint if dtype_hint is not None and
+                                        not isinstance(item, np.ndarray) else None,
+                                        g.unique_name(nm))
+                    names.append(t.op.name if t.value_index == 0 else t.name)
+        finally:
+            g._scope = g_scope
+        node = P.NodeDef(op_name, op_type, names, attrs)
+        return g._add(node, n_out, out_dtypes or [])
+
+
+def _first_dtype(*vals) -> Optional[DType]:
+    for v in vals:
+        if isinstance(v, Tensor):
+            return v.dtype
+    return None
+
+
+def _binary(op_type: str, x, y, name, out_dtype: Optional[DType] = None) -> Tensor:
+    dt = _first_dtype(x, y)
+    if dt is None:
+        x = convert_to_tensor(x)
+        dt = x.dtype
+    op = _op(op_type, [("x", x), ("y", y)], {"T": P.AttrValue.type(dt)}, name,
+             out_dtypes=[out_dtype or dt], dtype_hint=dt)
+    return op.outputs[0]
+
+
+def _unary(op_type: str, x, name) -> Tensor:
+    x = convert_to_tensor(x)
+    return _op(op_type, [("x", x)], {"T": P.AttrValue.type(x.dtype)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+
+# ------------------------------------------------------------------ public ops
+def placeholder(dtype, shape=None, name=None) -> Tensor:
+    dt = as_dtype(dtype)
+    g = get_default_graph()
+    nm = g.unique_name(name or "Placeholder")
+    shp = None if shape is None else [None if (d is None or (isinstance(d, int) and d < 0)) else int(d)
+                                      for d in (shape.as_list() if isinstance(shape, TensorShape) else shape)]
+    node = P.NodeDef(nm, "Placeholder", [], {"dtype": P.AttrValue.type(dt), "shape": P.AttrValue.shape(shp)})
+    return g._add(node, 1, [dt]).outputs[0]
+
+
+def placeholder_with_default(input, shape, name=None) -> Tensor:  # noqa: A002
+    input = convert_to_tensor(input)
+    return _op("PlaceholderWithDefault", [("input", input)],
+               {"dtype": P.AttrValue.type(input.dtype), "shape": P.AttrValue.shape(shape)}, name,
+               out_dtypes=[input.dtype]).outputs[0]
+
+
+def constant(value, dtype=None, shape=None, name="Const") -> Tensor:
+    g = get_default_graph()
+    return _const_node(g, value, as_dtype(dtype) if dtype is not None else None, g.unique_name(name), shape)
+
+
+def identity(input, name=None) -> Tensor:  # noqa: A002
+    return _unary("Identity", input, name)
+
+
+def stop_gradient(input, name=None) -> Tensor:  # noqa: A002
+    return _unary("StopGradient", input, name)
+
+
+def add(x, y, name=None):
+    return _binary("Add", x, y, name)
+
+
+def subtract(x, y, name=None):
+    return _binary("Sub", x, y, name)
+
+
+sub = subtract
+
+
+def multiply(x, y, name=None):
+    return _binary("Mul", x, y, name)
+
+
+mul = multiply
+
+
+def div(x, y, name=None):
+    return _binary("Div", x, y, name)
+
+
+def truediv(x, y, name=None):
+    dt = _first_dtype(x, y)
+    if dt is not None and dt.is_integer:
+        x = cast(x, float64)
+        y = cast(y, float64)
+    return _binary("RealDiv", x, y, name)
+
+
+divide = truediv
+realdiv = truediv
+
+
+def floordiv(x, y, name=None):
+    return _binary("FloorDiv", x, y, name)
+
+
+def mod(x, y, name=None):
+    return _binary("FloorMod", x, y, name)
+
+
+floormod = mod
+
+
+def maximum(x, y, name=None):
+    return _binary("Maximum", x, y, name)
+
+
+def minimum(x, y, name=None):
+    return _binary("Minimum", x, y, name)
+
+
+def pow(x, y, name=None):  # noqa: A001
+    return _binary("Pow", x, y, name)
+
+
+def squared_difference(x, y, name=None):
+    return _binary("SquaredDifference", x, y, name)
+
+
+def atan2(y, x, name=None):
+    return _binary("Atan2", y, x, name)
+
+
+def equal(x, y, name=None):
+    return _binary("Equal", x, y, name, out_dtype=bool_)
+
+
+def not_equal(x, y, name=None):
+    return _binary("NotEqual", x, y, name, out_dtype=bool_)
+
+
+def less(x, y, name=None):
+    return _binary("Less", x, y, name, out_dtype=bool_)
+
+
+def less_equal(x, y, name=None):
+    return _binary("LessEqual", x, y, name, out_dtype=bool_)
+
+
+def greater(x, y, name=None):
+    return _binary("Greater", x, y, name, out_dtype=bool_)
+
+
+def greater_equal(x, y, name=None):
+    return _binary("GreaterEqual", x, y, name, out_dtype=bool_)
+
+
+def logical_and(x, y, name=None):
+    return _op("LogicalAnd", [("x", x), ("y", y)], {}, name, out_dtypes=[bool_], dtype_hint=bool_).outputs[0]
+
+
+def logical_or(x, y, name=None):
+    return _op("LogicalOr", [("x", x), ("y", y)], {}, name, out_dtypes=[bool_], dtype_hint=bool_).outputs[0]
+
+
+def logical_not(x, name=None):
+    return _op("LogicalNot", [("x", x)], {}, name, out_dtypes=[bool_]).outputs[0]
+
+
+def add_n(inputs, name=None):
+    inputs = [convert_to_tensor(i) for i in inputs]
+    dt = inputs[0].dtype
+    return _op("AddN", [("inputs", inputs)], {"T": P.AttrValue.type(dt), "N": P.AttrValue.i(len(inputs))},
+               name, out_dtypes=[dt], list_inputs=("inputs",)).outputs[0]
+
+
+def _mk_unary(op_type):
+    def f(x, name=None):
+        return _unary(op_type, x, name)
+    f.__name__ = op_type.lower()
+    return f
+
+
+negative = _mk_unary("Neg")
+neg = negative
+abs = _mk_unary("Abs")  # noqa: A001
+square = _mk_unary("Square")
+sqrt = _mk_unary("Sqrt")
+rsqrt = _mk_unary("Rsqrt")
+exp = _mk_unary("Exp")
+log = _mk_unary("Log")
+log1p = _mk_unary("Log1p")
+expm1 = _mk_unary("Expm1")
+reciprocal = _mk_unary("Reciprocal")
+inv = _mk_unary("Inv")
+floor = _mk_unary("Floor")
+ceil = _mk_unary("Ceil")
+round = _mk_unary("Round")  # noqa: A001
+sign = _mk_unary("Sign")
+sin = _mk_unary("Sin")
+cos = _mk_unary("Cos")
+tan = _mk_unary("Tan")
+tanh = _mk_unary("Tanh")
+sigmoid = _mk_unary("Sigmoid")
+erf = _mk_unary("Erf")
+is_nan = _mk_unary("IsNan")
+is_inf = _mk_unary("IsInf")
+is_finite = _mk_unary("IsFinite")
+
+
+def _axis_input(input_tensor: Tensor, axis) -> Any:
+    if axis is None:
+        rk = input_tensor.get_shape().ndims
+        if rk is not None:
+            return constant(np.arange(rk, dtype=np.int32), dtype=int32)
+        r = rank(input_tensor)
+        return range(0, r, 1)
+    if isinstance(axis, Tensor):
+        return axis
+    return np.asarray(axis, dtype=np.int32)
+
+
+def _reduction(op_type: str, input_tensor, axis, keep_dims, name, reduction_indices, out_bool=False):
+    if axis is None:
+        axis = reduction_indices
+    x = convert_to_tensor(input_tensor)
+    ax = _axis_input(x, axis)
+    dt = bool_ if out_bool else x.dtype
+    attrs = {"T": P.AttrValue.type(x.dtype), "Tidx": P.AttrValue.type(int32),
+             "keep_dims": P.AttrValue.b(keep_dims)}
+    if out_bool:
+        attrs.pop("T")
+    return _op(op_type, [("input", x), ("reduction_indices", ax)], attrs, name, out_dtypes=[dt]).outputs[0]
+
+
+def reduce_sum(input_tensor, axis=None, keep_dims=False, name=None, reduction_indices=None, keepdims=None):
+    return _reduction("Sum", input_tensor, axis, bool_or(keepdims, keep_dims), name, reduction_indices)
+
+
+def reduce_min(input_tensor, axis=None, keep_dims=False, name=None, reduction_indices=None, keepdims=None):
+    return _reduction("Min", input_tensor, axis, bool_or(keepdims, keep_dims), name, reduction_indices)
+
+
+def reduce_max(input_tensor, axis=None, keep_dims=False, name=None, reduction_indices=None, keepdims=None):
+    return _reduction("Max", input_tensor, axis, bool_or(keepdims, keep_dims), name, reduction_indices)
+
+
+def reduce_prod(input_tensor, axis=None, keep_dims=False, name=None, reduction_indices=None, keepdims=None):
+    return _reduction("Prod", input_tensor, axis, bool_or(keepdims, keep_dims), name, reduction_indices)
+
+
+def reduce_mean(input_tensor, axis=None, keep_dims=False, name=None, reduction_indices=None, keepdims=None):
+    return _reduction("Mean", input_tensor, axis, bool_or(keepdims, keep_dims), name, reduction_indices)
+
+
+def reduce_all(input_tensor, axis=None, keep_dims=False, name=None, reduction_indices=None, keepdims=None):
+    return _reduction("All", input_tensor, axis, bool_or(keepdims, keep_dims), name, reduction_indices, True)
+
+
+def reduce_any(input_tensor, axis=None, keep_dims=False, name=None, reduction_indices=None, keepdims=None):
+    return _reduction("Any", input_tensor, axis, bool_or(keepdims, keep_dims), name, reduction_indices, True)
+
+
+def bool_or(a, b):
+    return b if a is None else a
+
+
+def _argreduce(op_type, input, axis, name, output_type):  # noqa: A002
+    x = convert_to_tensor(input)
+    ax = 0 if axis is None else axis
+    return _op(op_type, [("input", x), ("dimension", ax if isinstance(ax, Tensor) else np.int32(ax))],
+               {"T": P.AttrValue.type(x.dtype), "Tidx": P.AttrValue.type(int32),
+                "output_type": P.AttrValue.type(output_type)}, name,
+               out_dtypes=[as_dtype(output_type)]).outputs[0]
+
+
+def argmin(input, axis=None, name=None, dimension=None, output_type=int64):  # noqa: A002
+    return _argreduce("ArgMin", input, axis if axis is not None else dimension, name, output_type)
+
+
+def argmax(input, axis=None, name=None, dimension=None, output_type=int64):  # noqa: A002
+    return _argreduce("ArgMax", input, axis if axis is not None else dimension, name, output_type)
+
+
+def matmul(a, b, transpose_a=False, transpose_b=False, adjoint_a=False, adjoint_b=False, name=None):
+    a = convert_to_tensor(a)
+    b = convert_to_tensor(b, dtype=a.dtype)
+    ta, tb = transpose_a or adjoint_a, transpose_b or adjoint_b
+    ra, rb = a.get_shape().ndims, b.get_shape().ndims
+    if (ra is not None and ra > 2) or (rb is not None and rb > 2):
+        return _op("BatchMatMulV2", [("x", a), ("y", b)],
+                   {"T": P.AttrValue.type(a.dtype), "adj_x": P.AttrValue.b(ta), "adj_y": P.AttrValue.b(tb)},
+                   name, out_dtypes=[a.dtype]).outputs[0]
+    return _op("MatMul", [("a", a), ("b", b)],
+               {"T": P.AttrValue.type(a.dtype), "transpose_a": P.AttrValue.b(ta),
+                "transpose_b": P.AttrValue.b(tb)}, name, out_dtypes=[a.dtype]).outputs[0]
+
+
+def cast(x, dtype, name=None):
+    x = convert_to_tensor(x)
+    dt = as_dtype(dtype)
+    if dt == x.dtype:
+        return x
+    return _op("Cast", [("x", x)], {"SrcT": P.AttrValue.type(x.dtype), "DstT": P.AttrValue.type(dt)},
+               name, out_dtypes=[dt]).outputs[0]
+
+
+to_float = lambda x, name="ToFloat": cast(x, float32, name)  # noqa: E731
+to_double = lambda x, name="ToDouble": cast(x, float64, name)  # noqa: E731
+to_int32 = lambda x, name="ToInt32": cast(x, int32, name)  # noqa: E731
+to_int64 = lambda x, name="ToInt64": cast(x, int64, name)  # noqa: E731
+
+
+def reshape(tensor, shape, name=None):
+    t = convert_to_tensor(tensor)
+    shp = shape if isinstance(shape, Tensor) else np.asarray(shape, dtype=np.int32)
+    return _op("Reshape", [("tensor", t), ("shape", shp)],
+               {"T": P.AttrValue.type(t.dtype), "Tshape": P.AttrValue.type(int32)}, name,
+               out_dtypes=[t.dtype]).outputs[0]
+
+
+def squeeze(input, axis=None, name=None, squeeze_dims=None):  # noqa: A002
+    x = convert_to_tensor(input)
+    ax = axis if axis is not None else squeeze_dims
+    if isinstance(ax, int):
+        ax = [ax]
+    return _op("Squeeze", [("input", x)], {"T": P.AttrValue.type(x.dtype),
+                                           "squeeze_dims": P.AttrValue.ilist(ax or [])}, name,
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+def expand_dims(input, axis=None, name=None, dim=None):  # noqa: A002
+    x = convert_to_tensor(input)
+    ax = axis if axis is not None else dim
+    return _op("ExpandDims", [("input", x), ("dim", ax if isinstance(ax, Tensor) else np.int32(ax))],
+               {"T": P.AttrValue.type(x.dtype), "Tdim": P.AttrValue.type(int32)}, name,
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+def shape(input, name=None, out_type=int32):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("Shape", [("input", x)], {"T": P.AttrValue.type(x.dtype), "out_type": P.AttrValue.type(out_type)},
+               name, out_dtypes=[as_dtype(out_type)]).outputs[0]
+
+
+def size(input, name=None, out_type=int32):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("Size", [("input", x)], {"T": P.AttrValue.type(x.dtype), "out_type": P.AttrValue.type(out_type)},
+               name, out_dtypes=[as_dtype(out_type)]).outputs[0]
+
+
+def rank(input, name=None):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("Rank", [("input", x)], {"T": P.AttrValue.type(x.dtype)}, name, out_dtypes=[int32]).outputs[0]
+
+
+def fill(dims, value, name=None):
+    """`Fill` with `<name>/dims` and `<name>/value` constants
+    (reference: src/main/scala/org/tensorframes/dsl/package.scala:66-85)."""
+    vdt = value.dtype if isinstance(value, Tensor) else _to_numpy(value, None)[1]
+    d = dims if isinstance(dims, Tensor) else np.asarray(dims, dtype=np.int32)
+    return _op("Fill", [("dims", d), ("value", value)],
+               {"T": P.AttrValue.type(vdt), "index_type": P.AttrValue.type(int32)}, name,
+               out_dtypes=[vdt], dtype_hint=vdt).outputs[0]
+
+
+def zeros(shape, dtype=float32, name=None):
+    dt = as_dtype(dtype)
+    return fill(shape, np.zeros((), dtype=dt.as_numpy_dtype), name=name or "zeros")
+
+
+def ones(shape, dtype=float32, name=None):
+    dt = as_dtype(dtype)
+    return fill(shape, np.ones((), dtype=dt.as_numpy_dtype), name=name or "ones")
+
+
+def zeros_like(tensor, dtype=None, name=None):
+    return _unary("ZerosLike", tensor, name)
+
+
+def ones_like(tensor, dtype=None, name=None):
+    return _unary("OnesLike", tensor, name)
+
+
+def range(start, limit=None, delta=1, dtype=None, name="range"):  # noqa: A001
+    if limit is None:
+        start, limit = 0, start
+    dt = as_dtype(dtype) if dtype is not None else (_first_dtype(start, limit, delta) or int32)
+    return _op("Range", [("start", start), ("limit", limit), ("delta", delta)],
+               {"Tidx": P.AttrValue.type(dt)}, name, out_dtypes=[dt], dtype_hint=dt).outputs[0]
+
+
+def tile(input, multiples, name=None):  # noqa: A002
+    x = convert_to_tensor(input)
+    m = multiples if isinstance(multiples, Tensor) else np.asarray(multiples, dtype=np.int32)
+    return _op("Tile", [("input", x), ("multiples", m)],
+               {"T": P.AttrValue.type(x.dtype), "Tmultiples": P.AttrValue.type(int32)}, name,
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+def stack(values, axis=0, name="stack"):
+    dt = _first_dtype(*values) or _to_numpy(values[0], None)[1]
+    return _op("Pack", [("values", list(values))],
+               {"T": P.AttrValue.type(dt), "N": P.AttrValue.i(len(values)), "axis": P.AttrValue.i(axis)},
+               name, out_dtypes=[dt], dtype_hint=dt, list_inputs=("values",)).outputs[0]
+
+
+pack = stack
+
+
+def unstack(value, num=None, axis=0, name="unstack"):
+    x = convert_to_tensor(value)
+    if num is None:
+        num = x.get_shape().as_list()[axis]
+    op = _op("Unpack", [("value", x)], {"T": P.AttrValue.type(x.dtype), "num": P.AttrValue.i(num),
+                                        "axis": P.AttrValue.i(axis)}, name, n_out=num,
+             out_dtypes=[x.dtype] * num)
+    return op.outputs
+
+
+def concat(values, axis, name="concat"):
+    dt = _first_dtype(*values) or _to_numpy(values[0], None)[1]
+    return _op("ConcatV2", [("values", list(values)), ("axis", np.int32(axis) if not isinstance(axis, Tensor) else axis)],
+               {"T": P.AttrValue.type(dt), "N": P.AttrValue.i(len(values)), "Tidx": P.AttrValue.type(int32)},
+               name, out_dtypes=[dt], dtype_hint=dt, list_inputs=("values",)).outputs[0]
+
+
+def transpose(a, perm=None, name="transpose"):
+    x = convert_to_tensor(a)
+    if perm is None:
+        rk = x.get_shape().ndims
+        perm = list(reversed(builtin_range(rk)))
+    p = perm if isinstance(perm, Tensor) else np.asarray(perm, dtype=np.int32)
+    return _op("Transpose", [("x", x), ("perm", p)],
+               {"T": P.AttrValue.type(x.dtype), "Tperm": P.AttrValue.type(int32)}, name,
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+builtin_range = _builtins.range
+
+
+def slice(input_, begin, size, name=None):  # noqa: A001
+    x = convert_to_tensor(input_)
+    return _op("Slice", [("input", x), ("begin", np.asarray(begin, dtype=np.int32)),
+                         ("size", np.asarray(size, dtype=np.int32))],
+               {"T": P.AttrValue.type(x.dtype), "Index": P.AttrValue.type(int32)}, name,
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+def strided_slice(input_, begin, end, strides=None, begin_mask=0, end_mask=0, ellipsis_mask=0,
+                  new_axis_mask=0, shrink_axis_mask=0, name=None):
+    x = convert_to_tensor(input_)
+    if strides is None:
+        strides = [1] * len(begin)
+    return _op("StridedSlice", [("input", x), ("begin", np.asarray(begin, dtype=np.int32)),
+                                ("end", np.asarray(end, dtype=np.int32)),
+                                ("strides", np.asarray(strides, dtype=np.int32))],
+               {"T": P.AttrValue.type(x.dtype), "Index": P.AttrValue.type(int32),
+                "begin_mask": P.AttrValue.i(begin_mask), "end_mask": P.AttrValue.i(end_mask),
+                "ellipsis_mask": P.AttrValue.i(ellipsis_mask), "new_axis_mask": P.AttrValue.i(new_axis_mask),
+                "shrink_axis_mask": P.AttrValue.i(shrink_axis_mask)}, name or "strided_slice",
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+def _slice_helper(t: Tensor, item) -> Tensor:
+    if not isinstance(item, tuple):
+        item = (item,)
+    begin, end, strides = [], [], []
+    bm = em = elm = nam = sam = 0
+    for i, s in enumerate(item):
+        if s is Ellipsis:
+            begin.append(0); end.append(0); strides.append(1)
+            elm |= 1 << i
+        elif s is None:
+            begin.append(0); end.append(0); strides.append(1)
+            nam |= 1 << i
+        elif isinstance(s, builtins_slice):
+            begin.append(s.start or 0)
+            end.append(s.stop or 0)
+            strides.append(s.step or 1)
+            if s.start is None:
+                bm |= 1 << i
+            if s.stop is None:
+                em |= 1 << i
+        else:
+            begin.append(int(s)); end.append(int(s) + 1); strides.append(1)
+            sam |= 1 << i
+    return strided_slice(t, begin, end, strides, bm, em, elm, nam, sam)
+
+
+builtins_slice = _builtins.slice
+
+
+def gather(params, indices, axis=0, name=None):
+    p = convert_to_tensor(params)
+    ix = convert_to_tensor(indices) if isinstance(indices, Tensor) else np.asarray(indices, dtype=np.int32)
+    idt = ix.dtype if isinstance(ix, Tensor) else as_dtype(ix.dtype)
+    return _op("GatherV2", [("params", p), ("indices", ix), ("axis", np.int32(axis))],
+               {"Tparams": P.AttrValue.type(p.dtype), "Tindices": P.AttrValue.type(idt),
+                "Taxis": P.AttrValue.type(int32)}, name, out_dtypes=[p.dtype]).outputs[0]
+
+
+def one_hot(indices, depth, on_value=1.0, off_value=0.0, axis=-1, dtype=float32, name=None):
+    ix = convert_to_tensor(indices)
+    dt = as_dtype(dtype)
+    return _op("OneHot", [("indices", ix), ("depth", np.int32(depth)),
+                          ("on_value", np.asarray(on_value, dtype=dt.as_numpy_dtype)),
+                          ("off_value", np.asarray(off_value, dtype=dt.as_numpy_dtype))],
+               {"T": P.AttrValue.type(dt), "TI": P.AttrValue.type(ix.dtype), "axis": P.AttrValue.i(axis)},
+               name, out_dtypes=[dt]).outputs[0]
+
+
+def where(condition, x=None, y=None, name=None):
+    if x is None or y is None:
+        raise NotImplementedError("where(condition) (index form) is data-dependent and not supported")
+    dt = _first_dtype(x, y)
+    return _op("Select", [("condition", condition), ("t", x), ("e", y)], {"T": P.AttrValue.type(dt)},
+               name, out_dtypes=[dt], dtype_hint=dt).outputs[0]
+
+
+def unsorted_segment_sum(data, segment_ids, num_segments, name=None):
+    return _useg("UnsortedSegmentSum", data, segment_ids, num_segments, name)
+
+
+def unsorted_segment_max(data, segment_ids, num_segments, name=None):
+    return _useg("UnsortedSegmentMax", data, segment_ids, num_segments, name)
+
+
+def unsorted_segment_min(data, segment_ids, num_segments, name=None):
+    return _useg("UnsortedSegmentMin", data, segment_ids, num_segments, name)
+
+
+def unsorted_segment_prod(data, segment_ids, num_segments, name=None):
+    return _useg("UnsortedSegmentProd", data, segment_ids, num_segments, name)
+
+
+def _useg(op_type, data, segment_ids, num_segments, name):
+    x = convert_to_tensor(data)
+    ids = convert_to_tensor(segment_ids)
+    ns = num_segments if isinstance(num_segments, Tensor) else np.int32(num_segments)
+    return _op(op_type, [("data", x), ("segment_ids", ids), ("num_segments", ns)],
+               {"T": P.AttrValue.type(x.dtype), "Tindices": P.AttrValue.type(ids.dtype),
+                "Tnumsegments": P.AttrValue.type(int32)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+
+# ------------------------------------------------------------------ tf.nn
+class _NN:
+    @staticmethod
+    def relu(features, name=None):
+        return _unary("Relu", features, name)
+
+    @staticmethod
+    def relu6(features, name=None):
+        return _unary("Relu6", features, name)
+
+    @staticmethod
+    def elu(features, name=None):
+        return _unary("Elu", features, name)
+
+    @staticmethod
+    def selu(features, name=None):
+        return _unary("Selu", features, name)
+
+    @staticmethod
+    def sigmoid(x, name=None):
+        return _unary("Sigmoid", x, name)
+
+    @staticmethod
+    def tanh(x, name=None):
+        return _unary("Tanh", x, name)
+
+    @staticmethod
+    def softplus(features, name=None):
+        return _unary("Softplus", features, name)
+
+    @staticmethod
+    def softmax(logits, name=None):
+        return _op("Softmax", [("logits", logits)], {"T": P.AttrValue.type(logits.dtype)}, name,
+                   out_dtypes=[logits.dtype]).outputs[0]
+
+    @staticmethod
+    def log_softmax(logits, name=None):
+        return _op("LogSoftmax", [("logits", logits)], {"T": P.AttrValue.type(logits.dtype)}, name,
+                   out_dtypes=[logits.dtype]).outputs[0]
+
+    @staticmethod
+    def bias_add(value, bias, data_format=None, name=None):
+        v = convert_to_tensor(value)
+        return _op("BiasAdd", [("value", v), ("bias", bias)],
+                   {"T": P.AttrValue.type(v.dtype), "data_format": P.AttrValue.s(data_format or "NHWC")},
+                   name, out_dtypes=[v.dtype], dtype_hint=v.dtype).outputs[0]
+
+    @staticmethod
+    def conv2d(input, filter=None, strides=None, padding=None, use_cudnn_on_gpu=True,  # noqa: A002
+               data_format="NHWC", dilations=(1, 1, 1, 1), name=None, filters=None):
+        x = convert_to_tensor(input)
+        w = filter if filter is not None else filters
+        return _op("Conv2D", [("input", x), ("filter", w)],
+                   {"T": P.AttrValue.type(x.dtype), "strides": P.AttrValue.ilist(strides),
+                    "padding": P.AttrValue.s(padding), "data_format": P.AttrValue.s(data_format),
+                    "use_cudnn_on_gpu": P.AttrValue.b(use_cudnn_on_gpu),
+                    "dilations": P.AttrValue.ilist(dilations)}, name, out_dtypes=[x.dtype],
+                   dtype_hint=x.dtype).outputs[0]
+
+    @staticmethod
+    def max_pool(value, ksize, strides, padding, data_format="NHWC", name=None):
+        x = convert_to_tensor(value)
+        return _op("MaxPool", [("input", x)],
+                   {"T": P.AttrValue.type(x.dtype), "ksize": P.AttrValue.ilist(ksize),
+                    "strides": P.AttrValue.ilist(strides), "padding": P.AttrValue.s(padding),
+                    "data_format": P.AttrValue.s(data_format)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+    @staticmethod
+    def avg_pool(value, ksize, strides, padding, data_format="NHWC", name=None):
+        x = convert_to_tensor(value)
+        return _op("AvgPool", [("value", x)],
+                   {"T": P.AttrValue.type(x.dtype), "ksize": P.AttrValue.ilist(ksize),
+                    "strides": P.AttrValue.ilist(strides), "padding": P.AttrValue.s(padding),
+                    "data_format": P.AttrValue.s(data_format)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+    @staticmethod
+    def fused_batch_norm(x, scale, offset, mean, variance, epsilon=0.001, data_format="NHWC",
+                         is_training=False, name=None):
+        x = convert_to_tensor(x)
+        op = _op("FusedBatchNorm", [("x", x), ("scale", scale), ("offset", offset), ("mean", mean),
+                                    ("variance", variance)],
+                 {"T": P.AttrValue.type(x.dtype), "epsilon": P.AttrValue.f(epsilon),
+                  "data_format": P.AttrValue.s(data_format), "is_training": P.AttrValue.b(is_training)},
+                 name, n_out=5, out_dtypes=[x.dtype] * 5, dtype_hint=x.dtype)
+        return op.outputs[0], op.outputs[1], op.outputs[2]
+
+    @staticmethod
+    def top_k(input, k=1, sorted=True, name=None):  # noqa: A002
+        x = convert_to_tensor(input)
+        op = _op("TopKV2", [("input", x), ("k", np.int32(k))],
+                 {"T": P.AttrValue.type(x.dtype), "sorted": P.AttrValue.b(sorted)}, name, n_out=2,
+                 out_dtypes=[x.dtype, int32])
+        return op.outputs[0], op.outputs[1]
+
+
+nn = _NN()
+math = __import__("types").SimpleNamespace(
+    add=add, subtract=subtract, multiply=multiply, divide=truediv, square=square, sqrt=sqrt,
+    reduce_sum=reduce_sum, reduce_min=reduce_min, reduce_max=reduce_max, reduce_mean=reduce_mean,
+    argmin=argmin, argmax=argmax, reciprocal=reciprocal, exp=exp, log=log, abs=abs,
+    unsorted_segment_sum=unsorted_segment_sum, maximum=maximum, minimum=minimum,
+)
+
+
+# ------------------------------------------------------------------ local evaluation
+class Session:
+    """Runs a DSL graph on local tensors through the native executor (CPU or
+    the current GPU). Mirrors ``tf.Session().run(fetches, feed_dict)``."""
+
+    def __init__(self, graph: Optional[Graph] = None, device=None):
+        self.graph = graph or get_default_graph()
+        self.device = device
+
+    def run(self, fetches, feed_dict=None):
+        from ..engine import run_graph
+        single = not isinstance(fetches, (list, tuple))
+        fl = [fetches] if single else list(fetches)
+        feeds = {}
+        for k, v in (feed_dict or {}).items():
+            name = k.op.name if isinstance(k, Tensor) else str(k).split(":")[0]
+            feeds[name] = v
+        names = [f.name if isinstance(f, Tensor) else str(f) for f in fl]
+        outs = run_graph(self.graph.serialize(), names, feeds, device=self.device)
+        return outs[0] if single else outs
+
+    def close(self):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

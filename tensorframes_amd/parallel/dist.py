@@ -1,0 +1,157 @@
+"""Process-group context: one process per GPU, partitions pinned to ranks.
+
+The reference distributes work with Spark (mapPartitions tasks, Broadcast,
+RDD.reduce to the driver, a groupBy shuffle; reference:
+src/main/scala/org/tensorframes/impl/DebugRowOps.scala:376-391,500,524,576).
+Here every rank runs the same program (SPMD), owns partitions
+``p % world_size == rank`` and exchanges data with torch.distributed
+collectives: backend "nccl" (= RCCL over xGMI on MI355X) for device tensors,
+"gloo" for host objects and for CPU-only runs.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+_state = {"device_group": None, "cpu_group": None, "initialized_here": False}
+
+
+def env_world_size() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def is_distributed() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def rank() -> int:
+    return dist.get_rank() if is_distributed() else 0
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_distributed() else 1
+
+
+def local_rank() -> int:
+    return int(os.environ.get("LOCAL_RANK", str(rank())))
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> bool:
+    """Initialise the default process group from torchrun's env (idempotent).
+
+    Returns True when running with world_size > 1.
+    """
+    if dist.is_initialized():
+        _ensure_groups()
+        return dist.get_world_size() > 1
+    if env_world_size() <= 1:
+        return False
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    use_gpu = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local_rank() % max(torch.cuda.device_count(), 1))
+    kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+    if backend == "nccl":
+        kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
+    dist.init_process_group(**kwargs)
+    _state["initialized_here"] = True
+    _ensure_groups()
+    return dist.get_world_size() > 1
+
+
+def _ensure_groups():
+    if _state["device_group"] is None:
+        _state["device_group"] = dist.group.WORLD
+    if _state["cpu_group"] is None:
+        if dist.get_backend() == "gloo":
+            _state["cpu_group"] = dist.group.WORLD
+        else:
+            _state["cpu_group"] = dist.new_group(backend="gloo")
+
+
+def shutdown():
+    if dist.is_initialized() and _state["initialized_here"]:
+        dist.destroy_process_group()
+    _state.update(device_group=None, cpu_group=None, initialized_here=False)
+
+
+def owns(pid: int) -> bool:
+    return pid % world_size() == rank()
+
+
+def owner(pid: int) -> int:
+    return pid % world_size()
+
+
+def local_partitions(num_partitions: int) -> List[int]:
+    r, w = rank(), world_size()
+    return [p for p in range(num_partitions) if p % w == r]
+
+
+def barrier():
+    if is_distributed():
+        dist.barrier(group=_state["cpu_group"])
+
+
+# -- host-object collectives (small metadata / rows) over gloo
+def all_gather_object(obj: Any) -> List[Any]:
+    if not is_distributed():
+        return [obj]
+    _ensure_groups()
+    out = [None] * world_size()
+    dist.all_gather_object(out, obj, group=_state["cpu_group"])
+    return out
+
+
+def broadcast_object(obj: Any, src: int = 0) -> Any:
+    if not is_distributed():
+        return obj
+    _ensure_groups()
+    box = [obj]
+    dist.broadcast_object_list(box, src=src, group=_state["cpu_group"])
+    return box[0]
+
+
+def all_to_all_objects(per_dest: List[Any]) -> List[Any]:
+    """per_dest[r] goes to rank r; returns what each rank sent to us."""
+    if not is_distributed():
+        return [per_dest[0]]
+    gathered = all_gather_object(per_dest)
+    me = rank()
+    return [gathered[src][me] for src in range(world_size())]
+
+
+# -- tensor collectives: device tensors over RCCL, host tensors over gloo
+_OPS = {"Sum": dist.ReduceOp.SUM, "Min": dist.ReduceOp.MIN, "Max": dist.ReduceOp.MAX,
+        "Prod": dist.ReduceOp.PRODUCT}
+
+
+def all_reduce_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
+    if not is_distributed():
+        return t
+    _ensure_groups()
+    group = _state["device_group"] if t.is_cuda else _state["cpu_group"]
+    dist.all_reduce(t, op=_OPS[op], group=group)
+    return t
+
+
+def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
+    """Stack the same-shaped tensor of every rank: [world, *t.shape]."""
+    if not is_distributed():
+        return t.unsqueeze(0)
+    _ensure_groups()
+    t = t.contiguous()
+    if t.is_cuda:
+        out = torch.empty((world_size(),) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=_state["device_group"])
+        return out
+    parts = [torch.empty_like(t) for _ in range(world_size())]
+    dist.all_gather(parts, t, group=_state["cpu_group"])
+    return torch.stack(parts, 0)

@@ -1,0 +1,25 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(autouse=True)
+def _fresh_default_graph():
+    from tensorframes_amd.graph import dsl
+    dsl.reset_default_graph()
+    yield
+
+
+def gpu_available():
+    import torch
+    return torch.cuda.is_available()
