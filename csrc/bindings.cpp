@@ -161,14 +161,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           Graph::Infos infos = p.analyze(infos_from_py(hints));
           py::dict out;
           // per fetch and per feed: info of output 0 (or the indexed output)
-          for (auto& f : fetches) {
+          auto info_of = [&](const std::string& f) -> py::object {
             TensorRef r = g->resolve(f);
-            out[py::str(f)] = infos_to_py({infos[r.node][r.index]})[0];
-          }
-          for (auto& f : feeds) {
-            TensorRef r = g->resolve(f);
-            out[py::str(f)] = infos_to_py({infos[r.node][r.index]})[0];
-          }
+            TFA_CHECK(r.index < static_cast<int>(infos[r.node].size()), "tensor '", f,
+                      "' does not exist (node has ", infos[r.node].size(), " outputs)");
+            py::list l = infos_to_py({infos[r.node][r.index]});
+            return py::object(l[0]);
+          };
+          for (auto& f : fetches) out[py::str(f)] = info_of(f);
+          for (auto& f : feeds) out[py::str(f)] = info_of(f);
           return out;
         });
   m.def("infer_all", &infer_all);
@@ -223,6 +224,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return out;
   });
   m.def("empty_pinned", &empty_pinned);
+  m.def("trim_pinned_pool", &trim_pinned_pool);
+  m.def("is_pinned", [](const at::Tensor& t) {
+    // torch's is_pinned() only knows its own host allocator; ask HIP directly
+    if (t.is_cuda() || !t.numel()) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, t.data_ptr()) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+  });
+  m.def("pinned_pool_cached_bytes", &pinned_pool_cached_bytes);
   m.def("pin_host_tensor", &pin_host_tensor);
   m.def("unpin_host_tensor", &unpin_host_tensor);
 }

@@ -116,6 +116,14 @@ Program::Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetch
       }
     }
   }
+  // feeds outside the fetch closure still get an (inferred) info slot
+  {
+    std::set<int> in_order(order_.begin(), order_.end());
+    std::vector<int> extra;
+    for (int f : feed_nodes_)
+      if (!in_order.count(f)) extra.push_back(f);
+    order_.insert(order_.begin(), extra.begin(), extra.end());
+  }
   // every placeholder reached must be fed
   for (int n : order_) {
     const Node& nd = g_->node(n);
@@ -566,14 +574,84 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs) {
 }
 
 // ------------------------------------------------------------------ pinned memory
+// Page-locking is expensive (hipHostMalloc of 512 MB takes ~100 ms), so
+// pinned blocks are cached by 2 MiB-rounded size and handed out again when a
+// tensor using them dies. Bounded by TFA_PINNED_POOL_MB (default 64 GiB).
+namespace {
+class PinnedPool {
+ public:
+  static PinnedPool& get() {
+    static PinnedPool* p = new PinnedPool();
+    return *p;
+  }
+  void* alloc(size_t bytes, size_t* rounded) {
+    size_t r = (bytes + kGran - 1) / kGran * kGran;
+    *rounded = r;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = free_.find(r);
+      if (it != free_.end()) {
+        void* p = it->second;
+        free_.erase(it);
+        cached_ -= r;
+        return p;
+      }
+    }
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, r, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      trim(0);  // release cached blocks and retry once
+      HIP_OK(hipHostMalloc(&p, r, hipHostMallocDefault));
+    }
+    return p;
+  }
+  void release(void* p, size_t r) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.emplace(r, p);
+    cached_ += r;
+    while (cached_ > limit_ && !free_.empty()) {
+      auto it = std::prev(free_.end());
+      cached_ -= it->first;
+      hipHostFree(it->second);
+      free_.erase(it);
+    }
+  }
+  void trim(size_t keep) {
+    std::lock_guard<std::mutex> lk(mu_);
+    while (cached_ > keep && !free_.empty()) {
+      auto it = free_.begin();
+      cached_ -= it->first;
+      hipHostFree(it->second);
+      free_.erase(it);
+    }
+  }
+  size_t cached() const { return cached_; }
+
+ private:
+  PinnedPool() {
+    const char* e = std::getenv("TFA_PINNED_POOL_MB");
+    limit_ = (e ? std::strtoull(e, nullptr, 10) : 65536ull) << 20;
+  }
+  static constexpr size_t kGran = size_t(2) << 20;
+  std::mutex mu_;
+  std::multimap<size_t, void*> free_;
+  size_t cached_ = 0;
+  size_t limit_;
+};
+}  // namespace
+
 at::Tensor empty_pinned(const std::vector<int64_t>& sizes, at::ScalarType dt) {
   int64_t n = 1;
   for (auto s : sizes) n *= s;
   size_t bytes = static_cast<size_t>(std::max<int64_t>(n, 1)) * c10::elementSize(dt);
-  void* p = nullptr;
-  HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
-  return at::from_blob(p, sizes, [](void* q) { hipHostFree(q); }, at::TensorOptions().dtype(dt));
+  size_t r = 0;
+  void* p = PinnedPool::get().alloc(bytes, &r);
+  return at::from_blob(p, sizes, [r](void* q) { PinnedPool::get().release(q, r); },
+                       at::TensorOptions().dtype(dt));
 }
+
+void trim_pinned_pool() { PinnedPool::get().trim(0); }
+size_t pinned_pool_cached_bytes() { return PinnedPool::get().cached(); }
 
 void pin_host_tensor(const at::Tensor& t) {
   TFA_CHECK(!t.is_cuda(), "pin_host_tensor needs a host tensor");

@@ -85,6 +85,8 @@ class Program {
 
 // pinned host memory (hipHostMalloc, exact size; freed with hipHostFree)
 at::Tensor empty_pinned(const std::vector<int64_t>& sizes, at::ScalarType dt);
+void trim_pinned_pool();
+size_t pinned_pool_cached_bytes();
 // page-lock an existing host tensor's memory in place (hipHostRegister)
 void pin_host_tensor(const at::Tensor& t);
 void unpin_host_tensor(const at::Tensor& t);

@@ -85,7 +85,7 @@ def compute_device() -> torch.device:
 def to_device(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
     if t.device == dev:
         return t
-    return t.to(dev, non_blocking=t.is_pinned())
+    return t.to(dev, non_blocking=is_pinned(t))
 
 
 def empty_host(shape, dtype: torch.dtype, pinned: bool) -> torch.Tensor:
@@ -95,9 +95,13 @@ def empty_host(shape, dtype: torch.dtype, pinned: bool) -> torch.Tensor:
     return torch.empty(tuple(shape), dtype=dtype)
 
 
+def is_pinned(t: torch.Tensor) -> bool:
+    return (not t.is_cuda) and gpu_available() and (t.is_pinned() or _C.is_pinned(t))
+
+
 def pin(t: torch.Tensor) -> torch.Tensor:
     """Page-lock a host tensor for DMA (copy into pinned memory)."""
-    if not gpu_available() or t.is_cuda or t.is_pinned():
+    if not gpu_available() or t.is_cuda or is_pinned(t):
         return t
     out = _C.empty_pinned(list(t.shape), t.dtype)
     out.copy_(t)
@@ -128,7 +132,7 @@ def run_block_host(prog, inputs: List[torch.Tensor], separable: bool,
     res = []
     for o in outs:
         h = empty_host(tuple(o.shape), o.dtype, config.pinned_outputs)
-        h.copy_(o, non_blocking=h.is_pinned())
+        h.copy_(o, non_blocking=is_pinned(h))
         res.append(h)
     torch.cuda.current_stream(dev).synchronize()
     metrics.add("d2h_bytes", sum(o.numel() * o.element_size() for o in outs))

@@ -324,40 +324,40 @@ class Tensor:
 
     # -- operators (implicit constant lifting; reference: src/main/scala/org/tensorframes/dsl/Implicits.scala:121-123)
     def __add__(self, o):
-        return add(self, o)
+        return add(self, o, name="add")
 
     def __radd__(self, o):
-        return add(o, self)
+        return add(o, self, name="add")
 
     def __sub__(self, o):
-        return subtract(self, o)
+        return subtract(self, o, name="sub")
 
     def __rsub__(self, o):
-        return subtract(o, self)
+        return subtract(o, self, name="sub")
 
     def __mul__(self, o):
-        return multiply(self, o)
+        return multiply(self, o, name="mul")
 
     def __rmul__(self, o):
-        return multiply(o, self)
+        return multiply(o, self, name="mul")
 
     def __truediv__(self, o):
-        return truediv(self, o)
+        return truediv(self, o, name="truediv")
 
     def __rtruediv__(self, o):
-        return truediv(o, self)
+        return truediv(o, self, name="truediv")
 
     def __div__(self, o):
         return div(self, o)
 
     def __floordiv__(self, o):
-        return floordiv(self, o)
+        return floordiv(self, o, name="floordiv")
 
     def __mod__(self, o):
-        return mod(self, o)
+        return mod(self, o, name="mod")
 
     def __pow__(self, o):
-        return pow(self, o)
+        return pow(self, o, name="pow")
 
     def __neg__(self):
         return negative(self)
@@ -837,8 +837,7 @@ def fill(dims, value, name=None):
     (reference: src/main/scala/org/tensorframes/dsl/package.scala:66-85)."""
     vdt = value.dtype if isinstance(value, Tensor) else _to_numpy(value, None)[1]
     d = dims if isinstance(dims, Tensor) else np.asarray(dims, dtype=np.int32)
-    return _op("Fill", [("dims", d), ("value", value)],
-               {"T": P.AttrValue.type(vdt), "index_type": P.AttrValue.type(int32)}, name,
+    return _op("Fill", [("dims", d), ("value", value)], {"T": P.AttrValue.type(vdt)}, name,
                out_dtypes=[vdt], dtype_hint=vdt).outputs[0]
 
 

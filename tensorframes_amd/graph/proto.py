@@ -187,13 +187,34 @@ def _enc_shape(s: TensorShapeProto) -> bytes:
     return out
 
 
+def _typed_val_field(dtype: int, arr: np.ndarray) -> bytes:
+    """One element as a typed `*_val` field (what TF emits for single-element
+    tensors; larger ones use `tensor_content`)."""
+    v = arr.reshape(-1)[0]
+    if dtype == D.DT_FLOAT:
+        return _ld(5, struct.pack("<f", float(v)))
+    if dtype == D.DT_DOUBLE:
+        return _ld(6, struct.pack("<d", float(v)))
+    if dtype == D.DT_INT64:
+        return _ld(10, _varint(int(v)))
+    if dtype == D.DT_BOOL:
+        return _ld(11, _varint(1 if v else 0))
+    if dtype == D.DT_HALF:
+        return _ld(13, _varint(int(np.asarray(v, np.float16).view(np.uint16))))
+    return _ld(7, _varint(int(v)))
+
+
 def _enc_tensor(t: TensorProto) -> bytes:
     out = _key(1, 0) + _varint(t.dtype) + _ld(2, _enc_shape(TensorShapeProto(t.shape)))
     if t.dtype == D.DT_STRING:
         for s in t.strings or []:
             out += _ld(8, s)
     else:
-        out += _ld(4, t.content)
+        n = int(np.prod(t.shape)) if t.shape else 1
+        if n == 1 and t.dtype != D.DT_BFLOAT16:
+            out += _typed_val_field(t.dtype, t.to_numpy())
+        elif n > 1:
+            out += _ld(4, t.content)
     return out
 
 
@@ -506,10 +527,37 @@ def _txt_tensor(t: TensorProto, ind: str) -> List[str]:
         out += [f'{ind}string_val: "{s.decode(errors="replace")}"' for s in t.strings or []]
     else:
         arr = t.to_numpy().reshape(-1)
-        key = {D.DT_FLOAT: "float_val", D.DT_DOUBLE: "double_val", D.DT_INT64: "int64_val",
-               D.DT_BOOL: "bool_val"}.get(t.dtype, "int_val")
-        out += [f"{ind}{key}: {_num(v)}" for v in arr]
+        if arr.size > 1:
+            out.append(f'{ind}tensor_content: "{_c_escape(t.content)}"')
+        else:
+            key = {D.DT_FLOAT: "float_val", D.DT_DOUBLE: "double_val", D.DT_INT64: "int64_val",
+                   D.DT_BOOL: "bool_val"}.get(t.dtype, "int_val")
+            out += [f"{ind}{key}: {_num(v)}" for v in arr]
     return out
+
+
+def _c_escape(b: bytes) -> str:
+    """protobuf text-format byte escaping (octal for non-printables)."""
+    out = []
+    for c in b:
+        ch = chr(c)
+        if ch == "\n":
+            out.append("\\n")
+        elif ch == "\r":
+            out.append("\\r")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == '"':
+            out.append('\\"')
+        elif ch == "'":
+            out.append("\\'")
+        elif ch == "\\":
+            out.append("\\\\")
+        elif 32 <= c < 127:
+            out.append(ch)
+        else:
+            out.append(f"\\{c:03o}")
+    return "".join(out)
 
 
 def _num(v) -> str:

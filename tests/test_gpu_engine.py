@@ -1,0 +1,82 @@
+"""GPU engine paths: pipelined host->HBM->host chunk loop, device-resident
+frames, pinned pool, monoid reductions, segmented aggregate."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import tensorframes_amd as tfs  # noqa: E402
+from tensorframes_amd import engine, tf  # noqa: E402
+from tensorframes_amd._native import _C  # noqa: E402
+
+rng = np.random.default_rng(7)
+
+
+def test_pinned_pool_is_pinned_and_reused():
+    a = _C.empty_pinned([1 << 20], torch.float32)
+    assert _C.is_pinned(a)
+    assert not _C.is_pinned(torch.empty(1 << 20))
+    p = a.data_ptr()
+    del a
+    b = _C.empty_pinned([1 << 20], torch.float32)
+    assert b.data_ptr() == p  # came back from the pool
+
+
+@pytest.mark.parametrize("rows", [70000, 300001])
+def test_map_blocks_pipelined_matches_reference(rows):
+    x = rng.standard_normal((rows, 64)).astype(np.float32)
+    w = rng.standard_normal((64, 48)).astype(np.float32)
+    df = tfs.analyze(tfs.from_columns({"x": x}, num_partitions=3, pinned=True))
+    tfs.set_config(chunk_bytes=64 * 1024 * 10, min_chunked_rows=1000)
+    try:
+        with tf.Graph().as_default():
+            xb = tfs.block(df, "x")
+            y = tf.nn.relu(tf.matmul(xb, tf.constant(w)) + 1.0, name="y")
+            z = tf.reduce_sum(xb * xb, [1], name="z")
+            out = tfs.map_blocks([y, z], df)
+            got_y, got_z = out.to_numpy("y"), out.to_numpy("z")
+    finally:
+        tfs.set_config(chunk_bytes=128 << 20, min_chunked_rows=65536)
+    np.testing.assert_allclose(got_y, np.maximum(x.astype(np.float64) @ w + 1.0, 0), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(got_z, (x.astype(np.float64) ** 2).sum(1), rtol=1e-5, atol=1e-3)
+
+
+def test_device_resident_frame_stays_on_device():
+    x = rng.standard_normal((5000, 16)).astype(np.float64)
+    df = tfs.from_columns({"x": x}, num_partitions=2).cache_on_device()
+    with tf.Graph().as_default():
+        xb = tf.placeholder(tf.float64, [None, None], name="x")
+        y = tf.add(xb, 2.0, name="y")
+        out = tfs.map_blocks(y, df)
+        blocks = out.local_blocks()
+    assert all(b.columns["y"].is_cuda for b in blocks.values())
+    np.testing.assert_allclose(out.to_numpy("y"), x + 2.0)
+
+
+def test_reduce_blocks_monoid_on_gpu():
+    x = rng.standard_normal((100000, 1024)).astype(np.float32)
+    df = tfs.analyze(tfs.from_columns({"x": x}, num_partitions=8))
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.float32, [None, 1024], name="x_input")
+        s = tf.reduce_sum(xi, [0], name="x")
+        got = tfs.reduce_blocks(s, df)
+    np.testing.assert_allclose(got, x.astype(np.float64).sum(0), rtol=1e-4, atol=1e-2)
+
+
+def test_aggregate_segment_reduce_gpu():
+    n = 20000
+    keys = rng.integers(0, 50, n)
+    x = rng.standard_normal((n, 8))
+    df = tfs.create_dataframe([tfs.Row(key=int(k), x=list(v)) for k, v in zip(keys, x)])
+    df = tfs.analyze(df)
+    with tf.Graph().as_default():
+        xi = tfs.block(df, "x", tf_name="x_input")
+        s = tf.reduce_sum(xi, [0], name="x")
+        rows = tfs.aggregate(s, df.groupBy("key")).collect()
+    assert len(rows) == 50
+    for r in rows:
+        np.testing.assert_allclose(r.x, x[keys == r.key].sum(0), rtol=1e-10, atol=1e-9)
