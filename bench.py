@@ -97,7 +97,9 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
+        res = None
         for _ in range(steps):
+            res = None  # a step's output frame is dropped before the next step (like a loop body)
             res = fn()
         torch.cuda.synchronize()
         dist.barrier()
