@@ -153,8 +153,9 @@ class DataFrame:
     def _local_rows(self) -> List[tuple]:
         out = []
         names = self._schema.names
-        for pid in sorted(self._blocks()):
-            b = self._blocks()[pid]
+        blocks = self._blocks()  # evaluate once: a derived frame recomputes per call
+        for pid in sorted(blocks):
+            b = blocks[pid]
             cols = [column_values(b.columns[n]) for n in names]
             out.append((pid, [Row.from_fields(names, vals) for vals in zip(*cols)] if cols else
                         [Row.from_fields([], []) for _ in range(b.nrows)]))
@@ -194,8 +195,9 @@ class DataFrame:
     def to_numpy(self, column: str) -> np.ndarray:
         """All rows of a dense column as one array (gathered on every rank)."""
         local = []
-        for pid in sorted(self._blocks()):
-            c = self._blocks()[pid].columns[column]
+        blocks = self._blocks()
+        for pid in sorted(blocks):
+            c = blocks[pid].columns[column]
             local.append((pid, c.detach().cpu().numpy() if is_dense(c) else np.asarray(column_values(c), dtype=object)))
         parts = [x for chunk in dist.all_gather_object(local) for x in chunk]
         parts.sort(key=lambda x: x[0])

@@ -1,0 +1,83 @@
+"""Multi-process (SPMD) execution over torch.distributed / gloo on the CPU,
+world_size 2 and 3: partitions pinned to ranks, collect/count gathers,
+reduce_blocks / reduce_rows cross-rank combine (all-reduce for monoids,
+all-gather + one graph run otherwise), aggregate's key shuffle (all-to-all)."""
+import json
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TFA_DEVICE="cpu")
+    sys.path.insert(0, REPO)
+    import numpy as np
+
+    import tensorframes_amd as tfs
+    from tensorframes_amd import Row, tf
+    from tensorframes_amd.parallel import dist
+
+    assert dist.init(backend="gloo")
+    res = {}
+    data = [Row(key=str(i % 3), x=float(i), v=[float(i), float(2 * i)]) for i in range(20)]
+    df = tfs.analyze(tfs.create_dataframe(data, num_partitions=5))
+    res["local_parts"] = sorted(df.local_blocks())
+    res["count"] = df.count()
+    with tf.Graph().as_default():
+        x = tf.placeholder(tf.double, shape=[None], name="x")
+        out = tfs.map_blocks(tf.multiply(x, 2.0, name="z"), df)
+        res["z"] = [r.z for r in out.collect()]
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        res["sum"] = tfs.reduce_blocks(tf.reduce_sum(xi, [0], name="x"), df.select("x"))
+    with tf.Graph().as_default():
+        vi = tf.placeholder(tf.double, shape=[None, 2], name="v_input")
+        res["vmax"] = tfs.reduce_blocks(tf.reduce_max(vi, [0], name="v"), df.select("v")).tolist()
+    with tf.Graph().as_default():
+        # generic (non-monoid) associative graph: sum of squares of... identity of the sum
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        res["gen"] = tfs.reduce_blocks(tf.identity(tf.reduce_sum(xi, [0]), name="x"), df.select("x"))
+    with tf.Graph().as_default():
+        x1 = tf.placeholder(tf.double, shape=[], name="x_1")
+        x2 = tf.placeholder(tf.double, shape=[], name="x_2")
+        res["rows"] = tfs.reduce_rows(tf.add(x1, x2, name="x"), df.select("x"))
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        agg = tfs.aggregate(tf.reduce_sum(xi, [0], name="x"), df.select("key", "x").groupBy("key"))
+        res["agg"] = sorted([list(r) for r in agg.collect()])
+    res["repart"] = [r.x for r in df.repartition(4).select("x").collect()]
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_spmd_world(world, tmp_path):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+    xs = [float(i) for i in range(20)]
+    parts = sorted(p for o in outs for p in o["local_parts"])
+    assert parts == [0, 1, 2, 3, 4]
+    for r, o in enumerate(outs):
+        assert o["local_parts"] == [p for p in range(5) if p % world == r]
+        assert o["count"] == 20
+        assert o["z"] == [2 * x for x in xs]
+        assert o["sum"] == sum(xs) == o["gen"] == o["rows"]
+        assert o["vmax"] == [19.0, 38.0]
+        want = sorted([[k, sum(x for x in xs if str(int(x) % 3) == k)] for k in ("0", "1", "2")])
+        assert o["agg"] == want
+        assert o["repart"] == xs
