@@ -27,7 +27,8 @@ for s in $STEPS; do
     kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -x -q ;;
     bench) run bench 900 python bench.py --steps ${BENCH_STEPS:-5} --warmup ${BENCH_WARMUP:-2} ${BENCH_ARGS:-} ;;
     benchsmall) run benchsmall 600 python bench.py --steps 3 --warmup 1 --rows 1000000 ;;
-    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --mode host ${BENCH_ARGS:-} ;;
+    prof) export TMPDIR=/tmp; run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 3 --warmup 1 ${BENCH_ARGS:-} ;;
+    probe) run probe 600 python scripts/pcie_probe.py ;;
   esac
 done
 echo "all steps done"
