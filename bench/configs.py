@@ -1,0 +1,226 @@
+"""Benchmarks for every BASELINE.json config (the headline config 3 is
+/bench.py at the repo root).
+
+    python bench/configs.py plumbing            # 1: 10-row double DF, map_blocks Add(+3), CPU
+    python bench/configs.py add                 # 2: 1M x float32[128] map_blocks Add, 1 GPU
+    python bench/configs.py reduce              # 4: 10M x float32[1024] reduce_blocks Sum
+    python bench/configs.py inception           # 5: N x 224x224x3 Inception-v3 scoring
+    python bench/configs.py kmeans              # reference demo workload
+    torchrun --nproc-per-node N bench/configs.py reduce|inception ...
+
+Each prints one JSON line (rank 0). Data is synthetic, weights random-init.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import tensorframes_amd as tfs  # noqa: E402
+from tensorframes_amd import tf  # noqa: E402
+from tensorframes_amd._native import _C  # noqa: E402
+from tensorframes_amd.frame.block import Block  # noqa: E402
+from tensorframes_amd.frame.types import ArrayType, FloatType, StructField, StructType  # noqa: E402
+from tensorframes_amd.parallel import dist  # noqa: E402
+
+
+def sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    dist.barrier()
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    dt = time.perf_counter() - t0
+    if dist.is_distributed():
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce_(t, "Max")
+        dt = float(t.item())
+    return dt / steps
+
+
+def emit(d):
+    if dist.rank() == 0:
+        d.setdefault("n_gpus", dist.world_size() if torch.cuda.is_available() else 0)
+        print(json.dumps(d))
+
+
+def vec_schema(name="x"):
+    return StructType([StructField(name, ArrayType(FloatType(), False), False)])
+
+
+def gen_frame(rows, dim, nparts, pinned, device=None, name="x"):
+    """Synthetic float32[dim] frame: pinned host memory or device-resident."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+
+    def make(p):
+        a, b = (p * rows) // nparts, ((p + 1) * rows) // nparts
+        if device is not None:
+            t = torch.randn((b - a, dim), device=device, generator=torch.Generator(device=device).manual_seed(p))
+            return Block(b - a, {name: t})
+        host = _C.empty_pinned([b - a, dim], torch.float32) if pinned else torch.empty((b - a, dim))
+        step = 1 << 20
+        for s in range(0, b - a, step):
+            e = min(b - a, s + step)
+            src = torch.randn((e - s, dim), device=dev) if dev is not None else torch.randn((e - s, dim))
+            host[s:e].copy_(src)
+        return Block(b - a, {name: host})
+    return tfs.generate(vec_schema(name), nparts, make).cache()
+
+
+# ------------------------------------------------------------------ configs
+def cfg_plumbing(a):
+    tfs.set_config(device="cpu")
+    df = tfs.create_dataframe([tfs.Row(x=float(i)) for i in range(10)])
+    with tf.Graph().as_default():
+        x = tf.placeholder(tf.double, shape=[None], name="x")
+        z = tf.add(x, 3, name="z")
+
+        def step():
+            assert tfs.map_blocks(z, df).collect()[0].z == 3.0
+        ms = timed(step, a.steps, a.warmup) * 1e3
+    emit({"config": "1: 10-row double DF, map_blocks Add(+3), CPU plumbing", "metric": "latency",
+          "value": ms, "unit": "ms/call", "higher_is_better": False, "device": "cpu"})
+
+
+def cfg_add(a):
+    rows, dim = a.rows or 1_000_000, 128
+    nparts = max(1, dist.world_size()) * 4
+    res = {}
+    for mode in ("host", "device"):
+        df = gen_frame(rows, dim, nparts, pinned=True,
+                       device=torch.device("cuda", torch.cuda.current_device()) if mode == "device" else None)
+        df.local_blocks()
+        with tf.Graph().as_default():
+            x = tfs.block(tfs.analyze(df) if False else df, "x")
+            y = tf.add(x, 1.0, name="y")
+
+            def step():
+                tfs.map_blocks(y, df, trim=True).local_blocks()
+            res[mode] = timed(step, a.steps, a.warmup)
+    emit({"config": "2: 1M-row float32[128] map_blocks Add, 1 MI355X", "metric": "rows/sec",
+          "value": rows / res["host"], "unit": "rows/s", "higher_is_better": True,
+          "ms_per_step": res["host"] * 1e3, "device_resident_rows_per_sec": rows / res["device"],
+          "device_resident_ms_per_step": res["device"] * 1e3,
+          "device_resident_hbm_GBps": 2 * rows * dim * 4 / res["device"] / 1e9,
+          "rows": rows, "dtype": "fp32", "data": "synthetic"})
+
+
+def cfg_reduce(a):
+    rows, dim = a.rows or 10_000_000, 1024
+    nparts = max(1, dist.world_size()) * a.parts_per_gpu
+    res = {}
+    for mode in ("host", "device"):
+        dev = torch.device("cuda", torch.cuda.current_device())
+        df = gen_frame(rows, dim, nparts, pinned=True, device=dev if mode == "device" else None)
+        df.local_blocks()
+        with tf.Graph().as_default():
+            xi = tf.placeholder(tf.float32, [None, dim], name="x_input")
+            s = tf.reduce_sum(xi, [0], name="x")
+            out = {}
+
+            def step():
+                out["v"] = tfs.reduce_blocks(s, df)
+            res[mode] = timed(step, a.steps, a.warmup)
+        del df
+        torch.cuda.empty_cache()
+    emit({"config": "4: 10M-row float32[1024] reduce_blocks ReduceSum, partitions pinned to GPUs, RCCL all-reduce",
+          "metric": "rows/sec", "value": rows / res["host"], "unit": "rows/s", "higher_is_better": True,
+          "ms_per_step": res["host"] * 1e3, "device_resident_rows_per_sec": rows / res["device"],
+          "device_resident_ms_per_step": res["device"] * 1e3, "rows": rows,
+          "parallelism": f"dp{dist.world_size()}", "dtype": "fp32", "data": "synthetic"})
+
+
+def cfg_inception(a):
+    from tensorframes_amd.models import cnn
+    size = a.image_size
+    images = a.rows or 4096 * max(1, dist.world_size())
+    batch = a.batch
+    nparts = max(1, images // batch)
+    g, iname, oname = cnn.inception_v3(image_size=size)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    schema = StructType([StructField("image", ArrayType(ArrayType(ArrayType(FloatType(), False), False), False), False)])
+
+    def make(p):
+        n = ((p + 1) * images) // nparts - (p * images) // nparts
+        return Block(n, {"image": torch.rand((n, size, size, 3), device=dev)})
+    df = tfs.generate(schema, nparts, make)
+    prob = g.get_tensor_by_name(oname + ":0")
+
+    def step():
+        return tfs.map_blocks(prob, df, trim=True).count()
+    dt = timed(step, a.steps, a.warmup)
+    flops_per_image = _inception_flops(size)
+    emit({"config": f"5: {images} x {size}x{size}x3 images, map_blocks Inception-v3 scoring", "metric": "images/sec",
+          "value": images / dt, "unit": "images/s", "higher_is_better": True, "ms_per_step": dt * 1e3,
+          "batch_per_partition": batch, "tflops": images * flops_per_image / dt / 1e12,
+          "parallelism": f"dp{dist.world_size()}", "dtype": "fp32",
+          "data": "synthetic images generated in HBM; random-init frozen Inception-v3"})
+
+
+def _inception_flops(size):
+    """2*MACs of the conv/matmul layers, from the graph's own shapes."""
+    from tensorframes_amd.models import cnn
+    g, _, _ = cnn.inception_v3(image_size=size)
+    total = 0
+    for op in g.get_operations():
+        if op.type == "Conv2D":
+            out = op.outputs[0].get_shape().as_list()
+            w = op.inputs[1].get_shape().as_list()
+            total += 2 * out[1] * out[2] * out[3] * w[0] * w[1] * w[2]
+        elif op.type == "MatMul":
+            w = op.inputs[1].get_shape().as_list()
+            total += 2 * w[0] * w[1]
+    return total
+
+
+def cfg_kmeans(a):
+    from tensorframes_amd.models import kmeans
+    n, f, k = a.rows or 100_000, 100, 10
+    rng = np.random.default_rng(2)
+    pts = rng.uniform(0.0, 1.0, size=(n, f))
+    df = tfs.analyze(tfs.from_columns({"features": pts}, num_partitions=max(1, dist.world_size()) * 4)).cache()
+    c0 = np.random.default_rng(2).standard_normal((k, f))
+    out = {}
+    for variant, agg in (("aggregate", False), ("in_graph", True)):
+        t0 = time.perf_counter()
+        c, ds = kmeans.kmeans(df, c0, num_iters=a.steps, tf_aggregate=agg)
+        out[variant] = (time.perf_counter() - t0) / max(len(ds), 1)
+    emit({"config": "K-Means 100k x 100, k=10 (reference demo)", "metric": "ms/iteration",
+          "value": out["in_graph"] * 1e3, "unit": "ms", "higher_is_better": False,
+          "aggregate_variant_ms": out["aggregate"] * 1e3, "in_graph_variant_ms": out["in_graph"] * 1e3})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", choices=["plumbing", "add", "reduce", "inception", "kmeans"])
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--parts-per-gpu", type=int, default=1)
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--batch", type=int, default=128)
+    a = ap.parse_args()
+    dist.init()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(dist.local_rank() % torch.cuda.device_count())
+    {"plumbing": cfg_plumbing, "add": cfg_add, "reduce": cfg_reduce, "inception": cfg_inception,
+     "kmeans": cfg_kmeans}[a.config](a)
+    dist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -661,8 +661,37 @@ def _reduce_rows_schema(schema: StructType, summary: Dict[str, NodeSummary]) -> 
 
 
 # ------------------------------------------------------------------ aggregate
-def _stable_hash(key: tuple) -> int:
-    return zlib.crc32(repr(key).encode())
+def _key_array(col) -> np.ndarray:
+    if is_dense(col):
+        a = col.detach().cpu().numpy()
+        if a.ndim != 1:
+            raise TensorFramesError("groupBy keys must be scalar columns")
+        return a
+    return np.asarray(column_values(col), dtype=object)
+
+
+def _key_hash(arrays: List[np.ndarray]) -> np.ndarray:
+    """Process-independent 64-bit hash of the key tuple of every row."""
+    import pandas as pd
+    h = np.zeros(len(arrays[0]), dtype=np.uint64)
+    for a in arrays:
+        h = h * np.uint64(1000003) ^ pd.util.hash_array(a)
+    return h
+
+
+def _factorize(arrays: List[np.ndarray]):
+    """Row group codes (groups in sorted key order) + the unique key columns."""
+    per = [np.unique(a, return_inverse=True) for a in arrays]
+    codes = np.zeros(len(arrays[0]), dtype=np.int64)
+    for u, inv in per:
+        codes = codes * len(u) + inv.astype(np.int64)
+    ucodes, inv = np.unique(codes, return_inverse=True)
+    uniq_cols = []
+    rem = ucodes.copy()
+    for u, _ in reversed(per):
+        uniq_cols.append(u[rem % len(u)])
+        rem //= len(u)
+    return inv.astype(np.int64), list(reversed(uniq_cols))
 
 
 def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) -> DataFrame:
@@ -685,35 +714,34 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
     all_cols = keys + out_names
 
     def compute(blocks):
-        # 1. shuffle (key -> owner rank)
+        # 1. shuffle: rows go to rank hash(key) % world (all-to-all)
         w = dist.world_size()
         send = [[] for _ in range(w)]
         for pid, b in sorted(blocks.items()):
             if b.nrows == 0:
                 continue
-            kv = [column_values(b.columns[k]) for k in keys]
-            ktuples = list(zip(*kv))
-            dest = np.array([_stable_hash(t) % w for t in ktuples], dtype=np.int64) if w > 1 else np.zeros(len(ktuples), np.int64)
             host = b.select(all_cols).to(torch.device("cpu"))
+            if w == 1:
+                send[0].append(host)
+                continue
+            dest = (_key_hash([_key_array(host.columns[k]) for k in keys]) % np.uint64(w)).astype(np.int64)
             for r in range(w):
                 idx = np.nonzero(dest == r)[0]
                 if len(idx):
-                    send[r].append(host.take(idx.tolist()))
+                    send[r].append(host.take(idx))
         recv = dist.all_to_all_objects(send)
         mine = [blk for lst in recv for blk in lst]
         if not mine:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, w))}
         full = concat_blocks(mine, all_cols)
-        # 2. group ids, rows sorted by key
-        kv = [column_values(full.columns[k]) for k in keys]
-        ktuples = list(zip(*kv))
-        uniq = sorted(set(ktuples), key=_sort_key)
-        gid = {k: i for i, k in enumerate(uniq)}
-        codes = np.array([gid[k] for k in ktuples], dtype=np.int64)
+        # 2. group ids (vectorised factorisation), rows sorted by key
+        codes, uniq_cols = _factorize([_key_array(full.columns[k]) for k in keys])
+        ngroups = len(uniq_cols[0]) if uniq_cols else 0
         order = np.argsort(codes, kind="stable")
-        counts = np.bincount(codes, minlength=len(uniq))
+        counts = np.bincount(codes, minlength=ngroups)
         offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-        sorted_blk = full.take(order.tolist())
+        sorted_blk = full.take(order)
+        uniq = list(zip(*[u.tolist() for u in uniq_cols]))
         out_cols: Dict[str, Any] = {}
         for i, k in enumerate(keys):
             out_cols[k] = build_column([u[i] for u in uniq], _tf_of_field(df.schema[k]))
@@ -737,7 +765,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         o = summary[n]
         shape = (o.shape if o.shape is not None else Shape()).prepend(UNKNOWN)
         out_fields.append(ColumnInformation.struct_field(n, o.tf_dtype, shape))
-    return DataFrame(StructType(out_fields), _Derived(df, compute), max(1, dist.world_size()))
+    return DataFrame(StructType(out_fields), _Derived(df, compute, streamable=False), max(1, dist.world_size()))
 
 
 def _tf_of_field(f: StructField) -> Optional[int]:

@@ -57,12 +57,22 @@ class _Generated(_Source):
 
 
 class _Derived(_Source):
-    def __init__(self, parent: "DataFrame", fn: Callable[[Dict[int, Block]], Dict[int, Block]]):
+    """Partitions computed from the parent's. `fn` maps any subset of the
+    parent's local blocks {pid: block} to the same pids; when `streamable`,
+    actions may evaluate partition by partition (bounded memory)."""
+
+    def __init__(self, parent: "DataFrame", fn: Callable[[Dict[int, Block]], Dict[int, Block]],
+                 streamable: bool = True):
         self._parent = parent
         self._fn = fn
+        self.streamable = streamable
 
     def compute(self):
         return self._fn(self._parent._blocks())
+
+    def iterate(self):
+        for pid, b in self._parent._iter_blocks():
+            yield pid, self._fn({pid: b})[pid]
 
 
 # ------------------------------------------------------------------ DataFrame
@@ -119,6 +129,29 @@ class DataFrame:
             self._cached = b
         return b
 
+    def _iter_blocks(self):
+        """Local (pid, block) pairs in pid order, streamed through generated and
+        streamable derived sources so only one partition is alive at a time."""
+        if self._cached is not None or self._persist:
+            blocks = self._blocks()
+            for pid in sorted(blocks):
+                yield pid, blocks[pid]
+            return
+        src = self._source
+        if isinstance(src, _Generated):
+            for p in dist.local_partitions(src._n):
+                yield p, src._fn(p)
+        elif isinstance(src, _Derived) and src.streamable:
+            yield from src.iterate()
+        else:
+            blocks = self._blocks()
+            for pid in sorted(blocks):
+                yield pid, blocks[pid]
+
+    def foreach_block(self, fn: Callable[[int, Block], Any]) -> List[Any]:
+        """Applies fn(pid, block) to every local partition, streaming (an action)."""
+        return [fn(pid, b) for pid, b in self._iter_blocks()]
+
     def cache(self) -> "DataFrame":
         self._persist = True
         return self
@@ -153,9 +186,7 @@ class DataFrame:
     def _local_rows(self) -> List[tuple]:
         out = []
         names = self._schema.names
-        blocks = self._blocks()  # evaluate once: a derived frame recomputes per call
-        for pid in sorted(blocks):
-            b = blocks[pid]
+        for pid, b in self._iter_blocks():  # evaluated once, partition by partition
             cols = [column_values(b.columns[n]) for n in names]
             out.append((pid, [Row.from_fields(names, vals) for vals in zip(*cols)] if cols else
                         [Row.from_fields([], []) for _ in range(b.nrows)]))
@@ -169,7 +200,7 @@ class DataFrame:
         return [r for _, rows in parts for r in rows]
 
     def count(self) -> int:
-        n = sum(b.nrows for b in self._blocks().values())
+        n = sum(b.nrows for _, b in self._iter_blocks())
         return sum(dist.all_gather_object(n))
 
     def first(self) -> Optional[Row]:
@@ -240,7 +271,7 @@ class DataFrame:
             allb.sort(key=lambda x: x[0])
             full = concat_blocks([b for _, b in allb], names)
             return {p: full.slice(*_bounds(full.nrows, n, p)) for p in dist.local_partitions(n)}
-        return DataFrame(self._schema, _Derived(self, fn), n)
+        return DataFrame(self._schema, _Derived(self, fn, streamable=False), n)
 
     def coalesce(self, n: int) -> "DataFrame":
         return self.repartition(min(n, self._nparts))

@@ -204,11 +204,26 @@ class Graph:
     def serialize(self) -> bytes:
         return P.serialize_graphdef(self.as_graph_def())
 
+    def _shape_view(self) -> bytes:
+        """The graph for shape inference only: large constants are replaced by
+        placeholders of the same dtype/shape (their values never decide a
+        shape), so inference does not re-serialize megabytes of weights."""
+        nodes = []
+        for n in self._nodes:
+            if n.op == "Const" and "value" in n.attr:
+                t = n.attr["value"].value
+                numel = int(np.prod(t.shape)) if t.shape else 1
+                if numel > 1024:
+                    n = P.NodeDef(n.name, "Placeholder", [], {"dtype": P.AttrValue.type(t.dtype),
+                                                               "shape": P.AttrValue.shape(t.shape)})
+            nodes.append(n)
+        return P.serialize_graphdef(P.GraphDef(nodes))
+
     def _inferred(self) -> Dict[str, Any]:
         n = len(self._nodes)
         if self._infer_cache[0] != n:
             from .._native import _C
-            res = _C.infer_all(self.serialize())
+            res = _C.infer_all(self._shape_view())
             self._infer_cache = (n, res)
         return self._infer_cache[1]
 
@@ -250,6 +265,13 @@ def name_scope(name: str):
 
 # reference-DSL spellings (reference: src/main/scala/org/tensorframes/dsl/package.scala:31-35)
 scope = name_scope
+
+
+@contextlib.contextmanager
+def variable_scope(name_or_scope, default_name=None, reuse=None):
+    """Graphs here are frozen (no variables), so a variable scope is a name scope."""
+    with name_scope(name_or_scope or default_name) as s:
+        yield s
 
 
 @contextlib.contextmanager
@@ -1105,6 +1127,15 @@ class _NN:
                   "data_format": P.AttrValue.s(data_format), "is_training": P.AttrValue.b(is_training)},
                  name, n_out=5, out_dtypes=[x.dtype] * 5, dtype_hint=x.dtype)
         return op.outputs[0], op.outputs[1], op.outputs[2]
+
+    @staticmethod
+    def l2_normalize(x, axis=None, epsilon=1e-12, name=None, dim=None):
+        ax = axis if axis is not None else dim
+        with name_scope(name or "l2_normalize"):
+            x = convert_to_tensor(x)
+            sq = reduce_sum(square(x), ax, keep_dims=True)
+            inv = rsqrt(maximum(sq, np.asarray(epsilon, dtype=x.dtype.as_numpy_dtype)))
+            return multiply(x, inv, name=None)
 
     @staticmethod
     def top_k(input, k=1, sorted=True, name=None):  # noqa: A002
