@@ -63,7 +63,7 @@ def main():
     torch.cuda.set_device(dev)
 
     nparts = world * args.parts_per_gpu
-    schema = StructType([StructField("x", ArrayType(FloatType(), False), False)])
+    schema = StructType([tfs.tensor_field("x", tf.float32, [DIM])])
 
     # ---- synthetic data, generated on the GPU and staged into pinned host memory (untimed)
     from tensorframes_amd._native import _C

@@ -58,8 +58,8 @@ def emit(d):
         print(json.dumps(d))
 
 
-def vec_schema(name="x"):
-    return StructType([StructField(name, ArrayType(FloatType(), False), False)])
+def vec_schema(name="x", dim=None):
+    return StructType([tfs.tensor_field(name, tf.float32, [dim])])
 
 
 def gen_frame(rows, dim, nparts, pinned, device=None, name="x"):
@@ -78,7 +78,7 @@ def gen_frame(rows, dim, nparts, pinned, device=None, name="x"):
             src = torch.randn((e - s, dim), device=dev) if dev is not None else torch.randn((e - s, dim))
             host[s:e].copy_(src)
         return Block(b - a, {name: host})
-    return tfs.generate(vec_schema(name), nparts, make).cache()
+    return tfs.generate(vec_schema(name, dim), nparts, make).cache()
 
 
 # ------------------------------------------------------------------ configs
@@ -152,7 +152,7 @@ def cfg_inception(a):
     nparts = max(1, images // batch)
     g, iname, oname = cnn.inception_v3(image_size=size)
     dev = torch.device("cuda", torch.cuda.current_device())
-    schema = StructType([StructField("image", ArrayType(ArrayType(ArrayType(FloatType(), False), False), False), False)])
+    schema = StructType([tfs.tensor_field("image", tf.float32, [size, size, 3])])
 
     def make(p):
         n = ((p + 1) * images) // nparts - (p * images) // nparts

@@ -23,7 +23,7 @@ from .core import (TensorFramesError, aggregate, analyze, analyze_graph, block, 
 from .frame.column_info import (SHAPE_KEY, TYPE_KEY, ColumnInformation, DataFrameInfo, HighDimException,
                                 SparkTFColInfo)
 from .frame.dataframe import (DataFrame, GroupedData, create_dataframe, createDataFrame, from_columns,
-                              generate)
+                              generate, tensor_field)
 from .frame.dataframe import range_ as range  # noqa: A001
 from .frame.types import (ArrayType, BinaryType, DoubleType, FloatType, IntegerType, LongType, Row,
                           StringType, StructField, StructType)

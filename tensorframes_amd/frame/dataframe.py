@@ -465,17 +465,27 @@ createDataFrame = create_dataframe  # noqa: N816
 
 
 def _field_for_array(name: str, arr) -> StructField:
+    """Dense whole-column arrays know their cell shape: record it in the
+    metadata (lead dim unknown), so no `analyze` pass is needed."""
     if isinstance(arr, torch.Tensor):
         tf = D.as_dtype(arr.dtype).enum
-        ndim = arr.dim()
+        shape = tuple(arr.shape)
     else:
         arr = np.asarray(arr)
         if arr.dtype.kind in ("U", "S", "O"):
             return StructField(name, StringType() if arr.dtype.kind != "S" else BinaryType(), False)
         tf = D.as_dtype(arr.dtype).enum
-        ndim = arr.ndim
-    from .types import nested_array, sql_type_for_tf
-    return StructField(name, nested_array(sql_type_for_tf(tf), ndim - 1), False)
+        shape = tuple(arr.shape)
+    return tensor_field(name, tf, shape[1:])
+
+
+def tensor_field(name: str, dtype, cell_shape: Sequence[Optional[int]] = ()) -> StructField:
+    """A tensor column field: nested arrays of a numeric type with the block
+    shape ``[?, *cell_shape]`` in the metadata."""
+    from ..utils.shape import Shape
+    tf = D.as_dtype(dtype).enum
+    dims = [-1] + [-1 if d is None else int(d) for d in cell_shape]
+    return ColumnInformation.struct_field(name, tf, Shape(dims))
 
 
 def from_columns(columns: Dict[str, Any], num_partitions: Optional[int] = None,
