@@ -212,7 +212,7 @@ def main():
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--parts-per-gpu", type=int, default=1)
     ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=512)
     a = ap.parse_args()
     dist.init()
     if torch.cuda.is_available():

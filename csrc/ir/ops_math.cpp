@@ -422,6 +422,11 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
     k::fill(dt_of(out), out.data_ptr(), out.numel(), 0.0, stream_of(c));
     return;
   }
+  at::Tensor work;
+  if (size_t ws = k::gemm_workspace_bytes(dt_of(a), g)) {
+    work = at::empty({static_cast<int64_t>(ws)}, a.options().dtype(at::kByte));
+    g.workspace = work.data_ptr();
+  }
   k::gemm(dt_of(a), g, stream_of(c));
 }
 

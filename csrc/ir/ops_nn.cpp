@@ -117,6 +117,11 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
   a.x = x.data_ptr(); a.w = w.data_ptr(); a.y = out.data_ptr();
   a.bias = bias ? bias->data_ptr() : nullptr;
   a.act = act;
+  at::Tensor work;
+  if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
+    work = at::empty({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
+    a.workspace = work.data_ptr();
+  }
   k::conv2d_nhwc(DType::F32, a, stream_of(c));
 }
 

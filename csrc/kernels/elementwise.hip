@@ -360,17 +360,19 @@ struct CopyDesc {
   int64_t ds[kMaxRank];
 };
 
-template <typename E>
+template <typename E, typename I>
 __global__ __launch_bounds__(256) void strided_copy_kernel(const E* __restrict__ src, E* __restrict__ dst,
-                                                           int64_t n, CopyDesc d) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    int64_t rem = i, so = 0, dof = 0;
+                                                           I n, CopyDesc d) {
+  const I stride = (I)gridDim.x * blockDim.x;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    I rem = i;
+    int64_t so = 0, dof = 0;
     for (int k2 = d.rank - 1; k2 >= 0; --k2) {
-      int64_t q = rem / d.dims[k2];
-      int64_t r = rem - q * d.dims[k2];
-      so += r * d.ss[k2];
-      dof += r * d.ds[k2];
+      const I dim = (I)d.dims[k2];
+      const I q = rem / dim;
+      const I r = rem - q * dim;
+      so += (int64_t)r * d.ss[k2];
+      dof += (int64_t)r * d.ds[k2];
       rem = q;
     }
     dst[dof] = src[so];
@@ -528,24 +530,71 @@ void select(DType dt, const void* cond, const void* a, const void* b, void* out,
   TFA_LAUNCH_CHECK("select");
 }
 
+namespace {
+template <typename E>
+void strided_copy_e(const CopyDesc& d, int64_t n, const void* src, void* dst, hipStream_t s) {
+  if (n < (int64_t(1) << 31))
+    hipLaunchKernelGGL((strided_copy_kernel<E, uint32_t>), dim3(ew_grid(n)), dim3(256), 0, s, (const E*)src, (E*)dst,
+                       (uint32_t)n, d);
+  else
+    hipLaunchKernelGGL((strided_copy_kernel<E, int64_t>), dim3(ew_grid(n)), dim3(256), 0, s, (const E*)src, (E*)dst,
+                       n, d);
+}
+}  // namespace
+
+// Host-side normalisation before the launch: size-1 dims are dropped, dims
+// that are contiguous in BOTH operands are merged, and a unit-stride inner
+// dim is widened to 16-byte elements when sizes/alignment allow (a channel
+// concat of NHWC tensors becomes a rank-2 float4 copy).
 void strided_copy(int64_t elem_size, int rank, const int64_t* dims, const void* src,
                   const int64_t* src_strides, void* dst, const int64_t* dst_strides, hipStream_t s) {
   TFA_CHECK(rank >= 1 && rank <= kMaxRank, "strided_copy: bad rank ", rank);
   CopyDesc d;
-  d.rank = rank;
+  d.rank = 0;
   int64_t n = 1;
   for (int i = 0; i < rank; ++i) {
-    d.dims[i] = dims[i];
-    d.ss[i] = src_strides[i];
-    d.ds[i] = dst_strides[i];
     n *= dims[i];
+    if (dims[i] == 1) continue;
+    if (d.rank > 0 && d.ss[d.rank - 1] == src_strides[i] * dims[i] && d.ds[d.rank - 1] == dst_strides[i] * dims[i]) {
+      d.dims[d.rank - 1] *= dims[i];  // merge into the previous (outer) dim
+      d.ss[d.rank - 1] = src_strides[i];
+      d.ds[d.rank - 1] = dst_strides[i];
+      continue;
+    }
+    d.dims[d.rank] = dims[i];
+    d.ss[d.rank] = src_strides[i];
+    d.ds[d.rank] = dst_strides[i];
+    ++d.rank;
   }
   if (n <= 0) return;
+  if (d.rank == 0) {  // single element
+    d.rank = 1;
+    d.dims[0] = 1;
+    d.ss[0] = d.ds[0] = 1;
+  }
+  // widen a unit-stride inner dim to 16-byte elements
+  const int last = d.rank - 1;
+  if (elem_size < 16 && d.ss[last] == 1 && d.ds[last] == 1) {
+    const int64_t f = 16 / elem_size;
+    bool ok = d.dims[last] % f == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
+              (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+    for (int i = 0; ok && i < last; ++i) ok = d.ss[i] % f == 0 && d.ds[i] % f == 0;
+    if (ok) {
+      d.dims[last] /= f;
+      for (int i = 0; i < last; ++i) {
+        d.ss[i] /= f;
+        d.ds[i] /= f;
+      }
+      strided_copy_e<uint4>(d, n / f, src, dst, s);
+      TFA_LAUNCH_CHECK("strided_copy");
+      return;
+    }
+  }
   switch (elem_size) {
-    case 1: hipLaunchKernelGGL((strided_copy_kernel<uint8_t>), dim3(ew_grid(n)), dim3(256), 0, s, (const uint8_t*)src, (uint8_t*)dst, n, d); break;
-    case 2: hipLaunchKernelGGL((strided_copy_kernel<uint16_t>), dim3(ew_grid(n)), dim3(256), 0, s, (const uint16_t*)src, (uint16_t*)dst, n, d); break;
-    case 4: hipLaunchKernelGGL((strided_copy_kernel<uint32_t>), dim3(ew_grid(n)), dim3(256), 0, s, (const uint32_t*)src, (uint32_t*)dst, n, d); break;
-    case 8: hipLaunchKernelGGL((strided_copy_kernel<uint64_t>), dim3(ew_grid(n)), dim3(256), 0, s, (const uint64_t*)src, (uint64_t*)dst, n, d); break;
+    case 1: strided_copy_e<uint8_t>(d, n, src, dst, s); break;
+    case 2: strided_copy_e<uint16_t>(d, n, src, dst, s); break;
+    case 4: strided_copy_e<uint32_t>(d, n, src, dst, s); break;
+    case 8: strided_copy_e<uint64_t>(d, n, src, dst, s); break;
     default: TFA_CHECK(false, "strided_copy: element size ", elem_size);
   }
   TFA_LAUNCH_CHECK("strided_copy");

@@ -1,19 +1,24 @@
-// MFMA GEMM + implicit-GEMM Conv2D + pooling for gfx950 (CDNA4).
+// f32 MFMA GEMM + implicit-GEMM Conv2D for gfx950 (CDNA4).
 //
-// f32: v_mfma_f32_32x32x2_f32 (exact f32, no xf32 on gfx950). 128x128x16
-//      block tile, 4 waves as 2x2, each wave 64x64 = 2x2 MFMA tiles of 32x32.
-// f64: v_mfma_f64_16x16x4_f64. 64x64x16 block tile, 4 waves as 2x2, each
-//      wave 32x32 = 2x2 MFMA tiles of 16x16 (f64 has its own C/D layout).
-// Both: k-major LDS images (As[k][m], Bs[k][n]) so every MFMA operand read is
-// 32 consecutive floats per half-wave (conflict-free ds_read_b32), two LDS
-// stages with the next tile's global loads issued before the current tile's
-// MFMAs (register-staged pipeline, one barrier per K tile), bias + ReLU fused
-// into the epilogue, XCD-aware bijective block->tile remap so that blocks that
-// share an A row-panel run on one XCD (shared L2).
-// Conv2D (NHWC, filter HWIO) reuses the f32 core with an im2col-on-the-fly A
-// loader: A[m = (n,oh,ow)][k = (kh,kw,c)], B = filter viewed as [KH*KW*C, OC].
+// v_mfma_f32_32x32x2_f32 (exact f32: gfx950 has no xf32). One kernel
+// template over the block tile BMxBN (4 waves arranged WMxWN, each wave
+// owning (BM/WM)x(BN/WN) as 32x32 MFMA tiles) so the tile can follow the
+// problem: 128x128 for the big tall-skinny GEMMs, 128x64 / 64x64 / 128x32
+// for narrow conv layers, split-K for grids that cannot fill 256 CUs.
+//
+//  * k-major LDS images (As[k][m], Bs[k][n]): every MFMA operand read is 32
+//    consecutive floats per half-wave (conflict-free ds_read_b32);
+//  * two LDS stages; the next K tile's global loads are issued before the
+//    current tile's MFMAs (register-staged pipeline, one barrier per tile);
+//  * bias + ReLU/ReLU6 fused into the epilogue (or into the split-K reducer);
+//  * XCD-aware bijective block->tile remap: blocks sharing an A row panel
+//    run on one XCD and share its L2.
+// Conv2D (NHWC, filter HWIO) uses the same core with an im2col-on-the-fly A
+// loader: A[m = (n,oh,ow)][k = (kh,kw,c)], B = filter viewed as [KH*KW*C, OC];
+// 1x1 stride-1 convs are plain GEMMs over x viewed as [N*H*W, C].
 #include <cmath>
 
+#include "gemm_internal.h"
 #include "hip_common.h"
 
 namespace tfa {
@@ -22,19 +27,15 @@ namespace k {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int xcd_remap(int b, int nwg) {
-  // bijective: blocks with equal b % 8 (same XCD under round-robin dispatch)
-  // get a contiguous range of logical tile ids
   const int q = nwg / 8, r = nwg % 8, x = b % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <typename T>
-__device__ __forceinline__ T act_apply(T v, int act) {
-  if (act == 1) return v > T(0) ? v : T(0);
-  if (act == 2) return v > T(0) ? (v < T(6) ? v : T(6)) : T(0);
+__device__ __forceinline__ float act_apply(float v, int act) {
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 2) return v > 0.f ? (v < 6.f ? v : 6.f) : 0.f;
   return v;
 }
 
@@ -44,403 +45,339 @@ struct ConvGeom {
   int H, W, C, KW, OH, OW, sh, sw, dh, dw, pt, pl;
 };
 
-// ============================================================== f32 core
-constexpr int F_BM = 128, F_BN = 128, F_BK = 16, F_PAD = 4;
-constexpr int F_LDS = F_BM + F_PAD;  // == F_BN + F_PAD
+constexpr int BK = 16;
 
-struct F32Regs {
-  float a[2][4];
-  float b[2][4];
-};
-
-template <int AL, bool TB, bool VEC>
-__device__ __forceinline__ void f32_load_tile(F32Regs& R, const float* __restrict__ A,
-                                              const float* __restrict__ B, int64_t lda, int64_t ldb,
-                                              int64_t M, int64_t N, int64_t K, int64_t m0, int64_t n0,
-                                              int64_t k0, int tid, const ConvGeom& cg,
-                                              const int64_t* conv_base, const int* conv_ih,
-                                              const int* conv_iw) {
-  // ---- A tile (BM x BK)
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int idx = tid + 256 * p;
-    if (AL == A_KCONTIG || AL == A_CONV) {
-      const int row = idx >> 2, kq = idx & 3;
-      const int64_t gm = m0 + row, gk = k0 + 4 * kq;
-      if (AL == A_KCONTIG) {
-        const float* src = A + gm * lda + gk;
-        if (VEC && gm < M && gk < K) {
-          float4 v = *reinterpret_cast<const float4*>(src);
-          R.a[p][0] = v.x; R.a[p][1] = v.y; R.a[p][2] = v.z; R.a[p][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) R.a[p][j] = (gm < M && gk + j < K) ? src[j] : 0.f;
-        }
-      } else {
-        // implicit im2col: k = (kh*KW + kw)*C + c
-        if (VEC) {  // C % 4 == 0: the 4 k's share (kh, kw)
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (conv_base[p] >= 0 && gk < K) {
-            const int c = (int)(gk % cg.C);
-            const int t = (int)(gk / cg.C);
-            const int kw = t % cg.KW, kh = t / cg.KW;
-            const int ih = conv_ih[p] + kh * cg.dh, iw = conv_iw[p] + kw * cg.dw;
-            if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
-              v = *reinterpret_cast<const float4*>(A + conv_base[p] + ((int64_t)ih * cg.W + iw) * cg.C + c);
-          }
-          R.a[p][0] = v.x; R.a[p][1] = v.y; R.a[p][2] = v.z; R.a[p][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float v = 0.f;
-            const int64_t kk = gk + j;
-            if (conv_base[p] >= 0 && kk < K) {
-              const int c = (int)(kk % cg.C);
-              const int t = (int)(kk / cg.C);
-              const int kw = t % cg.KW, kh = t / cg.KW;
-              const int ih = conv_ih[p] + kh * cg.dh, iw = conv_iw[p] + kw * cg.dw;
-              if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
-                v = A[conv_base[p] + ((int64_t)ih * cg.W + iw) * cg.C + c];
-            }
-            R.a[p][j] = v;
-          }
-        }
-      }
-    } else {  // A_MCONTIG: A stored [K][M]
-      const int kr = idx >> 5, mq = idx & 31;
-      const int64_t gk = k0 + kr, gm = m0 + 4 * mq;
-      const float* src = A + gk * lda + gm;
-      if (VEC && gk < K && gm + 3 < M) {
-        float4 v = *reinterpret_cast<const float4*>(src);
-        R.a[p][0] = v.x; R.a[p][1] = v.y; R.a[p][2] = v.z; R.a[p][3] = v.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) R.a[p][j] = (gk < K && gm + j < M) ? src[j] : 0.f;
-      }
-    }
-  }
-  // ---- B tile (BK x BN)
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int idx = tid + 256 * p;
-    if (!TB) {  // B stored [K][N]
-      const int kr = idx >> 5, nq = idx & 31;
-      const int64_t gk = k0 + kr, gn = n0 + 4 * nq;
-      const float* src = B + gk * ldb + gn;
-      if (VEC && gk < K && gn + 3 < N) {
-        float4 v = *reinterpret_cast<const float4*>(src);
-        R.b[p][0] = v.x; R.b[p][1] = v.y; R.b[p][2] = v.z; R.b[p][3] = v.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) R.b[p][j] = (gk < K && gn + j < N) ? src[j] : 0.f;
-      }
-    } else {  // B stored [N][K]
-      const int col = idx >> 2, kq = idx & 3;
-      const int64_t gn = n0 + col, gk = k0 + 4 * kq;
-      const float* src = B + gn * ldb + gk;
-      if (VEC && gn < N && gk < K) {
-        float4 v = *reinterpret_cast<const float4*>(src);
-        R.b[p][0] = v.x; R.b[p][1] = v.y; R.b[p][2] = v.z; R.b[p][3] = v.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) R.b[p][j] = (gn < N && gk + j < K) ? src[j] : 0.f;
-      }
-    }
+__device__ __forceinline__ void ld4(float (&r)[4], const float* p, bool vec, bool ok0, bool ok1,
+                                    bool ok2, bool ok3) {
+  if (vec && ok3) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+  } else {
+    r[0] = ok0 ? p[0] : 0.f;
+    r[1] = ok1 ? p[1] : 0.f;
+    r[2] = ok2 ? p[2] : 0.f;
+    r[3] = ok3 ? p[3] : 0.f;
   }
 }
 
-template <int AL, bool TB>
-__device__ __forceinline__ void f32_store_tile(const F32Regs& R, float (*As)[F_LDS], float (*Bs)[F_LDS],
-                                               int tid) {
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int idx = tid + 256 * p;
-    if (AL == A_MCONTIG) {
-      const int kr = idx >> 5, mq = idx & 31;
-      *reinterpret_cast<float4*>(&As[kr][4 * mq]) = make_float4(R.a[p][0], R.a[p][1], R.a[p][2], R.a[p][3]);
-    } else {
-      const int row = idx >> 2, kq = idx & 3;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) As[4 * kq + j][row] = R.a[p][j];
-    }
-    if (!TB) {
-      const int kr = idx >> 5, nq = idx & 31;
-      *reinterpret_cast<float4*>(&Bs[kr][4 * nq]) = make_float4(R.b[p][0], R.b[p][1], R.b[p][2], R.b[p][3]);
-    } else {
-      const int col = idx >> 2, kq = idx & 3;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) Bs[4 * kq + j][col] = R.b[p][j];
-    }
-  }
-}
+template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC>
+__global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
+                                                         int64_t k_per_split) {
+  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves, >= one 32x32 tile each");
+  constexpr int APIECES = BM * BK / 4, BPIECES = BN * BK / 4;  // float4 pieces per tile
+  constexpr int AP = (APIECES + 255) / 256, BP = (BPIECES + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
 
-template <int AL, bool TB, bool VEC>
-__global__ __launch_bounds__(256, 2) void gemm_f32_mfma(GemmArgs g, int tiles_m, int tiles_n,
-                                                        ConvGeom cg) {
-  __shared__ __attribute__((aligned(16))) float As[2][F_BK][F_LDS];
-  __shared__ __attribute__((aligned(16))) float Bs[2][F_BK][F_LDS];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * F_BM;
-  const int64_t n0 = (int64_t)(wg % tiles_n) * F_BN;
-  const int64_t bz = blockIdx.z;
+  const int64_t m0 = (int64_t)(wg / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * BN;
+  const int64_t bz = blockIdx.y;  // batch
   const float* A = static_cast<const float*>(g.A) + bz * g.strideA;
   const float* B = static_cast<const float*>(g.B) + bz * g.strideB;
-  float* C = static_cast<float*>(g.C) + bz * g.strideC;
   const int64_t M = g.M, N = g.N, K = g.K;
+  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = min(K, kbeg + k_per_split);
+  constexpr bool v = VEC;
 
-  // conv: per-piece output pixel -> (image base offset, ih0, iw0)
-  int64_t conv_base[2] = {-1, -1};
-  int conv_ih[2] = {0, 0}, conv_iw[2] = {0, 0};
+  // conv: per A piece, output pixel -> (image base, ih0, iw0)
+  int64_t cbase[AP];
+  int cih[AP], ciw[AP];
   if (AL == A_CONV) {
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < AP; ++p) {
       const int64_t m = m0 + ((tid + 256 * p) >> 2);
+      cbase[p] = -1;
+      cih[p] = ciw[p] = 0;
       if (m < M) {
         const int64_t ow = m % cg.OW;
         const int64_t t = m / cg.OW;
         const int64_t oh = t % cg.OH;
         const int64_t n = t / cg.OH;
-        conv_base[p] = n * (int64_t)cg.H * cg.W * cg.C;
-        conv_ih[p] = (int)(oh * cg.sh - cg.pt);
-        conv_iw[p] = (int)(ow * cg.sw - cg.pl);
+        cbase[p] = n * (int64_t)cg.H * cg.W * cg.C;
+        cih[p] = (int)(oh * cg.sh - cg.pt);
+        ciw[p] = (int)(ow * cg.sw - cg.pl);
       }
     }
   }
 
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int64_t ktiles = (K + F_BK - 1) / F_BK;
-  F32Regs R;
-  f32_load_tile<AL, TB, VEC>(R, A, B, g.lda, g.ldb, M, N, K, m0, n0, 0, tid, cg, conv_base, conv_ih, conv_iw);
-  f32_store_tile<AL, TB>(R, As[0], Bs[0], tid);
-  __syncthreads();
-  int cur = 0;
-  for (int64_t kt = 0; kt < ktiles; ++kt) {
-    const bool has_next = kt + 1 < ktiles;
-    if (has_next)
-      f32_load_tile<AL, TB, VEC>(R, A, B, g.lda, g.ldb, M, N, K, m0, n0, (kt + 1) * F_BK, tid, cg,
-                                 conv_base, conv_ih, conv_iw);
-#pragma unroll
-    for (int kk = 0; kk < F_BK; kk += 2) {
-      const int kr = kk + (lane >> 5);
-      float a0 = As[cur][kr][wm * 64 + (lane & 31)];
-      float a1 = As[cur][kr][wm * 64 + 32 + (lane & 31)];
-      float b0 = Bs[cur][kr][wn * 64 + (lane & 31)];
-      float b1 = Bs[cur][kr][wn * 64 + 32 + (lane & 31)];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (has_next) f32_store_tile<AL, TB>(R, As[cur ^ 1], Bs[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
-  }
-
-  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  const float* bias = static_cast<const float*>(g.bias);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t col = n0 + wn * 64 + j * 32 + (lane & 31);
-    const float bv = (bias && col < N) ? bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < M && col < N) C[row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
-      }
-    }
-  }
-}
-
-// ============================================================== f64 core
-constexpr int D_BM = 64, D_BN = 64, D_BK = 16, D_PAD = 2;
-constexpr int D_LDS = D_BM + D_PAD;
-
-template <bool TA, bool TB>
-__global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) double As[2][D_BK][D_LDS];
-  __shared__ __attribute__((aligned(16))) double Bs[2][D_BK][D_LDS];
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nwg = tiles_m * tiles_n;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * D_BM;
-  const int64_t n0 = (int64_t)(wg % tiles_n) * D_BN;
-  const int64_t bz = blockIdx.z;
-  const double* A = static_cast<const double*>(g.A) + bz * g.strideA;
-  const double* B = static_cast<const double*>(g.B) + bz * g.strideB;
-  double* C = static_cast<double*>(g.C) + bz * g.strideC;
-  const int64_t M = g.M, N = g.N, K = g.K;
-
-  // each thread moves 4 doubles of A and 4 of B per K tile
-  double ra[4], rb[4];
+  float ra[AP][4], rb[BP][4];
   auto load = [&](int64_t k0) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int idx = tid + 256 * p;  // 0..1023
-      if (!TA) {  // A [M][K]: idx -> (row = idx>>4, k = idx&15)
-        const int64_t gm = m0 + (idx >> 4), gk = k0 + (idx & 15);
-        ra[p] = (gm < M && gk < K) ? A[gm * g.lda + gk] : 0.0;
-      } else {  // A [K][M]: idx -> (k = idx>>6, m = idx&63)
-        const int64_t gk = k0 + (idx >> 6), gm = m0 + (idx & 63);
-        ra[p] = (gm < M && gk < K) ? A[gk * g.lda + gm] : 0.0;
+    for (int p = 0; p < AP; ++p) {
+      const int idx = tid + 256 * p;
+      if (idx >= APIECES) break;
+      if (AL == A_MCONTIG) {
+        const int kr = idx / (BM / 4), mq = idx % (BM / 4);
+        const int64_t gk = k0 + kr, gm = m0 + 4 * mq;
+        const bool kk = gk < kend;
+        ld4(ra[p], A + gk * g.lda + gm, v, kk && gm < M, kk && gm + 1 < M, kk && gm + 2 < M, kk && gm + 3 < M);
+      } else {
+        const int row = idx >> 2, kq = idx & 3;
+        const int64_t gm = m0 + row, gk = k0 + 4 * kq;
+        if (AL == A_KCONTIG) {
+          const bool mm = gm < M;
+          ld4(ra[p], A + gm * g.lda + gk, v, mm && gk < kend, mm && gk + 1 < kend, mm && gk + 2 < kend,
+              mm && gk + 3 < kend);
+        } else if (v) {  // conv, C % 4 == 0: the 4 k's share (kh, kw)
+          float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (cbase[p] >= 0 && gk < kend) {
+            const int c = (int)(gk % cg.C);
+            const int t = (int)(gk / cg.C);
+            const int kw = t % cg.KW, kh = t / cg.KW;
+            const int ih = cih[p] + kh * cg.dh, iw = ciw[p] + kw * cg.dw;
+            if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
+              val = *reinterpret_cast<const float4*>(A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + c);
+          }
+          ra[p][0] = val.x; ra[p][1] = val.y; ra[p][2] = val.z; ra[p][3] = val.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float val = 0.f;
+            const int64_t kk = gk + j;
+            if (cbase[p] >= 0 && kk < kend) {
+              const int c = (int)(kk % cg.C);
+              const int t = (int)(kk / cg.C);
+              const int kw = t % cg.KW, kh = t / cg.KW;
+              const int ih = cih[p] + kh * cg.dh, iw = ciw[p] + kw * cg.dw;
+              if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
+                val = A[cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + c];
+            }
+            ra[p][j] = val;
+          }
+        }
       }
+    }
+#pragma unroll
+    for (int p = 0; p < BP; ++p) {
+      const int idx = tid + 256 * p;
+      if (idx >= BPIECES) break;
       if (!TB) {  // B [K][N]
-        const int64_t gk = k0 + (idx >> 6), gn = n0 + (idx & 63);
-        rb[p] = (gn < N && gk < K) ? B[gk * g.ldb + gn] : 0.0;
+        const int kr = idx / (BN / 4), nq = idx % (BN / 4);
+        const int64_t gk = k0 + kr, gn = n0 + 4 * nq;
+        const bool kk = gk < kend;
+        ld4(rb[p], B + gk * g.ldb + gn, v, kk && gn < N, kk && gn + 1 < N, kk && gn + 2 < N, kk && gn + 3 < N);
       } else {  // B [N][K]
-        const int64_t gn = n0 + (idx >> 4), gk = k0 + (idx & 15);
-        rb[p] = (gn < N && gk < K) ? B[gn * g.ldb + gk] : 0.0;
+        const int col = idx >> 2, kq = idx & 3;
+        const int64_t gn = n0 + col, gk = k0 + 4 * kq;
+        const bool nn = gn < N;
+        ld4(rb[p], B + gn * g.ldb + gk, v, nn && gk < kend, nn && gk + 1 < kend, nn && gk + 2 < kend,
+            nn && gk + 3 < kend);
       }
     }
   };
   auto store = [&](int st) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < AP; ++p) {
       const int idx = tid + 256 * p;
-      if (!TA) As[st][idx & 15][idx >> 4] = ra[p];
-      else As[st][idx >> 6][idx & 63] = ra[p];
-      if (!TB) Bs[st][idx >> 6][idx & 63] = rb[p];
-      else Bs[st][idx & 15][idx >> 4] = rb[p];
+      if (idx >= APIECES) break;
+      if (AL == A_MCONTIG) {
+        const int kr = idx / (BM / 4), mq = idx % (BM / 4);
+        *reinterpret_cast<float4*>(&As[st][kr][4 * mq]) = make_float4(ra[p][0], ra[p][1], ra[p][2], ra[p][3]);
+      } else {
+        const int row = idx >> 2, kq = idx & 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) As[st][4 * kq + j][row] = ra[p][j];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < BP; ++p) {
+      const int idx = tid + 256 * p;
+      if (idx >= BPIECES) break;
+      if (!TB) {
+        const int kr = idx / (BN / 4), nq = idx % (BN / 4);
+        *reinterpret_cast<float4*>(&Bs[st][kr][4 * nq]) = make_float4(rb[p][0], rb[p][1], rb[p][2], rb[p][3]);
+      } else {
+        const int col = idx >> 2, kq = idx & 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Bs[st][4 * kq + j][col] = rb[p][j];
+      }
     }
   };
 
-  f64x4 acc[2][2];
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int64_t ktiles = (K + D_BK - 1) / D_BK;
-  load(0);
-  store(0);
+  const int64_t ktiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (ktiles > 0) {
+    load(kbeg);
+    store(0);
+  }
   __syncthreads();
   int cur = 0;
   for (int64_t kt = 0; kt < ktiles; ++kt) {
     const bool has_next = kt + 1 < ktiles;
-    if (has_next) load((kt + 1) * D_BK);
+    if (has_next) load(kbeg + (kt + 1) * BK);
 #pragma unroll
-    for (int kk = 0; kk < D_BK; kk += 4) {
-      const int kr = kk + (lane >> 4);
-      double a0 = As[cur][kr][wm * 32 + (lane & 15)];
-      double a1 = As[cur][kr][wm * 32 + 16 + (lane & 15)];
-      double b0 = Bs[cur][kr][wn * 32 + (lane & 15)];
-      double b1 = Bs[cur][kr][wn * 32 + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    for (int kk = 0; kk < BK; kk += 2) {
+      const int kr = kk + (lane >> 5);
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[cur][kr][wm * (BM / WM) + i * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = Bs[cur][kr][wn * (BN / WN) + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     if (has_next) store(cur ^ 1);
     __syncthreads();
     cur ^= 1;
   }
-  // f64 C/D layout: col = lane&15, row = (lane>>4) + 4*r
-  const double* bias = static_cast<const double*>(g.bias);
+
+  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  float* ws = static_cast<float*>(g.workspace);
+  const float* bias = static_cast<const float*>(g.bias);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t col = n0 + wn * 32 + j * 16 + (lane & 15);
-    const double bv = (bias && col < N) ? bias[col] : 0.0;
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
+    if (col >= N) continue;
+    const float bv = (!ws && bias) ? bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
-        if (row < M && col < N) C[row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= M) continue;
+        if (ws)  // split-K partial slab [split][batch][M][N]
+          ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = acc[i][j][r];
+        else
+          static_cast<float*>(g.C)[bz * g.strideC + row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
       }
     }
   }
 }
 
-// ============================================================== integer GEMM (VALU)
-template <typename T>
-__global__ __launch_bounds__(256) void gemm_int(GemmArgs g) {
-  __shared__ T As[16][17];
-  __shared__ T Bs[16][17];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int64_t row = (int64_t)blockIdx.y * 16 + ty, col = (int64_t)blockIdx.x * 16 + tx;
-  const int64_t bz = blockIdx.z;
-  const T* A = static_cast<const T*>(g.A) + bz * g.strideA;
-  const T* B = static_cast<const T*>(g.B) + bz * g.strideB;
-  T* C = static_cast<T*>(g.C) + bz * g.strideC;
-  int64_t acc = 0;
-  for (int64_t k0 = 0; k0 < g.K; k0 += 16) {
-    const int64_t ka = k0 + tx, kb = k0 + ty;
-    const int64_t arow = (int64_t)blockIdx.y * 16 + ty;
-    const int64_t bcol = (int64_t)blockIdx.x * 16 + tx;
-    As[ty][tx] = (arow < g.M && ka < g.K) ? (g.ta ? A[ka * g.lda + arow] : A[arow * g.lda + ka]) : T(0);
-    Bs[ty][tx] = (bcol < g.N && kb < g.K) ? (g.tb ? B[bcol * g.ldb + kb] : B[kb * g.ldb + bcol]) : T(0);
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) acc += (int64_t)As[ty][kk] * (int64_t)Bs[kk][tx];
-    __syncthreads();
-  }
-  if (row < g.M && col < g.N) {
-    T v = T(acc);
-    if (g.bias) v += static_cast<const T*>(g.bias)[col];
-    C[row * g.ldc + col] = act_apply(v, g.act);
-  }
-}
-
-// ============================================================== pooling (NHWC)
-__global__ __launch_bounds__(256) void pool2d_kernel(PoolArgs a, int64_t n) {
-  const float* x = static_cast<const float*>(a.x);
-  float* y = static_cast<float*>(a.y);
+// split-K combine: fixed summation order over the splits (deterministic)
+__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ ws, float* __restrict__ C,
+                                                     const float* __restrict__ bias, int64_t M, int64_t N,
+                                                     int64_t ldc, int64_t strideC, int64_t batch,
+                                                     int splits, int act) {
+  const int64_t total = batch * M * N;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    int64_t c = i % a.C;
-    int64_t t = i / a.C;
-    int64_t ow = t % a.OW;
-    t /= a.OW;
-    int64_t oh = t % a.OH;
-    int64_t nn = t / a.OH;
-    const int64_t h0 = oh * a.sh - a.pad_t, w0 = ow * a.sw - a.pad_l;
-    float acc = a.is_max ? -INFINITY : 0.f;
-    int cnt = 0;
-    for (int64_t kh = 0; kh < a.KH; ++kh) {
-      const int64_t ih = h0 + kh;
-      if (ih < 0 || ih >= a.H) continue;
-      for (int64_t kw = 0; kw < a.KW; ++kw) {
-        const int64_t iw = w0 + kw;
-        if (iw < 0 || iw >= a.W) continue;
-        const float v = x[((nn * a.H + ih) * a.W + iw) * a.C + c];
-        if (a.is_max) acc = v > acc ? v : acc;
-        else acc += v;
-        ++cnt;
-      }
-    }
-    y[i] = a.is_max ? acc : (cnt ? acc / (float)cnt : 0.f);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += ws[z * total + i];
+    const int64_t col = i % N;
+    const int64_t row = (i / N) % M;
+    const int64_t b = i / (M * N);
+    if (bias) s += bias[col];
+    C[b * strideC + row * ldc + col] = act_apply(s, act);
   }
+}
+
+// ------------------------------------------------------------------ tile choice
+struct F32Plan {
+  int cfg;      // index into the tile table
+  int bm, bn;
+  int splits;
+  int64_t k_per_split;
+};
+
+constexpr int kTiles[5][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32}};
+
+F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  // narrow N picks a narrow tile (a 128-wide tile on N=32 wastes 3/4 of the MFMAs)
+  int cfg = N <= 32 ? 4 : (N <= 64 ? 1 : 0);
+  auto blocks = [&](int c) {
+    return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
+  };
+  // too few blocks to fill 256 CUs twice: shrink the tile
+  if (blocks(cfg) < 512) {
+    if (cfg == 0) cfg = N > 96 ? 2 : 3;
+    else if (cfg == 1) cfg = 3;
+  }
+  F32Plan p{cfg, kTiles[cfg][0], kTiles[cfg][1], 1, K};
+  int64_t nb = blocks(cfg);
+  // still under one block per CU: split K (each split >= 128 deep)
+  if (nb < 256 && K >= 256) {
+    int64_t s = std::min<int64_t>((512 + nb - 1) / nb, K / 128);
+    s = std::max<int64_t>(1, std::min<int64_t>(s, 16));
+    int64_t kps = ((K + s - 1) / s + BK - 1) / BK * BK;
+    p.splits = (int)((K + kps - 1) / kps);
+    p.k_per_split = kps;
+  }
+  return p;
+}
+
+template <int AL, bool TB, bool VEC>
+void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s) {
+  const int64_t tm = (g.M + p.bm - 1) / p.bm, tn = (g.N + p.bn - 1) / p.bn;
+  TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
+  TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");
+  dim3 grid((unsigned)(tm * tn), (unsigned)g.batch, (unsigned)p.splits);
+#define TFA_LAUNCH_TILE(BM_, BN_, WM_, WN_)                                                              \
+  hipLaunchKernelGGL((gemm_f32_tile<BM_, BN_, WM_, WN_, AL, TB, VEC>), grid, dim3(256), 0, s, g, (int)tm, (int)tn, \
+                     cg, p.k_per_split)
+  switch (p.cfg) {
+    case 0: TFA_LAUNCH_TILE(128, 128, 2, 2); break;
+    case 1: TFA_LAUNCH_TILE(128, 64, 2, 2); break;
+    case 2: TFA_LAUNCH_TILE(64, 128, 2, 2); break;
+    case 3: TFA_LAUNCH_TILE(64, 64, 2, 2); break;
+    default: TFA_LAUNCH_TILE(128, 32, 4, 1); break;
+  }
+#undef TFA_LAUNCH_TILE
 }
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-template <int AL, bool TB>
-void launch_f32(const GemmArgs& g, bool vec, const ConvGeom& cg, hipStream_t s) {
-  const int64_t tm = (g.M + F_BM - 1) / F_BM, tn = (g.N + F_BN - 1) / F_BN;
-  TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
-  TFA_CHECK(g.batch <= 65535, "gemm: batch too large");
-  dim3 grid((unsigned)(tm * tn), 1, (unsigned)g.batch);
-  if (vec)
-    hipLaunchKernelGGL((gemm_f32_mfma<AL, TB, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn, cg);
-  else
-    hipLaunchKernelGGL((gemm_f32_mfma<AL, TB, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn, cg);
+void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
+  F32Plan p = plan_f32(g0.M, g0.N, g0.K, g0.batch);
+  GemmArgs g = g0;
+  if (p.splits > 1) {
+    TFA_CHECK(g0.workspace != nullptr, "gemm: split-K needs a workspace (gemm_workspace_bytes)");
+  } else {
+    g.workspace = nullptr;
+  }
+#define TFA_VEC(AL_, TB_) \
+  (vec ? launch_cfg<AL_, TB_, true>(p, g, cg, s) : launch_cfg<AL_, TB_, false>(p, g, cg, s))
+  if (al == A_CONV) TFA_VEC(A_CONV, false);
+  else if (al == A_KCONTIG && !g.tb) TFA_VEC(A_KCONTIG, false);
+  else if (al == A_KCONTIG) TFA_VEC(A_KCONTIG, true);
+  else if (!g.tb) TFA_VEC(A_MCONTIG, false);
+  else TFA_VEC(A_MCONTIG, true);
+#undef TFA_VEC
+  if (p.splits > 1) {
+    int64_t total = g.batch * g.M * g.N;
+    hipLaunchKernelGGL(splitk_reduce, dim3(ew_grid(total)), dim3(256), 0, s, static_cast<const float*>(g.workspace),
+                       static_cast<float*>(g.C), static_cast<const float*>(g.bias), g.M, g.N, g.ldc, g.strideC,
+                       g.batch, p.splits, g.act);
+  }
+}
+
+size_t f32_ws_bytes(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  F32Plan p = plan_f32(M, N, K, batch);
+  return p.splits > 1 ? static_cast<size_t>(p.splits) * batch * M * N * sizeof(float) : 0;
+}
+
+bool conv_is_pointwise(const ConvArgs& a) {
+  return a.KH == 1 && a.KW == 1 && a.sh == 1 && a.sw == 1 && a.pad_t == 0 && a.pad_l == 0 &&
+         a.OH == a.H && a.OW == a.W;
 }
 
 }  // namespace
+
+size_t gemm_workspace_bytes(DType dt, const GemmArgs& g) {
+  if (dt != DType::F32 || g.M <= 0 || g.N <= 0) return 0;
+  return f32_ws_bytes(g.M, g.N, g.K, g.batch);
+}
+
+size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a) {
+  if (dt != DType::F32) return 0;
+  return f32_ws_bytes(a.N * a.OH * a.OW, a.OC, a.KH * a.KW * a.C, 1);
+}
 
 void gemm(DType dt, const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
@@ -450,26 +387,12 @@ void gemm(DType dt, const GemmArgs& g, hipStream_t s) {
     // 16-byte vector loads need 4-float aligned rows on the contiguous side
     bool vec = al16(g.A) && al16(g.B) && g.lda % 4 == 0 && g.ldb % 4 == 0 &&
                (g.batch == 1 || (g.strideA % 4 == 0 && g.strideB % 4 == 0));
-    if (!g.ta) vec = vec && g.K % 4 == 0;
-    if (g.tb) vec = vec && g.K % 4 == 0;
-    ConvGeom cg{};
-    if (!g.ta && !g.tb) launch_f32<A_KCONTIG, false>(g, vec, cg, s);
-    else if (!g.ta && g.tb) launch_f32<A_KCONTIG, true>(g, vec, cg, s);
-    else if (g.ta && !g.tb) launch_f32<A_MCONTIG, false>(g, vec, cg, s);
-    else launch_f32<A_MCONTIG, true>(g, vec, cg, s);
+    if (!g.ta || g.tb) vec = vec && g.K % 4 == 0;
+    run_f32(g, g.ta ? A_MCONTIG : A_KCONTIG, vec, ConvGeom{}, s);
   } else if (dt == DType::F64) {
-    const int64_t tm = (g.M + D_BM - 1) / D_BM, tn = (g.N + D_BN - 1) / D_BN;
-    TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
-    dim3 grid((unsigned)(tm * tn), 1, (unsigned)g.batch);
-    if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<false, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
-    else if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_f64_mfma<false, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
-    else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<true, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
-    else hipLaunchKernelGGL((gemm_f64_mfma<true, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+    gemm_f64_launch(g, s);
   } else if (dt == DType::I32 || dt == DType::I64) {
-    dim3 grid((unsigned)((g.N + 15) / 16), (unsigned)((g.M + 15) / 16), (unsigned)g.batch);
-    TFA_CHECK((g.M + 15) / 16 <= 65535, "int gemm: M too large");
-    if (dt == DType::I32) hipLaunchKernelGGL((gemm_int<int32_t>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_int<int64_t>), grid, dim3(256), 0, s, g);
+    gemm_int_launch(dt, g, s);
   } else {
     TFA_CHECK(false, "gemm: dtype ", dtype_name(dt), " not supported");
   }
@@ -484,29 +407,27 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
   g.M = a.N * a.OH * a.OW;
   g.N = a.OC;
   g.K = a.KH * a.KW * a.C;
-  g.A = a.x; g.lda = 0; g.strideA = 0;
+  g.A = a.x; g.lda = a.C; g.strideA = 0;
   g.B = a.w; g.ldb = a.OC; g.strideB = 0;
   g.C = a.y; g.ldc = a.OC; g.strideC = 0;
   g.ta = false; g.tb = false;
   g.bias = a.bias;
   g.act = a.act;
   g.batch = 1;
-  ConvGeom cg;
-  cg.H = (int)a.H; cg.W = (int)a.W; cg.C = (int)a.C; cg.KW = (int)a.KW;
-  cg.OH = (int)a.OH; cg.OW = (int)a.OW;
-  cg.sh = (int)a.sh; cg.sw = (int)a.sw; cg.dh = (int)a.dh; cg.dw = (int)a.dw;
-  cg.pt = (int)a.pad_t; cg.pl = (int)a.pad_l;
-  bool vec = a.C % 4 == 0 && al16(a.x) && al16(a.w) && a.OC % 4 == 0;
-  launch_f32<A_CONV, false>(g, vec, cg, s);
+  g.workspace = a.workspace;
+  if (conv_is_pointwise(a)) {  // 1x1/s1: x is already the [N*H*W, C] A matrix
+    bool vec = al16(a.x) && al16(a.w) && a.C % 4 == 0 && a.OC % 4 == 0;
+    run_f32(g, A_KCONTIG, vec, ConvGeom{}, s);
+  } else {
+    ConvGeom cg;
+    cg.H = (int)a.H; cg.W = (int)a.W; cg.C = (int)a.C; cg.KW = (int)a.KW;
+    cg.OH = (int)a.OH; cg.OW = (int)a.OW;
+    cg.sh = (int)a.sh; cg.sw = (int)a.sw; cg.dh = (int)a.dh; cg.dw = (int)a.dw;
+    cg.pt = (int)a.pad_t; cg.pl = (int)a.pad_l;
+    bool vec = a.C % 4 == 0 && al16(a.x) && al16(a.w) && a.OC % 4 == 0;
+    run_f32(g, A_CONV, vec, cg, s);
+  }
   TFA_LAUNCH_CHECK("conv2d");
-}
-
-void pool2d_nhwc(DType dt, const PoolArgs& a, hipStream_t s) {
-  TFA_CHECK(dt == DType::F32, "pool2d: f32 only");
-  int64_t n = a.N * a.OH * a.OW * a.C;
-  if (n <= 0) return;
-  hipLaunchKernelGGL(pool2d_kernel, dim3(ew_grid(n)), dim3(256), 0, s, a, n);
-  TFA_LAUNCH_CHECK("pool2d");
 }
 
 }  // namespace k

@@ -1,0 +1,249 @@
+// f64 MFMA GEMM, integer GEMM and NHWC pooling kernels for gfx950.
+//
+// f64: v_mfma_f64_16x16x4_f64. 64x64x16 block tile, 4 waves as 2x2, each
+// wave 32x32 = 2x2 MFMA tiles of 16x16 (f64 has its own C/D layout:
+// col = lane&15, row = (lane>>4) + 4*reg). k-major LDS images, two stages,
+// register-staged prefetch of the next K tile, bias/ReLU epilogue.
+#include <cmath>
+
+#include <type_traits>
+
+#include "gemm_internal.h"
+#include "hip_common.h"
+
+namespace tfa {
+namespace k {
+
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int xcd_remap64(int b, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <typename T>
+__device__ __forceinline__ T act_apply(T v, int act) {
+  if (act == 1) return v > T(0) ? v : T(0);
+  if (act == 2) return v > T(0) ? (v < T(6) ? v : T(6)) : T(0);
+  return v;
+}
+
+constexpr int D_BM = 64, D_BN = 64, D_BK = 16, D_PAD = 2;
+constexpr int D_LDS = D_BM + D_PAD;
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) double As[2][D_BK][D_LDS];
+  __shared__ __attribute__((aligned(16))) double Bs[2][D_BK][D_LDS];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = tiles_m * tiles_n;
+  const int wg = xcd_remap64(blockIdx.x, nwg);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * D_BM;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * D_BN;
+  const int64_t bz = blockIdx.z;
+  const double* A = static_cast<const double*>(g.A) + bz * g.strideA;
+  const double* B = static_cast<const double*>(g.B) + bz * g.strideB;
+  double* C = static_cast<double*>(g.C) + bz * g.strideC;
+  const int64_t M = g.M, N = g.N, K = g.K;
+
+  // each thread moves 4 doubles of A and 4 of B per K tile
+  double ra[4], rb[4];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int idx = tid + 256 * p;  // 0..1023
+      if (!TA) {  // A [M][K]: idx -> (row = idx>>4, k = idx&15)
+        const int64_t gm = m0 + (idx >> 4), gk = k0 + (idx & 15);
+        ra[p] = (gm < M && gk < K) ? A[gm * g.lda + gk] : 0.0;
+      } else {  // A [K][M]: idx -> (k = idx>>6, m = idx&63)
+        const int64_t gk = k0 + (idx >> 6), gm = m0 + (idx & 63);
+        ra[p] = (gm < M && gk < K) ? A[gk * g.lda + gm] : 0.0;
+      }
+      if (!TB) {  // B [K][N]
+        const int64_t gk = k0 + (idx >> 6), gn = n0 + (idx & 63);
+        rb[p] = (gn < N && gk < K) ? B[gk * g.ldb + gn] : 0.0;
+      } else {  // B [N][K]
+        const int64_t gn = n0 + (idx >> 4), gk = k0 + (idx & 15);
+        rb[p] = (gn < N && gk < K) ? B[gn * g.ldb + gk] : 0.0;
+      }
+    }
+  };
+  auto store = [&](int st) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int idx = tid + 256 * p;
+      if (!TA) As[st][idx & 15][idx >> 4] = ra[p];
+      else As[st][idx >> 6][idx & 63] = ra[p];
+      if (!TB) Bs[st][idx >> 6][idx & 63] = rb[p];
+      else Bs[st][idx & 15][idx >> 4] = rb[p];
+    }
+  };
+
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
+
+  const int64_t ktiles = (K + D_BK - 1) / D_BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int64_t kt = 0; kt < ktiles; ++kt) {
+    const bool has_next = kt + 1 < ktiles;
+    if (has_next) load((kt + 1) * D_BK);
+#pragma unroll
+    for (int kk = 0; kk < D_BK; kk += 4) {
+      const int kr = kk + (lane >> 4);
+      double a0 = As[cur][kr][wm * 32 + (lane & 15)];
+      double a1 = As[cur][kr][wm * 32 + 16 + (lane & 15)];
+      double b0 = Bs[cur][kr][wn * 32 + (lane & 15)];
+      double b1 = Bs[cur][kr][wn * 32 + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (has_next) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // f64 C/D layout: col = lane&15, row = (lane>>4) + 4*r
+  const double* bias = static_cast<const double*>(g.bias);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t col = n0 + wn * 32 + j * 16 + (lane & 15);
+    const double bv = (bias && col < N) ? bias[col] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
+        if (row < M && col < N) C[row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
+      }
+    }
+  }
+}
+
+// ============================================================== integer GEMM (VALU)
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_int(GemmArgs g) {
+  __shared__ T As[16][17];
+  __shared__ T Bs[16][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int64_t row = (int64_t)blockIdx.y * 16 + ty, col = (int64_t)blockIdx.x * 16 + tx;
+  const int64_t bz = blockIdx.z;
+  const T* A = static_cast<const T*>(g.A) + bz * g.strideA;
+  const T* B = static_cast<const T*>(g.B) + bz * g.strideB;
+  T* C = static_cast<T*>(g.C) + bz * g.strideC;
+  int64_t acc = 0;
+  for (int64_t k0 = 0; k0 < g.K; k0 += 16) {
+    const int64_t ka = k0 + tx, kb = k0 + ty;
+    const int64_t arow = (int64_t)blockIdx.y * 16 + ty;
+    const int64_t bcol = (int64_t)blockIdx.x * 16 + tx;
+    As[ty][tx] = (arow < g.M && ka < g.K) ? (g.ta ? A[ka * g.lda + arow] : A[arow * g.lda + ka]) : T(0);
+    Bs[ty][tx] = (bcol < g.N && kb < g.K) ? (g.tb ? B[bcol * g.ldb + kb] : B[kb * g.ldb + bcol]) : T(0);
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) acc += (int64_t)As[ty][kk] * (int64_t)Bs[kk][tx];
+    __syncthreads();
+  }
+  if (row < g.M && col < g.N) {
+    T v = T(acc);
+    if (g.bias) v += static_cast<const T*>(g.bias)[col];
+    C[row * g.ldc + col] = act_apply(v, g.act);
+  }
+}
+
+// ============================================================== pooling (NHWC)
+// One thread per V consecutive channels of one output pixel (V = 4: float4
+// loads/stores when C % 4 == 0). Index math is 32-bit when the tensors fit
+// (64-bit div/mod costs ~40 VALU ops on CDNA).
+template <bool MAX, int V, typename I>
+__global__ __launch_bounds__(256) void pool2d_kernel(PoolArgs a, I n_items) {
+  using vec_t = typename std::conditional<V == 4, float4, float>::type;
+  const float* x = static_cast<const float*>(a.x);
+  float* y = static_cast<float*>(a.y);
+  const I CV = (I)(a.C / V), OW = (I)a.OW, OH = (I)a.OH, H = (I)a.H, W = (I)a.W;
+  const I stride = (I)gridDim.x * blockDim.x;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
+    const I cv = i % CV;
+    I t = i / CV;
+    const I ow = t % OW;
+    t /= OW;
+    const I oh = t % OH;
+    const I nn = t / OH;
+    const int h0 = (int)(oh * (I)a.sh) - (int)a.pad_t, w0 = (int)(ow * (I)a.sw) - (int)a.pad_l;
+    const int hb = h0 < 0 ? 0 : h0, he = min(h0 + (int)a.KH, (int)H);
+    const int wb = w0 < 0 ? 0 : w0, we = min(w0 + (int)a.KW, (int)W);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = MAX ? -INFINITY : 0.f;
+    const float* base = x + (int64_t)nn * H * W * a.C + (int64_t)cv * V;
+    for (int ih = hb; ih < he; ++ih) {
+      for (int iw = wb; iw < we; ++iw) {
+        vec_t v = *reinterpret_cast<const vec_t*>(base + ((int64_t)ih * W + iw) * a.C);
+        const float* f = reinterpret_cast<const float*>(&v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = MAX ? fmaxf(acc[j], f[j]) : acc[j] + f[j];
+      }
+    }
+    const int cnt = (he - hb) * (we - wb);
+    vec_t o;
+    float* of = reinterpret_cast<float*>(&o);
+#pragma unroll
+    for (int j = 0; j < V; ++j) of[j] = MAX ? acc[j] : (cnt > 0 ? acc[j] / (float)cnt : 0.f);
+    *reinterpret_cast<vec_t*>(y + (int64_t)i * V) = o;
+  }
+}
+
+template <bool MAX>
+void pool2d_launch(const PoolArgs& a, hipStream_t s) {
+  const bool v4 = a.C % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
+  const int V = v4 ? 4 : 1;
+  const int64_t items = a.N * a.OH * a.OW * (a.C / V);
+  const bool small = a.N * a.H * a.W * a.C < (int64_t(1) << 31) && a.N * a.OH * a.OW * a.C < (int64_t(1) << 31);
+  const dim3 grid(ew_grid(items)), block(256);
+  if (v4 && small) hipLaunchKernelGGL((pool2d_kernel<MAX, 4, uint32_t>), grid, block, 0, s, a, (uint32_t)items);
+  else if (v4) hipLaunchKernelGGL((pool2d_kernel<MAX, 4, int64_t>), grid, block, 0, s, a, items);
+  else if (small) hipLaunchKernelGGL((pool2d_kernel<MAX, 1, uint32_t>), grid, block, 0, s, a, (uint32_t)items);
+  else hipLaunchKernelGGL((pool2d_kernel<MAX, 1, int64_t>), grid, block, 0, s, a, items);
+}
+
+}  // namespace
+
+void gemm_f64_launch(const GemmArgs& g, hipStream_t s) {
+  const int64_t tm = (g.M + D_BM - 1) / D_BM, tn = (g.N + D_BN - 1) / D_BN;
+  TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
+  TFA_CHECK(g.batch <= 65535, "gemm: batch too large");
+  dim3 grid((unsigned)(tm * tn), 1, (unsigned)g.batch);
+  if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<false, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+  else if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_f64_mfma<false, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<true, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+  else hipLaunchKernelGGL((gemm_f64_mfma<true, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+}
+
+void gemm_int_launch(DType dt, const GemmArgs& g, hipStream_t s) {
+  dim3 grid((unsigned)((g.N + 15) / 16), (unsigned)((g.M + 15) / 16), (unsigned)g.batch);
+  TFA_CHECK((g.M + 15) / 16 <= 65535, "int gemm: M too large");
+  if (dt == DType::I32) hipLaunchKernelGGL((gemm_int<int32_t>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_int<int64_t>), grid, dim3(256), 0, s, g);
+}
+
+void pool2d_nhwc(DType dt, const PoolArgs& a, hipStream_t s) {
+  TFA_CHECK(dt == DType::F32, "pool2d: f32 only");
+  if (a.N * a.OH * a.OW * a.C <= 0) return;
+  TFA_CHECK(a.KH > 0 && a.KW > 0 && a.sh > 0 && a.sw > 0, "pool2d: bad window");
+  if (a.is_max) pool2d_launch<true>(a, s);
+  else pool2d_launch<false>(a, s);
+  TFA_LAUNCH_CHECK("pool2d");
+}
+
+}  // namespace k
+}  // namespace tfa

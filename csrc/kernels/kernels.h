@@ -97,7 +97,10 @@ struct GemmArgs {
   const void* bias;  // nullable, length N
   int act;           // 0 none, 1 relu, 2 relu6
   int64_t batch;
+  void* workspace = nullptr;  // split-K partials (gemm_workspace_bytes)
 };
+// bytes of scratch the launch needs (0 = none); allocate before the launch
+size_t gemm_workspace_bytes(DType dt, const GemmArgs& g);
 void gemm(DType dt, const GemmArgs& g, hipStream_t s);
 
 // ------------------------------------------------------------ conv / pool (NHWC)
@@ -109,7 +112,9 @@ struct ConvArgs {
   int64_t pad_t, pad_l;
   const void* x; const void* w; void* y;
   const void* bias; int act;
+  void* workspace = nullptr;
 };
+size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a);
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s);
 struct PoolArgs {
   int64_t N, H, W, C, OH, OW, KH, KW, sh, sw, pad_t, pad_l;

@@ -29,6 +29,7 @@ for s in $STEPS; do
     benchsmall) run benchsmall 600 python bench.py --steps 3 --warmup 1 --rows 1000000 ;;
     prof) export TMPDIR=/tmp; run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 3 --warmup 1 ${BENCH_ARGS:-} ;;
     probe) run probe 600 python scripts/pcie_probe.py ;;
+    prof_inception) export TMPDIR=/tmp; run prof_inception 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_inc" -o run -- python bench/configs.py inception --rows 1024 --steps 2 --warmup 1 ;;
     cfg_add) run cfg_add 600 python bench/configs.py add ;;
     cfg_reduce) run cfg_reduce 900 python bench/configs.py reduce ${CFG_ARGS:-} ;;
     cfg_inception) run cfg_inception 900 python bench/configs.py inception ${CFG_ARGS:-} ;;

@@ -145,6 +145,45 @@ def test_matmul_f32_mfma(m, n, k, ta, tb):
     assert (got - want).abs().max().item() < tol
 
 
+# one shape per f32 tile config / split-K path of csrc/kernels/gemm.hip plan_f32
+@pytest.mark.parametrize("m,n,k,bias", [
+    (300, 32, 2048, True),     # 128x32 tile + split-K with bias+relu in the reducer
+    (5000, 64, 64, False),     # 128x64 -> 64x64 (too few blocks)
+    (200, 200, 4096, True),    # 64x128 + 16-way split-K
+    (70000, 100, 48, True),    # 128x128, ragged N
+    (33, 1000, 999, False),    # odd K with split-K (scalar loads)
+])
+def test_matmul_f32_tiles_splitk(m, n, k, bias):
+    g = tf.Graph()
+    a_ = rng.uniform(-1, 1, (m, k)).astype(np.float32)
+    b_ = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    c_ = rng.uniform(-1, 1, n).astype(np.float32)
+    with g.as_default():
+        a = tf.placeholder(tf.float32, [None, k], name="a")
+        y = tf.matmul(a, tf.constant(b_))
+        if bias:
+            y = tf.nn.relu(tf.nn.bias_add(y, tf.constant(c_)))
+        tf.identity(y, name="c")
+    got = run(g, ["c"], {"a": a_})[0].double()
+    want = torch.as_tensor(a_).double() @ torch.as_tensor(b_).double()
+    if bias:
+        want = torch.clamp_min(want + torch.as_tensor(c_).double(), 0)
+    assert (got - want).abs().max().item() < 4e-7 * k + 1e-6
+
+
+def test_batch_matmul_splitk():
+    g = tf.Graph()
+    with g.as_default():
+        a = tf.placeholder(tf.float32, [None, 100, 1024], name="a")
+        b = tf.placeholder(tf.float32, [None, 1024, 70], name="b")
+        tf.matmul(a, b, name="c")
+    a_ = rng.uniform(-1, 1, (4, 100, 1024)).astype(np.float32)
+    b_ = rng.uniform(-1, 1, (4, 1024, 70)).astype(np.float32)
+    got = run(g, ["c"], {"a": a_, "b": b_})[0].double()
+    want = torch.as_tensor(a_).double() @ torch.as_tensor(b_).double()
+    assert (got - want).abs().max().item() < 4e-7 * 1024
+
+
 @pytest.mark.parametrize("m,n,k", [(1000, 512, 512), (129, 77, 33), (100000, 10, 100)])
 def test_matmul_f64_mfma(m, n, k):
     g = tf.Graph()
@@ -182,6 +221,9 @@ def test_fused_gemm_bias_relu_identity_asymmetric():
     (1, 17, 17, 128, 1, 7, 64, 1, "SAME"),
     (3, 8, 8, 32, 3, 3, 16, 1, "SAME"),
     (2, 9, 9, 20, 5, 5, 12, 2, "SAME"),
+    (1, 8, 8, 256, 3, 3, 384, 1, "SAME"),   # small M, deep K: split-K conv
+    (2, 13, 11, 20, 1, 1, 50, 1, "SAME"),   # pointwise conv, C % 4 != 0 (scalar GEMM path)
+    (4, 35, 35, 192, 1, 1, 64, 1, "VALID"),  # pointwise conv -> plain GEMM, 128x64 tile
 ])
 def test_conv2d_implicit_gemm(cfg):
     n, h, w_, c, kh, kw, oc, s, pad = cfg
