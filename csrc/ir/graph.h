@@ -77,6 +77,7 @@ struct OpDef {
   // values of these input indices must be known at plan time (axes, shapes...)
   std::vector<int> host_inputs;
   bool stateful = false;
+  bool host_only = false;  // runs in the Python host stage; a program must be cut at it
 };
 
 class OpRegistry {

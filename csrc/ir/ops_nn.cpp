@@ -256,6 +256,106 @@ void register_nn_ops(OpRegistry& r) {
   r.add("MaxPool", make_pool(true));
   r.add("AvgPool", make_pool(false));
 
+  // ---- ResizeBilinear / ResizeNearestNeighbor (images [N,H,W,C], size int32[2])
+  auto make_resize = [](bool bilinear) {
+    OpDef d;
+    d.host_inputs = {1};
+    d.infer = [bilinear](InferCtx& c) {
+      const TensorInfo& x = c.input(0);
+      DType odt = bilinear ? DType::F32 : x.dtype;
+      auto sz = c.ivalue(1);
+      int64_t oh = sz ? (*sz).at(0) : -1, ow = sz ? (*sz).at(1) : -1;
+      if (sz) TFA_CHECK(sz->size() == 2 && oh > 0 && ow > 0, c.node.op, ": size must be 2 positive ints");
+      if (x.shape.unknown_rank) { c.set(0, odt, Shape({-1, oh, ow, -1})); return; }
+      TFA_CHECK(x.shape.rank() == 4, c.node.op, " needs a rank-4 [batch,height,width,channels] input");
+      c.set(0, odt, Shape({x.shape.dims[0], oh, ow, x.shape.dims[3]}));
+    };
+    d.rows = rows_batch;
+    d.compute = [bilinear](ExecCtx& c) {
+      at::Tensor x = c.input(0);
+      auto sz = c.host_ivalue(1);
+      TFA_CHECK(sz.size() == 2 && sz[0] > 0 && sz[1] > 0, c.node.op, ": size must be 2 positive ints");
+      const bool align = c.node.attr_b("align_corners", false);
+      const bool half = c.node.attr_b("half_pixel_centers", false);
+      TFA_CHECK(!(align && half), c.node.op, ": align_corners and half_pixel_centers are exclusive");
+      const int64_t H = x.size(1), W = x.size(2), OH = sz[0], OW = sz[1];
+      auto scale = [&](int64_t in, int64_t out) {
+        return (align && out > 1) ? float(in - 1) / float(out - 1) : float(in) / float(out);
+      };
+      const float sh = scale(H, OH), sw = scale(W, OW);
+      const int mode = align ? 1 : (half ? 2 : 0);
+      if (!c.gpu) {
+        // oracle: same formulas in float on the host
+        auto idx = [&](int64_t out, int64_t in, float s) {
+          at::Tensor d = at::arange(out, at::kFloat);
+          return mode == 2 ? (d + 0.5f) * s - 0.5f : d * s;
+        };
+        at::Tensor fy = idx(OH, H, sh), fx = idx(OW, W, sw);
+        if (!bilinear) {
+          auto pick = [&](const at::Tensor& f, int64_t out, int64_t in, float s) {
+            at::Tensor d = at::arange(out, at::kFloat);
+            at::Tensor v = mode == 1 ? at::round(d * s) : (mode == 2 ? at::floor((d + 0.5f) * s) : at::floor(d * s));
+            return v.to(at::kLong).clamp(0, in - 1);
+          };
+          at::Tensor iy = pick(fy, OH, H, sh), ix = pick(fx, OW, W, sw);
+          c.out[0] = x.index_select(1, iy).index_select(2, ix).contiguous();
+          return;
+        }
+        at::Tensor xf = x.to(at::kFloat);
+        at::Tensor y0 = at::floor(fy).to(at::kLong).clamp_min(0), y1 = at::ceil(fy).to(at::kLong).clamp_max(H - 1);
+        at::Tensor x0 = at::floor(fx).to(at::kLong).clamp_min(0), x1 = at::ceil(fx).to(at::kLong).clamp_max(W - 1);
+        y0 = y0.clamp_max(H - 1);
+        x0 = x0.clamp_max(W - 1);
+        at::Tensor ly = (fy - at::floor(fy)).view({1, OH, 1, 1}), lx = (fx - at::floor(fx)).view({1, 1, OW, 1});
+        at::Tensor top = xf.index_select(1, y0), bot = xf.index_select(1, y1);
+        at::Tensor tl = top.index_select(2, x0), tr = top.index_select(2, x1);
+        at::Tensor bl = bot.index_select(2, x0), br = bot.index_select(2, x1);
+        at::Tensor t = tl + (tr - tl) * lx, b = bl + (br - bl) * lx;
+        c.out[0] = (t + (b - t) * ly).contiguous();
+        return;
+      }
+      at::Tensor xc = materialize(c, x);
+      c.out[0] = c.alloc_out(0);
+      if (!c.out[0].numel()) return;
+      k::ResizeArgs a;
+      a.N = xc.size(0); a.H = H; a.W = W; a.C = xc.size(3); a.OH = OH; a.OW = OW;
+      a.sh = sh; a.sw = sw; a.mode = mode;
+      a.x = xc.data_ptr(); a.y = c.out[0].data_ptr();
+      if (bilinear) k::resize_bilinear(dt_of(xc), a, stream_of(c));
+      else k::resize_nearest(xc.element_size(), a, stream_of(c));
+    };
+    return d;
+  };
+  r.add("ResizeBilinear", make_resize(true));
+  r.add("ResizeNearestNeighbor", make_resize(false));
+
+  // ---- image decoders: host ops. Shapes/dtypes are inferred here so graphs
+  // containing them analyze; the decode itself runs in the Python host stage
+  // (tensorframes_amd/ops/host_ops.py), which feeds the decoded uint8 HWC
+  // tensor in place of the node's output (reference example:
+  // src/main/python/tensorframes_snippets/read_image.py:42,165).
+  auto make_decode = [](const char* op) {
+    OpDef d;
+    d.stateful = true;  // never constant-folded
+    d.host_only = true;
+    d.infer = [](InferCtx& c) {
+      TFA_CHECK(c.input(0).dtype == DType::STRING, c.node.op, ": contents must be a string tensor");
+      int64_t ch = c.node.attr_i("channels", 0);
+      DType odt = DType::U8;
+      if (c.node.op == "DecodePng" || c.node.op == "DecodeImage") {
+        int dt = static_cast<int>(c.node.attr_i("dtype", 4));
+        odt = static_cast<DType>(dt);
+      }
+      c.set(0, odt, Shape({-1, -1, ch > 0 ? ch : -1}));
+    };
+    d.compute = [op](ExecCtx& c) {
+      TFA_CHECK(false, op, " (node '", c.node.name, "') is a host op: it is decoded on the host by the "
+                "map_rows host stage; feed its output or use map_rows with a binary column");
+    };
+    return d;
+  };
+  for (const char* op : {"DecodeJpeg", "DecodePng", "DecodeImage", "DecodeBmp"}) r.add(op, make_decode(op));
+
   // ---- FusedBatchNorm (inference): y = x*s + b with s = scale/sqrt(var+eps)
   auto make_bn = [](int nout) {
     OpDef d;

@@ -315,11 +315,12 @@ void unary_typed(UnOp op, const void* x, void* y, int64_t n, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ cast / fill / range
-template <typename F, typename T>
+// TO_BOOL: BOOL and U8 share uint8_t storage; only a cast to BOOL is `x != 0`
+template <typename F, typename T, bool TO_BOOL = false>
 __global__ __launch_bounds__(256) void cast_kernel(const F* __restrict__ x, T* __restrict__ y, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    if constexpr (std::is_same<T, uint8_t>::value && !std::is_same<F, uint8_t>::value)
+    if constexpr (TO_BOOL)
       y[i] = x[i] != F(0);
     else
       y[i] = static_cast<T>(x[i]);
@@ -471,7 +472,7 @@ static void cast_from(DType to, const void* x, void* y, int64_t n, hipStream_t s
     case DType::F64: hipLaunchKernelGGL((cast_kernel<F, double>), dim3(ew_grid(n)), dim3(256), 0, s, px, (double*)y, n); break;
     case DType::I32: hipLaunchKernelGGL((cast_kernel<F, int32_t>), dim3(ew_grid(n)), dim3(256), 0, s, px, (int32_t*)y, n); break;
     case DType::I64: hipLaunchKernelGGL((cast_kernel<F, int64_t>), dim3(ew_grid(n)), dim3(256), 0, s, px, (int64_t*)y, n); break;
-    case DType::BOOL: hipLaunchKernelGGL((cast_kernel<F, uint8_t>), dim3(ew_grid(n)), dim3(256), 0, s, px, (uint8_t*)y, n); break;
+    case DType::BOOL: hipLaunchKernelGGL((cast_kernel<F, uint8_t, true>), dim3(ew_grid(n)), dim3(256), 0, s, px, (uint8_t*)y, n); break;
     case DType::U8: hipLaunchKernelGGL((cast_kernel<F, uint8_t>), dim3(ew_grid(n)), dim3(256), 0, s, px, (uint8_t*)y, n); break;
     case DType::I8: hipLaunchKernelGGL((cast_kernel<F, int8_t>), dim3(ew_grid(n)), dim3(256), 0, s, px, (int8_t*)y, n); break;
     case DType::I16: hipLaunchKernelGGL((cast_kernel<F, int16_t>), dim3(ew_grid(n)), dim3(256), 0, s, px, (int16_t*)y, n); break;

@@ -107,6 +107,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
     }
   }
 
+  // vec conv: this thread's A k-offset within a tile is fixed (4 * (tid & 3)), so the
+  // k -> (kh, kw, c) split is computed once and advanced by BK per tile (no divides in the loop)
+  int kc = 0, kkw = 0, kkh = 0;
+  if (AL == A_CONV && VEC) {
+    const int64_t k = kbeg + 4 * (tid & 3);
+    kc = (int)(k % cg.C);
+    const int t = (int)(k / cg.C);
+    kkw = t % cg.KW;
+    kkh = t / cg.KW;
+  }
+
   float ra[AP][4], rb[BP][4];
   auto load = [&](int64_t k0) {
 #pragma unroll
@@ -127,13 +138,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
               mm && gk + 3 < kend);
         } else if (v) {  // conv, C % 4 == 0: the 4 k's share (kh, kw)
           float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (cbase[p] >= 0 && gk < kend) {
-            const int c = (int)(gk % cg.C);
-            const int t = (int)(gk / cg.C);
-            const int kw = t % cg.KW, kh = t / cg.KW;
-            const int ih = cih[p] + kh * cg.dh, iw = ciw[p] + kw * cg.dw;
+          if (cbase[p] >= 0 && gk < kend) {  // (kc, kkw, kkh) = decomposition of gk, kept incrementally
+            const int ih = cih[p] + kkh * cg.dh, iw = ciw[p] + kkw * cg.dw;
             if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
-              val = *reinterpret_cast<const float4*>(A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + c);
+              val = *reinterpret_cast<const float4*>(A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + kc);
           }
           ra[p][0] = val.x; ra[p][1] = val.y; ra[p][2] = val.z; ra[p][3] = val.w;
         } else {
@@ -151,6 +159,16 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
             }
             ra[p][j] = val;
           }
+        }
+      }
+    }
+    if (AL == A_CONV && VEC) {
+      kc += BK;
+      while (kc >= cg.C) {
+        kc -= cg.C;
+        if (++kkw == cg.KW) {
+          kkw = 0;
+          ++kkh;
         }
       }
     }

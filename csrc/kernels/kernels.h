@@ -122,6 +122,15 @@ struct PoolArgs {
   const void* x; void* y;
 };
 void pool2d_nhwc(DType dt, const PoolArgs& a, hipStream_t s);
+// image resize, NHWC. mode: 0 legacy (src = dst*scale), 1 align_corners, 2 half_pixel_centers
+struct ResizeArgs {
+  int64_t N, H, W, C, OH, OW;
+  float sh, sw;  // in/out scale per axis
+  int mode;
+  const void* x; void* y;
+};
+void resize_bilinear(DType dt, const ResizeArgs& a, hipStream_t s);  // output f32
+void resize_nearest(int64_t elem_size, const ResizeArgs& a, hipStream_t s);
 // y = x * scale[c] + shift[c] (+relu), channel = last dim
 void channel_affine(DType dt, const void* x, const void* scale, const void* shift, void* y,
                     int64_t n, int64_t C, int act, hipStream_t s);

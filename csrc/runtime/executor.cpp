@@ -124,9 +124,15 @@ Program::Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetch
       if (!in_order.count(f)) extra.push_back(f);
     order_.insert(order_.begin(), extra.begin(), extra.end());
   }
-  // every placeholder reached must be fed
+  // every placeholder reached must be fed; host ops must be cut off (fed) to run
   for (int n : order_) {
     const Node& nd = g_->node(n);
+    if (!cut.count(n) && host_op_error_.empty()) {
+      const OpDef* od = OpRegistry::get().find(nd.op);
+      if (od && od->host_only)
+        host_op_error_ = str_cat(nd.op, " (node '", nd.name, "') is a host op: it is decoded on the host by "
+                                 "the map_rows host stage; feed its output or use map_rows with a binary column");
+    }
     if ((nd.op == "Placeholder" || nd.op == "PlaceholderV2") && !cut.count(n))
       TFA_CHECK(false, "placeholder '", nd.name, "' is needed by the fetches but is not fed");
   }
@@ -425,6 +431,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
 }
 
 std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
+  TFA_CHECK(host_op_error_.empty(), host_op_error_);
   auto p = plan_for(inputs);
   bool gpu = !inputs.empty() && inputs[0].is_cuda();
   void* stream = nullptr;
@@ -441,6 +448,7 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
 void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
                           const std::vector<std::vector<at::Tensor>>& seg_outputs,
                           int64_t chunk_rows, int device, int depth) {
+  TFA_CHECK(host_op_error_.empty(), host_op_error_);
   TFA_CHECK(seg_inputs.size() == seg_outputs.size(), "segments mismatch");
   TFA_CHECK(chunk_rows > 0, "chunk_rows must be > 0");
   depth = std::max(2, std::min(depth, 4));

@@ -66,6 +66,7 @@ class Program {
   std::string describe_plan(const std::vector<at::Tensor>& inputs);
 
  private:
+  std::string host_op_error_;  // set when a host-only op is reachable (analysis ok, running not)
   struct Step;
   struct Plan;
   std::shared_ptr<Plan> plan_for(const std::vector<at::Tensor>& inputs);

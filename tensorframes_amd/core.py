@@ -26,9 +26,10 @@ from .frame.block import (Block, ObjectColumn, RaggedColumn, build_column, colum
                           column_values, concat_blocks, is_dense)
 from .frame.column_info import ColumnInformation, SparkTFColInfo, explain_schema
 from .frame.dataframe import DataFrame, GroupedData, _Derived, _Materialized, _sort_key
-from .frame.types import (NumericType, Row, StructField, StructType, sql_type_for_tf)
+from .frame.types import (BinaryType, NumericType, Row, StringType, StructField, StructType, sql_type_for_tf)
 from .graph import dsl
 from .graph import proto as P
+from .ops import host_ops
 from .parallel import dist
 from .utils import dtypes as D
 from .utils.logging import logger, metrics
@@ -332,8 +333,22 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
     fields = {f.name: f for f in dframe.schema.fields}
     cols = ", ".join(dframe.schema.names)
     feed_dict = dict(feed_dict or {})
+    # image decoders run as a host stage; the program is cut at their outputs
+    host = _host_feeds(spec, feed_dict, fields)
+    host_srcs = {}
+    for hf in host:
+        if hf.column is not None:
+            _check(hf.column in fields, f"Graph input for {hf.op} '{hf.node}' is bound to column "
+                                        f"'{hf.column}', which does not exist. Dataframe columns: {cols}")
+            _check(isinstance(fields[hf.column].dataType, (BinaryType, StringType)),
+                   f"{hf.op} '{hf.node}' needs a binary column, but '{hf.column}' is "
+                   f"{fields[hf.column].dataType.simpleString()}")
+    for n in _host_contents(spec, host):
+        host_srcs[n] = True
     binding = {}
     for inp in inputs:
+        if inp.name in host_srcs:
+            continue
         cname = feed_dict.get(inp.name, inp.name)
         _check(cname in fields, f"Graph input {inp.name} found, but no column to match it. "
                                 f"Dataframe columns: {cols}")
@@ -356,11 +371,11 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
         cell = out.shape if out.shape is not None else Shape()
         out_fields.append(ColumnInformation.struct_field(out.name, st.tf_dtype, cell.prepend(UNKNOWN)))
     out_schema = StructType(out_fields + list(dframe.schema.fields))
-    feed_names = [i.name for i in inputs]
+    feed_names = [i.name for i in inputs if i.name not in host_srcs]
     feed_cols = [binding[n] for n in feed_names]
     ref_of = dict(zip(spec.fetch_names, spec.fetch_refs))
     fetch_refs = [ref_of[o.name] for o in outputs]
-    prog = engine.program(spec.graph_bytes, fetch_refs, feed_names)
+    prog = engine.program(spec.graph_bytes, fetch_refs, feed_names + [hf.node for hf in host])
     out_meta = [(o.name, o.tf_dtype, o.shape) for o in outputs]
 
     def compute(blocks):
@@ -369,9 +384,10 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
             b = blocks[pid]
             per_out: List[List[torch.Tensor]] = [[] for _ in outputs]
             cell_views = [_cells(b.columns[c]) for c in feed_cols]
-            dev = _rows_device(cell_views)
+            host_views = [_decoded_cells(hf, b) for hf in host]
+            dev = _rows_device(cell_views + host_views)
             for i in range(b.nrows):
-                ins = [cv[i] for cv in cell_views]
+                ins = [cv[i] for cv in cell_views] + [hv[i] for hv in host_views]
                 outs = engine.run_program(prog, ins, dev)
                 for j, o in enumerate(outs):
                     per_out[j].append(o.cpu() if o.is_cuda else o)
@@ -384,6 +400,52 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
         return res
 
     return DataFrame(out_schema, _Derived(dframe, compute), dframe.num_partitions)
+
+
+def _host_feeds(spec: GraphSpec, feed_dict: Dict[str, str], fields) -> list:
+    ops = set(engine.native_graph(spec.graph_bytes).node_ops())
+    if not ops.intersection(host_ops.DECODE_OPS):
+        return []
+    try:
+        return host_ops.plan_host_stage(P.parse_graphdef(spec.graph_bytes), spec.fetch_refs, feed_dict, fields)
+    except ValueError as e:
+        raise TensorFramesError(str(e))
+
+
+def _host_contents(spec: GraphSpec, host) -> List[str]:
+    """Names of the nodes feeding the host decoders' `contents`."""
+    if not host:
+        return []
+    g = engine.native_graph(spec.graph_bytes)
+    return [g.node_inputs(hf.node)[0].split(":")[0] for hf in host]
+
+
+class _LazyDecoded:
+    """Per-row decoded images of one block, decoded on a small thread pool
+    (PIL releases the GIL while decoding) ahead of the row loop."""
+
+    def __init__(self, hf, cells):
+        from concurrent.futures import ThreadPoolExecutor
+        self._pool = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
+        self._futs = [self._pool.submit(hf.decode, c) for c in cells]
+
+    def __getitem__(self, i):
+        return torch.from_numpy(self._futs[i].result())
+
+    def __len__(self):
+        return len(self._futs)
+
+    def __del__(self):
+        self._pool.shutdown(wait=False, cancel_futures=True)
+
+
+def _decoded_cells(hf, b: Block):
+    if hf.column is None:
+        t = torch.from_numpy(hf.const_value)
+        return [t] * b.nrows
+    col = b.columns[hf.column]
+    cells = col.values if isinstance(col, ObjectColumn) else list(col)
+    return _LazyDecoded(hf, cells)
 
 
 def _cells(col) -> List[torch.Tensor]:
@@ -399,9 +461,9 @@ def _rows_device(cell_views) -> torch.device:
     dominate); large cells (images, long vectors) run on the GPU."""
     if not engine.gpu_available():
         return torch.device("cpu")
-    if cell_views and cell_views[0] and cell_views[0][0].is_cuda:
+    if cell_views and len(cell_views[0]) and cell_views[0][0].is_cuda:
         return cell_views[0][0].device
-    biggest = max((cv[0].numel() for cv in cell_views if cv), default=0)
+    biggest = max((cv[0].numel() for cv in cell_views if len(cv)), default=0)
     return engine.compute_device() if biggest >= config.map_rows_gpu_min_elems else torch.device("cpu")
 
 

@@ -1147,6 +1147,90 @@ class _NN:
 
 
 nn = _NN()
+
+
+class _Image:
+    """``tf.image``: decoders (host ops, run by the map_rows host stage) and
+    resize / crop / dtype conversion (GPU kernels)."""
+
+    @staticmethod
+    def decode_jpeg(contents, channels=0, name=None):
+        return _op("DecodeJpeg", [("contents", contents)], {"channels": P.AttrValue.i(channels)}, name,
+                   out_dtypes=[uint8], dtype_hint=string).outputs[0]
+
+    @staticmethod
+    def decode_png(contents, channels=0, dtype=uint8, name=None):
+        dt = as_dtype(dtype)
+        return _op("DecodePng", [("contents", contents)], {"channels": P.AttrValue.i(channels),
+                                                    "dtype": P.AttrValue.type(dt)}, name,
+                   out_dtypes=[dt], dtype_hint=string).outputs[0]
+
+    @staticmethod
+    def decode_image(contents, channels=0, dtype=uint8, name=None):
+        dt = as_dtype(dtype)
+        return _op("DecodeImage", [("contents", contents)], {"channels": P.AttrValue.i(channels),
+                                                      "dtype": P.AttrValue.type(dt)}, name,
+                   out_dtypes=[dt], dtype_hint=string).outputs[0]
+
+    @staticmethod
+    def resize_bilinear(images, size, align_corners=False, half_pixel_centers=False, name=None):
+        x = convert_to_tensor(images)
+        return _op("ResizeBilinear", [("images", x), ("size", np.asarray(size, dtype=np.int32))],
+                   {"T": P.AttrValue.type(x.dtype), "align_corners": P.AttrValue.b(align_corners),
+                    "half_pixel_centers": P.AttrValue.b(half_pixel_centers)}, name,
+                   out_dtypes=[float32]).outputs[0]
+
+    @staticmethod
+    def resize_nearest_neighbor(images, size, align_corners=False, half_pixel_centers=False, name=None):
+        x = convert_to_tensor(images)
+        return _op("ResizeNearestNeighbor", [("images", x), ("size", np.asarray(size, dtype=np.int32))],
+                   {"T": P.AttrValue.type(x.dtype), "align_corners": P.AttrValue.b(align_corners),
+                    "half_pixel_centers": P.AttrValue.b(half_pixel_centers)}, name,
+                   out_dtypes=[x.dtype]).outputs[0]
+
+    @staticmethod
+    def resize_images(images, size, method=0, align_corners=False, name=None):
+        """TF-1.x ``resize_images``: 3-D images get a batch dim for the op (method
+        0 = bilinear, 1 = nearest)."""
+        x = convert_to_tensor(images)
+        rank = x.get_shape().ndims
+        with name_scope(name or "resize_images"):
+            if rank == 3:
+                x = expand_dims(x, 0)
+            fn = _Image.resize_bilinear if method == 0 else _Image.resize_nearest_neighbor
+            y = fn(x, size, align_corners=align_corners)
+            if rank == 3:
+                y = squeeze(y, [0])
+            return y
+
+    @staticmethod
+    def central_crop_to(image, height, width, name=None):
+        """Central crop of a [H, W, C] (or [N, H, W, C]) image with static H, W."""
+        x = convert_to_tensor(image)
+        dims = x.get_shape().as_list()
+        h, w = dims[-3], dims[-2]
+        if h is None or w is None:
+            raise ValueError("central_crop_to needs static image height/width (resize first)")
+        oy, ox = (h - height) // 2, (w - width) // 2
+        if len(dims) == 3:
+            return slice(x, [oy, ox, 0], [height, width, -1], name=name)
+        return slice(x, [0, oy, ox, 0], [-1, height, width, -1], name=name)
+
+    @staticmethod
+    def convert_image_dtype(image, dtype, name=None):
+        """uint8 [0,255] -> float [0,1) (and float -> float cast)."""
+        x = convert_to_tensor(image)
+        dt = as_dtype(dtype)
+        if x.dtype == dt:
+            return x
+        with name_scope(name or "convert_image"):
+            y = cast(x, dt)
+            if x.dtype == uint8 and dt.is_floating:
+                y = multiply(y, np.asarray(1.0 / 255.0, dtype=dt.as_numpy_dtype))
+            return y
+
+
+image = _Image()
 math = __import__("types").SimpleNamespace(
     add=add, subtract=subtract, multiply=multiply, divide=truediv, square=square, sqrt=sqrt,
     reduce_sum=reduce_sum, reduce_min=reduce_min, reduce_max=reduce_max, reduce_mean=reduce_mean,

@@ -59,15 +59,17 @@ def _avg_pool(x, k, s, padding="SAME"):
 
 
 def inception_v3(image_size: int = 299, num_classes: int = 1000, width: float = 1.0, seed: int = 0,
-                 input_name: str = "image", output_name: str = "prob", graph: Optional[tf.Graph] = None
-                 ) -> Tuple[tf.Graph, str, str]:
+                 input_name: str = "image", output_name: str = "prob", graph: Optional[tf.Graph] = None,
+                 inputs=None) -> Tuple[tf.Graph, str, str]:
     """Inception-v3 (Szegedy et al. 2015) as a frozen inference GraphDef.
     Global average pooling makes any input >= 75x75 valid (224x224 for the
-    BASELINE config). Returns (graph, input placeholder name, output name)."""
-    g = graph or tf.Graph()
+    BASELINE config). Returns (graph, input placeholder name, output name);
+    `inputs` (a [N,H,W,3] float32 tensor of `graph`) replaces the placeholder."""
+    g = graph or (inputs.graph if inputs is not None else tf.Graph())
     B = _Builder(seed, width)
     with g.as_default():
-        x = tf.placeholder(tf.float32, [None, image_size, image_size, 3], name=input_name)
+        x = inputs if inputs is not None else tf.placeholder(tf.float32, [None, image_size, image_size, 3],
+                                                             name=input_name)
         # stem
         y = B.conv(x, 32, 3, 3, 2, "VALID", "Conv2d_1a_3x3")
         y = B.conv(y, 32, 3, 3, 1, "VALID", "Conv2d_2a_3x3")
@@ -141,14 +143,15 @@ def inception_v3(image_size: int = 299, num_classes: int = 1000, width: float = 
 
 def vgg16(image_size: int = 224, num_classes: int = 1000, width: float = 1.0, fc_width: int = 4096,
           seed: int = 0, input_name: str = "image", output_name: str = "prob",
-          graph: Optional[tf.Graph] = None) -> Tuple[tf.Graph, str, str]:
+          graph: Optional[tf.Graph] = None, inputs=None) -> Tuple[tf.Graph, str, str]:
     """VGG-16 (Simonyan & Zisserman 2014) as a frozen GraphDef (the network of
     the reference's read_image.py)."""
-    g = graph or tf.Graph()
+    g = graph or (inputs.graph if inputs is not None else tf.Graph())
     B = _Builder(seed, width)
     cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
     with g.as_default():
-        x = tf.placeholder(tf.float32, [None, image_size, image_size, 3], name=input_name)
+        x = inputs if inputs is not None else tf.placeholder(tf.float32, [None, image_size, image_size, 3],
+                                                             name=input_name)
         y = x
         i = 0
         for c in cfg:
@@ -172,3 +175,37 @@ def top_k_classes(graph: tf.Graph, output_name: str = "prob", k: int = 5, name: 
         prob = graph.get_tensor_by_name(output_name + ":0")
         vals, idx = tf.nn.top_k(prob, k, name=name)
         return tf.identity(vals, name=name + "_values"), tf.identity(idx, name=name + "_indices")
+
+
+# ImageNet channel means (RGB, 0-255 scale), as in VGG preprocessing
+_RGB_MEANS = np.array([123.68, 116.78, 103.94], np.float32)
+
+
+def jpeg_scoring_graph(model: str = "vgg16", image_size: int = 224, resize_to: Optional[int] = None,
+                       contents=None, k: int = 5, **model_kw) -> tf.Graph:
+    """The reference's image-scoring graph (read_image.py:35-75): JPEG bytes ->
+    ``DecodeJpeg`` (host stage) -> float -> resize -> central crop -> mean
+    subtraction -> batch of one -> CNN -> softmax -> ``top_predictions``
+    (TopKV2). `contents` (bytes) becomes the ``DecodeJpeg/contents`` constant
+    that ``map_rows(..., feed_dict={'DecodeJpeg/contents': <binary column>})``
+    replaces row by row; None makes it a string placeholder of that name.
+    Outputs: ``index`` (int32 [k]) and ``value`` (float32 [k])."""
+    g = tf.Graph()
+    resize_to = resize_to or image_size + 32
+    with g.as_default():
+        if contents is None:
+            with tf.name_scope("DecodeJpeg/"):
+                contents = tf.placeholder(tf.string, [], name="contents")
+        im = tf.image.decode_jpeg(contents, channels=3)
+        x = tf.cast(im, tf.float32)
+        x = tf.image.resize_images(x, [resize_to, resize_to])
+        x = tf.image.central_crop_to(x, image_size, image_size)
+        x = tf.subtract(x, tf.constant(_RGB_MEANS))
+        x = tf.expand_dims(x, 0)
+        build = {"vgg16": vgg16, "inception_v3": inception_v3}[model]
+        build(image_size=image_size, inputs=x, graph=g, **model_kw)
+        prob = g.get_tensor_by_name("prob:0")
+        vals, idx = tf.nn.top_k(tf.squeeze(prob), k, name="top_predictions")
+        tf.identity(idx, name="index")
+        tf.identity(vals, name="value")
+    return g

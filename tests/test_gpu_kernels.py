@@ -267,3 +267,31 @@ def test_native_extension_loaded():
     import sys
     mods = [m for m in sys.modules if m.endswith("tensorframes_amd._C")]
     assert mods, "native extension not loaded"
+
+
+@pytest.mark.parametrize("align,half", [(False, False), (True, False), (False, True)])
+@pytest.mark.parametrize("dtype", [np.uint8, np.float32])
+def test_resize_bilinear_nearest(align, half, dtype):
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.as_dtype(dtype), [None, 37, 29, 3], name="x")
+        tf.image.resize_bilinear(x, [224, 224], align_corners=align, half_pixel_centers=half, name="bl")
+        tf.image.resize_nearest_neighbor(x, [15, 64], align_corners=align, half_pixel_centers=half, name="nn")
+    x_ = (rng.random((3, 37, 29, 3)) * 255).astype(dtype)
+    gpu, cpu = both(g, ["bl", "nn"], {"x": x_})
+    torch.testing.assert_close(gpu[0], cpu[0], rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(gpu[1], cpu[1], rtol=0, atol=0)
+
+
+def test_cast_float_to_uint8_truncates():
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None], name="x")
+        tf.cast(x, tf.uint8, name="u")
+        tf.cast(x, tf.bool, name="b")
+    x_ = np.array([0.0, 1.7, 200.2, 3.0], np.float32)
+    gpu, cpu = both(g, ["u", "b"], {"x": x_})
+    assert gpu[0].tolist() == [0, 1, 200, 3]
+    assert gpu[1].tolist() == [False, True, True, True]
+    for a, b in zip(gpu, cpu):
+        torch.testing.assert_close(a, b)
