@@ -125,6 +125,15 @@ at::Tensor host_tensor_to_at(const HostTensor& t) {
   return out;
 }
 
+at::Tensor host_tensor_view(const HostTensor& t) {
+  auto dims = dims_or_throw(t.shape, "constant");
+  if (t.bytes.empty()) return at::empty(dims, at::TensorOptions().dtype(to_scalar_type(t.dtype)));
+  TFA_CHECK(static_cast<int64_t>(t.bytes.size()) == t.num_elements() * dtype_size(t.dtype),
+            "constant: ", t.bytes.size(), " bytes for ", t.num_elements(), " elements");
+  return at::from_blob(const_cast<uint8_t*>(t.bytes.data()), dims,
+                       at::TensorOptions().dtype(to_scalar_type(t.dtype)));
+}
+
 std::vector<int64_t> to_int_vector(const at::Tensor& t) {
   at::Tensor c = t.to(at::kCPU).to(at::kLong).contiguous().reshape({-1});
   const int64_t* p = c.data_ptr<int64_t>();

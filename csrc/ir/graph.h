@@ -178,6 +178,8 @@ DType from_scalar_type(at::ScalarType s);
 
 // host value helpers
 at::Tensor host_tensor_to_at(const HostTensor& t);
+// zero-copy view of a HostTensor's bytes; valid while the owning Graph lives
+at::Tensor host_tensor_view(const HostTensor& t);
 std::vector<int64_t> to_int_vector(const at::Tensor& t);
 Shape shape_of(const at::Tensor& t);
 std::vector<int64_t> dims_or_throw(const Shape& s, const char* what);

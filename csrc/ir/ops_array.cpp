@@ -233,7 +233,9 @@ void register_array_ops(OpRegistry& r) {
     if (t.dtype == DType::STRING) {
       c.out[0].strings = std::make_shared<std::vector<std::string>>(t.strings);
     } else {
-      at::Tensor v = host_tensor_to_at(t);
+      // borrowed view of the GraphDef's bytes: no copy per plan (weights can be
+      // GBs); anything handed to a caller is copied by Program::device_const
+      at::Tensor v = host_tensor_view(t);
       if (dt != t.dtype) v = v.to(to_scalar_type(dt));
       c.out[0].value = v;
     }

@@ -203,6 +203,7 @@ std::shared_ptr<Program::Plan> Program::plan_for(const std::vector<at::Tensor>& 
   auto it = plans_.find(key);
   if (it != plans_.end()) return it->second;
   auto p = build_plan(inputs);
+  if (plans_.size() >= kMaxPlans) plans_.erase(plans_.begin());  // bounded (e.g. many image sizes)
   plans_[key] = p;
   stats_.plans_built++;
   return p;
@@ -363,15 +364,29 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
 
 at::Tensor Program::device_const(Plan& p, int slot, const at::Device& dev) {
   int di = dev.is_cuda() ? dev.index() : -1;
+  std::lock_guard<std::mutex> lk(const_mu_);
   auto& m = p.dev_consts[di];
   auto it = m.find(slot);
   if (it != m.end()) return it->second;
   TensorRef r{};
   for (auto& cs : p.const_slots)
     if (cs.first == slot) r = cs.second;
+  // graph Const values are the same in every plan: one device copy per program
+  // (plans differ per input shape, e.g. per image size in map_rows; the weights do not)
+  const bool graph_const = g_->node(r.node).op == "Const";
+  auto gkey = std::make_tuple(r.node, r.index, di);
+  if (graph_const) {
+    auto git = graph_consts_.find(gkey);
+    if (git != graph_consts_.end()) {
+      m[slot] = git->second;
+      return git->second;
+    }
+  }
   const at::Tensor& v = *p.infos[r.node][r.index].value;
-  at::Tensor t = dev.is_cuda() ? v.contiguous().to(dev, /*non_blocking=*/false) : v.contiguous();
+  // always a copy: constant values may be views of the GraphDef's bytes
+  at::Tensor t = dev.is_cuda() ? v.contiguous().to(dev, /*non_blocking=*/false) : v.clone();
   m[slot] = t;
+  if (graph_const) graph_consts_[gkey] = t;
   return t;
 }
 

@@ -11,6 +11,7 @@
 #include <ATen/ATen.h>
 
 #include <map>
+#include <tuple>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -80,7 +81,10 @@ class Program {
   std::vector<int> feed_nodes_;
   std::vector<int> order_;
   std::mutex mu_;
+  static constexpr size_t kMaxPlans = 256;
   std::map<std::string, std::shared_ptr<Plan>> plans_;
+  std::mutex const_mu_;
+  std::map<std::tuple<int, int, int>, at::Tensor> graph_consts_;  // (node, output, device) -> tensor
   ExecStats stats_;
 };
 
