@@ -18,7 +18,8 @@ with RCCL collectives across GPUs.
 """
 from . import _native  # noqa: F401  (loads / builds the native extension)
 from .config import Config, config, set_config
-from .core import (TensorFramesError, aggregate, analyze, analyze_graph, block, explain, map_blocks,
+from .core import (InputNotFoundException, InvalidDimensionException, InvalidTypeException,
+                   TensorFramesError, aggregate, analyze, analyze_graph, block, explain, map_blocks,
                    map_rows, print_schema, reduce_blocks, reduce_rows, row)
 from .frame.column_info import (SHAPE_KEY, TYPE_KEY, ColumnInformation, DataFrameInfo, HighDimException,
                                 SparkTFColInfo)
@@ -28,6 +29,7 @@ from .frame.dataframe import range_ as range  # noqa: A001
 from .frame.types import (ArrayType, BinaryType, DoubleType, FloatType, IntegerType, LongType, Row,
                           StringType, StructField, StructType)
 from .graph import dsl as tf  # noqa: F401
+from .operations import Operations, Ops, ShapeDescription, convert_block_to_row, explain_detailed, ops
 from .graph import dsl
 from .parallel import dist
 from .utils.logging import initialize_logging, metrics

@@ -43,9 +43,33 @@ class TensorFramesError(ValueError):
     """Validation error raised before any data is touched."""
 
 
-def _check(cond: bool, msg: str):
+class InputNotFoundException(TensorFramesError):
+    """A graph input has no column to feed it (reference: Operations.scala:7-8)."""
+
+
+class InvalidDimensionException(TensorFramesError):
+    """Column data has a shape the graph does not accept (reference: Operations.scala:10-12)."""
+
+
+class InvalidTypeException(TensorFramesError):
+    """Column dtype differs from the graph's (no autocast; reference: Operations.scala:14-15)."""
+
+
+def _check(cond: bool, msg: str, exc=TensorFramesError):
     if not cond:
-        raise TensorFramesError(msg)
+        raise exc(msg)
+
+
+def _check_input(cond: bool, msg: str):
+    _check(cond, msg, InputNotFoundException)
+
+
+def _check_type(cond: bool, msg: str):
+    _check(cond, msg, InvalidTypeException)
+
+
+def _check_dim(cond: bool, msg: str):
+    _check(cond, msg, InvalidDimensionException)
 
 
 # ------------------------------------------------------------------ graph specs
@@ -221,14 +245,14 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
     binding: Dict[str, str] = {}
     for inp in inputs:
         cname = feed_dict.get(inp.name, inp.name)
-        _check(cname in fields, f"Graph input {inp.name} found, but no column to match it. "
+        _check_input(cname in fields, f"Graph input {inp.name} found, but no column to match it. "
                                 f"Dataframe columns: {cols}")
         f = fields[cname]
         stf = _col_info(f)
-        _check(stf.tf_dtype == inp.tf_dtype,
+        _check_type(stf.tf_dtype == inp.tf_dtype,
                f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data type "
                f"of the column ({sql_type_for_tf(inp.tf_dtype) if inp.tf_dtype in (1, 2, 3, 9) else D.dtype_name(inp.tf_dtype)})")
-        _check(inp.shape is None or stf.shape.check_more_precise_than(inp.shape),
+        _check_dim(inp.shape is None or stf.shape.check_more_precise_than(inp.shape),
                f"The data column '{f.name}' has shape {stf.shape} (not compatible) with shape "
                f"{_shape_str(inp.shape)} requested by the TF graph")
         _check(inp.is_placeholder, f"Invalid type for input node {inp.name}. It has to be a placeholder")
@@ -350,15 +374,15 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
         if inp.name in host_srcs:
             continue
         cname = feed_dict.get(inp.name, inp.name)
-        _check(cname in fields, f"Graph input {inp.name} found, but no column to match it. "
+        _check_input(cname in fields, f"Graph input {inp.name} found, but no column to match it. "
                                 f"Dataframe columns: {cols}")
         f = fields[cname]
         stf = _col_info(f)
-        _check(stf.tf_dtype == inp.tf_dtype,
+        _check_type(stf.tf_dtype == inp.tf_dtype,
                f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data type "
                f"of the column ({D.dtype_name(inp.tf_dtype)})")
         cell = stf.shape.tail()
-        _check(inp.shape is None or cell.check_more_precise_than(inp.shape),
+        _check_dim(inp.shape is None or cell.check_more_precise_than(inp.shape),
                f"The data column '{f.name}' has shape {stf.shape} (not compatible) with shape "
                f"{_shape_str(inp.shape)} requested by the TF graph")
         _check(inp.is_placeholder, f"Invalid type for input node {inp.name}. It has to be a placeholder")
@@ -603,31 +627,31 @@ def _reduce_blocks_schema(schema: StructType, summary: Dict[str, NodeSummary]) -
     inputs = {n: s for n, s in summary.items() if s.is_input}
     out_list = ", ".join(sorted(outputs))
     missing = sorted(set(outputs) - set(fields))
-    _check(not missing, f"Based on the TF graph, some inputs are missing: {', '.join(missing)}. "
+    _check_input(not missing, f"Based on the TF graph, some inputs are missing: {', '.join(missing)}. "
                         f"Dataframe columns: {field_list}; Outputs: {out_list}")
     expected = {o + "_input" for o in outputs}
     extra = sorted(set(inputs) - expected)
     _check(not extra, f"Extra graph inputs have been found: {', '.join(extra)}. Dataframe columns: {field_list}")
     missing_in = sorted(expected - set(inputs))
-    _check(not missing_in, f"Some inputs are missing in the graph: {', '.join(missing_in)}. "
+    _check_input(not missing_in, f"Some inputs are missing in the graph: {', '.join(missing_in)}. "
                            f"Dataframe columns: {field_list}")
     order = [f.name for f in schema.fields if f.name in outputs]
     for name in order:
         f = fields[name]
         stf = _col_info(f)
         out = outputs[name]
-        _check(stf.tf_dtype == out.tf_dtype,
+        _check_type(stf.tf_dtype == out.tf_dtype,
                f"Output '{name}' has type {D.dtype_name(out.tf_dtype)} but the column type is {stf.dataType}")
         cell = stf.shape.tail()
-        _check(out.shape is None or out.shape.check_more_precise_than(cell),
+        _check_dim(out.shape is None or out.shape.check_more_precise_than(cell),
                f"Output '{name}' has shape {_shape_str(out.shape)}, not compatible with the shape of "
                f"field elements {cell}")
         in_stf_shape = cell.prepend(UNKNOWN)
         inp = inputs[name + "_input"]
-        _check(inp.shape is None or in_stf_shape.check_more_precise_than(inp.shape),
+        _check_dim(inp.shape is None or in_stf_shape.check_more_precise_than(inp.shape),
                f"The data column '{name}' has shape {in_stf_shape}, not compatible with shape "
                f"{_shape_str(inp.shape)} requested by the TF graph")
-        _check(stf.tf_dtype == inp.tf_dtype,
+        _check_type(stf.tf_dtype == inp.tf_dtype,
                f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data type "
                f"of the column ({D.dtype_name(inp.tf_dtype)})")
     return order, [n + "_input" for n in order]
@@ -700,23 +724,23 @@ def _reduce_rows_schema(schema: StructType, summary: Dict[str, NodeSummary]) -> 
     _check(not extra_in, f"Extra graph inputs have been found: {', '.join(extra_in)}. "
                          f"Dataframe columns: {field_list}")
     missing_in = sorted(expected - set(inputs))
-    _check(not missing_in, f"Some inputs are missing in th graph: {', '.join(missing_in)}. "
+    _check_input(not missing_in, f"Some inputs are missing in th graph: {', '.join(missing_in)}. "
                            f"Dataframe columns: {field_list}")
     for name, f in fields.items():
         stf = _col_info(f)
         out = outputs[name]
-        _check(stf.tf_dtype == out.tf_dtype,
+        _check_type(stf.tf_dtype == out.tf_dtype,
                f"Output '{name}' has type {D.dtype_name(out.tf_dtype)} but the column type is {stf.dataType}")
         cell = stf.shape.tail()
-        _check(out.shape is None or out.shape.check_more_precise_than(cell),
+        _check_dim(out.shape is None or out.shape.check_more_precise_than(cell),
                f"Output '{name}' has shape {_shape_str(out.shape)}, not compatible with the shapes"
                f"of field elements {cell}")
         for suffix in ("_1", "_2"):
             inp = inputs[name + suffix]
-            _check(inp.shape is None or cell.check_more_precise_than(inp.shape),
+            _check_dim(inp.shape is None or cell.check_more_precise_than(inp.shape),
                    f"The data column '{name}' has shape {stf.shape} (not compatible) with shape "
                    f"{_shape_str(inp.shape)} requested by the TF graph")
-            _check(stf.tf_dtype == inp.tf_dtype,
+            _check_type(stf.tf_dtype == inp.tf_dtype,
                    f"The type of node '{inp.name}' ({stf.dataType}) is not compatible with the data "
                    f"type of the column ({D.dtype_name(inp.tf_dtype)})")
     return [f.name for f in schema.fields]
