@@ -61,6 +61,7 @@ def main():
     assert torch.cuda.is_available(), "bench.py needs a GPU"
     dev = torch.device("cuda", dist.local_rank() % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    numa_cpus = dist.bind_numa(dev.index)  # before any pinned allocation
 
     nparts = world * args.parts_per_gpu
     schema = StructType([tfs.tensor_field("x", tf.float32, [DIM])])
@@ -159,6 +160,7 @@ def main():
             "device_resident_ms_per_step": None if dev_rows_per_s is None else results["device"] / args.steps * 1e3,
             "gemm_tflops_device_resident": None if dev_rows_per_s is None else dev_rows_per_s * 2 * DIM * DIM / 1e12,
             "max_abs_err": err,
+            "rank0_numa_bound_cpus": len(numa_cpus),
         }
         print(json.dumps(out))
     dist.shutdown()

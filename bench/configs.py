@@ -217,6 +217,7 @@ def main():
     dist.init()
     if torch.cuda.is_available():
         torch.cuda.set_device(dist.local_rank() % torch.cuda.device_count())
+        dist.bind_numa()
     {"plumbing": cfg_plumbing, "add": cfg_add, "reduce": cfg_reduce, "inception": cfg_inception,
      "kmeans": cfg_kmeans}[a.config](a)
     dist.shutdown()

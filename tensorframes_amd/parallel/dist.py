@@ -66,6 +66,58 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> bool:
     return dist.get_world_size() > 1
 
 
+def _parse_cpulist(text: str) -> List[int]:
+    cpus: List[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.extend(range(int(a), int(b) + 1))
+        else:
+            cpus.append(int(part))
+    return cpus
+
+
+def gpu_local_cpus(device_index: Optional[int] = None) -> List[int]:
+    """CPUs of the NUMA node closest to the GPU's PCIe root (sysfs
+    ``local_cpulist``); [] when unknown."""
+    import glob
+    if not torch.cuda.is_available():
+        return []
+    idx = torch.cuda.current_device() if device_index is None else device_index
+    p = torch.cuda.get_device_properties(idx)
+    pattern = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.*"
+    for d in sorted(glob.glob(pattern)):
+        try:
+            with open(os.path.join(d, "local_cpulist")) as f:
+                return _parse_cpulist(f.read())
+        except OSError:
+            continue
+    return []
+
+
+def bind_numa(device_index: Optional[int] = None) -> List[int]:
+    """Pin this process to the CPUs local to its GPU, so the page-locked
+    staging buffers it allocates afterwards land on the GPU's NUMA node (one
+    rank per GPU: each rank streams over its own PCIe link from local DRAM).
+    Disabled with TFA_NUMA_BIND=0. Returns the CPU set applied ([] = none)."""
+    if os.environ.get("TFA_NUMA_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+        return []
+    try:
+        local = set(gpu_local_cpus(device_index))
+        allowed = os.sched_getaffinity(0)
+    except Exception:  # noqa: BLE001 - topology is best-effort
+        return []
+    cpus = sorted(local & allowed)
+    if not cpus or set(cpus) == allowed:
+        return []
+    os.sched_setaffinity(0, cpus)
+    if torch.get_num_threads() > len(cpus):
+        torch.set_num_threads(len(cpus))
+    return cpus
+
+
 def _ensure_groups():
     if _state["device_group"] is None:
         _state["device_group"] = dist.group.WORLD

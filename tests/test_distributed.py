@@ -81,3 +81,10 @@ def test_spmd_world(world, tmp_path):
         want = sorted([[k, sum(x for x in xs if str(int(x) % 3) == k)] for k in ("0", "1", "2")])
         assert o["agg"] == want
         assert o["repart"] == xs
+
+
+def test_parse_cpulist_and_bind_numa_noop_without_gpu():
+    from tensorframes_amd.parallel import dist as D
+    assert D._parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert D._parse_cpulist("") == []
+    assert D.bind_numa() == []  # no GPU here: nothing to bind
