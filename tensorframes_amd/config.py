@@ -33,6 +33,10 @@ class Config:
     pinned_min_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_PINNED_MIN_BYTES", 1 << 20, int))
     # map_rows: cells at least this large run on the GPU, smaller ones on the host executor
     map_rows_gpu_min_elems: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_GPU_MIN", 16384, int))
+    # re-runs of a partition task after a runtime (non-validation) failure; 0 = fail fast
+    task_retries: int = dataclasses.field(default_factory=lambda: _env("TFA_TASK_RETRIES", 0, int))
+    # timeout of one collective (RCCL/gloo); a stuck collective aborts the job
+    collective_timeout_s: float = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_TIMEOUT_S", 600.0, float))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 

@@ -32,6 +32,7 @@ from .graph import proto as P
 from .ops import host_ops
 from .parallel import dist
 from .utils import dtypes as D
+from .utils import faults
 from .utils.logging import logger, metrics
 from .utils.shape import UNKNOWN, Shape
 
@@ -317,7 +318,8 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
             outs = engine.run_block_host(prog, ins, False)
             res[pid] = _assemble(b, outs, out_meta, trim)
 
-    return DataFrame(out_schema, _Derived(dframe, compute), dframe.num_partitions)
+    return DataFrame(out_schema, _Derived(dframe, faults.with_retries("map_blocks", compute)),
+                     dframe.num_partitions)
 
 
 def _assemble(b: Block, outs: List[torch.Tensor], out_meta, trim: bool) -> Block:
@@ -423,7 +425,8 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
         metrics.add("map_rows_rows", sum(b.nrows for b in blocks.values()))
         return res
 
-    return DataFrame(out_schema, _Derived(dframe, compute), dframe.num_partitions)
+    return DataFrame(out_schema, _Derived(dframe, faults.with_retries("map_rows", compute)),
+                     dframe.num_partitions)
 
 
 def _host_feeds(spec: GraphSpec, feed_dict: Dict[str, str], fields) -> list:
@@ -594,13 +597,19 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
 
     partials: List[List[torch.Tensor]] = [[] for _ in out_names]
     cols = [n for n in out_names]
-    for pid, b in sorted(dframe.local_blocks().items()):
-        if b.nrows == 0:
-            continue
-        ins = _dense_inputs(b, cols, "reduce_blocks")
-        on_device = all(t.is_cuda for t in ins)
-        outs = engine.run_program(prog, ins, ins[0].device if on_device else None)
-        for j, o in enumerate(outs):
+
+    def task(blocks):
+        res = {}
+        for pid, b in sorted(blocks.items()):
+            if b.nrows == 0:
+                continue
+            ins = _dense_inputs(b, cols, "reduce_blocks")
+            on_device = all(t.is_cuda for t in ins)
+            res[pid] = engine.run_program(prog, ins, ins[0].device if on_device else None)
+        return res
+    per_part = faults.with_retries("reduce_blocks", task)(dframe.local_blocks())
+    for pid in sorted(per_part):
+        for j, o in enumerate(per_part[pid]):
             partials[j].append(o)
 
     if uniform:
@@ -672,24 +681,34 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     results: Dict[str, np.ndarray] = {}
     if monoid is not None:
         partials: Dict[str, List[torch.Tensor]] = {n: [] for n in names}
-        for pid, b in sorted(dframe.local_blocks().items()):
-            if b.nrows == 0:
-                continue
+
+        def task(blocks):
+            res = {}
+            for pid, b in sorted(blocks.items()):
+                if b.nrows == 0:
+                    continue
+                row = {}
+                for n in names:
+                    col = b.columns[n]
+                    if is_dense(col):
+                        row[n] = _monoid_reduce(monoid[n], col)
+                    else:
+                        row[n] = _fold_rows(prog, names, [_cells(b.columns[m]) for m in names])[names.index(n)]
+                res[pid] = row
+            return res
+        per_part = faults.with_retries("reduce_rows", task)(dframe.local_blocks())
+        for pid in sorted(per_part):
             for n in names:
-                col = b.columns[n]
-                if is_dense(col):
-                    partials[n].append(_monoid_reduce(monoid[n], col))
-                else:
-                    partials[n].append(_fold_rows(prog, names, [_cells(b.columns[m]) for m in names])[names.index(n)])
+                partials[n].append(per_part[pid][n])
         for n in names:
             results[n] = _combine_across(partials[n], monoid[n]).cpu().numpy()
         return _unpack(results, spec, summary)
     # generic: sequential fold per partition, then fold the partials
-    partials_rows = []
-    for pid, b in sorted(dframe.local_blocks().items()):
-        if b.nrows == 0:
-            continue
-        partials_rows.append([t.cpu() for t in _fold_rows(prog, names, [_cells(b.columns[n]) for n in names])])
+    def fold_task(blocks):
+        return {pid: [t.cpu() for t in _fold_rows(prog, names, [_cells(b.columns[n]) for n in names])]
+                for pid, b in sorted(blocks.items()) if b.nrows > 0}
+    per_part = faults.with_retries("reduce_rows", fold_task)(dframe.local_blocks())
+    partials_rows = [per_part[pid] for pid in sorted(per_part)]
     allp = [x for chunk in dist.all_gather_object(partials_rows) for x in chunk]
     _check(len(allp) > 0, "Cannot reduce an empty DataFrame")
     acc = allp[0]

@@ -40,11 +40,17 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", str(rank())))
 
 
-def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> bool:
+def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> bool:
     """Initialise the default process group from torchrun's env (idempotent).
 
+    Collectives time out after `Config.collective_timeout_s`; RCCL errors and
+    timeouts abort the communicator instead of hanging (async error handling).
     Returns True when running with world_size > 1.
     """
+    from ..config import config
+    if timeout_s is None:
+        timeout_s = config.collective_timeout_s
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if dist.is_initialized():
         _ensure_groups()
         return dist.get_world_size() > 1
