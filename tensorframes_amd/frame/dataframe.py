@@ -152,6 +152,11 @@ class DataFrame:
         """Applies fn(pid, block) to every local partition, streaming (an action)."""
         return [fn(pid, b) for pid, b in self._iter_blocks()]
 
+    def write_checkpoint(self, path: str) -> str:
+        """Write every partition + the schema under `path` (see frame/checkpoint.py)."""
+        from .checkpoint import write_checkpoint
+        return write_checkpoint(self, path)
+
     def cache(self) -> "DataFrame":
         self._persist = True
         return self

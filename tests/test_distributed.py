@@ -60,6 +60,18 @@ def _worker(rank, world, port, outdir):
         agg = tfs.aggregate(tf.reduce_sum(xi, [0], name="x"), df.select("key", "x").groupBy("key"))
         res["agg"] = sorted([list(r) for r in agg.collect()])
     res["repart"] = [r.x for r in df.repartition(4).select("x").collect()]
+    # checkpoint: every rank writes its own partitions, reads them back
+    ck = os.path.join(outdir, "ck")
+    back = tfs.read_checkpoint(df.write_checkpoint(ck))
+    res["ck_parts"] = sorted(back.local_blocks())
+    res["ck_x"] = [r.x for r in back.collect()]
+    # a fault injected on rank 1 only is retried locally; results stay consistent
+    from tensorframes_amd.utils import faults
+    tfs.set_config(task_retries=1)
+    with faults.inject("map_blocks", rank=1, times=1):
+        with tf.Graph().as_default():
+            x = tf.placeholder(tf.double, shape=[None], name="x")
+            res["retry_z"] = [r.z for r in tfs.map_blocks(tf.add(x, 1.0, name="z"), df.select("x")).collect()]
     with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
         json.dump(res, f)
     dist.shutdown()
@@ -81,6 +93,8 @@ def test_spmd_world(world, tmp_path):
         want = sorted([[k, sum(x for x in xs if str(int(x) % 3) == k)] for k in ("0", "1", "2")])
         assert o["agg"] == want
         assert o["repart"] == xs
+        assert o["ck_parts"] == o["local_parts"] and o["ck_x"] == xs
+        assert o["retry_z"] == [x + 1.0 for x in xs]
 
 
 def test_parse_cpulist_and_bind_numa_noop_without_gpu():
