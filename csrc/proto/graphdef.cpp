@@ -1,9 +1,19 @@
 // Protobuf wire-format codec for the GraphDef subset (see graphdef.h).
 #include "graphdef.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace tfa {
+
+int64_t max_constant_bytes() {
+  static const int64_t cap = [] {
+    const char* e = std::getenv("TFA_MAX_CONST_BYTES");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t(1) << 36);
+  }();
+  return cap;
+}
 
 const char* dtype_name(DType d) {
   switch (d) {
@@ -167,6 +177,7 @@ Shape decode_shape(const std::string& bytes) {
         else
           d.skip(w);
       }
+      TFA_CHECK(size >= -1, "TensorShapeProto: invalid dim size ", size);
       s.dims.push_back(size);
     } else if (field == 3 && wt == 0) {
       s.unknown_rank = r.varint() != 0;
@@ -242,9 +253,18 @@ HostTensor decode_tensor(const std::string& bytes) {
     }
   }
   TFA_CHECK(!t.shape.unknown_rank, "TensorProto with unknown rank");
-  int64_t n = t.shape.num_elements();
-  TFA_CHECK(n >= 0, "TensorProto with unknown dims ", t.shape.str());
+  TFA_CHECK(t.shape.fully_known(), "TensorProto with unknown dims ", t.shape.str());
+  // overflow-checked element count, bounded: a few bytes of typed *_val can
+  // expand (fill rule) to a huge constant, so untrusted input is capped
+  int64_t n = 1;
+  const int64_t cap = max_constant_bytes();
+  for (int64_t d : t.shape.dims) {
+    TFA_CHECK(d == 0 || n <= cap / d, "TensorProto shape ", t.shape.str(), " exceeds the constant size limit (",
+              cap, " bytes; TFA_MAX_CONST_BYTES)");
+    n *= d;
+  }
   if (t.dtype == DType::STRING) {
+    TFA_CHECK(n <= cap / 32, "string TensorProto with ", n, " elements exceeds the constant size limit");
     t.strings.resize(n);
     for (int64_t i = 0; i < n; ++i)
       t.strings[i] = svals.empty() ? std::string() : svals[std::min<int64_t>(i, svals.size() - 1)];
@@ -252,11 +272,12 @@ HostTensor decode_tensor(const std::string& bytes) {
   }
   int64_t es = dtype_size(t.dtype);
   TFA_CHECK(es > 0, "unsupported TensorProto dtype ", static_cast<int>(t.dtype));
+  TFA_CHECK(n <= cap / es, "TensorProto of ", n, " elements exceeds the constant size limit (", cap, " bytes)");
   t.bytes.assign(n * es, 0);
   if (has_content) {
     TFA_CHECK(static_cast<int64_t>(content.size()) == n * es, "tensor_content has ", content.size(),
               " bytes, expected ", n * es, " for shape ", t.shape.str());
-    std::memcpy(t.bytes.data(), content.data(), content.size());
+    if (!content.empty()) std::memcpy(t.bytes.data(), content.data(), content.size());
     return t;
   }
   if (nvals == 0) return t;  // zero-filled

@@ -76,6 +76,8 @@ struct GraphDef {
   int producer = 0;
 };
 
+// upper bound on one decoded constant's bytes (env TFA_MAX_CONST_BYTES, default 64 GiB)
+int64_t max_constant_bytes();
 GraphDef parse_graphdef(const std::string& bytes);
 HostTensor parse_tensor_proto(const std::string& bytes);
 Shape parse_shape_proto(const std::string& bytes);

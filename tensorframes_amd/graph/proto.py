@@ -491,7 +491,21 @@ def _dec_node(b: bytes) -> NodeDef:
     return n
 
 
+class MalformedProtoError(ValueError):
+    """Bytes that do not decode as the expected protobuf message."""
+
+
 def parse_graphdef(b: bytes) -> GraphDef:
+    """Decode GraphDef bytes; malformed input raises MalformedProtoError."""
+    try:
+        return _parse_graphdef(b)
+    except MalformedProtoError:
+        raise
+    except (struct.error, IndexError, KeyError, UnicodeDecodeError, OverflowError, ValueError, TypeError) as e:
+        raise MalformedProtoError(f"malformed GraphDef ({type(e).__name__}: {e})") from None
+
+
+def _parse_graphdef(b: bytes) -> GraphDef:
     r = _R(b)
     g = GraphDef()
     for f, wt in r.fields():
