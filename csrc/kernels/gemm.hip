@@ -17,6 +17,8 @@
 // loader: A[m = (n,oh,ow)][k = (kh,kw,c)], B = filter viewed as [KH*KW*C, OC];
 // 1x1 stride-1 convs are plain GEMMs over x viewed as [N*H*W, C].
 #include <cmath>
+#include <cstdlib>
+#include <type_traits>
 
 #include "gemm_internal.h"
 #include "hip_common.h"
@@ -45,27 +47,29 @@ struct ConvGeom {
   int H, W, C, KW, OH, OW, sh, sw, dh, dw, pt, pl;
 };
 
-constexpr int BK = 16;
+constexpr int kBK = 16;          // k depth of one LDS stage
+constexpr int kSplitAlign = 32;  // split-K boundaries (multiple of kBK)
 
-__device__ __forceinline__ void ld4(float (&r)[4], const float* p, bool vec, bool ok0, bool ok1,
-                                    bool ok2, bool ok3) {
-  if (vec && ok3) {
-    float4 v = *reinterpret_cast<const float4*>(p);
-    r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-  } else {
-    r[0] = ok0 ? p[0] : 0.f;
-    r[1] = ok1 ? p[1] : 0.f;
-    r[2] = ok2 ? p[2] : 0.f;
-    r[3] = ok3 ? p[3] : 0.f;
-  }
+// bounds-checked 4-float load (edge tiles): vector when all 4 are valid
+__device__ __forceinline__ float4 ld4(const float* p, bool vec, bool ok0, bool ok1, bool ok2, bool ok3) {
+  if (vec && ok3) return *reinterpret_cast<const float4*>(p);
+  return make_float4(ok0 ? p[0] : 0.f, ok1 ? p[1] : 0.f, ok2 ? p[2] : 0.f, ok3 ? p[3] : 0.f);
 }
 
-template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC>
+// unchecked 4-float load (interior tiles)
+template <bool VEC>
+__device__ __forceinline__ float4 ld4_fast(const float* p) {
+  if constexpr (VEC) return *reinterpret_cast<const float4*>(p);
+  return make_float4(p[0], p[1], p[2], p[3]);
+}
+
+template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
 __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
                                                          int64_t k_per_split) {
   constexpr int LDA = BM + 4, LDB = BN + 4;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves, >= one 32x32 tile each");
+  constexpr int KQ = BK / 4;  // float4 pieces along k
   constexpr int APIECES = BM * BK / 4, BPIECES = BN * BK / 4;  // float4 pieces per tile
   constexpr int AP = (APIECES + 255) / 256, BP = (BPIECES + 255) / 256;
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
@@ -92,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
   if (AL == A_CONV) {
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
-      const int64_t m = m0 + ((tid + 256 * p) >> 2);
+      const int64_t m = m0 + (tid + 256 * p) / KQ;
       cbase[p] = -1;
       cih[p] = ciw[p] = 0;
       if (m < M) {
@@ -107,44 +111,59 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
     }
   }
 
-  // vec conv: this thread's A k-offset within a tile is fixed (4 * (tid & 3)), so the
+  // vec conv: this thread's A k-offset within a tile is fixed (4 * (tid % KQ)), so the
   // k -> (kh, kw, c) split is computed once and advanced by BK per tile (no divides in the loop)
   int kc = 0, kkw = 0, kkh = 0;
   if (AL == A_CONV && VEC) {
-    const int64_t k = kbeg + 4 * (tid & 3);
+    const int64_t k = kbeg + 4 * (tid % KQ);
     kc = (int)(k % cg.C);
     const int t = (int)(k / cg.C);
     kkw = t % cg.KW;
     kkh = t / cg.KW;
   }
 
-  float ra[AP][4], rb[BP][4];
-  auto load = [&](int64_t k0) {
+  // loaded tiles stay float4 until the LDS store (no register shuffles, so no
+  // early vmcnt wait: the global loads overlap the MFMAs of the current tile)
+  float4 ra[AP], rb[BP];
+  // CHECK=false: the block's tile lies fully inside M, N and its K range, so
+  // loads are unconditional (no exec-mask branches in the hot loop); only
+  // edge blocks take the bounds-checked path
+  auto load = [&](int64_t k0, auto chk) {
+    constexpr bool CHECK = decltype(chk)::value;
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
       const int idx = tid + 256 * p;
-      if (idx >= APIECES) break;
+      if (APIECES % 256 != 0 && idx >= APIECES) break;
       if (AL == A_MCONTIG) {
         const int kr = idx / (BM / 4), mq = idx % (BM / 4);
         const int64_t gk = k0 + kr, gm = m0 + 4 * mq;
-        const bool kk = gk < kend;
-        ld4(ra[p], A + gk * g.lda + gm, v, kk && gm < M, kk && gm + 1 < M, kk && gm + 2 < M, kk && gm + 3 < M);
+        if constexpr (CHECK) {
+          const bool kk = gk < kend;
+          ra[p] = ld4(A + gk * g.lda + gm, v, kk && gm < M, kk && gm + 1 < M, kk && gm + 2 < M, kk && gm + 3 < M);
+        } else {
+          ra[p] = ld4_fast<VEC>(A + gk * g.lda + gm);
+        }
       } else {
-        const int row = idx >> 2, kq = idx & 3;
+        const int row = idx / KQ, kq = idx % KQ;
         const int64_t gm = m0 + row, gk = k0 + 4 * kq;
         if (AL == A_KCONTIG) {
-          const bool mm = gm < M;
-          ld4(ra[p], A + gm * g.lda + gk, v, mm && gk < kend, mm && gk + 1 < kend, mm && gk + 2 < kend,
-              mm && gk + 3 < kend);
-        } else if (v) {  // conv, C % 4 == 0: the 4 k's share (kh, kw)
-          float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (cbase[p] >= 0 && gk < kend) {  // (kc, kkw, kkh) = decomposition of gk, kept incrementally
-            const int ih = cih[p] + kkh * cg.dh, iw = ciw[p] + kkw * cg.dw;
-            if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
-              val = *reinterpret_cast<const float4*>(A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + kc);
+          if constexpr (CHECK) {
+            const bool mm = gm < M;
+            ra[p] = ld4(A + gm * g.lda + gk, v, mm && gk < kend, mm && gk + 1 < kend, mm && gk + 2 < kend,
+                        mm && gk + 3 < kend);
+          } else {
+            ra[p] = ld4_fast<VEC>(A + gm * g.lda + gk);
           }
-          ra[p][0] = val.x; ra[p][1] = val.y; ra[p][2] = val.z; ra[p][3] = val.w;
+        } else if (v) {  // conv, C % 4 == 0: the 4 k's share (kh, kw) = incremental (kc, kkw, kkh)
+          const int ih = cih[p] + kkh * cg.dh, iw = ciw[p] + kkw * cg.dw;
+          const bool inb = cbase[p] >= 0 && (!CHECK || gk < kend) && ih >= 0 && ih < cg.H && iw >= 0 &&
+                           iw < cg.W;
+          // padding taps load a safe address and are zeroed by a select (branch-free)
+          const float* src = inb ? A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + kc : A;
+          const float4 val = *reinterpret_cast<const float4*>(src);
+          ra[p] = make_float4(inb ? val.x : 0.f, inb ? val.y : 0.f, inb ? val.z : 0.f, inb ? val.w : 0.f);
         } else {
+          float sv[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             float val = 0.f;
@@ -157,8 +176,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
               if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
                 val = A[cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + c];
             }
-            ra[p][j] = val;
+            sv[j] = val;
           }
+          ra[p] = make_float4(sv[0], sv[1], sv[2], sv[3]);
         }
       }
     }
@@ -175,18 +195,26 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
 #pragma unroll
     for (int p = 0; p < BP; ++p) {
       const int idx = tid + 256 * p;
-      if (idx >= BPIECES) break;
+      if (BPIECES % 256 != 0 && idx >= BPIECES) break;
       if (!TB) {  // B [K][N]
         const int kr = idx / (BN / 4), nq = idx % (BN / 4);
         const int64_t gk = k0 + kr, gn = n0 + 4 * nq;
-        const bool kk = gk < kend;
-        ld4(rb[p], B + gk * g.ldb + gn, v, kk && gn < N, kk && gn + 1 < N, kk && gn + 2 < N, kk && gn + 3 < N);
+        if constexpr (CHECK) {
+          const bool kk = gk < kend;
+          rb[p] = ld4(B + gk * g.ldb + gn, v, kk && gn < N, kk && gn + 1 < N, kk && gn + 2 < N, kk && gn + 3 < N);
+        } else {
+          rb[p] = ld4_fast<VEC>(B + gk * g.ldb + gn);
+        }
       } else {  // B [N][K]
-        const int col = idx >> 2, kq = idx & 3;
+        const int col = idx / KQ, kq = idx % KQ;
         const int64_t gn = n0 + col, gk = k0 + 4 * kq;
-        const bool nn = gn < N;
-        ld4(rb[p], B + gn * g.ldb + gk, v, nn && gk < kend, nn && gk + 1 < kend, nn && gk + 2 < kend,
-            nn && gk + 3 < kend);
+        if constexpr (CHECK) {
+          const bool nn = gn < N;
+          rb[p] = ld4(B + gn * g.ldb + gk, v, nn && gk < kend, nn && gk + 1 < kend, nn && gk + 2 < kend,
+                      nn && gk + 3 < kend);
+        } else {
+          rb[p] = ld4_fast<VEC>(B + gn * g.ldb + gk);
+        }
       }
     }
   };
@@ -194,27 +222,31 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
       const int idx = tid + 256 * p;
-      if (idx >= APIECES) break;
+      if (APIECES % 256 != 0 && idx >= APIECES) break;
       if (AL == A_MCONTIG) {
         const int kr = idx / (BM / 4), mq = idx % (BM / 4);
-        *reinterpret_cast<float4*>(&As[st][kr][4 * mq]) = make_float4(ra[p][0], ra[p][1], ra[p][2], ra[p][3]);
+        *reinterpret_cast<float4*>(&As[st][kr][4 * mq]) = ra[p];
       } else {
-        const int row = idx >> 2, kq = idx & 3;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) As[st][4 * kq + j][row] = ra[p][j];
+        const int row = idx / KQ, kq = idx % KQ;
+        As[st][4 * kq + 0][row] = ra[p].x;
+        As[st][4 * kq + 1][row] = ra[p].y;
+        As[st][4 * kq + 2][row] = ra[p].z;
+        As[st][4 * kq + 3][row] = ra[p].w;
       }
     }
 #pragma unroll
     for (int p = 0; p < BP; ++p) {
       const int idx = tid + 256 * p;
-      if (idx >= BPIECES) break;
+      if (BPIECES % 256 != 0 && idx >= BPIECES) break;
       if (!TB) {
         const int kr = idx / (BN / 4), nq = idx % (BN / 4);
-        *reinterpret_cast<float4*>(&Bs[st][kr][4 * nq]) = make_float4(rb[p][0], rb[p][1], rb[p][2], rb[p][3]);
+        *reinterpret_cast<float4*>(&Bs[st][kr][4 * nq]) = rb[p];
       } else {
-        const int col = idx >> 2, kq = idx & 3;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Bs[st][4 * kq + j][col] = rb[p][j];
+        const int col = idx / KQ, kq = idx % KQ;
+        Bs[st][4 * kq + 0][col] = rb[p].x;
+        Bs[st][4 * kq + 1][col] = rb[p].y;
+        Bs[st][4 * kq + 2][col] = rb[p].z;
+        Bs[st][4 * kq + 3][col] = rb[p].w;
       }
     }
   };
@@ -227,33 +259,50 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int64_t ktiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if (ktiles > 0) {
-    load(kbeg);
-    store(0);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int64_t kt = 0; kt < ktiles; ++kt) {
-    const bool has_next = kt + 1 < ktiles;
-    if (has_next) load(kbeg + (kt + 1) * BK);
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const int kr = kk + (lane >> 5);
-      float a[TM], b[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[cur][kr][wm * (BM / WM) + i * 32 + (lane & 31)];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[cur][kr][wn * (BN / WN) + j * 32 + (lane & 31)];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+  const int ktiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+  auto mainloop = [&](auto chk) {
+    if (ktiles > 0) {
+      load(kbeg, chk);
+      store(0);
     }
-    if (has_next) store(cur ^ 1);
     __syncthreads();
-    cur ^= 1;
-  }
+    int cur = 0;
+    for (int kt = 0; kt < ktiles; ++kt) {
+      const bool has_next = kt + 1 < ktiles;
+      if (has_next) load(kbeg + (int64_t)(kt + 1) * BK, chk);
+      // LDS operand reads run one k-step ahead of the MFMAs that use them
+      // (software pipelined; sched_barriers keep the compiler from sinking the
+      // reads next to their consumers, which exposed the LDS latency per step)
+      float a[2][TM], b[2][TN];
+      auto rd = [&](int buf, int kk) {
+        const int kr = kk + (lane >> 5);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[buf][i] = As[cur][kr][wm * (BM / WM) + i * 32 + (lane & 31)];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[buf][j] = Bs[cur][kr][wn * (BN / WN) + j * 32 + (lane & 31)];
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        if (kk + 1 < BK / 2) rd((kk + 1) & 1, 2 * (kk + 1));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk & 1][i], b[kk & 1][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (has_next) store(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  };
+  const bool interior = m0 + BM <= M && n0 + BN <= N && (kend - kbeg) % BK == 0;
+  if (interior)
+    mainloop(std::false_type{});
+  else
+    mainloop(std::true_type{});
 
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* ws = static_cast<float*>(g.workspace);
@@ -304,6 +353,7 @@ struct F32Plan {
   int64_t k_per_split;
 };
 
+// measured (scripts/gemm_bench.py): 256x128 / 128x256 and BK=32 variants were slower on every shape
 constexpr int kTiles[5][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32}};
 
 F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
@@ -317,13 +367,18 @@ F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
     if (cfg == 0) cfg = N > 96 ? 2 : 3;
     else if (cfg == 1) cfg = 3;
   }
+  static const int tile_env = [] {
+    const char* e = std::getenv("TFA_GEMM_TILE");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (tile_env >= 0 && tile_env < 5) cfg = tile_env;  // tuning override
   F32Plan p{cfg, kTiles[cfg][0], kTiles[cfg][1], 1, K};
   int64_t nb = blocks(cfg);
   // still under one block per CU: split K (each split >= 128 deep)
   if (nb < 256 && K >= 256) {
     int64_t s = std::min<int64_t>((512 + nb - 1) / nb, K / 128);
     s = std::max<int64_t>(1, std::min<int64_t>(s, 16));
-    int64_t kps = ((K + s - 1) / s + BK - 1) / BK * BK;
+    int64_t kps = ((K + s - 1) / s + kSplitAlign - 1) / kSplitAlign * kSplitAlign;
     p.splits = (int)((K + kps - 1) / kps);
     p.k_per_split = kps;
   }
@@ -336,9 +391,9 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
   TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");
   dim3 grid((unsigned)(tm * tn), (unsigned)g.batch, (unsigned)p.splits);
-#define TFA_LAUNCH_TILE(BM_, BN_, WM_, WN_)                                                              \
-  hipLaunchKernelGGL((gemm_f32_tile<BM_, BN_, WM_, WN_, AL, TB, VEC>), grid, dim3(256), 0, s, g, (int)tm, (int)tn, \
-                     cg, p.k_per_split)
+#define TFA_LAUNCH_TILE(BM_, BN_, WM_, WN_)                                                                  \
+  hipLaunchKernelGGL((gemm_f32_tile<BM_, BN_, WM_, WN_, AL, TB, VEC, kBK>), grid, dim3(256), 0, s, g, (int)tm, \
+                     (int)tn, cg, p.k_per_split)
   switch (p.cfg) {
     case 0: TFA_LAUNCH_TILE(128, 128, 2, 2); break;
     case 1: TFA_LAUNCH_TILE(128, 64, 2, 2); break;

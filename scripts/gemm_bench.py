@@ -1,0 +1,98 @@
+"""Kernel-level GEMM / Conv2D throughput on device-resident tensors (the f32
+MFMA core of csrc/kernels/gemm.hip), timed with HIP events.
+
+    python scripts/gemm_bench.py [--iters N] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tensorframes_amd import engine, tf  # noqa: E402
+
+GEMMS = [  # M, N, K, bias+relu
+    (2_500_000, 512, 512, True),   # headline partition (BASELINE config 3)
+    (262_144, 512, 512, True),
+    (4096, 4096, 4096, False),
+    (8192, 1024, 1024, False),
+    (1_000_000, 64, 256, True),
+    (100_000, 10, 100, False),
+]
+CONVS = [  # N, H, W, C, KH, KW, OC, stride, padding (Inception-v3 @224, batch 512)
+    (512, 111, 111, 32, 3, 3, 32, 1, "VALID"),
+    (512, 109, 109, 32, 3, 3, 64, 1, "SAME"),
+    (512, 25, 25, 192, 1, 1, 64, 1, "SAME"),
+    (512, 25, 25, 48, 5, 5, 64, 1, "SAME"),
+    (512, 25, 25, 64, 3, 3, 96, 1, "SAME"),
+    (512, 12, 12, 768, 1, 1, 192, 1, "SAME"),
+    (512, 12, 12, 128, 1, 7, 128, 1, "SAME"),
+    (512, 12, 12, 160, 7, 1, 192, 1, "SAME"),
+    (512, 5, 5, 1280, 1, 1, 320, 1, "SAME"),
+    (512, 5, 5, 448, 3, 3, 384, 1, "SAME"),
+]
+
+
+def timeit(prog, ins, iters):
+    engine.run_program(prog, ins, ins[0].device)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        engine.run_program(prog, ins, ins[0].device)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(0)
+    res = []
+    for m, n, k, br in GEMMS:
+        g = tf.Graph()
+        with g.as_default():
+            x = tf.placeholder(tf.float32, [None, k], name="x")
+            y = tf.matmul(x, tf.constant(rng.standard_normal((k, n)).astype(np.float32)))
+            if br:
+                y = tf.nn.relu(tf.nn.bias_add(y, tf.constant(rng.standard_normal(n).astype(np.float32))))
+            tf.identity(y, name="y")
+        prog = engine.program(g.serialize(), ["y"], ["x"])
+        xin = torch.randn((m, k), device=dev)
+        ms = timeit(prog, [xin], a.iters)
+        r = {"kind": "gemm", "M": m, "N": n, "K": k, "ms": ms, "tflops": 2 * m * n * k / ms / 1e9}
+        print(json.dumps(r), flush=True)
+        res.append(r)
+        del xin
+    for nb, h, w, c, kh, kw, oc, s, pad in CONVS:
+        g = tf.Graph()
+        with g.as_default():
+            x = tf.placeholder(tf.float32, [None, h, w, c], name="x")
+            f = tf.constant((rng.standard_normal((kh, kw, c, oc)) * 0.05).astype(np.float32))
+            y = tf.nn.conv2d(x, f, [1, s, s, 1], pad)
+            y = tf.nn.relu(tf.nn.bias_add(y, tf.constant(np.zeros(oc, np.float32))), name="y")
+        prog = engine.program(g.serialize(), ["y"], ["x"])
+        xin = torch.randn((nb, h, w, c), device=dev)
+        ms = timeit(prog, [xin], a.iters)
+        oh = (h - kh) // s + 1 if pad == "VALID" else (h + s - 1) // s
+        ow = (w - kw) // s + 1 if pad == "VALID" else (w + s - 1) // s
+        fl = 2 * nb * oh * ow * oc * kh * kw * c
+        r = {"kind": "conv", "shape": [nb, h, w, c, kh, kw, oc, s, pad], "ms": ms, "tflops": fl / ms / 1e9}
+        print(json.dumps(r), flush=True)
+        res.append(r)
+        del xin
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

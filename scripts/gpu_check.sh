@@ -35,6 +35,7 @@ for s in $STEPS; do
     cfg_inception) run cfg_inception 900 python bench/configs.py inception ${CFG_ARGS:-} ;;
     cfg_kmeans) run cfg_kmeans 600 python bench/configs.py kmeans ;;
     gpumodels) run gpumodels 900 python -m pytest tests/test_gpu_models.py -x -q ;;
+    gemmbench) run gemmbench 600 python scripts/gemm_bench.py --json gpurun_out/gemm_bench.json ;;
     images) run images 600 python -m pytest tests/test_image_ops.py -x -q ;;
     ex_image) run ex_image 600 python examples/read_image.py --images 64 ;;
     examples) run examples 900 bash -c "python examples/quickstart.py && python examples/harmonic_mean.py && python examples/kmeans_demo.py" ;;
