@@ -172,6 +172,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           for (auto& f : feeds) out[py::str(f)] = info_of(f);
           return out;
         });
+  m.def("infer_fed",
+        [](std::shared_ptr<Graph> g, std::vector<std::string> fetches, std::vector<std::string> feeds,
+           py::dict hints) {
+          // per-node infos of a program's closure under concrete feed infos
+          // (the map_rows vectorizer needs every tensor's rank)
+          Program p(g, fetches, feeds);
+          Graph::Infos infos = p.analyze(infos_from_py(hints));
+          py::dict out;
+          for (size_t i = 0; i < infos.size(); ++i)
+            if (!infos[i].empty()) out[py::str(g->node(static_cast<int>(i)).name)] = infos_to_py(infos[i]);
+          return out;
+        });
   m.def("infer_all", &infer_all);
   m.def("registered_ops", [] { return OpRegistry::get().names(); });
   m.def("roundtrip_graphdef",

@@ -33,10 +33,14 @@ class Config:
     pinned_min_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_PINNED_MIN_BYTES", 1 << 20, int))
     # map_rows: cells at least this large run on the GPU, smaller ones on the host executor
     map_rows_gpu_min_elems: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_GPU_MIN", 16384, int))
+    # map_rows: run same-shaped rows as one block through the lifted row graph
+    map_rows_vectorize: bool = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_VECTORIZE", True, bool))
     # re-runs of a partition task after a runtime (non-validation) failure; 0 = fail fast
     task_retries: int = dataclasses.field(default_factory=lambda: _env("TFA_TASK_RETRIES", 0, int))
     # timeout of one collective (RCCL/gloo); a stuck collective aborts the job
     collective_timeout_s: float = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_TIMEOUT_S", 600.0, float))
+    # CPU executor: programs with fewer input elements run on one intra-op thread
+    cpu_parallel_min_elems: int = dataclasses.field(default_factory=lambda: _env("TFA_CPU_PARALLEL_MIN_ELEMS", 4_000_000, int))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 

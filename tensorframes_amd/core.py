@@ -403,23 +403,36 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
     fetch_refs = [ref_of[o.name] for o in outputs]
     prog = engine.program(spec.graph_bytes, fetch_refs, feed_names + [hf.node for hf in host])
     out_meta = [(o.name, o.tf_dtype, o.shape) for o in outputs]
+    vec = _RowVectorizer(spec.graph_bytes, fetch_refs, feed_names,
+                         [summary[n].tf_dtype for n in feed_names]) if config.map_rows_vectorize and feed_names \
+        else None
 
     def compute(blocks):
         res = {}
         for pid in sorted(blocks):
             b = blocks[pid]
-            per_out: List[List[torch.Tensor]] = [[] for _ in outputs]
+            per_out: List[List[Optional[torch.Tensor]]] = [[None] * b.nrows for _ in outputs]
             cell_views = [_cells(b.columns[c]) for c in feed_cols]
             host_views = [_decoded_cells(hf, b) for hf in host]
             dev = _rows_device(cell_views + host_views)
+            # rows are enqueued back to back; device outputs stay on the GPU until
+            # the partition is done (one D2H per column instead of a sync per row)
+            done = vec.run_groups(b, feed_cols, cell_views, dev, per_out) if vec is not None and not host \
+                else [None] * b.nrows
             for i in range(b.nrows):
+                if done[i] is not None:
+                    continue
                 ins = [cv[i] for cv in cell_views] + [hv[i] for hv in host_views]
                 outs = engine.run_program(prog, ins, dev)
                 for j, o in enumerate(outs):
-                    per_out[j].append(o.cpu() if o.is_cuda else o)
+                    per_out[j][i] = o
+            host_rows = not any(len(cv) and cv[0].is_cuda for cv in cell_views)
             cols_out = {}
             for (name, dt, shp), vals in zip(out_meta, per_out):
-                cols_out[name] = _stack_cells(vals, dt, shp)
+                col = vals if isinstance(vals, torch.Tensor) else _stack_cells(vals, dt, shp)
+                if host_rows and isinstance(col, torch.Tensor) and col.is_cuda:
+                    col = col.cpu()
+                cols_out[name] = col
             cols_out.update(b.columns)
             res[pid] = Block(b.nrows, cols_out)
         metrics.add("map_rows_rows", sum(b.nrows for b in blocks.values()))
@@ -445,6 +458,74 @@ def _host_contents(spec: GraphSpec, host) -> List[str]:
         return []
     g = engine.native_graph(spec.graph_bytes)
     return [g.node_inputs(hf.node)[0].split(":")[0] for hf in host]
+
+
+class _RowVectorizer:
+    """map_rows fast path: rows with identical cell shapes run as ONE block
+    through the lifted (batched) form of the row graph
+    (graph/vectorize.py); graphs that cannot be lifted exactly keep the
+    per-row loop."""
+
+    def __init__(self, graph_bytes: bytes, fetch_refs: List[str], feed_names: List[str], feed_dtypes: List[int]):
+        self.graph_bytes = graph_bytes
+        self.fetch_refs = list(fetch_refs)
+        self.feed_names = list(feed_names)
+        self.feed_dtypes = list(feed_dtypes)
+        self._progs: Dict[tuple, Any] = {}  # cell ranks -> lifted program (or None)
+
+    def _program(self, cell_shapes: tuple):
+        key = tuple(len(s) for s in cell_shapes)
+        if key not in self._progs:
+            from .graph import vectorize
+            g = engine.native_graph(self.graph_bytes)
+            hints = {n: (dt, list(s)) for n, dt, s in zip(self.feed_names, self.feed_dtypes, cell_shapes)}
+            try:
+                infos = _C.infer_fed(g, self.fetch_refs, self.feed_names, hints)
+                lifted = vectorize.lift(P.parse_graphdef(self.graph_bytes), self.fetch_refs, self.feed_names, infos)
+            except ValueError:
+                lifted = None
+            self._progs[key] = None if lifted is None else \
+                engine.program(P.serialize_graphdef(lifted), self.fetch_refs, self.feed_names)
+            metrics.add("map_rows_vectorized_graphs" if lifted is not None else "map_rows_unliftable_graphs")
+        return self._progs[key]
+
+    def run_groups(self, b: Block, feed_cols: List[str], cell_views, dev, per_out) -> list:
+        done = [None] * b.nrows
+        if b.nrows == 0:
+            return done
+        cols = [b.columns[c] for c in feed_cols]
+        if all(is_dense(c) for c in cols):
+            groups = {tuple(tuple(c.shape[1:]) for c in cols): None}  # one group: the whole block
+        else:
+            groups = {}
+            for i in range(b.nrows):
+                groups.setdefault(tuple(tuple(cv[i].shape) for cv in cell_views), []).append(i)
+        for shapes, rows in groups.items():
+            prog = self._program(shapes)
+            if prog is None:
+                return done
+            if rows is None:
+                ins, idx, n = cols, None, b.nrows
+            else:
+                if len(rows) < 2:
+                    continue
+                ins = [torch.stack([cv[i] for i in rows], 0) for cv in cell_views]
+                idx, n = rows, len(rows)
+            outs = engine.run_program(prog, ins, dev)
+            if any(o.dim() == 0 or o.shape[0] != n for o in outs):
+                return done  # lifted graph did not keep the row dim: per-row loop
+            if idx is None:  # the whole block in one go: outputs are the columns
+                for j, o in enumerate(outs):
+                    per_out[j] = o
+                metrics.add("map_rows_vectorized_rows", n)
+                return [True] * n
+            for j, o in enumerate(outs):
+                for k, i in enumerate(idx):
+                    per_out[j][i] = o[k]
+            for i in idx:
+                done[i] = True
+        metrics.add("map_rows_vectorized_rows", sum(1 for d in done if d))
+        return done
 
 
 class _LazyDecoded:
@@ -500,7 +581,7 @@ def _stack_cells(vals: List[torch.Tensor], tf_dtype: int, shape: Optional[Shape]
     shapes = {tuple(v.shape) for v in vals}
     if len(shapes) == 1:
         return torch.stack(vals, 0)
-    return RaggedColumn([v.numpy() for v in vals], tf_dtype)
+    return RaggedColumn([v.cpu().numpy() for v in vals], tf_dtype)
 
 
 # ------------------------------------------------------------------ reductions

@@ -116,7 +116,30 @@ def run_program(prog, inputs: List[torch.Tensor], dev: Optional[torch.device] = 
     if dev.type == "cuda":
         with torch.cuda.device(dev):
             return list(prog.run(ins))
+    if sum(t.numel() for t in ins) < config.cpu_parallel_min_elems:
+        with _single_threaded():
+            return list(prog.run(ins))
     return list(prog.run(ins))
+
+
+_thread_lock = threading.Lock()
+
+
+class _single_threaded:
+    """Run small CPU programs on one intra-op thread: below a few million
+    elements the OpenMP fork/join costs more than the op (tens of ms per op on
+    virtualised hosts, measured)."""
+
+    def __enter__(self):
+        _thread_lock.acquire()
+        self.n = torch.get_num_threads()
+        if self.n != 1:
+            torch.set_num_threads(1)
+
+    def __exit__(self, *a):
+        if self.n != 1:
+            torch.set_num_threads(self.n)
+        _thread_lock.release()
 
 
 def run_block_host(prog, inputs: List[torch.Tensor], separable: bool,
