@@ -2,6 +2,8 @@
 // pinned host memory. Replaces the Py4J + JNI bridges of the reference
 // (reference: src/main/scala/org/tensorframes/impl/PythonInterface.scala:21-180).
 #include <torch/extension.h>
+
+#include <unordered_map>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPGuard.h>
 
@@ -116,6 +118,36 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              return v;
            })
       .def("has_node", [](const Graph& g, const std::string& n) { return g.find(n) >= 0; })
+      .def("node_attr_scalars",
+           [](const Graph& g, const std::string& name) {
+             // scalar attrs (i / f / b / type / s) of one node, no tensors
+             int i = g.find(name);
+             TFA_CHECK(i >= 0, "no node named '", name, "'");
+             py::dict d;
+             for (auto& kv : g.def().nodes[i].attr) {
+               const AttrValue& a = kv.second;
+               switch (a.kind) {
+                 case AttrValue::I: d[py::str(kv.first)] = a.i; break;
+                 case AttrValue::F: d[py::str(kv.first)] = a.f; break;
+                 case AttrValue::B: d[py::str(kv.first)] = a.b; break;
+                 case AttrValue::TYPE: d[py::str(kv.first)] = static_cast<int>(a.type); break;
+                 case AttrValue::S: d[py::str(kv.first)] = py::bytes(a.s); break;
+                 default: break;
+               }
+             }
+             return d;
+           })
+      .def("const_strings",
+           [](const Graph& g, const std::string& name) {
+             int i = g.find(name);
+             TFA_CHECK(i >= 0, "no node named '", name, "'");
+             const NodeDef& nd = g.def().nodes[i];
+             py::list l;
+             const AttrValue* v = nd.find_attr("value");
+             if (nd.op == "Const" && v && v->tensor && v->tensor->dtype == DType::STRING)
+               for (auto& str : v->tensor->strings) l.append(py::bytes(str));
+             return l;
+           })
       .def("serialize", [](const Graph& g) { return py::bytes(serialize_graphdef(g.def())); })
       .def("__len__", [](const Graph& g) { return g.nodes().size(); });
 
@@ -185,6 +217,43 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           return out;
         });
   m.def("infer_all", &infer_all);
+  // A GraphDef whose Const nodes above `max_elems` elements are replaced by
+  // same-typed Placeholders: structure-only views of big models for
+  // Python-side graph analysis (weights never cross into Python).
+  m.def("light_graphdef", [](py::bytes b, int64_t max_elems) {
+    GraphDef g = parse_graphdef(std::string(b));
+    for (auto& nd : g.nodes) {
+      if (nd.op != "Const") continue;
+      const AttrValue* v = nd.find_attr("value");
+      if (!v || !v->tensor || v->tensor->num_elements() <= max_elems) continue;
+      AttrValue dt;
+      dt.kind = AttrValue::TYPE;
+      dt.type = v->tensor->dtype;
+      AttrValue shp;
+      shp.kind = AttrValue::SHAPE;
+      shp.shape = v->tensor->shape;
+      nd.op = "Placeholder";
+      nd.attr.clear();
+      nd.attr["dtype"] = dt;
+      nd.attr["shape"] = shp;
+    }
+    return py::bytes(serialize_graphdef(g));
+  });
+  // `orig` with every node of `patch` replacing the same-named node (or
+  // appended when new): applies a Python-side rewrite of a light view back
+  // onto the full graph.
+  m.def("patch_graphdef", [](py::bytes orig, py::bytes patch) {
+    GraphDef g = parse_graphdef(std::string(orig));
+    GraphDef p = parse_graphdef(std::string(patch));
+    std::unordered_map<std::string, size_t> at;
+    for (size_t i = 0; i < g.nodes.size(); ++i) at[g.nodes[i].name] = i;
+    for (auto& nd : p.nodes) {
+      auto it = at.find(nd.name);
+      if (it != at.end()) g.nodes[it->second] = nd;
+      else g.nodes.push_back(nd);
+    }
+    return py::bytes(serialize_graphdef(g));
+  });
   m.def("registered_ops", [] { return OpRegistry::get().names(); });
   m.def("roundtrip_graphdef",
         [](py::bytes b) { return py::bytes(serialize_graphdef(parse_graphdef(std::string(b)))); });

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <string_view>
 
 namespace tfa {
 
@@ -98,7 +99,7 @@ struct Reader {
   const uint8_t* end;
   Reader(const void* data, size_t n)
       : p(static_cast<const uint8_t*>(data)), end(static_cast<const uint8_t*>(data) + n) {}
-  explicit Reader(const std::string& s) : Reader(s.data(), s.size()) {}
+  explicit Reader(std::string_view s) : Reader(s.data(), s.size()) {}
   bool done() const { return p >= end; }
 
   uint64_t varint() {
@@ -128,10 +129,11 @@ struct Reader {
     p += 8;
     return v;
   }
-  std::string bytes() {
+  // a view into the source buffer: nested messages (and weights) are not copied
+  std::string_view bytes() {
     uint64_t n = varint();
     TFA_CHECK(static_cast<uint64_t>(end - p) >= n, "protobuf: truncated length-delimited field");
-    std::string s(reinterpret_cast<const char*>(p), n);
+    std::string_view s(reinterpret_cast<const char*>(p), n);
     p += n;
     return s;
   }
@@ -150,7 +152,7 @@ struct Reader {
 template <typename F>
 void read_repeated(Reader& r, int wt, F&& one) {
   if (wt == 2) {
-    std::string payload = r.bytes();
+    std::string_view payload = r.bytes();
     Reader sub(payload);
     // wire type of the elements is implied by the callback
     while (!sub.done()) one(sub, /*packed=*/true);
@@ -159,14 +161,14 @@ void read_repeated(Reader& r, int wt, F&& one) {
   }
 }
 
-Shape decode_shape(const std::string& bytes) {
+Shape decode_shape(std::string_view bytes) {
   Shape s;
   Reader r(bytes);
   while (!r.done()) {
     uint64_t key = r.varint();
     int field = static_cast<int>(key >> 3), wt = static_cast<int>(key & 7);
     if (field == 2 && wt == 2) {
-      std::string dim = r.bytes();
+      std::string_view dim = r.bytes();
       Reader d(dim);
       int64_t size = 0;
       while (!d.done()) {
@@ -196,10 +198,10 @@ void append_pod(std::vector<uint8_t>& out, T v) {
   std::memcpy(out.data() + n, &v, sizeof(T));
 }
 
-HostTensor decode_tensor(const std::string& bytes) {
+HostTensor decode_tensor(std::string_view bytes) {
   HostTensor t;
   Reader r(bytes);
-  std::string content;
+  std::string_view content;
   bool has_content = false;
   std::vector<uint8_t> vals;  // typed values, in the element type
   int64_t nvals = 0;
@@ -248,7 +250,7 @@ HostTensor decode_tensor(const std::string& bytes) {
           ++nvals;
         });
         break;
-      case 8: svals.push_back(r.bytes()); break;
+      case 8: svals.emplace_back(r.bytes()); break;
       default: r.skip(wt);
     }
   }
@@ -273,13 +275,14 @@ HostTensor decode_tensor(const std::string& bytes) {
   int64_t es = dtype_size(t.dtype);
   TFA_CHECK(es > 0, "unsupported TensorProto dtype ", static_cast<int>(t.dtype));
   TFA_CHECK(n <= cap / es, "TensorProto of ", n, " elements exceeds the constant size limit (", cap, " bytes)");
-  t.bytes.assign(n * es, 0);
   if (has_content) {
     TFA_CHECK(static_cast<int64_t>(content.size()) == n * es, "tensor_content has ", content.size(),
               " bytes, expected ", n * es, " for shape ", t.shape.str());
-    if (!content.empty()) std::memcpy(t.bytes.data(), content.data(), content.size());
+    t.bytes.assign(reinterpret_cast<const uint8_t*>(content.data()),
+                   reinterpret_cast<const uint8_t*>(content.data()) + content.size());
     return t;
   }
+  t.bytes.assign(n * es, 0);
   if (nvals == 0) return t;  // zero-filled
   // Repeat-last-value fill rule (reference: src/main/protobuf/tensorflow/core/framework/tensor.proto:25-27).
   for (int64_t i = 0; i < n; ++i) {
@@ -313,16 +316,16 @@ HostTensor decode_tensor(const std::string& bytes) {
   return t;
 }
 
-AttrValue decode_attr(const std::string& bytes);
+AttrValue decode_attr(std::string_view bytes);
 
-AttrList decode_list(const std::string& bytes) {
+AttrList decode_list(std::string_view bytes) {
   AttrList l;
   Reader r(bytes);
   while (!r.done()) {
     uint64_t key = r.varint();
     int field = static_cast<int>(key >> 3), wt = static_cast<int>(key & 7);
     switch (field) {
-      case 2: l.s.push_back(r.bytes()); break;
+      case 2: l.s.emplace_back(r.bytes()); break;
       case 3:
         read_repeated(r, wt, [&](Reader& q, bool) { l.i.push_back(static_cast<int64_t>(q.varint())); });
         break;
@@ -348,7 +351,7 @@ AttrList decode_list(const std::string& bytes) {
   return l;
 }
 
-AttrValue decode_attr(const std::string& bytes) {
+AttrValue decode_attr(std::string_view bytes) {
   AttrValue a;
   Reader r(bytes);
   while (!r.done()) {
@@ -371,7 +374,7 @@ AttrValue decode_attr(const std::string& bytes) {
       case 9: a.kind = AttrValue::PLACEHOLDER; a.s = r.bytes(); break;
       case 10: {
         a.kind = AttrValue::FUNC;
-        std::string fn = r.bytes();
+        std::string_view fn = r.bytes();
         Reader q(fn);
         while (!q.done()) {
           uint64_t k = q.varint();
@@ -385,7 +388,7 @@ AttrValue decode_attr(const std::string& bytes) {
   return a;
 }
 
-NodeDef decode_node(const std::string& bytes) {
+NodeDef decode_node(std::string_view bytes) {
   NodeDef n;
   Reader r(bytes);
   while (!r.done()) {
@@ -394,10 +397,10 @@ NodeDef decode_node(const std::string& bytes) {
     switch (field) {
       case 1: n.name = r.bytes(); break;
       case 2: n.op = r.bytes(); break;
-      case 3: n.inputs.push_back(r.bytes()); break;
+      case 3: n.inputs.emplace_back(r.bytes()); break;
       case 4: n.device = r.bytes(); break;
       case 5: {
-        std::string entry = r.bytes();
+        std::string_view entry = r.bytes();
         Reader e(entry);
         std::string k;
         AttrValue v;
@@ -533,7 +536,7 @@ GraphDef parse_graphdef(const std::string& bytes) {
     if (field == 1 && wt == 2) {
       g.nodes.push_back(decode_node(r.bytes()));
     } else if (field == 4 && wt == 2) {
-      std::string v = r.bytes();
+      std::string_view v = r.bytes();
       Reader q(v);
       while (!q.done()) {
         uint64_t k = q.varint();

@@ -53,6 +53,8 @@ def main():
     for r in rows[:4]:
         print(r.image_uri, list(r["index"]), [round(v, 4) for v in r["value"]])
     print(f"{len(rows)} images in {dt:.2f}s ({len(rows) / dt:.1f} images/s, per-row map_rows)")
+    m = tfs.metrics.snapshot()
+    print({k: round(v, 1) for k, v in m.items() if k.startswith("map_rows")})
 
 
 if __name__ == "__main__":

@@ -422,8 +422,10 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
             for i in range(b.nrows):
                 if done[i] is not None:
                     continue
-                ins = [cv[i] for cv in cell_views] + [hv[i] for hv in host_views]
-                outs = engine.run_program(prog, ins, dev)
+                with metrics.timer("map_rows_inputs"):
+                    ins = [cv[i] for cv in cell_views] + [hv[i] for hv in host_views]
+                with metrics.timer("map_rows_run"):
+                    outs = engine.run_program(prog, ins, dev)
                 for j, o in enumerate(outs):
                     per_out[j][i] = o
             host_rows = not any(len(cv) and cv[0].is_cuda for cv in cell_views)
@@ -447,7 +449,7 @@ def _host_feeds(spec: GraphSpec, feed_dict: Dict[str, str], fields) -> list:
     if not ops.intersection(host_ops.DECODE_OPS):
         return []
     try:
-        return host_ops.plan_host_stage(P.parse_graphdef(spec.graph_bytes), spec.fetch_refs, feed_dict, fields)
+        return host_ops.plan_host_stage(engine.native_graph(spec.graph_bytes), spec.fetch_refs, feed_dict, fields)
     except ValueError as e:
         raise TensorFramesError(str(e))
 
@@ -481,12 +483,15 @@ class _RowVectorizer:
             hints = {n: (dt, list(s)) for n, dt, s in zip(self.feed_names, self.feed_dtypes, cell_shapes)}
             try:
                 infos = _C.infer_fed(g, self.fetch_refs, self.feed_names, hints)
-                lifted = vectorize.lift(P.parse_graphdef(self.graph_bytes), self.fetch_refs, self.feed_names, infos)
+                # analysed on a structure-only view (big constants elided); the
+                # rewritten nodes are patched back into the full graph natively
+                light = P.parse_graphdef(_C.light_graphdef(self.graph_bytes, 4096))
+                patch = vectorize.lift(light, self.fetch_refs, self.feed_names, infos, patch_only=True)
             except ValueError:
-                lifted = None
-            self._progs[key] = None if lifted is None else \
-                engine.program(P.serialize_graphdef(lifted), self.fetch_refs, self.feed_names)
-            metrics.add("map_rows_vectorized_graphs" if lifted is not None else "map_rows_unliftable_graphs")
+                patch = None
+            self._progs[key] = None if patch is None else engine.program(
+                _C.patch_graphdef(self.graph_bytes, P.serialize_graphdef(patch)), self.fetch_refs, self.feed_names)
+            metrics.add("map_rows_vectorized_graphs" if patch is not None else "map_rows_unliftable_graphs")
         return self._progs[key]
 
     def run_groups(self, b: Block, feed_cols: List[str], cell_views, dev, per_out) -> list:
@@ -601,17 +606,17 @@ _MONOID_PAIR_OPS = {"Add": "Sum", "AddV2": "Sum", "Mul": "Prod", "Minimum": "Min
 
 def _pair_monoid(spec: GraphSpec, names: List[str]) -> Optional[Dict[str, str]]:
     """For reduce_rows: {X: reduction} if every fetch is X = op(X_1, X_2) for a monoid op."""
-    g = P.parse_graphdef(spec.graph_bytes)
-    by = {n.name: n for n in g.node}
+    g = engine.native_graph(spec.graph_bytes)
+    ops = dict(zip(g.node_names(), g.node_ops()))
     out = {}
     for x in names:
-        n = by.get(x)
-        if n is None or n.op not in _MONOID_PAIR_OPS or len(n.input) != 2:
+        op = ops.get(x)
+        if op not in _MONOID_PAIR_OPS:
             return None
-        ins = sorted(i.split(":")[0] for i in n.input)
-        if ins != sorted([f"{x}_1", f"{x}_2"]):
+        inputs = list(g.node_inputs(x))
+        if len(inputs) != 2 or sorted(i.split(":")[0] for i in inputs) != sorted([f"{x}_1", f"{x}_2"]):
             return None
-        out[x] = _MONOID_PAIR_OPS[n.op]
+        out[x] = _MONOID_PAIR_OPS[op]
     return out
 
 

@@ -36,20 +36,42 @@ _lock = threading.Lock()
 _MAX_CACHE = 64
 
 
+_hash_memo: "OrderedDict[int, Tuple[bytes, str]]" = OrderedDict()
+_graph_bytes_cached = 0
+_MAX_GRAPH_BYTES = 8 << 30  # native graphs kept alive (model weights live in them)
+
+
 def _key(graph_bytes: bytes) -> str:
-    return hashlib.sha1(graph_bytes).hexdigest()
+    """Content hash of a GraphDef, memoised by object identity: the DSL hands
+    out the same bytes object until the graph changes, so big models
+    (hundreds of MB of weights) are hashed once, not per operator call."""
+    ent = _hash_memo.get(id(graph_bytes))
+    if ent is not None and ent[0] is graph_bytes:
+        return ent[1]
+    k = hashlib.sha1(graph_bytes).hexdigest()
+    with _lock:
+        _hash_memo[id(graph_bytes)] = (graph_bytes, k)
+        while len(_hash_memo) > 4:
+            _hash_memo.popitem(last=False)
+    return k
 
 
 def native_graph(graph_bytes: bytes):
+    global _graph_bytes_cached
     k = _key(graph_bytes)
     with _lock:
-        g = _graph_cache.get(k)
-        if g is None:
-            g = _C.Graph(graph_bytes)
-            _graph_cache[k] = g
-            while len(_graph_cache) > _MAX_CACHE:
-                _graph_cache.popitem(last=False)
-        return g
+        ent = _graph_cache.get(k)
+        if ent is not None:
+            _graph_cache.move_to_end(k)
+            return ent[0]
+    g = _C.Graph(graph_bytes)
+    with _lock:
+        _graph_cache[k] = (g, len(graph_bytes))
+        _graph_bytes_cached += len(graph_bytes)
+        while len(_graph_cache) > 1 and (len(_graph_cache) > _MAX_CACHE or _graph_bytes_cached > _MAX_GRAPH_BYTES):
+            _, (_, nb) = _graph_cache.popitem(last=False)
+            _graph_bytes_cached -= nb
+    return g
 
 
 def program(graph_bytes: bytes, fetches: Sequence[str], feeds: Sequence[str]):

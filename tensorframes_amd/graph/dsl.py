@@ -202,7 +202,15 @@ class Graph:
         return g
 
     def serialize(self) -> bytes:
-        return P.serialize_graphdef(self.as_graph_def())
+        """GraphDef bytes; cached while the graph is unchanged (nodes are only
+        ever appended, so the node count identifies the version)."""
+        n = len(self._nodes)
+        cached = getattr(self, "_ser_cache", None)
+        if cached is not None and cached[0] == n:
+            return cached[1]
+        b = P.serialize_graphdef(self.as_graph_def())
+        self._ser_cache = (n, b)
+        return b
 
     def _shape_view(self) -> bytes:
         """The graph for shape inference only: large constants are replaced by

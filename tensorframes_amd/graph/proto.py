@@ -174,8 +174,34 @@ def _key(field: int, wt: int) -> bytes:
     return _varint((field << 3) | wt)
 
 
-def _ld(field: int, payload: bytes) -> bytes:
-    return _key(field, 2) + _varint(len(payload)) + payload
+class _Rope:
+    """Concatenation without copying: big payloads (tensor_content of model
+    weights) are referenced, not re-copied at every nesting level, and
+    joined once by `serialize_graphdef`."""
+
+    __slots__ = ("parts", "n")
+
+    def __init__(self, parts):
+        self.parts = parts
+        self.n = sum(len(p) for p in parts)
+
+    def __len__(self):
+        return self.n
+
+    def __add__(self, o):
+        return _Rope(self.parts + (o.parts if isinstance(o, _Rope) else [o]))
+
+    def __radd__(self, o):
+        return _Rope((list(o.parts) if isinstance(o, _Rope) else [o]) + self.parts)
+
+
+def _ld(field: int, payload) -> bytes:
+    head = _key(field, 2) + _varint(len(payload))
+    if isinstance(payload, _Rope):
+        return _Rope([head] + payload.parts)
+    if len(payload) > 65536:
+        return _Rope([head, payload])
+    return head + payload
 
 
 def _enc_shape(s: TensorShapeProto) -> bytes:
@@ -274,10 +300,16 @@ def serialize_node(n: NodeDef) -> bytes:
 
 
 def serialize_graphdef(g: GraphDef) -> bytes:
-    out = b"".join(_ld(1, serialize_node(n)) for n in g.node)
+    parts = []
+    for n in g.node:
+        e = _ld(1, serialize_node(n))
+        if isinstance(e, _Rope):
+            parts.extend(e.parts)
+        else:
+            parts.append(e)
     if g.producer:
-        out += _ld(4, _key(1, 0) + _varint(g.producer))
-    return out
+        parts.append(_ld(4, _key(1, 0) + _varint(g.producer)))
+    return b"".join(parts)
 
 
 # ------------------------------------------------------------------ reader

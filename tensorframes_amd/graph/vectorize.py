@@ -58,17 +58,19 @@ def _split(inp: str) -> Tuple[str, int]:
 
 
 def lift(gdef: P.GraphDef, fetches: List[str], feeds: List[str],
-         infos: Dict[str, list]) -> Optional[P.GraphDef]:
+         infos: Dict[str, list], patch_only: bool = False) -> Optional[P.GraphDef]:
     """The block form of `gdef`, or None when the graph cannot be lifted
     exactly. `infos`: per-node inferred infos of the closure under the
-    concrete cell shapes of one row group (`_C.infer_fed`)."""
+    concrete cell shapes of one row group (`_C.infer_fed`). With
+    `patch_only`, only the rewritten and new nodes are returned (to be
+    applied with `_C.patch_graphdef` onto the full graph)."""
     try:
-        return _lift(gdef, fetches, feeds, infos)
+        return _lift(gdef, fetches, feeds, infos, patch_only)
     except _Refuse:
         return None
 
 
-def _lift(gdef, fetches, feeds, infos):
+def _lift(gdef, fetches, feeds, infos, patch_only=False):
     nodes = {n.name: n for n in gdef.node}
     feed_set = set(feeds)
     # closure of the fetches, cut at feeds
@@ -246,6 +248,9 @@ def _lift(gdef, fetches, feeds, infos):
             if shp is not None and not shp.value.unknown_rank:
                 m.attr["shape"] = P.AttrValue.shape([None] + [None if d < 0 else d for d in shp.value.dims])
             out_nodes[name] = m
+    if patch_only:
+        changed = [m for name, m in out_nodes.items() if m is not nodes[name]]
+        return P.GraphDef(changed + extra, gdef.producer)
     new = [out_nodes.get(n.name, n) for n in gdef.node] + extra
     return P.GraphDef(new, gdef.producer)
 

@@ -73,51 +73,56 @@ class HostFeed:
         return decode_image(cell, self.channels, self.dtype)
 
 
-def _closure(nodes, fetch_nodes: List[str], stop: set) -> List[str]:
+def _closure(inputs_of, fetch_nodes: List[str], stop: set) -> List[str]:
     seen, stack, order = set(), list(fetch_nodes), []
     while stack:
         n = stack.pop()
-        if n in seen or n not in nodes:
+        if n in seen:
             continue
         seen.add(n)
         order.append(n)
         if n in stop:
             continue
-        for i in nodes[n].input:
+        for i in inputs_of(n):
             stack.append(i.lstrip("^").split(":")[0])
     return order
 
 
-def plan_host_stage(gdef, fetch_refs: List[str], feed_dict: Dict[str, str],
+def plan_host_stage(graph, fetch_refs: List[str], feed_dict: Dict[str, str],
                     columns: Dict[str, object]) -> List[HostFeed]:
-    """The decoder nodes reachable from the fetches (`gdef`: a parsed
-    GraphDef), each bound to the binary column (through `feed_dict` on its
-    contents node, or a placeholder named like a column) or to its constant
-    contents."""
-    nodes = {n.name: n for n in gdef.node}
+    """The decoder nodes reachable from the fetches (`graph`: the native
+    graph; nothing is parsed in Python, so big models stay cheap), each bound
+    to the binary column (through `feed_dict` on its contents node, or a
+    placeholder named like a column) or to its constant contents."""
+    ops = dict(zip(graph.node_names(), graph.node_ops()))
+    cache: Dict[str, List[str]] = {}
+
+    def inputs_of(n):
+        if n not in cache:
+            cache[n] = list(graph.node_inputs(n)) if n in ops else []
+        return cache[n]
     fetch_nodes = [r.split(":")[0] for r in fetch_refs]
-    host = [n for n in _closure(nodes, fetch_nodes, set()) if nodes[n].op in DECODE_OPS]
+    host = [n for n in _closure(inputs_of, fetch_nodes, set()) if ops.get(n) in DECODE_OPS]
     # only the decoders not hidden behind another decoder
-    reachable = set(_closure(nodes, fetch_nodes, set(host)))
+    reachable = set(_closure(inputs_of, fetch_nodes, set(host)))
     feeds: List[HostFeed] = []
     for n in host:
         if n not in reachable:
             continue
-        nd = nodes[n]
-        attr = {k: v.value for k, v in nd.attr.items()}
-        src = nd.input[0].split(":")[0]
-        src_op = nodes[src].op if src in nodes else None
+        attr = graph.node_attr_scalars(n)
+        src = inputs_of(n)[0].split(":")[0]
+        src_op = ops.get(src)
         col = feed_dict.get(src)
         if col is None and src_op in ("Placeholder", "PlaceholderV2") and src in columns:
             col = src
-        hf = HostFeed(n, nd.op, int(attr.get("channels", 0)), int(attr.get("dtype", D.DT_UINT8)), col)
+        hf = HostFeed(n, ops[n], int(attr.get("channels", 0)), int(attr.get("dtype", D.DT_UINT8)), col)
         if col is None:
             if src_op != "Const":
-                raise ValueError(f"{nd.op} node '{n}': its contents '{src}' must be fed from a binary "
+                raise ValueError(f"{ops[n]} node '{n}': its contents '{src}' must be fed from a binary "
                                  f"column (feed_dict={{'{src}': <column>}})")
-            vals = list(np.asarray(nodes[src].attr["value"].value.to_numpy(), dtype=object).reshape(-1))
+            vals = graph.const_strings(src)
             if not vals:
-                raise ValueError(f"{nd.op} node '{n}': constant contents '{src}' is empty")
+                raise ValueError(f"{ops[n]} node '{n}': constant contents '{src}' is empty")
             hf.const_value = hf.decode(vals[0])
         feeds.append(hf)
     return feeds
