@@ -60,7 +60,9 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> bo
     os.environ.setdefault("MASTER_PORT", "29511")
     use_gpu = torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+        # TFA_DIST_BACKEND=gloo rehearses multi-rank logic where RCCL cannot
+        # run (e.g. several ranks sharing one GPU)
+        backend = os.environ.get("TFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if use_gpu:
         torch.cuda.set_device(local_rank() % max(torch.cuda.device_count(), 1))
     kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
