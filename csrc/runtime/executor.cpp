@@ -1,6 +1,8 @@
 // Planner + executor (see executor.h).
 #include "executor.h"
 
+#include <ATen/hip/HIPGraph.h>
+
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
@@ -71,6 +73,21 @@ struct Program::Plan {
   std::vector<int> fetch_slots;
   std::map<int, std::map<int, at::Tensor>> dev_consts;  // device index -> slot -> tensor
   int fused = 0;
+  // HIP-graph replay of this plan (small, repeated launches): static input
+  // buffers the inputs are copied into, the captured graph, its outputs
+  struct Captured {
+    std::mutex mu;
+    int64_t gpu_runs = 0;
+    bool failed = false;
+    int device = -1;
+    hipStream_t stream = nullptr;  // our own capture stream (never shared)
+    std::unique_ptr<at::cuda::CUDAGraph> graph;
+    std::vector<at::Tensor> static_in, static_out;
+    ~Captured() {
+      graph.reset();
+      if (stream) (void)hipStreamDestroy(stream);
+    }
+  } cap;
 };
 
 Program::Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetches,
@@ -445,6 +462,94 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
   return outs;
 }
 
+// HIP graphs: a plan that keeps being run with small inputs is launch-bound;
+// after kGraphWarmRuns ordinary runs its kernel sequence is captured once and
+// replayed (inputs copied into static buffers, outputs cloned out). Enabled
+// with TFA_HIP_GRAPHS=1 (default) for inputs up to TFA_HIP_GRAPH_MAX_BYTES.
+namespace {
+constexpr int64_t kGraphWarmRuns = 3;
+bool hip_graphs_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TFA_HIP_GRAPHS");
+    return !(e && std::string(e) == "0");
+  }();
+  return on && !debug_sync();
+}
+int64_t hip_graph_max_bytes() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("TFA_HIP_GRAPH_MAX_BYTES");
+    return e ? std::atoll(e) : (int64_t(16) << 20);
+  }();
+  return v;
+}
+}  // namespace
+
+bool Program::graphable(const Plan& p) const {
+  // every plan-time (host) input must be a known constant: a data-dependent
+  // one would need a device->host sync, which a capture cannot contain
+  static const std::set<std::string> kRuntimeHostCopies = {
+      "FusedBatchNorm", "FusedBatchNormV2", "FusedBatchNormV3", "Shape", "Size", "Rank"};
+  const OpRegistry& reg = OpRegistry::get();
+  for (auto& st : p.steps) {
+    const std::string& op = g_->node(st.node).op;
+    if (kRuntimeHostCopies.count(op)) return false;  // host->device copies at run time
+    const OpDef* od = reg.find(op);
+    if (!od) return false;
+    for (int hi : od->host_inputs) {
+      if (hi < 0 || hi >= static_cast<int>(st.in_info.size())) continue;
+      if (!st.in_info[hi]->value) return false;
+    }
+  }
+  return !p.steps.empty();
+}
+
+std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor>& inputs) {
+  auto& c = p.cap;  // caller holds c.mu
+  const int dev = inputs[0].device().index();
+  hipStream_t cur = c10::hip::getCurrentHIPStream(dev).stream();
+  if (!c.graph) {
+    c.device = dev;
+    TFA_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) == hipSuccess, "hipStreamCreate failed");
+    auto side = c10::hip::getStreamFromExternal(c.stream, dev);
+    for (auto& t : inputs) c.static_in.push_back(at::empty_like(t, at::MemoryFormat::Contiguous));
+    // static inputs hold valid data before the capture stream reads them
+    {
+      c10::hip::HIPStreamGuard sg(c10::hip::getCurrentHIPStream(dev));
+      for (size_t i = 0; i < inputs.size(); ++i) c.static_in[i].copy_(inputs[i], true);
+    }
+    hipEvent_t ev;
+    TFA_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+    (void)hipEventRecord(ev, cur);
+    (void)hipStreamWaitEvent(c.stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    auto g = std::make_unique<at::cuda::CUDAGraph>();
+    try {
+      c10::hip::HIPStreamGuard sg(side);
+      g->capture_begin({0, 0}, hipStreamCaptureModeThreadLocal);
+      c.static_out = execute(p, c.static_in, c.stream);
+      g->capture_end();
+    } catch (const std::exception& e) {
+      // the capture stream is abandoned (never reused); run normally from now on
+      c.failed = true;
+      c.static_in.clear();
+      c.static_out.clear();
+      g.release();  // a half-captured graph cannot be safely destroyed; leak it
+      stats_.graph_failures++;
+      return execute(p, inputs, cur);
+    }
+    c.graph = std::move(g);
+    // the capture stream's work (none executed yet) is ordered before replays on `cur`
+    stats_.graphs_captured++;
+  }
+  for (size_t i = 0; i < inputs.size(); ++i) c.static_in[i].copy_(inputs[i], true);
+  c.graph->replay();
+  std::vector<at::Tensor> outs;
+  outs.reserve(c.static_out.size());
+  for (auto& o : c.static_out) outs.push_back(o.clone());
+  stats_.graph_replays++;
+  return outs;
+}
+
 std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
   TFA_CHECK(host_op_error_.empty(), host_op_error_);
   auto p = plan_for(inputs);
@@ -454,6 +559,18 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
   if (gpu) {
     guard.emplace(inputs[0].device().index());
     stream = c10::hip::getCurrentHIPStream(inputs[0].device().index()).stream();
+    if (hip_graphs_enabled()) {
+      int64_t bytes = 0;
+      for (auto& t : inputs) bytes += t.numel() * t.element_size();
+      std::lock_guard<std::mutex> lk(p->cap.mu);
+      const bool same_dev = p->cap.device < 0 || p->cap.device == inputs[0].device().index();
+      if (!p->cap.failed && same_dev && bytes <= hip_graph_max_bytes() && ++p->cap.gpu_runs > kGraphWarmRuns &&
+          graphable(*p)) {
+        auto outs = run_graph(*p, inputs);
+        stats_.runs++;
+        return outs;
+      }
+    }
   }
   auto outs = execute(*p, inputs, stream);
   stats_.runs++;

@@ -35,6 +35,7 @@ struct ExecStats {
   int64_t d2h_bytes = 0;
   int64_t chunks = 0;
   double h2d_ms = 0, compute_ms = 0, d2h_ms = 0, wall_ms = 0;
+  int64_t graphs_captured = 0, graph_replays = 0, graph_failures = 0;
 };
 
 class Program {
@@ -74,6 +75,8 @@ class Program {
   std::shared_ptr<Plan> build_plan(const std::vector<at::Tensor>& inputs);
   std::vector<at::Tensor> execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream);
   at::Tensor device_const(Plan& p, int slot, const at::Device& dev);
+  bool graphable(const Plan& p) const;
+  std::vector<at::Tensor> run_graph(Plan& p, const std::vector<at::Tensor>& inputs);
 
   std::shared_ptr<Graph> g_;
   std::vector<std::string> fetch_names_, feed_names_;
