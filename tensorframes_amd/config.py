@@ -24,6 +24,8 @@ class Config:
     device: str = dataclasses.field(default_factory=lambda: _env("TFA_DEVICE", "auto", str))
     # target bytes of one input column per pipelined chunk (host->device->host)
     chunk_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_CHUNK_BYTES", 128 << 20, int))
+    # a pipelined job is cut into at least this many chunks (when chunks stay >= 4 MB)
+    min_pipeline_chunks: int = dataclasses.field(default_factory=lambda: _env("TFA_MIN_PIPELINE_CHUNKS", 16, int))
     # ring depth of the copy/compute pipeline
     pipeline_depth: int = dataclasses.field(default_factory=lambda: _env("TFA_PIPELINE_DEPTH", 3, int))
     # partitions smaller than this run in one shot (no chunking)

@@ -184,9 +184,17 @@ def run_block_host(prog, inputs: List[torch.Tensor], separable: bool,
     return res
 
 
-def chunk_rows_for(inputs: List[torch.Tensor]) -> int:
+def chunk_rows_for(inputs: List[torch.Tensor], total_rows: Optional[int] = None) -> int:
+    """Rows per pipelined chunk: at most `chunk_bytes` of the widest input,
+    and small enough that a job yields >= `min_pipeline_chunks` chunks (a
+    3-stage pipeline only overlaps once it has several chunks in flight),
+    but not below 4 MB per DMA."""
     row_bytes = max((t[0].numel() * t.element_size() if t.shape[0] else 1) for t in inputs) if inputs else 1
-    return max(1024, int(config.chunk_bytes // max(row_bytes, 1)))
+    row_bytes = max(row_bytes, 1)
+    rows = int(config.chunk_bytes // row_bytes)
+    if total_rows:
+        rows = min(rows, -(-total_rows // max(1, config.min_pipeline_chunks)))
+    return max(1024, (4 << 20) // row_bytes, rows)
 
 
 def run_segments_pipelined(prog, segments: List[List[torch.Tensor]],
@@ -198,7 +206,8 @@ def run_segments_pipelined(prog, segments: List[List[torch.Tensor]],
     dev = compute_device()
     segs = [[pin(t.contiguous()) for t in seg] for seg in segments]
     outs = [[empty_host(shape, dt, True) for (shape, dt) in spec] for spec in out_specs]
-    chunk = chunk_rows_for(segs[0]) if segs and segs[0] else 1 << 16
+    total = sum(seg[0].shape[0] for seg in segs if seg)
+    chunk = chunk_rows_for(segs[0], total) if segs and segs[0] else 1 << 16
     with metrics.timer("pipelined"):
         prog.run_chunked(segs, outs, chunk, dev.index or 0, config.pipeline_depth)
     st = prog.stats()
