@@ -152,6 +152,16 @@ class DataFrame:
         """Applies fn(pid, block) to every local partition, streaming (an action)."""
         return [fn(pid, b) for pid, b in self._iter_blocks()]
 
+    def to_arrow(self):
+        """All rows as a `pyarrow.Table` (frame/arrow_io.py)."""
+        from .arrow_io import to_arrow
+        return to_arrow(self)
+
+    def write_parquet(self, path: str, row_group_rows: int = 1 << 20) -> str:
+        """One Parquet file per partition under `path` (frame/arrow_io.py)."""
+        from .arrow_io import write_parquet
+        return write_parquet(self, path, row_group_rows)
+
     def write_checkpoint(self, path: str) -> str:
         """Write every partition + the schema under `path` (see frame/checkpoint.py)."""
         from .checkpoint import write_checkpoint

@@ -65,6 +65,11 @@ def _worker(rank, world, port, outdir):
     back = tfs.read_checkpoint(df.write_checkpoint(ck))
     res["ck_parts"] = sorted(back.local_blocks())
     res["ck_x"] = [r.x for r in back.collect()]
+    # parquet: each rank writes its partitions, reads its row groups back
+    pq_dir = os.path.join(outdir, "pq")
+    back_pq = tfs.read_parquet(df.select("x", "v").write_parquet(pq_dir), num_partitions=5)
+    res["pq_x"] = [r.x for r in back_pq.collect()]
+    res["pq_parts"] = sorted(back_pq.local_blocks())
     # a fault injected on rank 1 only is retried locally; results stay consistent
     from tensorframes_amd.utils import faults
     tfs.set_config(task_retries=1)
@@ -95,6 +100,7 @@ def test_spmd_world(world, tmp_path):
         assert o["repart"] == xs
         assert o["ck_parts"] == o["local_parts"] and o["ck_x"] == xs
         assert o["retry_z"] == [x + 1.0 for x in xs]
+        assert o["pq_x"] == xs and o["pq_parts"] == o["local_parts"]
 
 
 def test_parse_cpulist_and_bind_numa_noop_without_gpu():
