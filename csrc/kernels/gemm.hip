@@ -121,6 +121,19 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
     kkw = t % cg.KW;
     kkh = t / cg.KW;
   }
+  // scalar conv (C % 4 != 0, e.g. RGB input): the same incremental split per
+  // element of the thread's 4 k's
+  int sc[4] = {0, 0, 0, 0}, skw[4] = {0, 0, 0, 0}, skh[4] = {0, 0, 0, 0};
+  if (AL == A_CONV && !VEC) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t k = kbeg + 4 * (tid % KQ) + j;
+      sc[j] = (int)(k % cg.C);
+      const int t = (int)(k / cg.C);
+      skw[j] = t % cg.KW;
+      skh[j] = t / cg.KW;
+    }
+  }
 
   // loaded tiles stay float4 until the LDS store (no register shuffles, so no
   // early vmcnt wait: the global loads overlap the MFMAs of the current tile)
@@ -166,17 +179,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
           float sv[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float val = 0.f;
-            const int64_t kk = gk + j;
-            if (cbase[p] >= 0 && kk < kend) {
-              const int c = (int)(kk % cg.C);
-              const int t = (int)(kk / cg.C);
-              const int kw = t % cg.KW, kh = t / cg.KW;
-              const int ih = cih[p] + kh * cg.dh, iw = ciw[p] + kw * cg.dw;
-              if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W)
-                val = A[cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + c];
-            }
-            sv[j] = val;
+            const int ih = cih[p] + skh[j] * cg.dh, iw = ciw[p] + skw[j] * cg.dw;
+            const bool inb = cbase[p] >= 0 && gk + j < kend && ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W;
+            const float* src = inb ? A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + sc[j] : A;
+            const float val = *src;
+            sv[j] = inb ? val : 0.f;
           }
           ra[p] = make_float4(sv[0], sv[1], sv[2], sv[3]);
         }
@@ -189,6 +196,19 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
         if (++kkw == cg.KW) {
           kkw = 0;
           ++kkh;
+        }
+      }
+    }
+    if (AL == A_CONV && !VEC) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sc[j] += BK;
+        while (sc[j] >= cg.C) {
+          sc[j] -= cg.C;
+          if (++skw[j] == cg.KW) {
+            skw[j] = 0;
+            ++skh[j];
+          }
         }
       }
     }
