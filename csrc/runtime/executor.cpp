@@ -499,6 +499,8 @@ bool Program::graphable(const Plan& p) const {
       if (hi < 0 || hi >= static_cast<int>(st.in_info.size())) continue;
       if (!st.in_info[hi]->value) return false;
     }
+    // scalar operands read on the host at run time when not constant
+    if (op == "Fill" && st.in_info.size() > 1 && !st.in_info[1]->value) return false;
   }
   return !p.steps.empty();
 }
