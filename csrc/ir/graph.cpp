@@ -12,6 +12,7 @@ OpRegistry& OpRegistry::get() {
     register_array_ops(*reg);
     register_math_ops(*reg);
     register_nn_ops(*reg);
+    register_extra_ops(*reg);
     return reg;
   }();
   return *r;

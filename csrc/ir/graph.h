@@ -98,6 +98,7 @@ class OpRegistry {
 void register_array_ops(OpRegistry& r);
 void register_math_ops(OpRegistry& r);
 void register_nn_ops(OpRegistry& r);
+void register_extra_ops(OpRegistry& r);
 
 struct InferCtx {
   const Node& node;

@@ -56,6 +56,9 @@ bool is_cmp(k::BinOp op) {
          op == k::BinOp::GT || op == k::BinOp::GE || op == k::BinOp::LAND || op == k::BinOp::LOR;
 }
 
+}  // namespace
+
+// shared with ops_extra.cpp (ClipByValue)
 void gpu_binary(ExecCtx& c, k::BinOp op, const at::Tensor& a0, const at::Tensor& b0) {
   at::Tensor a = materialize(c, a0), b = materialize(c, b0);
   const auto& od = c.out_shape().dims;
@@ -81,6 +84,8 @@ void gpu_binary(ExecCtx& c, k::BinOp op, const at::Tensor& a0, const at::Tensor&
   k::binary(op, dt, a.data_ptr(), b.data_ptr(), out.data_ptr(), n, mode, inner,
             mode == 4 ? &bc : nullptr, stream_of(c));
 }
+
+namespace {
 
 OpDef make_binary(k::BinOp op) {
   OpDef d;

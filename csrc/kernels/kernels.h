@@ -131,6 +131,40 @@ struct ResizeArgs {
 };
 void resize_bilinear(DType dt, const ResizeArgs& a, hipStream_t s);  // output f32
 void resize_nearest(int64_t elem_size, const ResizeArgs& a, hipStream_t s);
+// ------------------------------------------------------------ wider op set (extra.hip)
+// Pad / PadV2 (mode 0, constant = cbits reinterpreted as the element) and
+// MirrorPad (mode 1 REFLECT, 2 SYMMETRIC); in_strides in elements
+struct PadArgs {
+  int rank = 0, mode = 0;
+  int64_t out_dims[kMaxRank], in_dims[kMaxRank], in_strides[kMaxRank], before[kMaxRank];
+};
+void pad_nd(int64_t elem_size, const PadArgs& a, const void* x, void* y, uint64_t cbits, hipStream_t s);
+// cumulative sum / product along the middle dim of [outer, n, inner]
+void scan(bool prod, DType dt, const void* x, void* y, int64_t outer, int64_t n, int64_t inner, bool exclusive,
+          bool reverse, hipStream_t s);
+void leaky_relu(DType dt, const void* x, void* y, int64_t n, double alpha, hipStream_t s);
+struct DepthwiseArgs {
+  int64_t N, H, W, C, M, KH, KW, OH, OW, sh, sw, dh, dw, pad_t, pad_l;
+  const void* x; const void* w; void* y;
+};
+void depthwise_conv2d_nhwc(const DepthwiseArgs& a, hipStream_t s);  // f32
+void lrn(DType dt, const void* x, void* y, int64_t n, int64_t C, int radius, double bias, double alpha, double beta,
+         hipStream_t s);
+struct GatherNdArgs {
+  int K = 0;
+  int64_t dims[kMaxRank], strides[kMaxRank];  // strides in units of `inner` slices
+};
+void gather_nd(int64_t elem_size, DType idt, const void* params, const void* idx, void* out, int64_t nidx,
+               int64_t inner, const GatherNdArgs& a, hipStream_t s);
+struct WhereArgs {
+  int rank = 0;
+  int64_t dims[kMaxRank];
+};
+// pos = inclusive prefix count of mask (int64); where_coords writes [count, rank]
+void mask_prefix(const uint8_t* mask, int64_t* pos, int64_t n, hipStream_t s);
+void where_coords(const uint8_t* mask, const int64_t* pos, int64_t* out, int64_t n, const WhereArgs& a,
+                  hipStream_t s);
+
 // y = x * scale[c] + shift[c] (+relu), channel = last dim
 void channel_affine(DType dt, const void* x, const void* scale, const void* shift, void* y,
                     int64_t n, int64_t C, int act, hipStream_t s);

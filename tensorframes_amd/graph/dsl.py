@@ -925,6 +925,83 @@ def unstack(value, num=None, axis=0, name="unstack"):
     return op.outputs
 
 
+def pad(tensor, paddings, mode="CONSTANT", constant_values=0, name=None):
+    x = convert_to_tensor(tensor)
+    pads = np.asarray(paddings, dtype=np.int32) if not isinstance(paddings, Tensor) else paddings
+    mode = mode.upper()
+    if mode == "CONSTANT":
+        if constant_values == 0:
+            return _op("Pad", [("input", x), ("paddings", pads)],
+                       {"T": P.AttrValue.type(x.dtype), "Tpaddings": P.AttrValue.type(int32)}, name or "Pad",
+                       out_dtypes=[x.dtype]).outputs[0]
+        return _op("PadV2", [("input", x), ("paddings", pads),
+                             ("constant_values", np.asarray(constant_values, dtype=x.dtype.as_numpy_dtype))],
+                   {"T": P.AttrValue.type(x.dtype), "Tpaddings": P.AttrValue.type(int32)}, name or "PadV2",
+                   out_dtypes=[x.dtype]).outputs[0]
+    if mode not in ("REFLECT", "SYMMETRIC"):
+        raise ValueError(f"Unknown padding mode: {mode}")
+    return _op("MirrorPad", [("input", x), ("paddings", pads)],
+               {"T": P.AttrValue.type(x.dtype), "Tpaddings": P.AttrValue.type(int32),
+                "mode": P.AttrValue.s(mode)}, name or "MirrorPad", out_dtypes=[x.dtype]).outputs[0]
+
+
+def split(value, num_or_size_splits, axis=0, num=None, name="split"):
+    x = convert_to_tensor(value)
+    if isinstance(num_or_size_splits, int):
+        n = num_or_size_splits
+        op = _op("Split", [("split_dim", np.int32(axis)), ("value", x)],
+                 {"T": P.AttrValue.type(x.dtype), "num_split": P.AttrValue.i(n)}, name, n_out=n,
+                 out_dtypes=[x.dtype] * n)
+        return op.outputs
+    sizes = np.asarray(num_or_size_splits, dtype=np.int32).reshape(-1)
+    n = int(num if num is not None else sizes.size)
+    op = _op("SplitV", [("value", x), ("size_splits", sizes), ("split_dim", np.int32(axis))],
+             {"T": P.AttrValue.type(x.dtype), "Tlen": P.AttrValue.type(int32), "num_split": P.AttrValue.i(n)},
+             name, n_out=n, out_dtypes=[x.dtype] * n)
+    return op.outputs
+
+
+def _scan(op_type, x, axis, exclusive, reverse, name):
+    x = convert_to_tensor(x)
+    return _op(op_type, [("x", x), ("axis", np.int32(axis))],
+               {"T": P.AttrValue.type(x.dtype), "Tidx": P.AttrValue.type(int32),
+                "exclusive": P.AttrValue.b(exclusive), "reverse": P.AttrValue.b(reverse)}, name,
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+def cumsum(x, axis=0, exclusive=False, reverse=False, name=None):
+    return _scan("Cumsum", x, axis, exclusive, reverse, name)
+
+
+def cumprod(x, axis=0, exclusive=False, reverse=False, name=None):
+    return _scan("Cumprod", x, axis, exclusive, reverse, name)
+
+
+def clip_by_value(t, clip_value_min, clip_value_max, name=None):
+    x = convert_to_tensor(t)
+    return _op("ClipByValue", [("t", x), ("clip_value_min", clip_value_min), ("clip_value_max", clip_value_max)],
+               {"T": P.AttrValue.type(x.dtype)}, name, out_dtypes=[x.dtype], dtype_hint=x.dtype).outputs[0]
+
+
+def reverse(tensor, axis, name=None):
+    x = convert_to_tensor(tensor)
+    return _op("ReverseV2", [("tensor", x), ("axis", np.asarray(axis, dtype=np.int32).reshape(-1))],
+               {"T": P.AttrValue.type(x.dtype), "Tidx": P.AttrValue.type(int32)}, name,
+               out_dtypes=[x.dtype]).outputs[0]
+
+
+reverse_v2 = reverse
+
+
+def gather_nd(params, indices, name=None):
+    p = convert_to_tensor(params)
+    i = convert_to_tensor(indices) if isinstance(indices, Tensor) else convert_to_tensor(
+        np.asarray(indices, dtype=np.int32))
+    return _op("GatherNd", [("params", p), ("indices", i)],
+               {"Tparams": P.AttrValue.type(p.dtype), "Tindices": P.AttrValue.type(i.dtype)}, name,
+               out_dtypes=[p.dtype]).outputs[0]
+
+
 def concat(values, axis, name="concat"):
     dt = _first_dtype(*values) or _to_numpy(values[0], None)[1]
     return _op("ConcatV2", [("values", list(values)), ("axis", np.int32(axis) if not isinstance(axis, Tensor) else axis)],
@@ -1108,6 +1185,37 @@ class _NN:
                     "use_cudnn_on_gpu": P.AttrValue.b(use_cudnn_on_gpu),
                     "dilations": P.AttrValue.ilist(dilations)}, name, out_dtypes=[x.dtype],
                    dtype_hint=x.dtype).outputs[0]
+
+    @staticmethod
+    def depthwise_conv2d_native(input, filter, strides, padding, data_format="NHWC",  # noqa: A002
+                                dilations=(1, 1, 1, 1), name=None):
+        x = convert_to_tensor(input)
+        return _op("DepthwiseConv2dNative", [("input", x), ("filter", filter)],
+                   {"T": P.AttrValue.type(x.dtype), "strides": P.AttrValue.ilist(strides),
+                    "padding": P.AttrValue.s(padding), "data_format": P.AttrValue.s(data_format),
+                    "dilations": P.AttrValue.ilist(dilations)}, name, out_dtypes=[x.dtype],
+                   dtype_hint=x.dtype).outputs[0]
+
+    @staticmethod
+    def depthwise_conv2d(input, filter, strides, padding, rate=None, name=None, data_format="NHWC"):  # noqa: A002
+        r = [1, 1] if rate is None else list(rate)
+        return _NN.depthwise_conv2d_native(input, filter, strides, padding, data_format,
+                                           [1, r[0], r[1], 1], name or "depthwise")
+
+    @staticmethod
+    def leaky_relu(features, alpha=0.2, name=None):
+        x = convert_to_tensor(features)
+        return _op("LeakyRelu", [("features", x)], {"T": P.AttrValue.type(x.dtype), "alpha": P.AttrValue.f(alpha)},
+                   name, out_dtypes=[x.dtype]).outputs[0]
+
+    @staticmethod
+    def local_response_normalization(input, depth_radius=5, bias=1.0, alpha=1.0, beta=0.5, name=None):  # noqa: A002
+        x = convert_to_tensor(input)
+        return _op("LRN", [("input", x)], {"T": P.AttrValue.type(x.dtype), "depth_radius": P.AttrValue.i(depth_radius),
+                                           "bias": P.AttrValue.f(bias), "alpha": P.AttrValue.f(alpha),
+                                           "beta": P.AttrValue.f(beta)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+    lrn = local_response_normalization
 
     @staticmethod
     def max_pool(value, ksize, strides, padding, data_format="NHWC", name=None):

@@ -295,3 +295,37 @@ def test_cast_float_to_uint8_truncates():
     assert gpu[1].tolist() == [False, True, True, True]
     for a, b in zip(gpu, cpu):
         torch.testing.assert_close(a, b)
+
+
+def test_extra_ops_gpu_vs_cpu():
+    """Pad/MirrorPad, Split(V), Cumsum/Cumprod (row-block scan incl. chunk
+    carry, and the strided-line path), LeakyRelu, ClipByValue, ReverseV2,
+    DepthwiseConv2dNative, LRN, GatherNd: HIP kernels vs the CPU executor."""
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 700], name="x")
+        img = tf.placeholder(tf.float32, [None, 13, 11, 8], name="img")
+        ii = tf.placeholder(tf.int64, [None, 700], name="ii")
+        tf.pad(x, [[1, 2], [3, 0]], constant_values=-2.0, name="pad")
+        tf.pad(img, [[0, 0], [2, 1], [1, 3], [0, 0]], mode="REFLECT", name="refl")
+        tf.pad(img, [[0, 0], [1, 1], [3, 2], [0, 0]], mode="SYMMETRIC", name="sym")
+        tf.identity(tf.split(x, [100, -1, 50], axis=1)[1], name="split")
+        tf.cumsum(x, 1, name="cs")
+        tf.cumsum(x, 1, exclusive=True, reverse=True, name="cser")
+        tf.cumsum(ii, 1, name="csi")
+        tf.cumprod(x * 0.001 + 1.0, 0, name="cp")
+        tf.nn.leaky_relu(x, 0.3, name="lr")
+        tf.clip_by_value(x, -0.25, 0.5, name="clip")
+        tf.reverse(img, [1, 3], name="rev")
+        w = np.random.default_rng(2).standard_normal((3, 3, 8, 2)).astype(np.float32)
+        tf.identity(tf.nn.depthwise_conv2d(img, tf.constant(w), [1, 2, 2, 1], "SAME"), name="dw")
+        tf.nn.lrn(img, depth_radius=2, bias=1.0, alpha=0.5, beta=0.75, name="lrn")
+        tf.gather_nd(img, tf.constant(np.array([[0, 1, 2], [2, 12, 10], [1, 0, 0]], np.int32)), name="gnd")
+    x_ = rng.standard_normal((37, 700)).astype(np.float32)
+    img_ = rng.standard_normal((3, 13, 11, 8)).astype(np.float32)
+    ii_ = rng.integers(-5, 5, (37, 700))
+    names = ["pad", "refl", "sym", "split", "cs", "cser", "csi", "cp", "lr", "clip", "rev", "dw", "lrn", "gnd"]
+    gpu, cpu = both(g, names, {"x": x_, "img": img_, "ii": ii_})
+    for n, a, b in zip(names, gpu, cpu):
+        assert a.shape == b.shape, n
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-4, msg=n)
