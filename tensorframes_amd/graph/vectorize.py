@@ -29,7 +29,7 @@ _UNARY = {
     "Abs", "Neg", "Square", "Sqrt", "Rsqrt", "Exp", "Expm1", "Log", "Log1p", "Reciprocal", "Inv", "Relu",
     "Relu6", "Elu", "Selu", "Sigmoid", "Tanh", "Softplus", "Softsign", "Floor", "Ceil", "Round", "Rint",
     "Sign", "Sin", "Cos", "Tan", "Erf", "LogicalNot", "IsNan", "IsInf", "IsFinite", "Cast", "Identity",
-    "StopGradient", "Snapshot", "PreventGradient", "CheckNumerics", "ZerosLike", "OnesLike",
+    "StopGradient", "Snapshot", "PreventGradient", "CheckNumerics", "ZerosLike", "OnesLike", "LeakyRelu",
 }
 _BINARY = {
     "Add", "AddV2", "Sub", "Mul", "Div", "RealDiv", "FloorDiv", "FloorMod", "TruncateDiv", "TruncateMod",
@@ -148,7 +148,7 @@ def _lift(gdef, fetches, feeds, infos, patch_only=False):
         m = P.NodeDef(nd.name, op, list(nd.input), dict(nd.attr), nd.device)
         if op in _UNARY:
             pass
-        elif op in _BINARY or op in ("Select", "SelectV2", "AddN"):
+        elif op in _BINARY or op in ("Select", "SelectV2", "AddN", "ClipByValue"):
             if op == "BiasAdd" and nd.attr.get("data_format") and nd.attr["data_format"].value == b"NCHW":
                 raise _Refuse("BiasAdd NCHW")
             ranks = [rank(n, i) for n, i in data_ins]
@@ -224,6 +224,20 @@ def _lift(gdef, fetches, feeds, infos, patch_only=False):
                 raise _Refuse("pack of batched and constant parts")
             ax = nd.attr["axis"].value if "axis" in nd.attr else 0
             m.attr["axis"] = P.AttrValue.i(ax + 1 if ax >= 0 else ax)
+        elif op in ("Cumsum", "Cumprod", "ReverseV2"):
+            if bflags[1]:
+                raise _Refuse(f"data-dependent {op} axis")
+            m.input = shifted_const(nd, 1, lambda a: shift_axes(a, 0))
+        elif op in ("Pad", "PadV2", "MirrorPad"):
+            if any(bflags[1:]):
+                raise _Refuse("data-dependent padding")
+            m.input = shifted_const(nd, 1, lambda p: np.concatenate(
+                [np.zeros((1, 2), np.asarray(p).dtype), np.asarray(p).reshape(-1, 2)]).astype(np.asarray(p).dtype))
+        elif op in ("Split", "SplitV"):
+            ax_i = 0 if op == "Split" else 2
+            if any(b for k, b in enumerate(bflags) if k != (1 if op == "Split" else 0)):
+                raise _Refuse("data-dependent split")
+            m.input = shifted_const(nd, ax_i, lambda a: shift_axes(a, 0))
         elif op == "MatMul":
             # cell [m,k] x const [k,n] -> batched [B,m,k] x [k,n]
             if bflags[1] or rank(*data_ins[0]) != 2 or nd.attr.get("transpose_a") and nd.attr["transpose_a"].value:

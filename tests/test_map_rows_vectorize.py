@@ -54,7 +54,14 @@ def g_pack_cast(v, s):
     return tf.cast(tf.stack([s, s * 2.0]) > 3.0, tf.int32, name="o")
 
 
-LIFTABLE = [g_add, g_mix, g_reduce, g_argmax, g_softmax, g_expand_transpose, g_matmul, g_pack_cast]
+def g_extra_ops(v, s):
+    y = tf.pad(tf.nn.leaky_relu(v, 0.3), [[1, 2]], mode="REFLECT")
+    a, b = tf.split(tf.cumsum(y, 0, reverse=True), [3, -1], 0)
+    return tf.add(tf.reduce_sum(tf.clip_by_value(tf.reverse(b, [0]), -1.0, 1.0), [0]), tf.reduce_max(a, [0]),
+                  name="o")
+
+
+LIFTABLE = [g_add, g_mix, g_reduce, g_argmax, g_softmax, g_expand_transpose, g_matmul, g_pack_cast, g_extra_ops]
 
 
 def _run(builder, df, vectorize):
