@@ -417,7 +417,10 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
   g.M = M; g.N = N; g.K = K;
   g.A = a.data_ptr(); g.lda = a.size(-1); g.strideA = bstride(a);
   g.B = b.data_ptr(); g.ldb = b.size(-1); g.strideB = bstride(b);
-  g.C = out.data_ptr(); g.ldc = N; g.strideC = M * N;
+  // `out` may be a column slice of a wider [M, *] tensor (concat write-into-slice)
+  const int64_t ldc = (out.dim() >= 2 && batch == 1) ? out.stride(-2) : N;
+  TFA_CHECK(out.stride(-1) == 1 && (batch == 1 || out.is_contiguous()), "MatMul: unsupported output layout");
+  g.C = out.data_ptr(); g.ldc = ldc; g.strideC = M * N;
   g.ta = ta; g.tb = tb;
   g.bias = bias ? bias->data_ptr() : nullptr;
   g.act = act;

@@ -117,6 +117,11 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
   a.x = x.data_ptr(); a.w = w.data_ptr(); a.y = out.data_ptr();
   a.bias = bias ? bias->data_ptr() : nullptr;
   a.act = act;
+  // `out` may be a channel slice of a wider NHWC tensor (concat write-into-slice)
+  TFA_CHECK(out.stride(3) == 1 && out.stride(1) == out.size(2) * out.stride(2) &&
+                out.stride(0) == out.size(1) * out.stride(1),
+            "Conv2D: output must be NHWC-contiguous up to the channel stride");
+  a.ldc = out.stride(2);
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
     work = at::empty({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));

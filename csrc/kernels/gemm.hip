@@ -502,7 +502,7 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
   g.K = a.KH * a.KW * a.C;
   g.A = a.x; g.lda = a.C; g.strideA = 0;
   g.B = a.w; g.ldb = a.OC; g.strideB = 0;
-  g.C = a.y; g.ldc = a.OC; g.strideC = 0;
+  g.C = a.y; g.ldc = a.ldc > 0 ? a.ldc : a.OC; g.strideC = 0;
   g.ta = false; g.tb = false;
   g.bias = a.bias;
   g.act = a.act;

@@ -113,6 +113,7 @@ struct ConvArgs {
   const void* x; const void* w; void* y;
   const void* bias; int act;
   void* workspace = nullptr;
+  int64_t ldc = 0;  // output pixel stride in elements (0 = OC; > OC writes a channel slice)
 };
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a);
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s);

@@ -62,6 +62,14 @@ struct Program::Step {
   int bias_slot = -1;
   int act = 0;
   std::vector<int> release;  // slots dropped after the step
+  // write-into-slice (GPU): a GEMM/CONV step whose only consumer is a
+  // last-axis ConcatV2 writes straight into its channel range of the concat
+  // output (allocated by the first such producer); the concat then copies
+  // only the remaining inputs
+  int alias_slot = -1;           // producer: concat output slot
+  int64_t alias_offset = 0;      // producer: first channel in the concat output
+  const TensorInfo* alias_info = nullptr;  // producer: concat output info
+  std::vector<char> preplaced;   // concat: per value input, already written in place
 };
 
 struct Program::Plan {
@@ -366,6 +374,48 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
   }
   for (auto& f : fetches_) p->fetch_slots.push_back(slot_for(f));
 
+  // write-into-slice for last-axis ConcatV2 of f32 GEMM/CONV outputs
+  {
+    std::map<int, size_t> step_of_out;  // slot -> producing step
+    for (size_t i = 0; i < p->steps.size(); ++i)
+      for (int s : p->steps[i].out_slots) step_of_out[s] = i;
+    for (size_t ci = 0; ci < p->steps.size(); ++ci) {
+      Step& cs = p->steps[ci];
+      const Node& cn = g_->node(cs.node);
+      if (cs.kind != Step::OP || cn.op != "ConcatV2" || cs.in_slots.size() < 3) continue;
+      const TensorInfo& oi = cs.out_info[0];
+      const int nv = static_cast<int>(cs.in_slots.size()) - 1;
+      const TensorInfo* ax = cs.in_info[nv];
+      if (!ax->value || oi.dtype != DType::F32 || !oi.shape.fully_known() || oi.shape.rank() < 2) continue;
+      const int64_t axis = to_int_vector(*ax->value)[0];
+      if (axis != -1 && axis != oi.shape.rank() - 1) continue;
+      cs.preplaced.assign(nv, 0);
+      int64_t off = 0;
+      for (int v = 0; v < nv; ++v) {
+        const int slot = cs.in_slots[v];
+        const TensorInfo* vi = cs.in_info[v];
+        const int64_t len = vi->shape.dims.back();
+        auto it = step_of_out.find(slot);
+        if (it != step_of_out.end()) {
+          Step& ps = p->steps[it->second];
+          const TensorRef out_ref{ps.out_node, 0};
+          const bool single_use = uses[out_ref] == 1 && !fetched.count(out_ref);
+          if ((ps.kind == Step::CONV || ps.kind == Step::GEMM) && single_use && ps.alias_slot < 0 &&
+              ps.out_info[0].dtype == DType::F32) {
+            ps.alias_slot = cs.out_slots[0];
+            ps.alias_offset = off;
+            ps.alias_info = &cs.out_info[0];
+            cs.preplaced[v] = 1;
+          }
+        }
+        off += len;
+      }
+      bool any = false;
+      for (char c : cs.preplaced) any = any || c;
+      if (!any) cs.preplaced.clear();
+    }
+  }
+
   // liveness: release each slot after its last reading step (fetches/consts are kept)
   std::vector<int> last(p->nslots, -1);
   for (size_t i = 0; i < p->steps.size(); ++i) {
@@ -425,8 +475,34 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
       std::unique_ptr<RangeGuard> rg;
       if (gpu) rg = std::make_unique<RangeGuard>(nd.op + ":" + nd.name);
       try {
-        if (st.kind == Step::OP) {
+        if (st.kind == Step::OP && gpu && !st.preplaced.empty()) {
+          // concat whose producers wrote in place: copy only the other inputs
+          at::Tensor& out = slots[st.out_slots[0]];
+          TFA_CHECK(out.defined(), "internal: concat output not allocated by its producers");
+          int64_t off = 0;
+          const int64_t ax = out.dim() - 1;
+          for (size_t v = 0; v < st.preplaced.size(); ++v) {
+            const int64_t len = c.in[v].size(ax);
+            if (!st.preplaced[v] && len > 0) gpu_copy(c.in[v], out.narrow(ax, off, len), stream_of(c));
+            off += len;
+          }
+          c.out[0] = out;
+        } else if (st.kind == Step::OP) {
           reg.find(nd.op)->compute(c);
+        } else if (gpu && st.alias_slot >= 0) {
+          at::Tensor& whole = slots[st.alias_slot];
+          if (!whole.defined())
+            whole = at::empty(dims_or_throw(st.alias_info->shape, "concat output"),
+                              at::TensorOptions().dtype(at::kFloat).device(dev));
+          at::Tensor out = whole.narrow(whole.dim() - 1, st.alias_offset, st.out_info[0].shape.dims.back());
+          at::Tensor bias;
+          if (st.bias_slot >= 0) bias = slots[st.bias_slot];
+          const at::Tensor* bp = st.bias_slot >= 0 ? &bias : nullptr;
+          if (st.kind == Step::GEMM)
+            run_gemm(c, c.in[0], c.in[1], nd.attr_b("transpose_a", false), nd.attr_b("transpose_b", false), bp, st.act, out);
+          else
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out);
+          c.out[0] = out;
         } else {
           at::Tensor out = gpu ? c.alloc_out(0) : at::Tensor();
           at::Tensor bias;
@@ -710,6 +786,12 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs) {
     if (st.out_node != st.node) os << " -> " << g_->node(st.out_node).name;
     if (st.bias_slot >= 0) os << " +bias";
     if (st.act) os << (st.act == 1 ? " +relu" : " +relu6");
+    if (st.alias_slot >= 0) os << " ->concat-slice@" << st.alias_offset;
+    if (!st.preplaced.empty()) {
+      int n = 0;
+      for (char c : st.preplaced) n += c;
+      os << " (" << n << " inputs written in place)";
+    }
     os << ' ' << st.out_info[0].shape.str() << '\n';
   }
   return os.str();

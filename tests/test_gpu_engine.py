@@ -108,3 +108,36 @@ def test_hip_graph_replay_matches_eager_and_outputs_do_not_alias():
     for o, r in zip(outs, refs):
         for a, b in zip(o, r):
             torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-4)
+
+
+def test_concat_write_into_slice_matches_cpu():
+    """Inception-style block: conv branches (+bias+relu) concatenated on the
+    channel axis write straight into the concat output; a pooled branch and
+    a reused branch are copied. Result must equal the CPU executor."""
+    import numpy as np
+    from tensorframes_amd import engine, tf
+    r = np.random.default_rng(9)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 9, 9, 16], name="x")
+
+        def conv(t, oc, k):
+            w = tf.constant((r.standard_normal((k, k, t.get_shape().as_list()[-1], oc)) * 0.1).astype(np.float32))
+            b = tf.constant(r.standard_normal(oc).astype(np.float32))
+            return tf.nn.relu(tf.nn.bias_add(tf.nn.conv2d(t, w, [1, 1, 1, 1], "SAME"), b))
+        a = conv(x, 12, 1)
+        b = conv(conv(x, 8, 1), 20, 3)
+        shared = conv(x, 4, 1)
+        p = tf.nn.avg_pool(x, [1, 3, 3, 1], [1, 1, 1, 1], "SAME")
+        cat = tf.concat([a, b, p, shared], 3)
+        tf.identity(cat, name="y")
+        tf.identity(shared * 2.0, name="z")  # `shared` has two consumers: not aliased
+    prog = engine.program(g.serialize(), ["y", "z"], ["x"])
+    x_ = torch.randn((3, 9, 9, 16))
+    dev = torch.device("cuda", 0)
+    plan = prog.describe([x_.to(dev)])
+    assert plan.count("->concat-slice@") == 2 and "(2 inputs written in place)" in plan
+    gpu = engine.run_program(prog, [x_.to(dev)], dev)
+    cpu = engine.run_program(prog, [x_], torch.device("cpu"))
+    for a_, b_ in zip(gpu, cpu):
+        torch.testing.assert_close(a_.cpu(), b_, rtol=1e-4, atol=1e-4)
