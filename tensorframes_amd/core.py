@@ -691,7 +691,19 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
                 continue
             ins = _dense_inputs(b, cols, "reduce_blocks")
             on_device = all(t.is_cuda for t in ins)
-            res[pid] = engine.run_program(prog, ins, ins[0].device if on_device else None)
+            chunk = engine.chunk_rows_for(ins)
+            if not on_device and engine.gpu_available() and b.nrows > 2 * chunk:
+                # a host partition bigger than the staging budget streams through
+                # HBM chunk by chunk; the partials are folded by the same graph
+                # (the associativity contract of reduce_blocks)
+                dev = engine.compute_device()
+                parts = [engine.run_program(prog, [t[a:a + chunk] for t in ins], dev)
+                         for a in range(0, b.nrows, chunk)]
+                stacked = [torch.stack([p[j] for p in parts], 0) for j in range(len(parts[0]))]
+                res[pid] = engine.run_program(prog, stacked, dev)
+                metrics.add("reduce_blocks_chunks", len(parts))
+            else:
+                res[pid] = engine.run_program(prog, ins, ins[0].device if on_device else None)
         return res
     per_part = faults.with_retries("reduce_blocks", task)(dframe.local_blocks())
     for pid in sorted(per_part):

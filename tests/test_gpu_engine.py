@@ -141,3 +141,25 @@ def test_concat_write_into_slice_matches_cpu():
     cpu = engine.run_program(prog, [x_], torch.device("cpu"))
     for a_, b_ in zip(gpu, cpu):
         torch.testing.assert_close(a_.cpu(), b_, rtol=1e-4, atol=1e-4)
+
+
+def test_reduce_blocks_streams_large_host_partitions():
+    """A host partition larger than the staging budget is reduced chunk by
+    chunk on the GPU and the partials folded by the same graph."""
+    import numpy as np
+    import tensorframes_amd as tfs
+    from tensorframes_amd import tf
+    from tensorframes_amd.utils.logging import metrics
+    x = np.random.default_rng(4).standard_normal((100_000, 64)).astype(np.float32)
+    df = tfs.from_columns({"x": x}, num_partitions=1)
+    old = tfs.config.chunk_bytes
+    tfs.set_config(chunk_bytes=1 << 20)
+    try:
+        before = metrics.snapshot().get("reduce_blocks_chunks", 0)
+        with tf.Graph().as_default():
+            xi = tf.placeholder(tf.float32, [None, 64], name="x_input")
+            s, mx = tfs.reduce_blocks([tf.reduce_sum(xi, [0], name="x")], df), None
+        assert metrics.snapshot().get("reduce_blocks_chunks", 0) - before >= 6
+    finally:
+        tfs.set_config(chunk_bytes=old)
+    np.testing.assert_allclose(s, x.astype(np.float64).sum(0), rtol=1e-4, atol=1e-2)
