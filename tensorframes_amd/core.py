@@ -691,7 +691,9 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
                 continue
             ins = _dense_inputs(b, cols, "reduce_blocks")
             on_device = all(t.is_cuda for t in ins)
-            chunk = engine.chunk_rows_for(ins)
+            # reductions stage 8 pipeline chunks at a time: per-chunk overhead stays
+            # negligible and device memory bounded (1 GiB at the default chunk_bytes)
+            chunk = 8 * engine.chunk_rows_for(ins)
             if not on_device and engine.gpu_available() and b.nrows > 2 * chunk:
                 # a host partition bigger than the staging budget streams through
                 # HBM chunk by chunk; the partials are folded by the same graph
