@@ -23,7 +23,7 @@ STEPS=${STEPS:-"smoke tests bench"}
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 1200 python -m pytest tests -m gpu -x -q ;;
+    tests) run tests 1200 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -x -q ;;
     bench) run bench 900 python bench.py --steps ${BENCH_STEPS:-5} --warmup ${BENCH_WARMUP:-2} ${BENCH_ARGS:-} ;;
     benchsmall) run benchsmall 600 python bench.py --steps 3 --warmup 1 --rows 1000000 ;;
