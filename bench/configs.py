@@ -168,6 +168,7 @@ def cfg_inception(a):
           "value": images / dt, "unit": "images/s", "higher_is_better": True, "ms_per_step": dt * 1e3,
           "batch_per_partition": batch, "tflops": images * flops_per_image / dt / 1e12,
           "parallelism": f"dp{dist.world_size()}", "dtype": "fp32",
+          "compute_precision": a.precision,
           "data": "synthetic images generated in HBM; random-init frozen Inception-v3"})
 
 
@@ -213,7 +214,10 @@ def main():
     ap.add_argument("--parts-per-gpu", type=int, default=1)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--precision", choices=["f32", "bf16x3", "bf16"], default="f32",
+                    help="float32 MatMul/Conv2D compute mode (Config.precision); f32 = exact")
     a = ap.parse_args()
+    tfs.set_config(precision=a.precision)
     dist.init()
     if torch.cuda.is_available():
         torch.cuda.set_device(dist.local_rank() % torch.cuda.device_count())

@@ -16,8 +16,10 @@
 // Conv2D (NHWC, filter HWIO) uses the same core with an im2col-on-the-fly A
 // loader: A[m = (n,oh,ow)][k = (kh,kw,c)], B = filter viewed as [KH*KW*C, OC];
 // 1x1 stride-1 convs are plain GEMMs over x viewed as [N*H*W, C].
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "gemm_internal.h"
@@ -460,22 +462,68 @@ bool conv_is_pointwise(const ConvArgs& a) {
          a.OH == a.H && a.OW == a.W;
 }
 
+std::atomic<int>& precision_state() {
+  static std::atomic<int> mode([] {
+    const char* e = std::getenv("TFA_PRECISION");
+    if (!e) return 0;
+    if (!std::strcmp(e, "bf16")) return 1;
+    if (!std::strcmp(e, "bf16x3")) return 2;
+    return 0;
+  }());
+  return mode;
+}
+
+// bf16 paths: batch 1, 16-byte A rows (K % 4 / C % 4), no transposed A
+bool bf16_candidate(const GemmArgs& g) {
+  return f32_precision() != 0 && g.batch == 1 && !g.ta && g.lda % 4 == 0 && g.K % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(g.A) & 15) == 0;
+}
+
+GemmArgs conv_as_gemm(const ConvArgs& a) {
+  GemmArgs g{};
+  g.M = a.N * a.OH * a.OW;
+  g.N = a.OC;
+  g.K = a.KH * a.KW * a.C;
+  g.A = a.x; g.lda = a.C; g.strideA = 0;
+  g.B = a.w; g.ldb = a.OC; g.strideB = 0;
+  g.C = a.y; g.ldc = a.ldc > 0 ? a.ldc : a.OC; g.strideC = 0;
+  g.ta = false; g.tb = false;
+  g.bias = a.bias;
+  g.act = a.act;
+  g.batch = 1;
+  g.workspace = a.workspace;
+  return g;
+}
+
 }  // namespace
+
+void set_f32_precision(int mode) {
+  TFA_CHECK(mode >= 0 && mode <= 2, "precision mode must be 0 (f32), 1 (bf16) or 2 (bf16x3)");
+  precision_state().store(mode);
+}
+int f32_precision() { return precision_state().load(); }
 
 size_t gemm_workspace_bytes(DType dt, const GemmArgs& g) {
   if (dt != DType::F32 || g.M <= 0 || g.N <= 0) return 0;
+  if (bf16_candidate(g)) return bf16_workspace_bytes(f32_precision(), g.N, g.K);
   return f32_ws_bytes(g.M, g.N, g.K, g.batch);
 }
 
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a) {
   if (dt != DType::F32) return 0;
-  return f32_ws_bytes(a.N * a.OH * a.OW, a.OC, a.KH * a.KW * a.C, 1);
+  const GemmArgs g = conv_as_gemm(a);
+  if (bf16_candidate(g)) return bf16_workspace_bytes(f32_precision(), g.N, g.K);
+  return f32_ws_bytes(g.M, g.N, g.K, 1);
 }
 
 void gemm(DType dt, const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
   TFA_CHECK(g.K > 0, "gemm: K must be > 0");
   TFA_CHECK(g.A && g.B && g.C, "gemm: null operand");
+  if (dt == DType::F32 && bf16_candidate(g) && bf16_gemm_eligible(g, false, 0)) {
+    bf16_gemm_launch(f32_precision(), g, false, Im2colGeom{}, s);
+    return;
+  }
   if (dt == DType::F32) {
     // 16-byte vector loads need 4-float aligned rows on the contiguous side
     bool vec = al16(g.A) && al16(g.B) && g.lda % 4 == 0 && g.ldb % 4 == 0 &&
@@ -496,18 +544,16 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
   TFA_CHECK(dt == DType::F32, "conv2d: f32 only");
   TFA_CHECK(a.N > 0 && a.OH > 0 && a.OW > 0 && a.OC > 0, "conv2d: empty output");
   TFA_CHECK(a.H < (1 << 30) && a.W < (1 << 30) && a.C < (1 << 30), "conv2d: dims too large");
-  GemmArgs g{};
-  g.M = a.N * a.OH * a.OW;
-  g.N = a.OC;
-  g.K = a.KH * a.KW * a.C;
-  g.A = a.x; g.lda = a.C; g.strideA = 0;
-  g.B = a.w; g.ldb = a.OC; g.strideB = 0;
-  g.C = a.y; g.ldc = a.ldc > 0 ? a.ldc : a.OC; g.strideC = 0;
-  g.ta = false; g.tb = false;
-  g.bias = a.bias;
-  g.act = a.act;
-  g.batch = 1;
-  g.workspace = a.workspace;
+  GemmArgs g = conv_as_gemm(a);
+  if (bf16_candidate(g) && bf16_gemm_eligible(g, true, a.C)) {
+    Im2colGeom cg;
+    cg.H = (int)a.H; cg.W = (int)a.W; cg.C = (int)a.C; cg.KW = (int)a.KW;
+    cg.OH = (int)a.OH; cg.OW = (int)a.OW;
+    cg.sh = (int)a.sh; cg.sw = (int)a.sw; cg.dh = (int)a.dh; cg.dw = (int)a.dw;
+    cg.pt = (int)a.pad_t; cg.pl = (int)a.pad_l;
+    bf16_gemm_launch(f32_precision(), g, !conv_is_pointwise(a), cg, s);
+    return;
+  }
   if (conv_is_pointwise(a)) {  // 1x1/s1: x is already the [N*H*W, C] A matrix
     bool vec = al16(a.x) && al16(a.w) && a.C % 4 == 0 && a.OC % 4 == 0;
     run_f32(g, A_KCONTIG, vec, ConvGeom{}, s);

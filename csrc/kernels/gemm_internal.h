@@ -7,5 +7,15 @@ namespace tfa {
 namespace k {
 void gemm_f64_launch(const GemmArgs& g, hipStream_t s);
 void gemm_int_launch(DType dt, const GemmArgs& g, hipStream_t s);
+
+// implicit-GEMM conv geometry (NHWC input, filter viewed as [KH*KW*C, OC])
+struct Im2colGeom {
+  int H, W, C, KW, OH, OW, sh, sw, dh, dw, pt, pl;
+};
+
+// reduced-precision f32 GEMM on bf16 MFMA (gemm_bf16.hip); mode 1 = bf16, 2 = bf16x3
+size_t bf16_workspace_bytes(int mode, int64_t N, int64_t K);
+bool bf16_gemm_eligible(const GemmArgs& g, bool conv, int64_t conv_c);
+void bf16_gemm_launch(int mode, const GemmArgs& g, bool conv, const Im2colGeom& cg, hipStream_t s);
 }  // namespace k
 }  // namespace tfa

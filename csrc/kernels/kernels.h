@@ -102,6 +102,11 @@ struct GemmArgs {
 // bytes of scratch the launch needs (0 = none); allocate before the launch
 size_t gemm_workspace_bytes(DType dt, const GemmArgs& g);
 void gemm(DType dt, const GemmArgs& g, hipStream_t s);
+// Compute mode of float32 MatMul / Conv2D: 0 exact f32 (default), 1 bf16
+// operands, 2 bf16x3 (hi/lo split, ~16-bit operands); f32 accumulate in all.
+// Initial value from TFA_PRECISION (f32 | bf16 | bf16x3).
+void set_f32_precision(int mode);
+int f32_precision();
 
 // ------------------------------------------------------------ conv / pool (NHWC)
 struct ConvArgs {

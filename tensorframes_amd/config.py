@@ -43,6 +43,10 @@ class Config:
     collective_timeout_s: float = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_TIMEOUT_S", 600.0, float))
     # CPU executor: programs with fewer input elements run on one intra-op thread
     cpu_parallel_min_elems: int = dataclasses.field(default_factory=lambda: _env("TFA_CPU_PARALLEL_MIN_ELEMS", 4_000_000, int))
+    # float32 MatMul / Conv2D compute mode on the GPU: "f32" (exact, default),
+    # "bf16" (bf16 operands) or "bf16x3" (hi/lo bf16 split, ~16-bit operands);
+    # f32 accumulation and f32 tensors in every mode (kernels/gemm_bf16.hip)
+    precision: str = dataclasses.field(default_factory=lambda: _env("TFA_PRECISION", "f32", str))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 
@@ -57,3 +61,19 @@ def set_config(**kw):
         setattr(config, k, v)
     if "debug_sync" in kw:
         os.environ["TFA_DEBUG_SYNC"] = "1" if kw["debug_sync"] else "0"
+    if "precision" in kw:
+        apply_precision()
+
+
+PRECISION_MODES = {"f32": 0, "bf16": 1, "bf16x3": 2}
+
+
+def apply_precision():
+    """Push `config.precision` to the native kernel library and drop cached
+    plans (a captured HIP graph holds the kernels of the mode it was built in)."""
+    if config.precision not in PRECISION_MODES:
+        raise ValueError(f"precision must be one of {sorted(PRECISION_MODES)}, got {config.precision!r}")
+    from ._native import _C
+    from . import engine
+    _C.set_f32_precision(PRECISION_MODES[config.precision])
+    engine.clear_program_cache()

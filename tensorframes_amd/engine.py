@@ -90,6 +90,11 @@ def program(graph_bytes: bytes, fetches: Sequence[str], feeds: Sequence[str]):
     return p
 
 
+def clear_program_cache():
+    with _lock:
+        _prog_cache.clear()
+
+
 # ------------------------------------------------------------------ devices
 def gpu_available() -> bool:
     return config.device != "cpu" and torch.cuda.is_available()
