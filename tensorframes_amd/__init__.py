@@ -26,6 +26,7 @@ from .frame.column_info import (SHAPE_KEY, TYPE_KEY, ColumnInformation, DataFram
 from .frame.dataframe import (DataFrame, GroupedData, create_dataframe, createDataFrame, from_columns,
                               generate, tensor_field)
 from .frame.arrow_io import from_arrow, read_parquet, to_arrow, write_parquet
+from .frame.spark_io import from_spark, to_spark
 from .frame.checkpoint import read_checkpoint, write_checkpoint
 from .frame.dataframe import range_ as range  # noqa: A001
 from .frame.types import (ArrayType, BinaryType, DoubleType, FloatType, IntegerType, LongType, Row,

@@ -55,6 +55,8 @@ config = Config()
 
 
 def set_config(**kw):
+    if "precision" in kw and kw["precision"] not in PRECISION_MODES:
+        raise ValueError(f"precision must be one of {sorted(PRECISION_MODES)}, got {kw['precision']!r}")
     for k, v in kw.items():
         if not hasattr(config, k):
             raise AttributeError(f"unknown config key {k}")

@@ -83,6 +83,31 @@ class GraphSpec:
     dsl_fetches: Optional[list] = None
 
 
+def _frame(df):
+    """Spark DataFrames are accepted anywhere a DataFrame is: brought in through
+    Arrow with their tensor metadata (frame/spark_io.py)."""
+    from .frame import spark_io
+    if spark_io.is_spark_dataframe(df):
+        return spark_io.from_spark(df)
+    return df
+
+
+def _schema_frame(df):
+    """Like _frame, but only the schema is needed (block/row placeholders):
+    a Spark DataFrame is not collected."""
+    from .frame import spark_io
+    if spark_io.is_spark_dataframe(df):
+        return spark_io.from_spark(df.limit(0) if hasattr(df, "limit") else df, num_partitions=1)
+    return df
+
+
+def _grouped(gd):
+    from .frame import spark_io
+    if spark_io.is_spark_grouped(gd):
+        return spark_io.from_spark_grouped(gd)
+    return gd
+
+
 def _strip(name: str) -> str:
     return name[:-2] if name.endswith(":0") else name
 
@@ -236,6 +261,7 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
     the number of rows may differ from the input (reference:
     src/main/python/tensorframes/core.py:213-253; DebugRowOps.scala:305-393).
     """
+    dframe = _frame(dframe)
     spec = _resolve(fetches, graph, shape_hints)
     summary = analyze_graph(spec)
     inputs = [s for s in summary.values() if s.is_input]
@@ -352,6 +378,7 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
     Placeholders have the shape of one cell; `feed_dict` maps placeholder ->
     column (defaults to the placeholder's own name). Cells whose first dim is
     unknown may vary in length from row to row."""
+    dframe = _frame(dframe)
     spec = _resolve(fetches, graph, shape_hints)
     summary = analyze_graph(spec)
     inputs = [s for s in summary.values() if s.is_input]
@@ -673,6 +700,7 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     applied to every partition and then to the stack of partial results, so it
     must be associative (reference: core.py:255-291; DebugRowOps.scala:80-170,503-526).
     Sum/Min/Max/Prod over axis 0 take the native reduction + RCCL all-reduce path."""
+    dframe = _frame(dframe)
     spec = _resolve(fetches, graph, shape_hints)
     summary = analyze_graph(spec)
     out_names, in_names = _reduce_blocks_schema(dframe.schema, summary)
@@ -772,6 +800,7 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     (reference: core.py:138-173; DebugRowOps.scala:172-262,479-501).
     `x = x_1 (+|*|min|max) x_2` graphs run as one native block reduction per
     partition + an RCCL all-reduce."""
+    dframe = _frame(dframe)
     spec = _resolve(fetches, graph, shape_hints)
     summary = analyze_graph(spec)
     names = _reduce_rows_schema(dframe.schema, summary)
@@ -907,6 +936,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
     Rows are hash-partitioned by key across ranks (all-to-all), sorted by key
     on each rank, and Sum/Min/Max/Prod graphs run as one native segmented
     reduction over all keys; other graphs run once per key."""
+    grouped_data = _grouped(grouped_data)
     df = grouped_data.df
     keys = grouped_data.keys
     spec = _resolve(fetches, graph, shape_hints)
@@ -1001,6 +1031,7 @@ def analyze(dframe: DataFrame) -> DataFrame:
     schema metadata: the lead dim is the partition size when all non-empty
     partitions agree (else unknown), cell dims that vary become unknown
     (reference: src/main/scala/org/tensorframes/ExperimentalOperations.scala:35-157)."""
+    dframe = _frame(dframe)
     local = {}
     for pid, b in dframe.local_blocks().items():
         if b.nrows == 0:
@@ -1038,6 +1069,7 @@ def analyze(dframe: DataFrame) -> DataFrame:
 
 def print_schema(dframe: DataFrame):
     """Prints the schema with the tensor metadata (reference: DebugRowOps.scala:528-545)."""
+    dframe = _schema_frame(dframe)
     print(explain_schema(dframe.schema), end="")
 
 
@@ -1048,11 +1080,13 @@ def explain(dframe: DataFrame) -> str:
 def block(df: DataFrame, col_name: str, tf_name: Optional[str] = None):
     """Placeholder for blocks of column `col_name` (lead dim always unknown)
     (reference: src/main/python/tensorframes/core.py:338-351,368-391)."""
+    df = _schema_frame(df)
     return _auto_placeholder(df, col_name, tf_name, is_block=True)
 
 
 def row(df: DataFrame, col_name: str, tf_name: Optional[str] = None):
     """Placeholder for one cell of column `col_name` (reference: core.py:353-366)."""
+    df = _schema_frame(df)
     return _auto_placeholder(df, col_name, tf_name, is_block=False)
 
 
