@@ -34,6 +34,7 @@ from .frame.types import (ArrayType, BinaryType, DoubleType, FloatType, IntegerT
 from .graph import dsl as tf  # noqa: F401
 from .operations import Operations, Ops, ShapeDescription, convert_block_to_row, explain_detailed, ops
 from .graph import dsl
+from . import scala_dsl  # noqa: F401  (the Scala DSL vocabulary)
 from .parallel import dist
 from .utils.logging import initialize_logging, metrics
 from .utils.shape import Shape
