@@ -23,7 +23,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 import tensorframes_amd as tfs  # noqa: E402
-from tensorframes_amd import tf  # noqa: E402
+from tensorframes_amd import engine, tf  # noqa: E402
 from tensorframes_amd._native import _C  # noqa: E402
 from tensorframes_amd.frame.block import Block  # noqa: E402
 from tensorframes_amd.frame.types import ArrayType, FloatType, StructField, StructType  # noqa: E402
@@ -94,6 +94,54 @@ def cfg_plumbing(a):
         ms = timed(step, a.steps, a.warmup) * 1e3
     emit({"config": "1: 10-row double DF, map_blocks Add(+3), CPU plumbing", "metric": "latency",
           "value": ms, "unit": "ms/call", "higher_is_better": False, "device": "cpu"})
+
+
+def cfg_refperf(a):
+    """The reference's perf suites (all `ignore`d there, timings printed, never
+    recorded; src/test/scala/org/tensorframes/perf/*.scala):
+      PerformanceSuite:14-26        20M-row range DF, map_blocks x+x, then a sum, x10
+      ConvertPerformanceSuite:19-63 rows -> tensor, 10M Int scalar cells / one 10M vector
+      ConvertBackPerformanceSuite   tensor -> rows, 10M Int cells
+    Here the conversions are Arrow columns <-> block tensors (the engine's
+    columnar path) and Python Row objects -> frame (the boxed path)."""
+    import pyarrow as pa
+    n = a.rows or 20_000_000
+    nparts = max(1, dist.world_size()) * 4
+    df = tfs.range(n, num_partitions=nparts).cache()
+    df.local_blocks()
+    with tf.Graph().as_default():
+        x = tfs.block(df, "id", tf_name="id")
+        y = tf.add(x, x, name="y")
+    with tf.Graph().as_default():
+        yi = tf.placeholder(tf.int64, [None], name="y_input")
+        total = tf.reduce_sum(yi, [0], name="y")
+
+    def step():
+        out = tfs.map_blocks(y, df, trim=True)
+        s = tfs.reduce_blocks(total, out)
+        assert int(s) == n * (n - 1)
+    t_map = timed(step, a.steps, a.warmup)
+    # rows -> tensor: 10M int32 cells from an Arrow column (zero-copy block tensors)
+    cells = 10_000_000
+    col = pa.array(np.arange(cells, dtype=np.int32))
+    t_conv = timed(lambda: tfs.from_arrow(pa.table({"x": col}), 1).local_blocks(), a.steps, a.warmup)
+    vec = pa.FixedSizeListArray.from_arrays(col, cells)  # one 10M-element vector cell
+    t_conv_vec = timed(lambda: tfs.from_arrow(pa.table({"x": vec}), 1).local_blocks(), a.steps, a.warmup)
+    # tensor -> rows: 10M int32 cells back to an Arrow column
+    back = tfs.from_columns({"x": np.arange(cells, dtype=np.int32)}, num_partitions=1).cache()
+    back.local_blocks()
+    t_back = timed(lambda: back.to_arrow(), a.steps, a.warmup)
+    # boxed path: 1M Python Row objects -> frame
+    rows = [tfs.Row(x=i) for i in range(1_000_000)]
+    t_rows = timed(lambda: tfs.create_dataframe(rows, num_partitions=1).local_blocks(), 1, 0)
+    emit({"config": "reference perf suites (PerformanceSuite / Convert / ConvertBack)",
+          "map_blocks_x_plus_x_then_sum_20M_rows_ms": t_map * 1e3,
+          "map_blocks_x_plus_x_then_sum_rows_per_sec": n / t_map,
+          "convert_10M_int_cells_arrow_ms": t_conv * 1e3,
+          "convert_one_10M_vector_arrow_ms": t_conv_vec * 1e3,
+          "convert_back_10M_int_cells_arrow_ms": t_back * 1e3,
+          "convert_1M_python_rows_ms": t_rows * 1e3,
+          "device": str(engine.compute_device()), "data": "synthetic"})
 
 
 def cfg_add(a):
@@ -207,7 +255,7 @@ def cfg_kmeans(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["plumbing", "add", "reduce", "inception", "kmeans"])
+    ap.add_argument("config", choices=["plumbing", "add", "reduce", "inception", "kmeans", "refperf"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--rows", type=int, default=0)
@@ -223,7 +271,7 @@ def main():
         torch.cuda.set_device(dist.local_rank() % torch.cuda.device_count())
         dist.bind_numa()
     {"plumbing": cfg_plumbing, "add": cfg_add, "reduce": cfg_reduce, "inception": cfg_inception,
-     "kmeans": cfg_kmeans}[a.config](a)
+     "kmeans": cfg_kmeans, "refperf": cfg_refperf}[a.config](a)
     dist.shutdown()
 
 
