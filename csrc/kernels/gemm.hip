@@ -16,8 +16,11 @@
 // Conv2D (NHWC, filter HWIO) uses the same core with an im2col-on-the-fly A
 // loader: A[m = (n,oh,ow)][k = (kh,kw,c)], B = filter viewed as [KH*KW*C, OC];
 // 1x1 stride-1 convs are plain GEMMs over x viewed as [N*H*W, C].
+#include <array>
 #include <atomic>
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -376,28 +379,21 @@ struct F32Plan {
 };
 
 // measured (scripts/gemm_bench.py): 256x128 / 128x256 and BK=32 variants were slower on every shape
-constexpr int kTiles[5][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32}};
+// {BM, BN}; the N-widths 96/160/192 fit Inception-style channel counts without
+// padding a 128-wide tile (a 128 tile on N=96 computes 25% zeros)
+constexpr int kNumTiles = 9;
+constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
+                                      {128, 96}, {128, 192}, {128, 160}, {64, 192}};
 
-F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
-  // narrow N picks a narrow tile (a 128-wide tile on N=32 wastes 3/4 of the MFMAs)
-  int cfg = N <= 32 ? 4 : (N <= 64 ? 1 : 0);
-  auto blocks = [&](int c) {
-    return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
-  };
-  // too few blocks to fill 256 CUs twice: shrink the tile
-  if (blocks(cfg) < 512) {
-    if (cfg == 0) cfg = N > 96 ? 2 : 3;
-    else if (cfg == 1) cfg = 3;
-  }
-  static const int tile_env = [] {
-    const char* e = std::getenv("TFA_GEMM_TILE");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (tile_env >= 0 && tile_env < 5) cfg = tile_env;  // tuning override
+int64_t tile_blocks(int c, int64_t M, int64_t N, int64_t batch) {
+  return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
+}
+
+// the launch plan of tile `cfg`: split K when the grid is under one block per CU
+F32Plan plan_for(int cfg, int64_t M, int64_t N, int64_t K, int64_t batch) {
   F32Plan p{cfg, kTiles[cfg][0], kTiles[cfg][1], 1, K};
-  int64_t nb = blocks(cfg);
-  // still under one block per CU: split K (each split >= 128 deep)
-  if (nb < 256 && K >= 256) {
+  const int64_t nb = tile_blocks(cfg, M, N, batch);
+  if (nb < 256 && K >= 256) {  // each split >= 128 deep
     int64_t s = std::min<int64_t>((512 + nb - 1) / nb, K / 128);
     s = std::max<int64_t>(1, std::min<int64_t>(s, 16));
     int64_t kps = ((K + s - 1) / s + kSplitAlign - 1) / kSplitAlign * kSplitAlign;
@@ -405,6 +401,28 @@ F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
     p.k_per_split = kps;
   }
   return p;
+}
+
+int tile_env() {
+  static const int v = [] {
+    const char* e = std::getenv("TFA_GEMM_TILE");
+    const int t = e ? std::atoi(e) : -1;
+    return t >= 0 && t < kNumTiles ? t : -1;
+  }();
+  return v;
+}
+
+// Heuristic plan (also the fallback of the autotuner and what sizes the split-K workspace)
+F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  // narrow N picks a narrow tile (a 128-wide tile on N=32 wastes 3/4 of the MFMAs)
+  int cfg = N <= 32 ? 4 : (N <= 64 ? 1 : 0);
+  // too few blocks to fill 256 CUs twice: shrink the tile
+  if (tile_blocks(cfg, M, N, batch) < 512) {
+    if (cfg == 0) cfg = N > 96 ? 2 : 3;
+    else if (cfg == 1) cfg = 3;
+  }
+  if (tile_env() >= 0) cfg = tile_env();  // tuning override
+  return plan_for(cfg, M, N, K, batch);
 }
 
 template <int AL, bool TB, bool VEC>
@@ -421,21 +439,18 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 1: TFA_LAUNCH_TILE(128, 64, 2, 2); break;
     case 2: TFA_LAUNCH_TILE(64, 128, 2, 2); break;
     case 3: TFA_LAUNCH_TILE(64, 64, 2, 2); break;
-    default: TFA_LAUNCH_TILE(128, 32, 4, 1); break;
+    case 4: TFA_LAUNCH_TILE(128, 32, 4, 1); break;
+    case 5: TFA_LAUNCH_TILE(128, 96, 4, 1); break;
+    case 6: TFA_LAUNCH_TILE(128, 192, 2, 2); break;
+    case 7: TFA_LAUNCH_TILE(128, 160, 4, 1); break;
+    default: TFA_LAUNCH_TILE(64, 192, 2, 2); break;
   }
 #undef TFA_LAUNCH_TILE
 }
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
-  F32Plan p = plan_f32(g0.M, g0.N, g0.K, g0.batch);
-  GemmArgs g = g0;
-  if (p.splits > 1) {
-    TFA_CHECK(g0.workspace != nullptr, "gemm: split-K needs a workspace (gemm_workspace_bytes)");
-  } else {
-    g.workspace = nullptr;
-  }
+void launch_plan(const F32Plan& p, const GemmArgs& g, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
 #define TFA_VEC(AL_, TB_) \
   (vec ? launch_cfg<AL_, TB_, true>(p, g, cg, s) : launch_cfg<AL_, TB_, false>(p, g, cg, s))
   if (al == A_CONV) TFA_VEC(A_CONV, false);
@@ -444,6 +459,99 @@ void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream
   else if (!g.tb) TFA_VEC(A_MCONTIG, false);
   else TFA_VEC(A_MCONTIG, true);
 #undef TFA_VEC
+}
+
+// ---- tile autotuner. The best tile depends on the grid the shape makes (an
+// Inception 12x12 conv runs 35% faster on 64x64 tiles than on 128x128, the
+// 10M-row headline GEMM is fastest on 128x128), so the first launch of a new
+// (shape, loader) times the single-pass tiles on the caller's stream and keeps
+// the fastest. Split-K shapes keep the heuristic plan (the summation order, and
+// so the result bits, never depend on a timing). Never during stream capture.
+// TFA_GEMM_AUTOTUNE=0 disables it; TFA_GEMM_TILE=<cfg> forces a tile.
+using TuneKey = std::array<int64_t, 20>;
+std::mutex& tune_mu() {
+  static std::mutex m;
+  return m;
+}
+std::map<TuneKey, int>& tune_cache() {
+  static std::map<TuneKey, int> c;
+  return c;
+}
+bool autotune_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("TFA_GEMM_AUTOTUNE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v && tile_env() < 0;
+}
+
+F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
+  GemmArgs g = g0;
+  g.workspace = nullptr;  // single-pass candidates only (a workspace would select the split-K epilogue)
+  const TuneKey key{g.M, g.N, g.K, g.batch, al, g.tb, vec, cg.H, cg.W, cg.C, cg.KW, cg.OH, cg.OW,
+                    cg.sh, cg.sw, cg.dh, cg.dw, cg.pt, cg.pl, g.ldc == g.N};
+  {
+    std::lock_guard<std::mutex> lk(tune_mu());
+    auto it = tune_cache().find(key);
+    if (it != tune_cache().end()) return plan_for(it->second, g.M, g.N, g.K, g.batch);
+  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return heur;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return heur;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return heur;
+  }
+  // two rounds over the candidates, each timed over 3 launches after a warm-up;
+  // a candidate's time is its better round (short kernels are noisy)
+  float cand_ms[kNumTiles];
+  for (int c = 0; c < kNumTiles; ++c) cand_ms[c] = 1e30f;
+  for (int round = 0; round < 2; ++round) {
+    for (int c = 0; c < kNumTiles; ++c) {
+      const F32Plan q = plan_for(c, g.M, g.N, g.K, g.batch);
+      if (q.splits != 1) continue;
+      if (c != heur.cfg && kTiles[c][1] >= 2 * g.N && kTiles[c][1] > 32) continue;  // mostly-padding tile
+      if (round == 0) launch_plan(q, g, al, vec, cg, s);  // warm
+      (void)hipEventRecord(e0, s);
+      for (int r = 0; r < 3; ++r) launch_plan(q, g, al, vec, cg, s);
+      (void)hipEventRecord(e1, s);
+      float ms = 0.f;
+      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+      cand_ms[c] = std::min(cand_ms[c], ms);
+    }
+  }
+  int best = heur.cfg;
+  for (int c = 0; c < kNumTiles; ++c)
+    if (cand_ms[c] < cand_ms[best]) best = c;
+  static const bool log = std::getenv("TFA_GEMM_TUNE_LOG") != nullptr;
+  if (log) {
+    std::fprintf(stderr, "[gemm tune] M=%lld N=%lld K=%lld al=%d conv=%dx%dx%d heur=%d best=%d |",
+                 (long long)g.M, (long long)g.N, (long long)g.K, al, cg.H, cg.W, cg.C, heur.cfg, best);
+    for (int c = 0; c < kNumTiles; ++c)
+      if (cand_ms[c] < 1e29f) std::fprintf(stderr, " %d:%.4f", c, cand_ms[c] / 3);
+    std::fprintf(stderr, "\n");
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  TFA_LAUNCH_CHECK("gemm autotune");
+  {
+    std::lock_guard<std::mutex> lk(tune_mu());
+    tune_cache()[key] = best;
+  }
+  return plan_for(best, g.M, g.N, g.K, g.batch);
+}
+
+void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
+  F32Plan p = plan_f32(g0.M, g0.N, g0.K, g0.batch);
+  if (p.splits == 1 && autotune_on()) p = tuned_plan(p, g0, al, vec, cg, s);
+  GemmArgs g = g0;
+  if (p.splits > 1) {
+    TFA_CHECK(g0.workspace != nullptr, "gemm: split-K needs a workspace (gemm_workspace_bytes)");
+  } else {
+    g.workspace = nullptr;
+  }
+  launch_plan(p, g, al, vec, cg, s);
   if (p.splits > 1) {
     int64_t total = g.batch * g.M * g.N;
     hipLaunchKernelGGL(splitk_reduce, dim3(ew_grid(total)), dim3(256), 0, s, static_cast<const float*>(g.workspace),

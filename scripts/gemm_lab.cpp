@@ -3,7 +3,7 @@
 // and checks sampled outputs against a double-accumulated reference kernel.
 //
 //   scripts/build_gemm_lab.sh            (hipcc, links build/hip/*.o)
-//   TFA_GEMM_GLDS=0|1 TFA_GLDS_STAGES=3|4 ./build/gemm_lab [iters]
+//   [TFA_GEMM_TILE=cfg] [TFA_PRECISION=f32|bf16|bf16x3] ./build/gemm_lab [iters]
 //
 // One JSON line per shape: {"kind", "shape", "ms", "tflops", "max_rel_err"}.
 #include <hip/hip_runtime.h>
@@ -132,8 +132,8 @@ double time_ms(F f, int iters) {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 10;
-  const char* mode = std::getenv("TFA_GEMM_GLDS");
-  const char* st = std::getenv("TFA_GLDS_STAGES");
+  const char* mode = std::getenv("TFA_GEMM_TILE");
+  const char* st = std::getenv("TFA_PRECISION");
   struct G { int64_t M, N, K; bool tb, bias; };
   const G gemms[] = {{2500000, 512, 512, false, true}, {262144, 512, 512, false, true}, {4096, 4096, 4096, false, false},
                      {8192, 1024, 1024, false, false}, {1000000, 64, 256, false, true}, {4096, 4096, 4096, true, false},
@@ -158,7 +158,7 @@ int main(int argc, char** argv) {
                        smp.ref, smp.mag, g.act);
     CK(hipDeviceSynchronize());
     const double err = smp.check(C, s.N);
-    std::printf("{\"kind\": \"gemm\", \"glds\": \"%s\", \"stages\": \"%s\", \"shape\": [%ld, %ld, %ld, %d], "
+    std::printf("{\"kind\": \"gemm\", \"tile\": \"%s\", \"precision\": \"%s\", \"shape\": [%ld, %ld, %ld, %d], "
                 "\"ms\": %.4f, \"tflops\": %.2f, \"max_rel_err\": %.3e}\n",
                 mode ? mode : "default", st ? st : "default", (long)s.M, (long)s.N, (long)s.K, (int)s.tb, ms,
                 2.0 * s.M * s.N * s.K / ms / 1e9, err);
@@ -172,7 +172,9 @@ int main(int argc, char** argv) {
                       {512, 25, 25, 48, 5, 5, 64, 1, true},    {512, 25, 25, 64, 3, 3, 96, 1, true},
                       {512, 12, 12, 128, 1, 7, 128, 1, true},  {512, 12, 12, 160, 7, 1, 192, 1, true},
                       {512, 5, 5, 448, 3, 3, 384, 1, true},    {512, 25, 25, 288, 3, 3, 384, 2, false},
-                      {64, 224, 224, 3, 3, 3, 32, 2, false}};
+                      {64, 224, 224, 3, 3, 3, 32, 2, false},   {512, 12, 12, 160, 1, 7, 160, 1, true},
+                      {512, 5, 5, 1280, 1, 1, 320, 1, true},   {512, 5, 5, 2048, 1, 1, 448, 1, true},
+                      {512, 12, 12, 768, 1, 1, 192, 1, true},  {512, 25, 25, 256, 1, 1, 48, 1, true}};
   for (const Cv& c : convs) {
     tfa::k::ConvArgs a{};
     a.N = c.N; a.H = c.H; a.W = c.W; a.C = c.C; a.KH = c.KH; a.KW = c.KW; a.OC = c.OC;
@@ -203,7 +205,7 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     const double err = smp.check(y, c.OC);
     const double flop = 2.0 * M * c.OC * c.KH * c.KW * c.C;
-    std::printf("{\"kind\": \"conv\", \"glds\": \"%s\", \"stages\": \"%s\", \"shape\": [%ld, %ld, %ld, %ld, %ld, "
+    std::printf("{\"kind\": \"conv\", \"tile\": \"%s\", \"precision\": \"%s\", \"shape\": [%ld, %ld, %ld, %ld, %ld, "
                 "%ld, %ld, %ld, \"%s\"], \"ms\": %.4f, \"tflops\": %.2f, \"max_rel_err\": %.3e}\n",
                 mode ? mode : "default", st ? st : "default", (long)c.N, (long)c.H, (long)c.W, (long)c.C,
                 (long)c.KH, (long)c.KW, (long)c.OC, (long)c.s, c.same ? "SAME" : "VALID", ms, flop / ms / 1e9, err);
