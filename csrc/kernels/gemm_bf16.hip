@@ -16,7 +16,10 @@
 // stride: the 16-lane groups of a ds_read_b128 hit 16 distinct 16-byte bank
 // slots). MFMA fragment of lane l: row l&31, k = 8*(l>>5) .. +7 of the 16-deep
 // step = one ds_read_b128 per operand per step. C/D layout as the f32 form.
+#include <array>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "gemm_internal.h"
 #include "hip_common.h"
@@ -264,26 +267,85 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
 
 int64_t padded_k(int64_t K) { return (K + kBK - 1) / kBK * kBK; }
 
+constexpr int kBf16Tiles[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+
 template <int AL, bool X3>
-void launch(const GemmArgs& g, const Im2colGeom& cg, const uint16_t* bh, const uint16_t* bl, int64_t Kp,
-            hipStream_t s) {
-  auto blocks = [&](int bm, int bn) { return ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn); };
-  int bm = 128, bn = g.N <= 64 ? 64 : 128;
-  if (blocks(bm, bn) < 512) {  // fill 256 CUs at least twice: shrink the tile
-    if (bn == 128 && blocks(128, 64) >= 512) bn = 64;
-    else { bm = 64; bn = g.N <= 64 ? 64 : (blocks(64, 128) >= 512 ? 128 : 64); }
-  }
+void launch_tile(int t, const GemmArgs& g, const Im2colGeom& cg, const uint16_t* bh, const uint16_t* bl, int64_t Kp,
+                 hipStream_t s) {
+  const int bm = kBf16Tiles[t][0], bn = kBf16Tiles[t][1];
   const int64_t tm = (g.M + bm - 1) / bm, tn = (g.N + bn - 1) / bn;
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm bf16: grid too large");
   dim3 grid((unsigned)(tm * tn));
 #define TFA_BF16(BM_, BN_)                                                                                \
   hipLaunchKernelGGL((gemm_bf16_tile<BM_, BN_, 2, 2, AL, X3>), grid, dim3(256), 0, s, g, (int)tm, (int)tn, cg, \
                      bh, bl, Kp)
-  if (bm == 128 && bn == 128) TFA_BF16(128, 128);
-  else if (bm == 128) TFA_BF16(128, 64);
-  else if (bn == 128) TFA_BF16(64, 128);
-  else TFA_BF16(64, 64);
+  switch (t) {
+    case 0: TFA_BF16(128, 128); break;
+    case 1: TFA_BF16(128, 64); break;
+    case 2: TFA_BF16(64, 128); break;
+    default: TFA_BF16(64, 64); break;
+  }
 #undef TFA_BF16
+}
+
+int heuristic_tile(const GemmArgs& g) {
+  auto blocks = [&](int t) {
+    return ((g.M + kBf16Tiles[t][0] - 1) / kBf16Tiles[t][0]) * ((g.N + kBf16Tiles[t][1] - 1) / kBf16Tiles[t][1]);
+  };
+  int t = g.N <= 64 ? 1 : 0;
+  if (blocks(t) < 512) t = (t == 0 && blocks(1) >= 512) ? 1 : (g.N > 64 && blocks(2) >= 512 ? 2 : 3);
+  return t;
+}
+
+// first launch of a (shape, mode, conv geometry) times the four tiles on the
+// caller's stream and keeps the fastest (as the f32 core's tuner; never under
+// stream capture; TFA_GEMM_AUTOTUNE=0 keeps the heuristic)
+template <int AL, bool X3>
+void launch(const GemmArgs& g, const Im2colGeom& cg, const uint16_t* bh, const uint16_t* bl, int64_t Kp,
+            hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::array<int64_t, 16>, int> cache;
+  static const bool tune = [] {
+    const char* e = std::getenv("TFA_GEMM_AUTOTUNE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const std::array<int64_t, 16> key{g.M, g.N, g.K, g.ldc == g.N, cg.H, cg.W, cg.C, cg.KW, cg.OH, cg.OW,
+                                    cg.sh, cg.sw, cg.dh, cg.dw, cg.pt, cg.pl};
+  int t = heuristic_tile(g);
+  bool found = false;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      t = it->second;
+      found = true;
+    }
+  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (!found && tune && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+      float best = 1e30f;
+      for (int round = 0; round < 2; ++round)
+        for (int c = 0; c < 4; ++c) {
+          if (kBf16Tiles[c][1] >= 2 * g.N && c != t) continue;  // mostly-padding tile
+          if (round == 0) launch_tile<AL, X3>(c, g, cg, bh, bl, Kp, s);
+          (void)hipEventRecord(e0, s);
+          for (int r = 0; r < 3; ++r) launch_tile<AL, X3>(c, g, cg, bh, bl, Kp, s);
+          (void)hipEventRecord(e1, s);
+          float ms = 0.f;
+          if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best) {
+            best = ms;
+            t = c;
+          }
+        }
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      std::lock_guard<std::mutex> lk(mu);
+      cache[key] = t;
+    }
+  }
+  launch_tile<AL, X3>(t, g, cg, bh, bl, Kp, s);
 }
 
 }  // namespace
