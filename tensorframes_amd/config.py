@@ -55,6 +55,8 @@ config = Config()
 
 
 def set_config(**kw):
+    """Update `config` fields (`set_config(precision="bf16x3", task_retries=2)`);
+    unknown keys raise AttributeError, a bad precision ValueError."""
     if "precision" in kw and kw["precision"] not in PRECISION_MODES:
         raise ValueError(f"precision must be one of {sorted(PRECISION_MODES)}, got {kw['precision']!r}")
     for k, v in kw.items():

@@ -1074,6 +1074,8 @@ def print_schema(dframe: DataFrame):
 
 
 def explain(dframe: DataFrame) -> str:
+    """The schema with tensor metadata as text, one field per line
+    (`root |-- y: array (nullable = false) double[?,2]`; reference: DebugRowOps.scala:528-545)."""
     return explain_schema(dframe.schema)
 
 

@@ -548,6 +548,8 @@ def generate(schema: StructType, num_partitions: int, fn: Callable[[int], Block]
 
 
 def range_(n: int, num_partitions: Optional[int] = None, name: str = "id") -> DataFrame:
+    """DataFrame of one int64 column `id` = 0..n-1, generated lazily per
+    partition (Spark's `sqlContext.range`, used by the reference's perf suite)."""
     nparts = num_partitions or max(1, dist.world_size())
 
     def fn(p):
