@@ -275,6 +275,48 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // Segmented reduction over rows sorted by segment (CSR offsets, int64):
   // the groupBy/aggregate monoid fast path. Device tensors run the HIP
   // kernel; host tensors the ATen reference.
+  // Unsorted segmented reduction: out[ids[i]] op= x[i] (rows in any order),
+  // the map-side combine of groupBy/aggregate. ids int32/int64 on x's device.
+  m.def("unsorted_segment_reduce", [](const std::string& op, const at::Tensor& x, const at::Tensor& ids,
+                                      int64_t nseg) {
+    TFA_CHECK(x.dim() >= 1 && ids.dim() == 1 && ids.size(0) == x.size(0), "unsorted_segment_reduce: ids must be [rows]");
+    TFA_CHECK(ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt, "unsorted_segment_reduce: int ids");
+    TFA_CHECK(ids.device() == x.device(), "unsorted_segment_reduce: ids and x on different devices");
+    k::RedOp rop = op == "Sum" ? k::RedOp::SUM : op == "Min" ? k::RedOp::MIN : op == "Max" ? k::RedOp::MAX
+                 : op == "Prod" ? k::RedOp::PROD : k::RedOp::ALL;
+    TFA_CHECK(rop != k::RedOp::ALL, "unsorted_segment_reduce: unsupported op ", op);
+    std::vector<int64_t> osz = x.sizes().vec();
+    osz[0] = nseg;
+    const int64_t nrows = x.size(0);
+    if (!x.is_cuda()) {
+      at::Tensor xs = x.reshape({nrows, -1});
+      at::Tensor is = ids.to(at::kLong);
+      at::Tensor out;
+      if (rop == k::RedOp::SUM) {
+        out = at::zeros({nseg, xs.size(1)}, x.options()).index_add_(0, is, xs);
+      } else if (rop == k::RedOp::PROD) {
+        out = at::ones({nseg, xs.size(1)}, x.options()).index_reduce_(0, is, xs, "prod", true);
+      } else {
+        const bool mx = rop == k::RedOp::MAX;
+        out = at::empty({nseg, xs.size(1)}, x.options());
+        out = out.index_reduce_(0, is, xs, mx ? "amax" : "amin", false);
+      }
+      return out.reshape(osz).contiguous();
+    }
+    c10::hip::HIPGuard guard(x.device().index());
+    at::Tensor xc = x.contiguous(), ic = ids.contiguous();
+    at::Tensor out = at::empty(osz, xc.options());
+    if (!out.numel()) return out;
+    const int64_t inner = out.numel() / nseg;
+    const DType dt = from_scalar_type(xc.scalar_type());
+    size_t ws = k::unsorted_segment_workspace_bytes(rop, dt, nrows, inner, nseg);
+    at::Tensor work;
+    if (ws) work = at::empty({static_cast<int64_t>(ws)}, xc.options().dtype(at::kByte));
+    k::unsorted_segment_reduce(rop, dt, from_scalar_type(ic.scalar_type()), xc.data_ptr(), ic.data_ptr(),
+                               out.data_ptr(), nrows, inner, nseg, ws ? work.data_ptr() : nullptr,
+                               c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    return out;
+  });
   m.def("segment_reduce", [](const std::string& op, const at::Tensor& x, const at::Tensor& offsets) {
     TFA_CHECK(x.dim() >= 1, "segment_reduce needs rank >= 1");
     TFA_CHECK(offsets.scalar_type() == at::kLong && offsets.dim() == 1, "offsets must be int64[nseg+1]");

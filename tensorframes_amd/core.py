@@ -948,7 +948,53 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
     uniform = set(monoid) == set(out_names)
     all_cols = keys + out_names
 
+    def combine(blocks):
+        """Monoid graphs: map-side combine. Each partition is reduced per key on
+        its own device (unsorted segmented reduction), only the per-key partials
+        (one row per key and partition) are shuffled, then reduced again."""
+        w = dist.world_size()
+        send = [[] for _ in range(w)]
+        for pid, b in sorted(blocks.items()):
+            if b.nrows == 0:
+                continue
+            kcols = [_key_array(b.columns[k]) for k in keys]
+            codes, uniq_cols = _factorize(kcols)
+            ng = len(uniq_cols[0]) if uniq_cols else 0
+            cols: Dict[str, Any] = {}
+            for i, k in enumerate(keys):
+                cols[k] = build_column(uniq_cols[i].tolist(), _tf_of_field(df.schema[k]))
+            for n in out_names:
+                x = b.columns[n]
+                dev = engine.compute_device() if x.is_cuda or engine.gpu_available() else x.device
+                xd = x.to(dev) if x.device != dev else x
+                ids = torch.from_numpy(codes).to(dev)
+                cols[n] = _C.unsorted_segment_reduce(monoid[n], xd.contiguous(), ids, ng).cpu()
+            part = Block(ng, cols)
+            if w == 1:
+                send[0].append(part)
+                continue
+            dest = (_key_hash([_key_array(part.columns[k]) for k in keys]) % np.uint64(w)).astype(np.int64)
+            for r in range(w):
+                idx = np.nonzero(dest == r)[0]
+                if len(idx):
+                    send[r].append(part.take(idx))
+        mine = [blk for lst in dist.all_to_all_objects(send) for blk in lst]
+        if not mine:
+            return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, w))}
+        full = concat_blocks(mine, all_cols)
+        codes, uniq_cols = _factorize([_key_array(full.columns[k]) for k in keys])
+        ng = len(uniq_cols[0]) if uniq_cols else 0
+        out_cols: Dict[str, Any] = {}
+        for i, k in enumerate(keys):
+            out_cols[k] = build_column(uniq_cols[i].tolist(), _tf_of_field(df.schema[k]))
+        ids = torch.from_numpy(codes)
+        for n in out_names:
+            out_cols[n] = _C.unsorted_segment_reduce(monoid[n], full.columns[n].contiguous(), ids, ng)
+        return {dist.rank(): Block(ng, out_cols)}
+
     def compute(blocks):
+        if uniform and all(is_dense(b.columns[n]) for b in blocks.values() for n in out_names):
+            return combine(blocks)
         # 1. shuffle: rows go to rank hash(key) % world (all-to-all)
         w = dist.world_size()
         send = [[] for _ in range(w)]
@@ -980,19 +1026,15 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         out_cols: Dict[str, Any] = {}
         for i, k in enumerate(keys):
             out_cols[k] = build_column([u[i] for u in uniq], _tf_of_field(df.schema[k]))
-        if uniform and all(is_dense(sorted_blk.columns[n]) for n in out_names):
-            for n in out_names:
-                out_cols[n] = _segment_reduce(monoid[n], sorted_blk.columns[n], offsets)
-        else:
-            per = {n: [] for n in out_names}
-            for g in range(len(uniq)):
-                seg = sorted_blk.slice(int(offsets[g]), int(offsets[g + 1]))
-                ins = _dense_inputs(seg, out_names, "aggregate")
-                outs = engine.run_program(prog, ins)
-                for n, o in zip(out_names, outs):
-                    per[n].append(o.cpu())
-            for n in out_names:
-                out_cols[n] = torch.stack(per[n], 0)
+        per = {n: [] for n in out_names}
+        for g in range(len(uniq)):
+            seg = sorted_blk.slice(int(offsets[g]), int(offsets[g + 1]))
+            ins = _dense_inputs(seg, out_names, "aggregate")
+            outs = engine.run_program(prog, ins)
+            for n, o in zip(out_names, outs):
+                per[n].append(o.cpu())
+        for n in out_names:
+            out_cols[n] = torch.stack(per[n], 0)
         return {dist.rank(): Block(len(uniq), out_cols)}
 
     out_fields = [df.schema[k] for k in keys]
@@ -1015,14 +1057,6 @@ def _empty_agg_cols(df, keys, out_names):
         stf = _col_info(df.schema[n])
         cols[n] = _empty_output(stf.shape, stf.tf_dtype)
     return cols
-
-
-def _segment_reduce(op: str, col: torch.Tensor, offsets: np.ndarray) -> torch.Tensor:
-    dev = engine.compute_device()
-    x = col.to(dev) if col.device != dev else col
-    off = torch.from_numpy(offsets).to(dev)
-    y = _C.segment_reduce(op, x.contiguous(), off)
-    return y.cpu() if not col.is_cuda else y
 
 
 # ------------------------------------------------------------------ analyze / schema
