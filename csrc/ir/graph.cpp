@@ -328,7 +328,11 @@ std::vector<int> Graph::placeholders() const {
   return v;
 }
 
-static constexpr int64_t kFoldLimit = int64_t(1) << 22;  // elements
+// Largest result folded on the host (elements): shape arithmetic and small
+// constant expressions. A big CONST-class tensor (a Tile of centroids to the
+// block row count, K-Means) is cheaper to compute on the device each run than
+// to build with ATen on the host at every analysis/plan and upload.
+static constexpr int64_t kFoldLimit = int64_t(1) << 16;
 
 Graph::Infos Graph::infer(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds,
                           bool concrete) const {
