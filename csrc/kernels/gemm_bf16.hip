@@ -138,9 +138,16 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
     kkh = t / cg.KW;
   }
 
-  float4 ra[AP];
-  uint4 rbh[BP], rbl[X3 ? BP : 1];
-  auto load = [&](int64_t k0) {
+  // register-staged tiles, two sets: the global loads of tile t+2 are in
+  // flight while tile t is computed and tile t+1 is written to LDS
+  struct Regs {
+    float4 ra[AP];
+    uint4 rbh[BP], rbl[X3 ? BP : 1];
+  };
+  auto load = [&](int64_t k0, Regs& R) {
+    float4* ra = R.ra;
+    uint4* rbh = R.rbh;
+    uint4* rbl = R.rbl;
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
       const int64_t k = k0 + 4 * kq;
@@ -175,7 +182,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
       if (X3) rbl[p] = ok ? *reinterpret_cast<const uint4*>(Blo + off) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store = [&](int st) {
+  auto store = [&](int st, const Regs& R) {
+    const float4* ra = R.ra;
+    const uint4* rbh = R.rbh;
+    const uint4* rbl = R.rbl;
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
       const int r = (tid + 256 * p) >> 3;
@@ -208,13 +218,16 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
 
   const int ktiles = (int)((K + kBK - 1) / kBK);
   const int li = lane & 31, lh = lane >> 5;
-  load(0);
-  store(0);
+  // bf16x3 keeps one register set (its 230-VGPR two-set form measured 7% slower);
+  // bf16 prefetches two tiles ahead (1.1-1.4x, scripts/gemm_lab.cpp)
+  constexpr bool kDeep = !X3;
+  Regs r0, r1;
+  load(0, r0);
+  store(0, r0);
+  if (kDeep && ktiles > 1) load(kBK, r0);
   __syncthreads();
   int cur = 0;
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const bool has_next = kt + 1 < ktiles;
-    if (has_next) load((int64_t)(kt + 1) * kBK);
+  auto compute = [&]() {
 #pragma unroll
     for (int s = 0; s < kBK / 16; ++s) {
       bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -242,9 +255,29 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
-    if (has_next) store(cur ^ 1);
+  };
+  // iteration kt: `nxt` holds tile kt+1, `far` receives tile kt+2
+  auto step = [&](int kt, Regs& nxt, Regs& far) {
+    if (kt + 2 < ktiles) load((int64_t)(kt + 2) * kBK, far);
+    compute();
+    if (kt + 1 < ktiles) store(cur ^ 1, nxt);
     __syncthreads();
     cur ^= 1;
+  };
+  if constexpr (kDeep) {
+    for (int kt = 0; kt < ktiles; kt += 2) {
+      step(kt, r0, r1);
+      if (kt + 1 < ktiles) step(kt + 1, r1, r0);
+    }
+  } else {
+    for (int kt = 0; kt < ktiles; ++kt) {
+      const bool has_next = kt + 1 < ktiles;
+      if (has_next) load((int64_t)(kt + 1) * kBK, r0);
+      compute();
+      if (has_next) store(cur ^ 1, r0);
+      __syncthreads();
+      cur ^= 1;
+    }
   }
 
   const float* bias = static_cast<const float*>(g.bias);
