@@ -13,6 +13,7 @@ OpRegistry& OpRegistry::get() {
     register_math_ops(*reg);
     register_nn_ops(*reg);
     register_extra_ops(*reg);
+    register_more_ops(*reg);
     return reg;
   }();
   return *r;

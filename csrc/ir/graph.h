@@ -99,6 +99,7 @@ void register_array_ops(OpRegistry& r);
 void register_math_ops(OpRegistry& r);
 void register_nn_ops(OpRegistry& r);
 void register_extra_ops(OpRegistry& r);
+void register_more_ops(OpRegistry& r);
 
 struct InferCtx {
   const Node& node;

@@ -1128,6 +1128,42 @@ def _useg(op_type, data, segment_ids, num_segments, name):
 
 
 # ------------------------------------------------------------------ tf.nn
+def broadcast_to(input, shape, name=None):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("BroadcastTo", [("input", x), ("shape", np.asarray(shape, dtype=np.int32))],
+               {"T": P.AttrValue.type(x.dtype), "Tidx": P.AttrValue.type(int32)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+
+def depth_to_space(input, block_size, name=None, data_format="NHWC"):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("DepthToSpace", [("input", x)],
+               {"T": P.AttrValue.type(x.dtype), "block_size": P.AttrValue.i(block_size),
+                "data_format": P.AttrValue.s(data_format)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+
+def space_to_depth(input, block_size, name=None, data_format="NHWC"):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("SpaceToDepth", [("input", x)],
+               {"T": P.AttrValue.type(x.dtype), "block_size": P.AttrValue.i(block_size),
+                "data_format": P.AttrValue.s(data_format)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+
+def space_to_batch_nd(input, block_shape, paddings, name=None):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("SpaceToBatchND", [("input", x), ("block_shape", np.asarray(block_shape, dtype=np.int32)),
+                                  ("paddings", np.asarray(paddings, dtype=np.int32))],
+               {"T": P.AttrValue.type(x.dtype), "Tblock_shape": P.AttrValue.type(int32),
+                "Tpaddings": P.AttrValue.type(int32)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+
+def batch_to_space_nd(input, block_shape, crops, name=None):  # noqa: A002
+    x = convert_to_tensor(input)
+    return _op("BatchToSpaceND", [("input", x), ("block_shape", np.asarray(block_shape, dtype=np.int32)),
+                                  ("crops", np.asarray(crops, dtype=np.int32))],
+               {"T": P.AttrValue.type(x.dtype), "Tblock_shape": P.AttrValue.type(int32),
+                "Tcrops": P.AttrValue.type(int32)}, name, out_dtypes=[x.dtype]).outputs[0]
+
+
 class _NN:
     @staticmethod
     def relu(features, name=None):
@@ -1166,6 +1202,63 @@ class _NN:
     def log_softmax(logits, name=None):
         return _op("LogSoftmax", [("logits", logits)], {"T": P.AttrValue.type(logits.dtype)}, name,
                    out_dtypes=[logits.dtype]).outputs[0]
+
+    @staticmethod
+    def l2_loss(t, name=None):
+        return _op("L2Loss", [("t", t)], {"T": P.AttrValue.type(t.dtype)}, name, out_dtypes=[t.dtype]).outputs[0]
+
+    @staticmethod
+    def softmax_cross_entropy_with_logits(_sentinel=None, labels=None, logits=None, dim=-1, name=None):
+        """Per-row loss (the op's first output; reference TF-1.x semantics)."""
+        op = _op("SoftmaxCrossEntropyWithLogits", [("features", logits), ("labels", labels)],
+                 {"T": P.AttrValue.type(logits.dtype)}, name, n_out=2, out_dtypes=[logits.dtype, logits.dtype])
+        return op.outputs[0]
+
+    softmax_cross_entropy_with_logits_v2 = softmax_cross_entropy_with_logits
+
+    @staticmethod
+    def sparse_softmax_cross_entropy_with_logits(_sentinel=None, labels=None, logits=None, name=None):
+        lab = convert_to_tensor(labels)
+        op = _op("SparseSoftmaxCrossEntropyWithLogits", [("features", logits), ("labels", lab)],
+                 {"T": P.AttrValue.type(logits.dtype), "Tlabels": P.AttrValue.type(lab.dtype)}, name, n_out=2,
+                 out_dtypes=[logits.dtype, logits.dtype])
+        return op.outputs[0]
+
+    @staticmethod
+    def depth_to_space(input, block_size, name=None, data_format="NHWC"):  # noqa: A002
+        return depth_to_space(input, block_size, name, data_format)
+
+    @staticmethod
+    def space_to_depth(input, block_size, name=None, data_format="NHWC"):  # noqa: A002
+        return space_to_depth(input, block_size, name, data_format)
+
+    @staticmethod
+    def atrous_conv2d(value, filters, rate, padding, name=None):
+        """TF-1.x emission: SpaceToBatchND -> VALID Conv2D -> BatchToSpaceND
+        (paddings/crops computed for the static spatial size; SAME or VALID)."""
+        x = convert_to_tensor(value)
+        h, w = x.get_shape().as_list()[1:3]
+        fh, fw = (filters.get_shape().as_list()[:2] if isinstance(filters, Tensor) else np.shape(filters)[:2])
+        if h is None or w is None:
+            raise ValueError("atrous_conv2d needs a static spatial size")
+        ekh, ekw = (fh - 1) * rate + 1, (fw - 1) * rate + 1
+        if padding == "SAME":
+            ph, pw = ekh - 1, ekw - 1
+            pads = [[ph // 2, ph - ph // 2], [pw // 2, pw - pw // 2]]
+        else:
+            pads = [[0, 0], [0, 0]]
+        # extra bottom/right padding so that the padded size divides by rate
+        base = [[pads[0][0], pads[0][1]], [pads[1][0], pads[1][1]]]
+        crops = [[0, 0], [0, 0]]
+        for i, s in enumerate((h, w)):
+            tot = s + base[i][0] + base[i][1]
+            extra = (-tot) % rate
+            base[i][1] += extra
+            crops[i][1] = extra
+        with name_scope(name or "atrous_conv2d"):
+            stb = space_to_batch_nd(x, [rate, rate], base)
+            y = _NN.conv2d(stb, filters, [1, 1, 1, 1], "VALID")
+            return batch_to_space_nd(y, [rate, rate], crops)
 
     @staticmethod
     def bias_add(value, bias, data_format=None, name=None):
