@@ -1,6 +1,7 @@
 // More TF-1.x ops of frozen inference graphs: BroadcastTo, DepthToSpace /
 // SpaceToDepth, SpaceToBatchND / BatchToSpaceND (the dilated-conv rewrite TF 1.x
-// emits for atrous convolutions), L2Loss, SoftmaxCrossEntropyWithLogits and
+// emits for atrous convolutions), Conv2DBackpropInput (tf.nn.conv2d_transpose,
+// decoder / upsampling layers), L2Loss, SoftmaxCrossEntropyWithLogits and
 // SparseSoftmaxCrossEntropyWithLogits (evaluation losses).
 // (The reference ran whatever op a user's GraphDef held through libtensorflow;
 // reference: src/main/scala/org/tensorframes/impl/TensorFlowOps.scala:76-95.)
@@ -268,6 +269,127 @@ OpDef make_batch_to_space() {
   return d;
 }
 
+// ---------------------------------------------------------------- Conv2DBackpropInput
+// dx = conv2d_transpose(dy, W): on the GPU, dy is scattered with the forward
+// stride into a zero buffer padded by (effective kernel - 1 - forward pad) and
+// convolved (stride 1, the forward dilation, VALID) with W flipped in space and
+// with its channel axes swapped, on the f32 MFMA implicit-GEMM conv kernel.
+struct TransposedGeom {
+  int64_t N, H, W, IC, OH, OW, OC, KH, KW, sh, sw, dh, dw, pt, pl;
+};
+
+TransposedGeom transposed_geom(const Node& n, const std::vector<int64_t>& in_sizes, const std::vector<int64_t>& w,
+                               const std::vector<int64_t>& dy) {
+  TFA_CHECK(data_format(n) == "NHWC", n.op, ": only data_format NHWC is supported");
+  TFA_CHECK(in_sizes.size() == 4 && w.size() == 4 && dy.size() == 4, n.op, ": rank-4 sizes/filter/out_backprop");
+  auto st = n.attr_ilist("strides", {1, 1, 1, 1});
+  auto dl = n.attr_ilist("dilations", {1, 1, 1, 1});
+  TFA_CHECK(st.size() == 4 && st[0] == 1 && st[3] == 1, n.op, ": strides must be [1,sh,sw,1]");
+  std::string pad = n.attr_s("padding");
+  TFA_CHECK(pad == "SAME" || pad == "VALID", n.op, ": unsupported padding '", pad, "'");
+  TransposedGeom g;
+  g.N = in_sizes[0]; g.H = in_sizes[1]; g.W = in_sizes[2]; g.IC = in_sizes[3];
+  g.KH = w[0]; g.KW = w[1]; g.OC = w[3];
+  TFA_CHECK(w[2] == g.IC, n.op, ": filter in-channels ", w[2], " != input_sizes channels ", g.IC);
+  g.sh = st[1]; g.sw = st[2];
+  g.dh = dl.size() == 4 ? dl[1] : 1; g.dw = dl.size() == 4 ? dl[2] : 1;
+  auto fwd = [&](int64_t in, int64_t k, int64_t s, int64_t d, int64_t& out, int64_t& pb) {
+    const int64_t eff = (k - 1) * d + 1;
+    if (pad == "SAME") {
+      out = (in + s - 1) / s;
+      pb = std::max<int64_t>((out - 1) * s + eff - in, 0) / 2;
+    } else {
+      out = in >= eff ? (in - eff) / s + 1 : 0;
+      pb = 0;
+    }
+  };
+  fwd(g.H, g.KH, g.sh, g.dh, g.OH, g.pt);
+  fwd(g.W, g.KW, g.sw, g.dw, g.OW, g.pl);
+  TFA_CHECK(dy[1] == g.OH && dy[2] == g.OW && dy[3] == g.OC && (dy[0] == g.N || dy[0] < 0), n.op,
+            ": out_backprop shape [", dy[0], ",", dy[1], ",", dy[2], ",", dy[3], "] does not match the forward conv of ",
+            "input_sizes (expected spatial ", g.OH, "x", g.OW, ", channels ", g.OC, ")");
+  return g;
+}
+
+OpDef make_conv2d_backprop_input() {
+  OpDef d;
+  d.host_inputs = {0};
+  d.infer = [](InferCtx& c) {
+    auto sv = c.ivalue(0);
+    const TensorInfo& dy = c.input(2);
+    TFA_CHECK(dy.dtype == c.input(1).dtype, "Conv2DBackpropInput: filter/out_backprop dtype mismatch");
+    if (!sv) {
+      c.set(0, dy.dtype, Shape({-1, -1, -1, -1}));
+      return;
+    }
+    TFA_CHECK(sv->size() == 4, "Conv2DBackpropInput: input_sizes must have 4 values");
+    std::vector<int64_t> out = *sv;
+    // the batch follows out_backprop (input_sizes often carries the traced batch)
+    if (!dy.shape.unknown_rank && dy.shape.rank() == 4) out[0] = dy.shape.dims[0];
+    c.set(0, dy.dtype, Shape(out));
+  };
+  d.rows = [](InferCtx& c) {
+    if (c.all_const()) { c.out[0].row = RowClass::CONST; return; }
+    const bool ok = c.input(2).row == RowClass::ROW && c.input(1).row == RowClass::CONST;
+    c.out[0].row = ok ? RowClass::ROW : RowClass::MIXED;
+  };
+  d.compute = [](ExecCtx& c) {
+    at::Tensor w = c.input(1), dy = c.input(2);
+    std::vector<int64_t> sizes = c.host_ivalue(0);
+    sizes[0] = dy.size(0);
+    TransposedGeom g = transposed_geom(c.node, sizes, w.sizes().vec(), dy.sizes().vec());
+    const int64_t ekh = (g.KH - 1) * g.dh + 1, ekw = (g.KW - 1) * g.dw + 1;
+    if (!c.gpu) {  // oracle: ATen's transposed conv, then TF's asymmetric crop
+      at::Tensor y = at::conv_transpose2d(dy.permute({0, 3, 1, 2}), w.permute({3, 2, 0, 1}), {}, {g.sh, g.sw},
+                                          {0, 0}, {0, 0}, 1, {g.dh, g.dw});
+      // positions past the last window (VALID / stride remainders) receive nothing
+      const int64_t lack_h = std::max<int64_t>(g.pt + g.H - y.size(2), 0);
+      const int64_t lack_w = std::max<int64_t>(g.pl + g.W - y.size(3), 0);
+      if (lack_h || lack_w) y = at::constant_pad_nd(y, {0, lack_w, 0, lack_h}, 0);
+      y = y.narrow(2, g.pt, g.H).narrow(3, g.pl, g.W);
+      c.out[0] = y.permute({0, 2, 3, 1}).contiguous();
+      return;
+    }
+    require_gpu_dtype(dy, {at::kFloat}, "Conv2DBackpropInput");
+    hipStream_t s = stream_of(c);
+    c.out[0] = c.alloc_out(0);
+    if (!c.out[0].numel()) return;
+    // zero buffer [N, H + ekh - 1, W + ekw - 1, OC] with dy scattered at stride (sh, sw)
+    const int64_t PH = g.H + ekh - 1, PW = g.W + ekw - 1;
+    at::Tensor buf = at::empty({g.N, PH, PW, g.OC}, dy.options());
+    k::fill(DType::F32, buf.data_ptr(), buf.numel(), 0.0, s);
+    const int64_t top = ekh - 1 - g.pt, left = ekw - 1 - g.pl;
+    if (dy.numel()) {
+      at::Tensor dst = buf.slice(1, top, top + (g.OH - 1) * g.sh + 1, g.sh)
+                           .slice(2, left, left + (g.OW - 1) * g.sw + 1, g.sw);
+      gpu_copy(dy, dst, s);
+    }
+    // W'[kh][kw][oc][ic] = W[KH-1-kh][KW-1-kw][ic][oc] (negative source strides)
+    at::Tensor wc = materialize(c, w);
+    at::Tensor wf = at::empty({g.KH, g.KW, g.OC, g.IC}, wc.options());
+    {
+      const int64_t dims[4] = {g.KH, g.KW, g.OC, g.IC};
+      const int64_t sst[4] = {-g.KW * g.IC * g.OC, -g.IC * g.OC, 1, g.OC};
+      const int64_t dst_st[4] = {g.KW * g.OC * g.IC, g.OC * g.IC, g.IC, 1};
+      const float* src0 = wc.data_ptr<float>() + ((g.KH - 1) * g.KW + (g.KW - 1)) * g.IC * g.OC;
+      k::strided_copy(4, 4, dims, src0, sst, wf.data_ptr(), dst_st, s);
+    }
+    k::ConvArgs a;
+    a.N = g.N; a.H = PH; a.W = PW; a.C = g.OC;
+    a.KH = g.KH; a.KW = g.KW; a.OC = g.IC; a.OH = g.H; a.OW = g.W;
+    a.sh = a.sw = 1; a.dh = g.dh; a.dw = g.dw; a.pad_t = a.pad_l = 0;
+    a.x = buf.data_ptr(); a.w = wf.data_ptr(); a.y = c.out[0].data_ptr();
+    a.bias = nullptr; a.act = 0;
+    at::Tensor work;
+    if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
+      work = at::empty({static_cast<int64_t>(ws)}, buf.options().dtype(at::kByte));
+      a.workspace = work.data_ptr();
+    }
+    k::conv2d_nhwc(DType::F32, a, s);
+  };
+  return d;
+}
+
 // ---------------------------------------------------------------- L2Loss
 OpDef make_l2loss() {
   OpDef d;
@@ -395,6 +517,7 @@ void register_more_ops(OpRegistry& r) {
   r.add("SpaceToDepth", make_depth_space(false));
   r.add("SpaceToBatchND", make_space_to_batch());
   r.add("BatchToSpaceND", make_batch_to_space());
+  r.add("Conv2DBackpropInput", make_conv2d_backprop_input());
   r.add("L2Loss", make_l2loss());
   r.add("SoftmaxCrossEntropyWithLogits", make_xent(false));
   r.add("SparseSoftmaxCrossEntropyWithLogits", make_xent(true));

@@ -1204,6 +1204,20 @@ class _NN:
                    out_dtypes=[logits.dtype]).outputs[0]
 
     @staticmethod
+    def conv2d_transpose(value, filter, output_shape, strides, padding="SAME",  # noqa: A002
+                         data_format="NHWC", name=None, dilations=(1, 1, 1, 1)):
+        """tf.nn.conv2d_transpose: a Conv2DBackpropInput node; `filter` is
+        [height, width, output_channels, in_channels] as in TF."""
+        x = convert_to_tensor(value)
+        return _op("Conv2DBackpropInput",
+                   [("input_sizes", np.asarray(output_shape, dtype=np.int32)), ("filter", filter),
+                    ("out_backprop", x)],
+                   {"T": P.AttrValue.type(x.dtype), "strides": P.AttrValue.ilist(strides),
+                    "padding": P.AttrValue.s(padding), "data_format": P.AttrValue.s(data_format),
+                    "dilations": P.AttrValue.ilist(dilations), "use_cudnn_on_gpu": P.AttrValue.b(True)},
+                   name or "conv2d_transpose", out_dtypes=[x.dtype], dtype_hint=x.dtype).outputs[0]
+
+    @staticmethod
     def l2_loss(t, name=None):
         return _op("L2Loss", [("t", t)], {"T": P.AttrValue.type(t.dtype)}, name, out_dtypes=[t.dtype]).outputs[0]
 

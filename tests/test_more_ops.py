@@ -1,5 +1,6 @@
 """BroadcastTo, DepthToSpace / SpaceToDepth, SpaceToBatchND / BatchToSpaceND
-(and the TF-1.x atrous_conv2d built from them), L2Loss and the two softmax
+(and the TF-1.x atrous_conv2d built from them), Conv2DBackpropInput
+(tf.nn.conv2d_transpose), L2Loss and the two softmax
 cross-entropy ops: CPU executor against numpy / torch references; the GPU
 kernels against the CPU executor (gpu-marked)."""
 import numpy as np
@@ -122,3 +123,60 @@ def test_more_ops_gpu_matches_cpu():
     for name, a, b in zip(FETCHES, gpu, cpu):
         assert a.shape == b.shape, name
         np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5, err_msg=name)
+
+
+def conv2d_transpose_ref(dy, w, out_shape, s, padding):
+    """Direct definition: dx[n, h, w, ic] = sum dy[n, oh, ow, oc] * W[kh, kw, ic, oc]
+    over h = oh*s + kh - pad_top (the forward conv's window positions)."""
+    n, H, W, ic = out_shape
+    kh, kw, _, oc = w.shape
+    oh_, ow_ = dy.shape[1:3]
+    if padding == "SAME":
+        pt = max((oh_ - 1) * s + kh - H, 0) // 2
+        pl = max((ow_ - 1) * s + kw - W, 0) // 2
+    else:
+        pt = pl = 0
+    dx = np.zeros(out_shape)
+    for oh in range(oh_):
+        for ow in range(ow_):
+            for a in range(kh):
+                for b in range(kw):
+                    h, x = oh * s + a - pt, ow * s + b - pl
+                    if 0 <= h < H and 0 <= x < W:
+                        dx[:, h, x, :] += dy[:, oh, ow, :] @ w[a, b].T
+    return dx
+
+
+@pytest.mark.parametrize("H,W,k,s,padding", [(8, 8, 3, 2, "SAME"), (7, 9, 3, 2, "SAME"), (6, 6, 3, 2, "VALID"),
+                                             (5, 5, 2, 1, "SAME"), (9, 8, 4, 3, "VALID")])
+def test_conv2d_transpose(H, W, k, s, padding):
+    ic, oc, n = 3, 5, 2
+    oh = -(-H // s) if padding == "SAME" else (H - k) // s + 1
+    ow = -(-W // s) if padding == "SAME" else (W - k) // s + 1
+    dy = rng.standard_normal((n, oh, ow, oc))
+    w = rng.standard_normal((k, k, ic, oc))
+    g = tf.Graph()
+    with g.as_default():
+        d = tf.placeholder(tf.float64, [None, oh, ow, oc], name="dy")
+        tf.nn.conv2d_transpose(d, tf.constant(w), [n, H, W, ic], [1, s, s, 1], padding, name="dx")
+    (dx,) = run(g, ["dx"], {"dy": dy})
+    np.testing.assert_allclose(dx, conv2d_transpose_ref(dy, w, (n, H, W, ic), s, padding), rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("H,W,k,s,padding", [(8, 8, 3, 2, "SAME"), (7, 9, 3, 2, "SAME"), (6, 6, 3, 2, "VALID"),
+                                             (16, 16, 4, 2, "SAME")])
+def test_conv2d_transpose_gpu(H, W, k, s, padding):
+    ic, oc, n = 8, 12, 3
+    oh = -(-H // s) if padding == "SAME" else (H - k) // s + 1
+    ow = -(-W // s) if padding == "SAME" else (W - k) // s + 1
+    dy = rng.standard_normal((n, oh, ow, oc)).astype(np.float32)
+    w = rng.standard_normal((k, k, ic, oc)).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        d = tf.placeholder(tf.float32, [None, oh, ow, oc], name="dy")
+        tf.nn.conv2d_transpose(d, tf.constant(w), [n, H, W, ic], [1, s, s, 1], padding, name="dx")
+    (got,) = run(g, ["dx"], {"dy": dy}, torch.device("cuda", 0))
+    want = conv2d_transpose_ref(dy.astype(np.float64), w.astype(np.float64), (n, H, W, ic), s, padding)
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4)
