@@ -35,10 +35,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int kBK = 32;        // k depth of one LDS stage (two 16-deep MFMA steps)
 constexpr int kRow = kBK + 8;  // LDS row stride in bf16
 
+// round-to-nearest-even f32 -> bf16: a plain cast, which hipcc lowers to
+// v_cvt_pk_bf16_f32 on gfx950 (one instruction per pair; NaN stays NaN)
 __device__ __forceinline__ uint32_t bf16_bits_rne(float x) {
-  uint32_t u = __float_as_uint(x);
-  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (finite inputs)
-  return u >> 16;
+  const __bf16 h = static_cast<__bf16>(x);
+  return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h));
 }
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
 
