@@ -403,14 +403,16 @@ F32Plan plan_for(int cfg, int64_t M, int64_t N, int64_t K, int64_t batch) {
   return p;
 }
 
-int tile_env() {
-  static const int v = [] {
+// forced f32 tile (-1 = heuristic + autotuner): TFA_GEMM_TILE or set_gemm_tile()
+std::atomic<int>& forced_tile() {
+  static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_GEMM_TILE");
     const int t = e ? std::atoi(e) : -1;
     return t >= 0 && t < kNumTiles ? t : -1;
-  }();
+  }());
   return v;
 }
+int tile_env() { return forced_tile().load(); }
 
 // Heuristic plan (also the fallback of the autotuner and what sizes the split-K workspace)
 F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
@@ -604,6 +606,12 @@ GemmArgs conv_as_gemm(const ConvArgs& a) {
 }
 
 }  // namespace
+
+void set_gemm_tile(int cfg) {
+  TFA_CHECK(cfg >= -1 && cfg < kNumTiles, "gemm tile must be -1 (auto) or 0..", kNumTiles - 1);
+  forced_tile().store(cfg);
+}
+int gemm_tile_count() { return kNumTiles; }
 
 void set_f32_precision(int mode) {
   TFA_CHECK(mode >= 0 && mode <= 2, "precision mode must be 0 (f32), 1 (bf16) or 2 (bf16x3)");

@@ -106,6 +106,9 @@ void gemm(DType dt, const GemmArgs& g, hipStream_t s);
 // operands, 2 bf16x3 (hi/lo split, ~16-bit operands); f32 accumulate in all.
 // Initial value from TFA_PRECISION (f32 | bf16 | bf16x3).
 void set_f32_precision(int mode);
+// Force one tile of the f32 core (-1 = heuristic + autotuner); for tests/tuning.
+void set_gemm_tile(int cfg);
+int gemm_tile_count();
 int f32_precision();
 
 // ------------------------------------------------------------ conv / pool (NHWC)

@@ -109,3 +109,34 @@ def test_bf16_is_faster_than_f32_on_a_big_gemm():
     diff = (res["f32"][1] - res["bf16x3"][1]).abs().max().item()
     assert 0 < diff < 1e-2
     assert res["bf16x3"][0] < res["f32"][0]
+
+
+def test_every_f32_tile_gives_bitwise_identical_results():
+    """The tile autotuner may pick any single-pass tile of the f32 core: every
+    tile sums each output's K products in the same order (BK=16 LDS steps of
+    32x32x2 MFMAs), so the results are bit-identical whichever tile wins.
+    (Shapes sized so every forced tile stays single-pass: a split-K plan sums in
+    another order, and the tuner never picks one.)"""
+    rng = np.random.default_rng(9)
+    x = rng.uniform(-1, 1, (40000, 300)).astype(np.float32)
+    w = rng.uniform(-1, 1, (300, 256)).astype(np.float32)
+    img = rng.uniform(-1, 1, (96, 20, 20, 32)).astype(np.float32)
+    f = rng.uniform(-1, 1, (3, 3, 32, 192)).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        xi = tf.placeholder(tf.float32, [None, 300], name="x")
+        tf.matmul(xi, tf.constant(w), name="y")
+        ii = tf.placeholder(tf.float32, [None, 20, 20, 32], name="img")
+        tf.nn.conv2d(ii, tf.constant(f), [1, 1, 1, 1], "SAME", name="c")
+    outs = {}
+    try:
+        for cfg in range(_C.gemm_tile_count()):
+            _C.set_gemm_tile(cfg)
+            outs[cfg] = run(g, ["y", "c"], {"x": x, "img": img})
+    finally:
+        _C.set_gemm_tile(-1)
+    auto = run(g, ["y", "c"], {"x": x, "img": img})
+    for cfg, (y, c) in outs.items():
+        assert np.array_equal(y, outs[0][0]), f"tile {cfg}: GEMM differs"
+        assert np.array_equal(c, outs[0][1]), f"tile {cfg}: conv differs"
+    assert np.array_equal(auto[0], outs[0][0]) and np.array_equal(auto[1], outs[0][1])
