@@ -433,6 +433,12 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
     vec = _RowVectorizer(spec.graph_bytes, fetch_refs, feed_names,
                          [summary[n].tf_dtype for n in feed_names]) if config.map_rows_vectorize and feed_names \
         else None
+    row_feeds = feed_names + [hf.node for hf in host]
+    bcut = None
+    if config.map_rows_vectorize and row_feeds and (host or vec is not None):
+        bcut = _BatchCut(spec.graph_bytes, fetch_refs, row_feeds)
+        if bcut.cut is None:
+            bcut = None
 
     def compute(blocks):
         res = {}
@@ -446,6 +452,15 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
             # the partition is done (one D2H per column instead of a sync per row)
             done = vec.run_groups(b, feed_cols, cell_views, dev, per_out) if vec is not None and not host \
                 else [None] * b.nrows
+            if bcut is not None and b.nrows >= 2 and any(d is None for d in done):
+                todo = [i for i in range(b.nrows) if done[i] is None]
+                sub = [[None] * len(todo) for _ in outputs]
+                bcut.run(len(todo), lambda k: [cv[todo[k]] for cv in cell_views] + [hv[todo[k]] for hv in host_views],
+                         dev, sub)
+                for j in range(len(outputs)):
+                    for k, i in enumerate(todo):
+                        per_out[j][i] = sub[j][k]
+                done = [True] * b.nrows
             for i in range(b.nrows):
                 if done[i] is not None:
                     continue
@@ -487,6 +502,168 @@ def _host_contents(spec: GraphSpec, host) -> List[str]:
         return []
     g = engine.native_graph(spec.graph_bytes)
     return [g.node_inputs(hf.node)[0].split(":")[0] for hf in host]
+
+
+class _BatchCut:
+    """map_rows fast path for per-row graphs that build a batch of one
+    (`expand_dims(preprocessed_image, 0)` -> CNN, the reference's read_image
+    scoring graph: src/main/python/tensorframes_snippets/read_image.py:35-75).
+
+    The graph is cut at the first tensor that (a) every fetch depends on the row
+    inputs only through, and (b) has a static shape with leading dim 1. The part
+    above the cut runs per row (cells may differ in shape, e.g. decoded JPEGs);
+    the cut tensors of a chunk of rows are concatenated along dim 0 and the part
+    below runs ONCE per chunk. Accepted only when the planner classifies every
+    fetch as row-local with the cut fed as rows (nothing mixes rows) and the
+    batched fetch shapes are [R] + the per-row shape (or its tail when the
+    per-row shape leads with 1); otherwise the per-row loop is kept."""
+
+    CHUNK = 64
+
+    def __init__(self, graph_bytes: bytes, fetch_refs: List[str], row_feeds: List[str]):
+        self.graph_bytes, self.fetch_refs, self.row_feeds = graph_bytes, list(fetch_refs), list(row_feeds)
+        self.cut = None
+        self.modes: List[str] = []
+        try:
+            self._find()
+        except ValueError:
+            self.cut = None
+        metrics.add("map_rows_batch_cut" if self.cut else "map_rows_no_batch_cut")
+
+    def _find(self):
+        g = engine.native_graph(self.graph_bytes)
+        infos = _C.infer_fed(g, self.fetch_refs, self.row_feeds, {})
+        names = list(g.node_names())
+        inputs = {n: [i.split(":")[0].lstrip("^") for i in g.node_inputs(n)] for n in names if n in infos}
+        consumers: Dict[str, List[str]] = {}
+        for n, ins in inputs.items():
+            for i in ins:
+                consumers.setdefault(i, []).append(n)
+        fetch_nodes = {f.split(":")[0] for f in self.fetch_refs}
+
+        def reaches_fetch(avoid: str) -> bool:
+            seen, stack = set(), [f for f in self.row_feeds if f != avoid]
+            while stack:
+                n = stack.pop()
+                if n in seen or n == avoid:
+                    continue
+                seen.add(n)
+                if n in fetch_nodes:
+                    return True
+                stack.extend(consumers.get(n, []))
+            return False
+
+        # candidates in graph order (GraphDef order is topological for builder graphs)
+        for n in names:
+            if n not in infos or n in self.row_feeds:
+                continue
+            info = infos[n][0]
+            shp = info["shape"]
+            if info["const"] or shp is None or not shp or shp[0] != 1 or any(d is None or d < 0 for d in shp):
+                continue
+            if reaches_fetch(n):
+                continue
+            if self._accept(g, n, info["dtype"], shp):
+                self.cut = n
+                self.cut_dtype = info["dtype"]
+                return
+
+    def _drop_batch_squeezes(self, node: str, one: Dict[str, Any]):
+        """Squeezes below the cut that drop the batch-of-one dim are rewritten
+        to keep it (`squeeze(prob)` before top_k in the reference's snippet).
+        Everything downstream of such a squeeze then sees one extra leading
+        dim, so it must be an op whose meaning does not depend on the leading
+        axes: elementwise ops, Cast/Identity and the last-axis ops. Returns the
+        patched graph bytes (or the original ones), or None to refuse."""
+        from .graph import vectorize as V
+        light = P.parse_graphdef(_C.light_graphdef(self.graph_bytes, 4096))
+        by_name = {nd.name: nd for nd in light.node}
+        consumers: Dict[str, List[str]] = {}
+        for nd in light.node:
+            for i in nd.input:
+                consumers.setdefault(i.split(":")[0].lstrip("^"), []).append(nd.name)
+        below, stack = set(), [node]
+        while stack:
+            n = stack.pop()
+            for c in consumers.get(n, []):
+                if c not in below:
+                    below.add(c)
+                    stack.append(c)
+        patch, shifted = [], set()
+        for n in sorted(below, key=[nd.name for nd in light.node].index):
+            nd = by_name[n]
+            if nd.op != "Squeeze" or n not in one:
+                continue
+            src = nd.input[0].split(":")[0]
+            ins = one.get(src, [{}])[0].get("shape")
+            if not ins or ins[0] != 1:
+                continue
+            dims = list(nd.attr["squeeze_dims"].value.get("i", [])) if "squeeze_dims" in nd.attr else []
+            rank = len(ins)
+            if dims and 0 not in dims and -rank not in dims:
+                continue
+            keep = [d for d in (dims or [i for i, d in enumerate(ins) if d == 1]) if d not in (0, -rank)]
+            attr = {k: v for k, v in nd.attr.items() if k == "T"}
+            if keep:
+                attr["squeeze_dims"] = P.AttrValue.ilist(keep)
+            patch.append(P.NodeDef(n, "Squeeze" if keep else "Identity", nd.input, attr, nd.device))
+            shifted.add(n)
+        if not patch:
+            return self.graph_bytes
+        ok_ops = V._UNARY | V._BINARY | V._LAST_AXIS | {"Identity", "Cast", "TopKV2", "StopGradient"}
+        stack, seen = list(shifted), set()
+        while stack:
+            n = stack.pop()
+            for c in consumers.get(n, []):
+                if c in seen:
+                    continue
+                seen.add(c)
+                if by_name[c].op not in ok_ops:
+                    return None
+                stack.append(c)
+        return _C.patch_graphdef(self.graph_bytes, P.serialize_graphdef(P.GraphDef(patch)))
+
+    def _accept(self, g, node: str, dtype: int, shp: List[int]) -> bool:
+        try:
+            one = _C.infer_fed(g, self.fetch_refs, [node], {node: (dtype, list(shp))})
+            post_bytes = self._drop_batch_squeezes(node, one)
+            if post_bytes is None:
+                return False
+            pg = g if post_bytes is self.graph_bytes else engine.native_graph(post_bytes)
+            three = _C.infer_fed(pg, self.fetch_refs, [node], {node: (dtype, [3] + list(shp[1:]))})
+            prog = engine.program(post_bytes, self.fetch_refs, [node])
+            if not prog.row_separable({node: (dtype, [3] + list(shp[1:]))}):
+                return False
+        except ValueError:  # the part below the cut does not accept a batch
+            return False
+        modes = []
+        for f in self.fetch_refs:
+            base, _, idx = f.partition(":")
+            a = one[base][int(idx or 0)]["shape"]
+            b = three[base][int(idx or 0)]["shape"]
+            if a is None or b is None or any(d is None or d < 0 for d in list(a) + list(b)):
+                return False
+            if list(b) == [3] + list(a):
+                modes.append("index")
+            elif a and a[0] == 1 and list(b) == [3] + list(a[1:]):
+                modes.append("slice")
+            else:
+                return False
+        self.modes = modes
+        self.pre = engine.program(self.graph_bytes, [node + ":0"], self.row_feeds)
+        self.post = prog
+        return True
+
+    def run(self, nrows: int, row_inputs, dev, per_out) -> None:
+        """row_inputs(i) -> the per-row feed tensors; fills per_out[j][i]."""
+        for a in range(0, nrows, self.CHUNK):
+            rows = range(a, min(nrows, a + self.CHUNK))
+            cut = [engine.run_program(self.pre, row_inputs(i), dev)[0] for i in rows]
+            outs = engine.run_program(self.post, [torch.cat(cut, 0)], dev)
+            for j, (o, mode) in enumerate(zip(outs, self.modes)):
+                for k, i in enumerate(rows):
+                    per_out[j][i] = o[k] if mode == "index" else o[k:k + 1]
+        metrics.add("map_rows_batch_cut_rows", nrows)
 
 
 class _RowVectorizer:
