@@ -1105,6 +1105,44 @@ def _factorize(arrays: List[np.ndarray]):
     return inv.astype(np.int64), list(reversed(uniq_cols))
 
 
+def _shuffle_blocks(send: List[List[Block]], names: List[str], tf_types: Dict[str, Optional[int]]) -> List[Block]:
+    """The groupBy shuffle: send[r] = blocks for rank r; returns the blocks
+    this rank received. Dense columns (same dtype and cell shape on every
+    rank) travel as tensors in one all_to_all per column, device-resident
+    ones over RCCL; other columns (strings, ragged cells) as pickled values."""
+    w = dist.world_size()
+    if w == 1:
+        return list(send[0])
+    per = [concat_blocks(s, names) if s else None for s in send]
+    recv_rows = dist.all_to_all_counts([0 if p is None else p.nrows for p in per])
+
+    def meta(n):
+        cols = [p.columns[n] for p in per if p is not None and p.nrows]
+        if not cols:
+            return None
+        if all(is_dense(c) for c in cols) and len({(c.dtype, tuple(c.shape[1:])) for c in cols}) == 1:
+            return ("dense", str(cols[0].dtype).split(".")[-1], tuple(cols[0].shape[1:]), all(c.is_cuda for c in cols))
+        return ("obj",)
+
+    metas = dist.all_gather_object([meta(n) for n in names])
+    cols: Dict[str, Any] = {}
+    for j, n in enumerate(names):
+        ms = [m[j] for m in metas if m[j] is not None]
+        dense = all(m[0] == "dense" for m in ms) and len({m[1:3] for m in ms}) == 1
+        if dense:
+            dtype, cell = getattr(torch, ms[0][1]), ms[0][2]
+            dev = engine.compute_device() if all(m[3] for m in ms) and dist.gpu_collectives() else torch.device("cpu")
+            chunks = [p.columns[n].to(dev) if p is not None and p.nrows else
+                      torch.empty((0,) + cell, dtype=dtype, device=dev) for p in per]
+            cols[n] = dist.all_to_all_tensors(chunks, recv_rows)
+        else:
+            got = dist.all_to_all_objects([column_values(p.columns[n]) if p is not None and p.nrows else []
+                                           for p in per])
+            cols[n] = build_column([v for g in got for v in g], tf_types[n])
+    # (every rank takes part in every exchange above, even with nothing to receive)
+    return [Block(sum(recv_rows), cols)] if sum(recv_rows) else []
+
+
 def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) -> DataFrame:
     """Algebraic aggregation over `df.groupBy(keys)`: the reduce_blocks graph
     contract applied per key. Output = key columns ++ fetched columns, one row
@@ -1124,6 +1162,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
     monoid = {m[0]: m[2] for m in prog.monoids()}
     uniform = set(monoid) == set(out_names)
     all_cols = keys + out_names
+    tf_types = {k: _tf_of_field(df.schema[k]) for k in all_cols}
 
     def combine(blocks):
         """Monoid graphs: map-side combine. Each partition is reduced per key on
@@ -1145,7 +1184,9 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 dev = engine.compute_device() if x.is_cuda or engine.gpu_available() else x.device
                 xd = x.to(dev) if x.device != dev else x
                 ids = torch.from_numpy(codes).to(dev)
-                cols[n] = _C.unsorted_segment_reduce(monoid[n], xd.contiguous(), ids, ng).cpu()
+                red = _C.unsorted_segment_reduce(monoid[n], xd.contiguous(), ids, ng)
+                # partials stay in HBM when the shuffle can move them over RCCL
+                cols[n] = red if (w > 1 and red.is_cuda and dist.gpu_collectives()) else red.cpu()
             part = Block(ng, cols)
             if w == 1:
                 send[0].append(part)
@@ -1155,7 +1196,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 idx = np.nonzero(dest == r)[0]
                 if len(idx):
                     send[r].append(part.take(idx))
-        mine = [blk for lst in dist.all_to_all_objects(send) for blk in lst]
+        mine = _shuffle_blocks(send, all_cols, tf_types)
         if not mine:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, w))}
         full = concat_blocks(mine, all_cols)
@@ -1166,7 +1207,8 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             out_cols[k] = build_column(uniq_cols[i].tolist(), _tf_of_field(df.schema[k]))
         ids = torch.from_numpy(codes)
         for n in out_names:
-            out_cols[n] = _C.unsorted_segment_reduce(monoid[n], full.columns[n].contiguous(), ids, ng)
+            x = full.columns[n].contiguous()
+            out_cols[n] = _C.unsorted_segment_reduce(monoid[n], x, ids.to(x.device), ng).cpu()
         return {dist.rank(): Block(ng, out_cols)}
 
     def compute(blocks):
@@ -1187,8 +1229,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 idx = np.nonzero(dest == r)[0]
                 if len(idx):
                     send[r].append(host.take(idx))
-        recv = dist.all_to_all_objects(send)
-        mine = [blk for lst in recv for blk in lst]
+        mine = _shuffle_blocks(send, all_cols, tf_types)
         if not mine:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, w))}
         full = concat_blocks(mine, all_cols)

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import pickle
 from typing import Any, List, Optional
 
 import torch
@@ -180,12 +181,57 @@ def broadcast_object(obj: Any, src: int = 0) -> Any:
 
 
 def all_to_all_objects(per_dest: List[Any]) -> List[Any]:
-    """per_dest[r] goes to rank r; returns what each rank sent to us."""
+    """per_dest[r] goes to rank r; returns what each rank sent to us. A true
+    pairwise exchange: the pickled payloads travel in one gloo all_to_all
+    (each rank receives only its own share, not the whole shuffle)."""
     if not is_distributed():
         return [per_dest[0]]
-    gathered = all_gather_object(per_dest)
-    me = rank()
-    return [gathered[src][me] for src in range(world_size())]
+    _ensure_groups()
+    payload = [pickle.dumps(o, protocol=pickle.HIGHEST_PROTOCOL) for o in per_dest]
+    sizes = all_to_all_counts([len(b) for b in payload])
+    send = torch.frombuffer(bytearray(b"".join(payload)), dtype=torch.uint8) if any(payload) else \
+        torch.empty(0, dtype=torch.uint8)
+    recv = torch.empty(sum(sizes), dtype=torch.uint8)
+    dist.all_to_all_single(recv, send, sizes, [len(b) for b in payload], group=_state["cpu_group"])
+    out, off, raw = [], 0, recv.numpy().tobytes()
+    for n in sizes:
+        out.append(pickle.loads(raw[off:off + n]))  # payloads written by our own ranks
+        off += n
+    return out
+
+
+def all_to_all_counts(send_counts: List[int]) -> List[int]:
+    """send_counts[r] = what we send to rank r; returns what each rank sends us."""
+    if not is_distributed():
+        return [int(send_counts[0])]
+    _ensure_groups()
+    t = torch.tensor([int(c) for c in send_counts], dtype=torch.int64)
+    out = torch.empty_like(t)
+    dist.all_to_all_single(out, t, group=_state["cpu_group"])
+    return out.tolist()
+
+
+def gpu_collectives() -> bool:
+    """Device tensors can go straight to RCCL (False under a gloo rehearsal)."""
+    _ensure_groups()
+    return dist.get_backend(_state["device_group"]) == "nccl"
+
+
+def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torch.Tensor:
+    """chunks[r] (one dtype and trailing shape) goes to rank r; returns the
+    received rows, concatenated in source-rank order. Device tensors move in
+    ONE RCCL all_to_all over xGMI (the groupBy shuffle: SURVEY D4, reference
+    DebugRowOps.scala:576), host tensors over gloo."""
+    x = torch.cat(chunks, 0).contiguous()
+    if not is_distributed():
+        return x
+    _ensure_groups()
+    if x.is_cuda and not gpu_collectives():
+        return all_to_all_tensors([c.cpu() for c in chunks], recv_rows).to(x.device)
+    group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
+    out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_to_all_single(out, x, [int(r) for r in recv_rows], [int(c.shape[0]) for c in chunks], group=group)
+    return out
 
 
 # -- tensor collectives: device tensors over RCCL, host tensors over gloo

@@ -33,7 +33,7 @@ def _worker(rank, world, port, outdir):
 
     assert dist.init(backend="gloo")
     res = {}
-    data = [Row(key=str(i % 3), x=float(i), v=[float(i), float(2 * i)]) for i in range(20)]
+    data = [Row(key=str(i % 3), k=i % 4, x=float(i), v=[float(i), float(2 * i)]) for i in range(20)]
     df = tfs.analyze(tfs.create_dataframe(data, num_partitions=5))
     res["local_parts"] = sorted(df.local_blocks())
     res["count"] = df.count()
@@ -59,6 +59,22 @@ def _worker(rank, world, port, outdir):
         xi = tf.placeholder(tf.double, shape=[None], name="x_input")
         agg = tfs.aggregate(tf.reduce_sum(xi, [0], name="x"), df.select("key", "x").groupBy("key"))
         res["agg"] = sorted([list(r) for r in agg.collect()])
+    with tf.Graph().as_default():
+        # integer keys + vector cells: both shuffle as tensors (all_to_all_single)
+        vi = tf.placeholder(tf.double, shape=[None, 2], name="v_input")
+        agg = tfs.aggregate(tf.reduce_sum(vi, [0], name="v"), df.select("k", "v").groupBy("k"))
+        res["agg_int"] = sorted([[r.k, list(r.v)] for r in agg.collect()])
+    with tf.Graph().as_default():
+        # not a recognised monoid: rows shuffle, then one graph run per key
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        agg = tfs.aggregate(tf.identity(tf.reduce_sum(xi * xi, [0]), name="x"), df.select("k", "x").groupBy("k"))
+        res["agg_gen"] = sorted([[r.k, r.x] for r in agg.collect()])
+    with tf.Graph().as_default():
+        # one key: every other rank receives nothing from the shuffle
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        one = tfs.create_dataframe([Row(c="a", x=float(i)) for i in range(20)], num_partitions=5)
+        agg = tfs.aggregate(tf.reduce_min(xi, [0], name="x"), one.groupBy("c"))
+        res["agg_one"] = [list(r) for r in agg.collect()]
     res["repart"] = [r.x for r in df.repartition(4).select("x").collect()]
     # checkpoint: every rank writes its own partitions, reads them back
     ck = os.path.join(outdir, "ck")
@@ -97,6 +113,10 @@ def test_spmd_world(world, tmp_path):
         assert o["vmax"] == [19.0, 38.0]
         want = sorted([[k, sum(x for x in xs if str(int(x) % 3) == k)] for k in ("0", "1", "2")])
         assert o["agg"] == want
+        assert o["agg_int"] == [[k, [sum(x for x in xs if int(x) % 4 == k), 2 * sum(x for x in xs if int(x) % 4 == k)]]
+                                for k in range(4)]
+        assert o["agg_gen"] == [[k, sum(x * x for x in xs if int(x) % 4 == k)] for k in range(4)]
+        assert o["agg_one"] == [["a", 0.0]]
         assert o["repart"] == xs
         assert o["ck_parts"] == o["local_parts"] and o["ck_x"] == xs
         assert o["retry_z"] == [x + 1.0 for x in xs]
