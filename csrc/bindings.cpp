@@ -186,6 +186,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["graphs_captured"] = s.graphs_captured;
         d["graph_replays"] = s.graph_replays;
         d["graph_failures"] = s.graph_failures;
+        d["graphs_declined"] = s.graphs_declined;
         return d;
       });
 

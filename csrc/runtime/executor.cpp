@@ -87,6 +87,10 @@ struct Program::Plan {
     std::mutex mu;
     int64_t gpu_runs = 0;
     bool failed = false;
+    // host time of warm eager runs vs replays: a replay (input copy + graph
+    // launch + output clone) can cost more than launching a few kernels
+    int64_t eager_ns = 0, eager_n = 0, replay_ns = 0, replay_n = 0;
+    bool declined = false;
     int device = -1;
     hipStream_t stream = nullptr;  // our own capture stream (never shared)
     std::unique_ptr<at::cuda::CUDAGraph> graph;
@@ -540,16 +544,32 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
 
 // HIP graphs: a plan that keeps being run with small inputs is launch-bound;
 // after kGraphWarmRuns ordinary runs its kernel sequence is captured once and
-// replayed (inputs copied into static buffers, outputs cloned out). Enabled
-// with TFA_HIP_GRAPHS=1 (default) for inputs up to TFA_HIP_GRAPH_MAX_BYTES.
+// replayed (inputs copied into static buffers, outputs cloned out). A replay
+// has a fixed cost (input copy, graph launch, output clone: ~80-150 us on
+// MI355X, scripts/map_rows_overhead.py), so only plans of at least
+// kGraphMinSteps kernels are captured: a 5-kernel image-preprocessing plan
+// runs in 25 us eager vs 85-160 us replayed, a 40-op elementwise chain in
+// 440 us eager vs 190 us replayed. The first kGraphProbeRuns replays are also
+// timed (host side) against the warm eager runs and the graph is dropped when
+// replaying costs more. TFA_HIP_GRAPHS: 1 (default) adaptive, 2 always
+// replay (any size), 0 never. Inputs up to TFA_HIP_GRAPH_MAX_BYTES.
 namespace {
 constexpr int64_t kGraphWarmRuns = 3;
-bool hip_graphs_enabled() {
-  static const bool on = [] {
+constexpr int64_t kGraphProbeRuns = 5;
+constexpr size_t kGraphMinSteps = 16;
+int hip_graphs_mode() {
+  static const int mode = [] {
     const char* e = std::getenv("TFA_HIP_GRAPHS");
-    return !(e && std::string(e) == "0");
+    if (!e) return 1;
+    const std::string v(e);
+    return v == "0" ? 0 : (v == "2" ? 2 : 1);
   }();
-  return on && !debug_sync();
+  return debug_sync() ? 0 : mode;
+}
+bool hip_graphs_enabled() { return hip_graphs_mode() != 0; }
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 int64_t hip_graph_max_bytes() {
   static const int64_t v = [] {
@@ -640,13 +660,33 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
     if (hip_graphs_enabled()) {
       int64_t bytes = 0;
       for (auto& t : inputs) bytes += t.numel() * t.element_size();
-      std::lock_guard<std::mutex> lk(p->cap.mu);
-      const bool same_dev = p->cap.device < 0 || p->cap.device == inputs[0].device().index();
-      if (!p->cap.failed && same_dev && bytes <= hip_graph_max_bytes() && ++p->cap.gpu_runs > kGraphWarmRuns &&
-          graphable(*p)) {
-        auto outs = run_graph(*p, inputs);
-        stats_.runs++;
-        return outs;
+      auto& c = p->cap;
+      std::lock_guard<std::mutex> lk(c.mu);
+      const bool same_dev = c.device < 0 || c.device == inputs[0].device().index();
+      const bool big_enough = hip_graphs_mode() == 2 || p->steps.size() >= kGraphMinSteps;
+      if (!c.failed && !c.declined && same_dev && big_enough && bytes <= hip_graph_max_bytes() && graphable(*p)) {
+        if (++c.gpu_runs > kGraphWarmRuns) {
+          const bool captured = c.graph != nullptr;
+          const int64_t t0 = now_ns();
+          auto outs = run_graph(*p, inputs);
+          if (captured && c.graph && hip_graphs_mode() == 1 && c.eager_n > 0) {
+            c.replay_ns += now_ns() - t0;
+            if (++c.replay_n == kGraphProbeRuns && c.replay_ns * c.eager_n > c.eager_ns * c.replay_n) {
+              c.declined = true;  // eager launches are cheaper for this plan
+              stats_.graphs_declined++;
+            }
+          }
+          stats_.runs++;
+          return outs;
+        }
+        if (c.gpu_runs > 1) {  // warm eager runs (the first one uploads constants)
+          const int64_t t0 = now_ns();
+          auto outs = execute(*p, inputs, stream);
+          c.eager_ns += now_ns() - t0;
+          c.eager_n++;
+          stats_.runs++;
+          return outs;
+        }
       }
     }
   }

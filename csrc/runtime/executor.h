@@ -35,7 +35,7 @@ struct ExecStats {
   int64_t d2h_bytes = 0;
   int64_t chunks = 0;
   double h2d_ms = 0, compute_ms = 0, d2h_ms = 0, wall_ms = 0;
-  int64_t graphs_captured = 0, graph_replays = 0, graph_failures = 0;
+  int64_t graphs_captured = 0, graph_replays = 0, graph_failures = 0, graphs_declined = 0;
 };
 
 class Program {

@@ -243,6 +243,10 @@ def all_reduce_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
     if not is_distributed():
         return t
     _ensure_groups()
+    if t.is_cuda and not gpu_collectives():  # gloo rehearsal: stage through the host
+        h = t.cpu()
+        dist.all_reduce(h, op=_OPS[op], group=_state["cpu_group"])
+        return t.copy_(h)
     group = _state["device_group"] if t.is_cuda else _state["cpu_group"]
     dist.all_reduce(t, op=_OPS[op], group=group)
     return t
@@ -254,6 +258,8 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
         return t.unsqueeze(0)
     _ensure_groups()
     t = t.contiguous()
+    if t.is_cuda and not gpu_collectives():
+        return all_gather_tensor(t.cpu()).to(t.device)
     if t.is_cuda:
         out = torch.empty((world_size(),) + tuple(t.shape), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t, group=_state["device_group"])

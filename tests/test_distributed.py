@@ -8,6 +8,7 @@ import socket
 import sys
 
 import pytest
+import torch
 import torch.multiprocessing as mp
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,9 +22,11 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TFA_DEVICE="cpu")
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if device == "cpu":
+        os.environ["TFA_DEVICE"] = "cpu"
     sys.path.insert(0, REPO)
     import numpy as np
 
@@ -32,7 +35,8 @@ def _worker(rank, world, port, outdir):
     from tensorframes_amd.parallel import dist
 
     assert dist.init(backend="gloo")
-    res = {}
+    from tensorframes_amd import engine
+    res = {"device": engine.compute_device().type}
     data = [Row(key=str(i % 3), k=i % 4, x=float(i), v=[float(i), float(2 * i)]) for i in range(20)]
     df = tfs.analyze(tfs.create_dataframe(data, num_partitions=5))
     res["local_parts"] = sorted(df.local_blocks())
@@ -101,7 +105,22 @@ def _worker(rank, world, port, outdir):
 @pytest.mark.parametrize("world", [2, 3])
 def test_spmd_world(world, tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    _check_results(tmp_path, world, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(torch.cuda.device_count() == 0, reason="needs a GPU")
+def test_spmd_two_ranks_share_one_gpu(tmp_path):
+    """The same SPMD program with both ranks computing on the GPU (gloo
+    rehearsal: device tensors are staged through the host for collectives,
+    since RCCL cannot put two ranks on one GPU)."""
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), "gpu"), nprocs=2, join=True)
+    _check_results(tmp_path, 2, "cuda")
+
+
+def _check_results(tmp_path, world, device):
     outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+    assert all(o["device"] == device for o in outs)
     xs = [float(i) for i in range(20)]
     parts = sorted(p for o in outs for p in o["local_parts"])
     assert parts == [0, 1, 2, 3, 4]

@@ -89,9 +89,13 @@ def test_hip_graph_replay_matches_eager_and_outputs_do_not_alias():
     import numpy as np
     from tensorframes_amd import engine, tf
     g = tf.Graph()
-    w = np.random.default_rng(3).standard_normal((64, 32)).astype(np.float32)
+    rng = np.random.default_rng(3)
+    w = rng.standard_normal((64, 32)).astype(np.float32)
     with g.as_default():
         x = tf.placeholder(tf.float32, [None, 64], name="x")
+        # enough kernels for capture to pay off (kGraphMinSteps)
+        for i in range(16):
+            x = tf.nn.relu(tf.matmul(x, tf.constant(rng.standard_normal((64, 64)).astype(np.float32) / 8)))
         h = tf.nn.relu(tf.matmul(x, tf.constant(w)))
         y = tf.reduce_sum(tf.square(h - 1.0), [1], name="y")
         tf.nn.softmax(h * 0.1, name="p")

@@ -5,6 +5,7 @@ must be refused (reference semantics: one session.run per row,
 src/main/scala/org/tensorframes/impl/DebugRowOps.scala:832-856)."""
 import numpy as np
 import pytest
+import torch
 
 import tensorframes_amd as tfs
 from tensorframes_amd import tf
@@ -108,3 +109,24 @@ def test_explicit_squeeze_dims():
     assert v1.shape == v0.shape == (5, 4, 3)
     np.testing.assert_allclose(v1, v0, rtol=1e-6)
     np.testing.assert_allclose(i1, i0, rtol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_batch_cut_on_gpu_matches_cpu_loop():
+    """Rows forced onto the GPU: the per-row part runs on a side stream, the
+    batched part on the compute stream; results equal the CPU per-row loop."""
+    df = image_frame(150)  # > one chunk of 64 rows
+    g = scoring_graph()
+    old = tfs.config.map_rows_gpu_min_elems
+    try:
+        tfs.set_config(map_rows_gpu_min_elems=0)
+        metrics.reset()
+        v1, i1, p1 = run_rows(g, df, True)
+        m = metrics.snapshot()
+        assert m.get("map_rows_batch_cut_rows", 0) == m["map_rows_rows"] > 0
+    finally:
+        tfs.set_config(map_rows_gpu_min_elems=old)
+    v0, i0, p0 = run_rows(g, df, False)
+    np.testing.assert_allclose(p1, p0, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(v1, v0, rtol=1e-4, atol=1e-5)
