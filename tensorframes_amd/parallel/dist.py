@@ -13,6 +13,7 @@ from __future__ import annotations
 import datetime
 import os
 import pickle
+import time
 from typing import Any, List, Optional
 
 import torch
@@ -161,13 +162,48 @@ def barrier():
         dist.barrier(group=_state["cpu_group"])
 
 
+class _traced:
+    """Observability for one collective: a roctx range
+    (`rocprofv3 --marker-trace` shows it next to the kernels) and metrics
+    counters `collective_<name>` (calls), `collective_bytes`,
+    `collective_ms` (host time: RCCL calls return once enqueued, gloo ones
+    when done)."""
+
+    def __init__(self, name: str, nbytes: int = 0):
+        self.name, self.nbytes = name, int(nbytes)
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+        self.rng = torch.cuda.is_initialized()
+        if self.rng:
+            try:
+                torch.cuda.nvtx.range_push(f"tfa.collective.{self.name}")
+            except Exception:  # no roctx in this build
+                self.rng = False
+        return self
+
+    def __exit__(self, *exc):
+        if self.rng:
+            torch.cuda.nvtx.range_pop()
+        from ..utils.logging import metrics
+        metrics.add(f"collective_{self.name}", 1)
+        metrics.add("collective_bytes", self.nbytes)
+        metrics.add("collective_ms", (time.perf_counter() - self.t0) * 1e3)
+        return False
+
+
+def _nbytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
+
+
 # -- host-object collectives (small metadata / rows) over gloo
 def all_gather_object(obj: Any) -> List[Any]:
     if not is_distributed():
         return [obj]
     _ensure_groups()
     out = [None] * world_size()
-    dist.all_gather_object(out, obj, group=_state["cpu_group"])
+    with _traced("all_gather_object"):
+        dist.all_gather_object(out, obj, group=_state["cpu_group"])
     return out
 
 
@@ -192,7 +228,8 @@ def all_to_all_objects(per_dest: List[Any]) -> List[Any]:
     send = torch.frombuffer(bytearray(b"".join(payload)), dtype=torch.uint8) if any(payload) else \
         torch.empty(0, dtype=torch.uint8)
     recv = torch.empty(sum(sizes), dtype=torch.uint8)
-    dist.all_to_all_single(recv, send, sizes, [len(b) for b in payload], group=_state["cpu_group"])
+    with _traced("all_to_all_objects", _nbytes(send)):
+        dist.all_to_all_single(recv, send, sizes, [len(b) for b in payload], group=_state["cpu_group"])
     out, off, raw = [], 0, recv.numpy().tobytes()
     for n in sizes:
         out.append(pickle.loads(raw[off:off + n]))  # payloads written by our own ranks
@@ -230,7 +267,9 @@ def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torc
         return all_to_all_tensors([c.cpu() for c in chunks], recv_rows).to(x.device)
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
     out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_to_all_single(out, x, [int(r) for r in recv_rows], [int(c.shape[0]) for c in chunks], group=group)
+    with _traced("all_to_all", _nbytes(x)):
+        dist.all_to_all_single(out, x, [int(r) for r in recv_rows], [int(c.shape[0]) for c in chunks],
+                               group=group)
     return out
 
 
@@ -244,11 +283,10 @@ def all_reduce_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
         return t
     _ensure_groups()
     if t.is_cuda and not gpu_collectives():  # gloo rehearsal: stage through the host
-        h = t.cpu()
-        dist.all_reduce(h, op=_OPS[op], group=_state["cpu_group"])
-        return t.copy_(h)
+        return t.copy_(all_reduce_(t.cpu(), op))
     group = _state["device_group"] if t.is_cuda else _state["cpu_group"]
-    dist.all_reduce(t, op=_OPS[op], group=group)
+    with _traced("all_reduce", _nbytes(t)):
+        dist.all_reduce(t, op=_OPS[op], group=group)
     return t
 
 
@@ -262,8 +300,10 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
         return all_gather_tensor(t.cpu()).to(t.device)
     if t.is_cuda:
         out = torch.empty((world_size(),) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t, group=_state["device_group"])
+        with _traced("all_gather", _nbytes(t)):
+            dist.all_gather_into_tensor(out, t, group=_state["device_group"])
         return out
     parts = [torch.empty_like(t) for _ in range(world_size())]
-    dist.all_gather(parts, t, group=_state["cpu_group"])
+    with _traced("all_gather", _nbytes(t)):
+        dist.all_gather(parts, t, group=_state["cpu_group"])
     return torch.stack(parts, 0)

@@ -97,6 +97,8 @@ def _worker(rank, world, port, outdir, device="cpu"):
         with tf.Graph().as_default():
             x = tf.placeholder(tf.double, shape=[None], name="x")
             res["retry_z"] = [r.z for r in tfs.map_blocks(tf.add(x, 1.0, name="z"), df.select("x")).collect()]
+    from tensorframes_amd.utils.logging import metrics
+    res["coll"] = {k: v for k, v in metrics.snapshot().items() if k.startswith("collective_")}
     with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
         json.dump(res, f)
     dist.shutdown()
@@ -121,6 +123,9 @@ def test_spmd_two_ranks_share_one_gpu(tmp_path):
 def _check_results(tmp_path, world, device):
     outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
     assert all(o["device"] == device for o in outs)
+    for o in outs:  # collectives are counted (metrics) on every rank
+        assert o["coll"].get("collective_all_to_all", 0) >= 1 and o["coll"].get("collective_all_reduce", 0) >= 1
+        assert o["coll"]["collective_bytes"] > 0
     xs = [float(i) for i in range(20)]
     parts = sorted(p for o in outs for p in o["local_parts"])
     assert parts == [0, 1, 2, 3, 4]
