@@ -243,14 +243,21 @@ def cfg_kmeans(a):
     pts = rng.uniform(0.0, 1.0, size=(n, f))
     df = tfs.analyze(tfs.from_columns({"features": pts}, num_partitions=max(1, dist.world_size()) * 4)).cache()
     c0 = np.random.default_rng(2).standard_normal((k, f))
+    frames = {"host": df}
+    if engine.gpu_available():
+        # iterative workloads keep the staged partitions in HBM
+        frames["device"] = df.cache_on_device(engine.compute_device())
     out = {}
-    for variant, agg in (("aggregate", False), ("in_graph", True)):
-        t0 = time.perf_counter()
-        c, ds = kmeans.kmeans(df, c0, num_iters=a.steps, tf_aggregate=agg)
-        out[variant] = (time.perf_counter() - t0) / max(len(ds), 1)
+    for where, frame in frames.items():
+        for variant, agg in (("aggregate", False), ("in_graph", True)):
+            kmeans.kmeans(frame, c0, num_iters=max(a.warmup, 1), tf_aggregate=agg)  # plans, tile tuning
+            t0 = time.perf_counter()
+            c, ds = kmeans.kmeans(frame, c0, num_iters=a.steps, tf_aggregate=agg)
+            out[f"{variant}_{where}"] = (time.perf_counter() - t0) / max(len(ds), 1) * 1e3
+    best = out.get("in_graph_device", out["in_graph_host"])
     emit({"config": "K-Means 100k x 100, k=10 (reference demo)", "metric": "ms/iteration",
-          "value": out["in_graph"] * 1e3, "unit": "ms", "higher_is_better": False,
-          "aggregate_variant_ms": out["aggregate"] * 1e3, "in_graph_variant_ms": out["in_graph"] * 1e3})
+          "value": best, "unit": "ms", "higher_is_better": False,
+          **{f"{k}_ms": v for k, v in out.items()}})
 
 
 def main():
