@@ -37,6 +37,8 @@ class Config:
     map_rows_gpu_min_elems: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_GPU_MIN", 16384, int))
     # map_rows: run same-shaped rows as one block through the lifted row graph
     map_rows_vectorize: bool = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_VECTORIZE", True, bool))
+    # map_rows batch-of-one cut: rows whose cut tensors are concatenated into one batched run
+    map_rows_batch_rows: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_BATCH", 64, int))
     # re-runs of a partition task after a runtime (non-validation) failure; 0 = fail fast
     task_retries: int = dataclasses.field(default_factory=lambda: _env("TFA_TASK_RETRIES", 0, int))
     # timeout of one collective (RCCL/gloo); a stuck collective aborts the job

@@ -513,13 +513,11 @@ class _BatchCut:
     The graph is cut at the first tensor that (a) every fetch depends on the row
     inputs only through, and (b) has a static shape with leading dim 1. The part
     above the cut runs per row (cells may differ in shape, e.g. decoded JPEGs);
-    the cut tensors of a chunk of rows are concatenated along dim 0 and the part
-    below runs ONCE per chunk. Accepted only when the planner classifies every
+    the cut tensors of a chunk of rows (`Config.map_rows_batch_rows`) are
+    concatenated along dim 0 and the part below runs ONCE per chunk. Accepted only when the planner classifies every
     fetch as row-local with the cut fed as rows (nothing mixes rows) and the
     batched fetch shapes are [R] + the per-row shape (or its tail when the
     per-row shape leads with 1); otherwise the per-row loop is kept."""
-
-    CHUNK = 64
 
     def __init__(self, graph_bytes: bytes, fetch_refs: List[str], row_feeds: List[str]):
         self.graph_bytes, self.fetch_refs, self.row_feeds = graph_bytes, list(fetch_refs), list(row_feeds)
@@ -668,8 +666,9 @@ class _BatchCut:
             side = self._side.get(dev.index)
             if side is None:
                 side = self._side[dev.index] = torch.cuda.Stream(dev)
-        for a in range(0, nrows, self.CHUNK):
-            rows = range(a, min(nrows, a + self.CHUNK))
+        step = max(1, int(config.map_rows_batch_rows))
+        for a in range(0, nrows, step):
+            rows = range(a, min(nrows, a + step))
             cut = []
             for i in rows:
                 t0 = time.perf_counter()

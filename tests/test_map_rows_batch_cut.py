@@ -130,3 +130,18 @@ def test_batch_cut_on_gpu_matches_cpu_loop():
     v0, i0, p0 = run_rows(g, df, False)
     np.testing.assert_allclose(p1, p0, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(v1, v0, rtol=1e-4, atol=1e-5)
+
+
+def test_batch_rows_config_chunks_the_rows():
+    """7 rows in chunks of 3 (3 + 3 + 1): same results as the per-row loop."""
+    df = image_frame()
+    g = scoring_graph()
+    old = tfs.config.map_rows_batch_rows
+    try:
+        tfs.set_config(map_rows_batch_rows=3)
+        v1, i1, p1 = run_rows(g, df, True)
+    finally:
+        tfs.set_config(map_rows_batch_rows=old)
+    v0, i0, p0 = run_rows(g, df, False)
+    np.testing.assert_allclose(p1, p0, rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(i1, i0)
