@@ -157,3 +157,30 @@ def test_decode_op_outside_host_stage_fails_loudly():
     with pytest.raises(ValueError, match="host op"):
         prog = engine.program(g.serialize(), ["img"], [])
         engine.run_program(prog, [], torch.device("cpu"))
+
+
+def test_jpeg_scoring_graph_batch_cut_matches_per_row_loop():
+    """The reference's read_image pipeline (DecodeJpeg host stage -> resize ->
+    crop -> mean subtraction -> batch of one -> VGG -> softmax -> top_k of the
+    squeezed probabilities): the batch-of-one cut gives the per-row results."""
+    from tensorframes_amd.models import cnn
+    from tensorframes_amd.utils.logging import metrics
+    df, raw = _image_frame("JPEG")
+    g = cnn.jpeg_scoring_graph("vgg16", image_size=32, contents=raw[0], width=0.0625, fc_width=32, k=3)
+    outs = {}
+    old = tfs.config.map_rows_vectorize
+    try:
+        for vec in (True, False):
+            tfs.set_config(map_rows_vectorize=vec)
+            metrics.reset()
+            with g.as_default():
+                res = tfs.map_rows(["index", "value"], df, feed_dict={"DecodeJpeg/contents": "image_data"})
+                rows = res.collect()
+            outs[vec] = ([list(r["index"]) for r in rows], np.array([list(r["value"]) for r in rows]))
+            cut_rows = metrics.snapshot().get("map_rows_batch_cut_rows", 0)
+            assert (cut_rows == len(raw)) if vec else cut_rows == 0
+    finally:
+        tfs.set_config(map_rows_vectorize=old)
+    assert outs[True][0] == outs[False][0]
+    # float32 sums in another order (batched GEMM vs per-row): probabilities to ~1e-6
+    np.testing.assert_allclose(outs[True][1], outs[False][1], rtol=1e-4, atol=1e-6)
