@@ -779,7 +779,11 @@ class _LazyDecoded:
 
     def __init__(self, hf, cells):
         from concurrent.futures import ThreadPoolExecutor
-        self._pool = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
+        # 4 by default: the decoders' Python parts hold the GIL and slow the row
+        # loop that feeds the GPU (JPEG -> VGG-16 on MI355X: 1/2/4/8/16 threads ->
+        # 1388/2097/2303/1800/1743 img/s, profiles/r1_read_image/)
+        workers = int(os.environ.get("TFA_DECODE_THREADS", "0")) or min(4, os.cpu_count() or 1)
+        self._pool = ThreadPoolExecutor(max_workers=workers)
         self._futs = [self._pool.submit(hf.decode, c) for c in cells]
 
     def __getitem__(self, i):
