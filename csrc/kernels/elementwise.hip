@@ -1,11 +1,13 @@
 // Elementwise + data-movement kernels for gfx950.
 //
-// Memory-bound: 16-byte vector loads/stores per lane (dwordx4), grid-stride
-// over <= 2048 blocks of 256 threads (4 waves), the hot arithmetic ops
+// Memory-bound: 16-byte vector loads/stores per lane (dwordx4), 4 vectors per
+// lane in flight, one block of 256 threads (4 waves) per 1024 vectors (the
+// binary/unary hot paths; other kernels grid-stride over <= 2048 blocks), the hot arithmetic ops
 // specialised at compile time (Add/Sub/Mul/Div/Max/Min on f32/f64 for the
 // same-shape, scalar and row-broadcast forms), the rest through a wave-uniform
 // op switch.
 #include <cmath>
+#include <cstdlib>
 
 #include "hip_common.h"
 
@@ -124,20 +126,33 @@ __global__ __launch_bounds__(256) void binary_vec_kernel(int op, const T* __rest
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   T sa = MODE == 2 ? a[0] : T(0);
   T sb = MODE == 1 ? b[0] : T(0);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    Vec<T, VEC> va, vb;
-    Vec<TO, VEC> vo;
-    if (MODE != 2) va = reinterpret_cast<const Vec<T, VEC>*>(a)[i];
-    if (MODE == 0) vb = reinterpret_cast<const Vec<T, VEC>*>(b)[i];
-    if (MODE == 3) vb = *reinterpret_cast<const Vec<T, VEC>*>(b + ((i * VEC) % inner));
-    if (MODE == 2) vb = reinterpret_cast<const Vec<T, VEC>*>(b)[i];
+  // U vectors per lane per step, all loads issued before any use: 4x the
+  // bytes in flight of one-vector-per-step (HBM needs ~64 KB in flight per CU;
+  // with the uncapped grid, 1M x 128 f32 Add 5.3 -> 5.8 TB/s, scripts/hbm_probe.py)
+  constexpr int U = VEC > 1 ? 4 : 1;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; base < nvec; base += stride * U) {
+    Vec<T, VEC> va[U], vb[U];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      T x = MODE == 2 ? sa : va.v[j];
-      T y = MODE == 1 ? sb : vb.v[j];
-      vo.v[j] = apply_bin<T, TO, OPC>(op, x, y);
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + (int64_t)u * blockDim.x;
+      if (i >= nvec) break;
+      if (MODE != 2) va[u] = reinterpret_cast<const Vec<T, VEC>*>(a)[i];
+      if (MODE == 0 || MODE == 2) vb[u] = reinterpret_cast<const Vec<T, VEC>*>(b)[i];
+      if (MODE == 3) vb[u] = *reinterpret_cast<const Vec<T, VEC>*>(b + ((i * VEC) % inner));
     }
-    reinterpret_cast<Vec<TO, VEC>*>(out)[i] = vo;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + (int64_t)u * blockDim.x;
+      if (i >= nvec) break;
+      Vec<TO, VEC> vo;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        T x = MODE == 2 ? sa : va[u].v[j];
+        T y = MODE == 1 ? sb : vb[u].v[j];
+        vo.v[j] = apply_bin<T, TO, OPC>(op, x, y);
+      }
+      reinterpret_cast<Vec<TO, VEC>*>(out)[i] = vo;
+    }
   }
   // tail
   for (int64_t i = nvec * VEC + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -162,6 +177,18 @@ __global__ __launch_bounds__(256) void binary_bcast_kernel(int op, const T* __re
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// block cap of the unrolled streaming kernels: effectively none (one block per
+// 256 x 4 vectors). Measured on MI355X, f32 Add of 4M x 128 (scripts/hbm_probe.py):
+// 2048 blocks (grid-stride) 5.0 TB/s, 16384 5.3, uncapped 5.7 (ATen 6.1); 1M x 128:
+// 5.6 / 5.8 / 5.8 (ATen 6.0). TFA_EW_MAX_BLOCKS overrides.
+int ew_max_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("TFA_EW_MAX_BLOCKS");
+    return e ? std::atoi(e) : (1 << 22);
+  }();
+  return v;
+}
+
 template <typename T, typename TO, int MODE, int OPC>
 void launch_vec(int op, const T* a, const T* b, TO* out, int64_t n, int64_t inner, hipStream_t s) {
   constexpr int VEC = 16 / sizeof(T);
@@ -169,7 +196,7 @@ void launch_vec(int op, const T* a, const T* b, TO* out, int64_t n, int64_t inne
                 (MODE != 3 || inner % VEC == 0) && (sizeof(TO) * VEC) % sizeof(TO) == 0;
   if (std::is_same<TO, uint8_t>::value && !aligned16(out)) vec_ok = false;
   if (vec_ok) {
-    hipLaunchKernelGGL((binary_vec_kernel<T, TO, MODE, VEC, OPC>), dim3(ew_grid((n + VEC - 1) / VEC)),
+    hipLaunchKernelGGL((binary_vec_kernel<T, TO, MODE, VEC, OPC>), dim3(ew_grid((n / VEC + 3) / 4, 256, ew_max_blocks())),
                        dim3(256), 0, s, op, a, b, out, n, inner);
   } else {
     hipLaunchKernelGGL((binary_vec_kernel<T, TO, MODE, 1, OPC>), dim3(ew_grid(n)), dim3(256), 0, s,
@@ -270,11 +297,23 @@ __global__ __launch_bounds__(256) void unary_kernel(int op, const T* __restrict_
                                                     T* __restrict__ y, int64_t n) {
   const int64_t nvec = n / VEC;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    Vec<T, VEC> v = reinterpret_cast<const Vec<T, VEC>*>(x)[i];
+  constexpr int U = VEC > 1 ? 4 : 1;  // loads of U vectors in flight per lane (see binary_vec_kernel)
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; base < nvec; base += stride * U) {
+    Vec<T, VEC> v[U];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) v.v[j] = un_apply<T>(op, v.v[j]);
-    reinterpret_cast<Vec<T, VEC>*>(y)[i] = v;
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + (int64_t)u * blockDim.x;
+      if (i >= nvec) break;
+      v[u] = reinterpret_cast<const Vec<T, VEC>*>(x)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + (int64_t)u * blockDim.x;
+      if (i >= nvec) break;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) v[u].v[j] = un_apply<T>(op, v[u].v[j]);
+      reinterpret_cast<Vec<T, VEC>*>(y)[i] = v[u];
+    }
   }
   for (int64_t i = nvec * VEC + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     y[i] = un_apply<T>(op, x[i]);
@@ -307,7 +346,7 @@ void unary_typed(UnOp op, const void* x, void* y, int64_t n, hipStream_t s) {
   }
   constexpr int VEC = 16 / sizeof(T);
   if (aligned16(x) && aligned16(y))
-    hipLaunchKernelGGL((unary_kernel<T, VEC>), dim3(ew_grid((n + VEC - 1) / VEC)), dim3(256), 0, s,
+    hipLaunchKernelGGL((unary_kernel<T, VEC>), dim3(ew_grid((n / VEC + 3) / 4, 256, ew_max_blocks())), dim3(256), 0, s,
                        (int)op, static_cast<const T*>(x), static_cast<T*>(y), n);
   else
     hipLaunchKernelGGL((unary_kernel<T, 1>), dim3(ew_grid(n)), dim3(256), 0, s, (int)op,

@@ -4,6 +4,7 @@
 // All float sums accumulate in f64 and every multi-block reduction goes
 // through a fixed-order partial-slab pass (no float atomics), so results are
 // bitwise reproducible run to run.
+#include <cstdlib>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -136,18 +137,22 @@ __global__ __launch_bounds__(256) void col_reduce_vec(const T* __restrict__ x, T
   const int64_t r1 = min(r, r0 + rows_per_split);
   const V* p = reinterpret_cast<const V*>(x + (o * r) * inner) + cg;
   const int64_t rs = inner / VEC;  // row stride in vectors
-  A acc[2][VEC];
+  // 4 rows in flight per thread (4 x 16-byte loads issued before their use)
+  constexpr int U = 4;
+  A acc[U][VEC];
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) acc[0][j] = acc[1][j] = ident<OP, A>();
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[u][j] = ident<OP, A>();
   int64_t i = r0;
-  for (; i + 2 <= r1; i += 2) {
-    V v0 = p[(i + 0) * rs];
-    V v1 = p[(i + 1) * rs];
+  for (; i + U <= r1; i += U) {
+    V v[U];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      acc[0][j] = combine<OP, A>(acc[0][j], A(v0.v[j]));
-      acc[1][j] = combine<OP, A>(acc[1][j], A(v1.v[j]));
-    }
+    for (int u = 0; u < U; ++u) v[u] = p[(i + u) * rs];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[u][j] = combine<OP, A>(acc[u][j], A(v[u].v[j]));
   }
   for (; i < r1; ++i) {
     V v0 = p[i * rs];
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(256) void col_reduce_vec(const T* __restrict__ x, T
   }
 #pragma unroll
   for (int j = 0; j < VEC; ++j) {
-    A a = combine<OP, A>(acc[0][j], acc[1][j]);
+    A a = combine<OP, A>(combine<OP, A>(acc[0][j], acc[1][j]), combine<OP, A>(acc[2][j], acc[3][j]));
     int64_t col = cg * VEC + j;
     if (part == nullptr) y[o * inner + col] = finish<OP, T, A>(a, r);
     else part[(s * outer + o) * inner + col] = a;
@@ -192,9 +197,47 @@ __global__ __launch_bounds__(256) void col_final(const typename AccT<T>::type* _
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     A acc = ident<OP, A>();
+#pragma unroll 8
     for (int64_t s = 0; s < S; ++s) acc = combine<OP, A>(acc, part[s * n + i]);
     y[i] = finish<OP, T, A>(acc, r);
   }
+}
+
+// Fold S partial slabs [S][n] into G = ceil(S / F) slabs (F consecutive slabs
+// per thread, fixed order), so the final pass is not one thread per column
+// walking all S slabs: with n = 1024 columns and S = 2048 that serial walk
+// took as long as streaming the 4 GB input.
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void col_fold(const typename AccT<T>::type* __restrict__ part,
+                                                typename AccT<T>::type* __restrict__ part2, int64_t n,
+                                                int64_t S, int64_t F) {
+  using A = typename AccT<T>::type;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t s0 = (int64_t)blockIdx.y * F, s1 = min(S, s0 + F);
+  A acc = ident<OP, A>();
+#pragma unroll 8
+  for (int64_t s = s0; s < s1; ++s) acc = combine<OP, A>(acc, part[s * n + i]);
+  part2[(int64_t)blockIdx.y * n + i] = acc;
+}
+
+constexpr int64_t kFoldAbove = 64;  // fold first when more partial slabs than this
+constexpr int64_t kFoldBy = 32;     // slabs per fold thread
+
+inline int64_t fold_slabs(int64_t S) { return S > kFoldAbove ? (S + kFoldBy - 1) / kFoldBy : 0; }
+
+// part [S][n] -> y (through one fold pass when S is large); part2 follows part in the workspace
+template <typename T, int OP>
+void final_pass(typename AccT<T>::type* part, T* y, int64_t n, int64_t S, int64_t r, hipStream_t s) {
+  const int64_t G = fold_slabs(S);
+  if (G > 0 && G <= 65535) {
+    auto* part2 = part + S * n;
+    hipLaunchKernelGGL((col_fold<T, OP>), dim3((unsigned)((n + 255) / 256), (unsigned)G), dim3(256), 0, s, part,
+                       part2, n, S, kFoldBy);
+    hipLaunchKernelGGL((col_final<T, OP>), dim3(ew_grid(n)), dim3(256), 0, s, part2, y, n, G, r);
+    return;
+  }
+  hipLaunchKernelGGL((col_final<T, OP>), dim3(ew_grid(n)), dim3(256), 0, s, part, y, n, S, r);
 }
 
 struct RedPlan {
@@ -224,7 +267,10 @@ RedPlan plan_reduce(int64_t outer, int64_t r, int64_t inner) {
   int64_t cols = (inner + p.vec - 1) / p.vec;
   p.col_blocks = (cols + 255) / 256;
   int64_t blocks = p.col_blocks * outer;
-  int64_t target = 2048;
+  static const int64_t target = [] {
+    const char* e = std::getenv("TFA_RED_TARGET_BLOCKS");
+    return e ? std::atoll(e) : int64_t(2048);
+  }();
   int64_t S = blocks >= target ? 1 : (target + blocks - 1) / blocks;
   int64_t max_s = std::max<int64_t>(1, r / 64);
   p.S = std::min<int64_t>(std::min<int64_t>(S, max_s), 65535);
@@ -258,7 +304,7 @@ void reduce_typed(const void* xv, void* yv, int64_t outer, int64_t r, int64_t in
     }
     hipLaunchKernelGGL((row_split<T, OP>), dim3((unsigned)S, (unsigned)outer), dim3(256), 0, s, x, part2, outer, r,
                        rows_per_split);
-    hipLaunchKernelGGL((col_final<T, OP>), dim3(ew_grid(outer)), dim3(256), 0, s, part2, y, outer, S, r);
+    final_pass<T, OP>(part2, y, outer, S, r, s);
     return;
   }
   TFA_CHECK(outer <= 65535, "reduce: outer dim ", outer, " too large for the column path");
@@ -275,8 +321,7 @@ void reduce_typed(const void* xv, void* yv, int64_t outer, int64_t r, int64_t in
     hipLaunchKernelGGL((col_reduce<T, OP>), g2, dim3(256), 0, s, x, y, part, outer, r, inner, rows_per_split);
   }
   if (S > 1) {
-    int64_t n = outer * inner;
-    hipLaunchKernelGGL((col_final<T, OP>), dim3(ew_grid(n)), dim3(256), 0, s, part, y, n, S, r);
+    final_pass<T, OP>(part, y, outer * inner, S, r, s);
   }
 }
 
@@ -514,7 +559,8 @@ size_t reduce_workspace_bytes(DType dt, int64_t outer, int64_t r, int64_t inner)
     default: return 0;
   }
   if (S <= 1) return 0;
-  return static_cast<size_t>(S) * outer * inner * 8;  // accumulators are 8 bytes
+  // accumulators are 8 bytes: S partial slabs + the folded ones
+  return static_cast<size_t>(S + fold_slabs(S)) * outer * inner * 8;
 }
 
 void reduce(RedOp op, DType dt, const void* x, void* y, int64_t outer, int64_t r, int64_t inner,
