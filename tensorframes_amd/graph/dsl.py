@@ -107,6 +107,11 @@ class Graph:
         self._scope: List[str] = []
         self._infer_cache: Tuple[int, Dict[str, Any]] = (-1, {})
         self._lock = threading.Lock()
+        # per-node wire encodings (nodes are append-only and never mutated once
+        # added), so re-serializing a growing graph costs O(new nodes): shape
+        # inference after every op otherwise re-encoded the whole graph
+        self._enc_full: List[List[bytes]] = []
+        self._enc_view: List[List[bytes]] = []
 
     # -- context
     @contextlib.contextmanager
@@ -208,24 +213,37 @@ class Graph:
         cached = getattr(self, "_ser_cache", None)
         if cached is not None and cached[0] == n:
             return cached[1]
-        b = P.serialize_graphdef(self.as_graph_def())
+        parts = [p for e in self._node_parts(False) for p in e]
+        parts.append(P._ld(4, P._key(1, 0) + P._varint(24)))  # versions { producer: 24 }
+        b = b"".join(parts)
         self._ser_cache = (n, b)
         return b
+
+    @staticmethod
+    def _view_node(n: P.NodeDef) -> P.NodeDef:
+        if n.op == "Const" and "value" in n.attr:
+            t = n.attr["value"].value
+            numel = int(np.prod(t.shape)) if t.shape else 1
+            if numel > 1024:
+                return P.NodeDef(n.name, "Placeholder", [], {"dtype": P.AttrValue.type(t.dtype),
+                                                          "shape": P.AttrValue.shape(t.shape)})
+        return n
+
+    def _node_parts(self, view: bool) -> List[List[bytes]]:
+        """Encoded `node` fields (GraphDef field 1) of every node, extended with
+        the nodes added since the last call."""
+        with self._lock:
+            cache = self._enc_view if view else self._enc_full
+            for n in self._nodes[len(cache):]:
+                e = P._ld(1, P.serialize_node(self._view_node(n) if view else n))
+                cache.append(list(e.parts) if isinstance(e, P._Rope) else [e])
+            return cache[:len(self._nodes)]
 
     def _shape_view(self) -> bytes:
         """The graph for shape inference only: large constants are replaced by
         placeholders of the same dtype/shape (their values never decide a
         shape), so inference does not re-serialize megabytes of weights."""
-        nodes = []
-        for n in self._nodes:
-            if n.op == "Const" and "value" in n.attr:
-                t = n.attr["value"].value
-                numel = int(np.prod(t.shape)) if t.shape else 1
-                if numel > 1024:
-                    n = P.NodeDef(n.name, "Placeholder", [], {"dtype": P.AttrValue.type(t.dtype),
-                                                               "shape": P.AttrValue.shape(t.shape)})
-            nodes.append(n)
-        return P.serialize_graphdef(P.GraphDef(nodes))
+        return b"".join(p for e in self._node_parts(True) for p in e)
 
     def _inferred(self) -> Dict[str, Any]:
         n = len(self._nodes)

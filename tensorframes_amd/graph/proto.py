@@ -159,7 +159,12 @@ class GraphDef:
 
 
 # ------------------------------------------------------------------ writer
+_SMALL_VARINTS = tuple(bytes([i]) for i in range(128))
+
+
 def _varint(v: int) -> bytes:
+    if 0 <= v < 0x80:
+        return _SMALL_VARINTS[v]
     if v < 0:
         v += 1 << 64
     out = bytearray()
@@ -170,8 +175,14 @@ def _varint(v: int) -> bytes:
     return bytes(out)
 
 
+_KEYS = {}
+
+
 def _key(field: int, wt: int) -> bytes:
-    return _varint((field << 3) | wt)
+    k = _KEYS.get((field, wt))
+    if k is None:
+        k = _KEYS[(field, wt)] = _varint((field << 3) | wt)
+    return k
 
 
 class _Rope:
