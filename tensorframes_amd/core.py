@@ -11,6 +11,7 @@ as RCCL collectives.
 """
 from __future__ import annotations
 
+import functools
 import os
 import time
 import zlib
@@ -864,14 +865,21 @@ def _pair_monoid(spec: GraphSpec, names: List[str]) -> Optional[Dict[str, str]]:
     return out
 
 
-def _reducer_program(op: str, tf_dtype: int, cell_rank: int):
-    """Native program `y = op(x, axis=0)` (used for monoid fast paths)."""
+@functools.lru_cache(maxsize=256)
+def _reducer_graph(op: str, tf_dtype: int, cell_rank: int) -> bytes:
     g = dsl.Graph()
     with g.as_default():
         x = dsl.placeholder(D.DType(tf_dtype), shape=[None] + [None] * cell_rank, name="x")
         fn = {"Sum": dsl.reduce_sum, "Min": dsl.reduce_min, "Max": dsl.reduce_max, "Prod": dsl.reduce_prod}[op]
         fn(x, axis=[0], name="y")
-    return engine.program(g.serialize(), ["y"], ["x"])
+    return g.serialize()
+
+
+def _reducer_program(op: str, tf_dtype: int, cell_rank: int):
+    """Native program `y = op(x, axis=0)` (used for monoid fast paths). The
+    graph bytes are memoised (same object every call), so the engine's
+    program cache hits without re-building or re-hashing the graph."""
+    return engine.program(_reducer_graph(op, tf_dtype, cell_rank), ["y"], ["x"])
 
 
 def _monoid_reduce(op: str, t: torch.Tensor, dev: Optional[torch.device] = None) -> torch.Tensor:
