@@ -2,8 +2,12 @@
 10M-row float32[512] DataFrame (BASELINE.json config 3, the north-star metric
 "rows/sec map_blocks MatMul on 10M-row DF at 1/2/4/8 MI355X").
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W          (spawns N ranks itself)
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+With `--gpus N > 1` and no torchrun environment, the parent process never
+touches the GPU: it starts N fresh child processes (parallel/launch.py), one
+rank per GPU, and exits with their status.
 
 The 10M rows are split over the ranks (strong scaling: total work fixed),
 4 partitions per rank. Data is synthetic (random normal) and the weights are
@@ -45,23 +49,56 @@ def parse():
     ap.add_argument("--rows", type=int, default=TOTAL_ROWS)
     ap.add_argument("--parts-per-gpu", type=int, default=4)
     ap.add_argument("--mode", choices=["host", "device", "both"], default="both")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: rehearse the launcher/collectives on the host (gloo), e.g. in CPU tests")
     return ap.parse_args()
 
 
+
+def _launcher():
+    """parallel/launch.py loaded by path: the launcher parent imports neither
+    the package nor its HIP runtime (it never touches the GPU)."""
+    import importlib.util
+    root = os.path.dirname(os.path.abspath(__file__))
+    if os.path.basename(root) == "bench":
+        root = os.path.dirname(root)
+    spec = importlib.util.spec_from_file_location(
+        "_tfa_launch", os.path.join(root, "tensorframes_amd", "parallel", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
 def main():
     args = parse()
+    spawn_if_needed = _launcher().spawn_if_needed
+    extra = {"TFA_DEVICE": "cpu"} if args.device == "cpu" else None
+    rc = spawn_if_needed(args.gpus, extra_env=extra)
+    if rc is not None:  # we were the launcher parent; the ranks did the work
+        sys.exit(rc)
+    if args.device == "cpu":
+        os.environ["TFA_DEVICE"] = "cpu"
     import tensorframes_amd as tfs
     from tensorframes_amd import tf
     from tensorframes_amd.frame.block import Block
     from tensorframes_amd.frame.types import ArrayType, FloatType, StructField, StructType
     from tensorframes_amd.parallel import dist
 
-    dist.init()
+    use_gpu = args.device == "cuda"
+    dist.init(backend=None if use_gpu else "gloo")
     rank, world = dist.rank(), dist.world_size()
-    assert torch.cuda.is_available(), "bench.py needs a GPU"
-    dev = torch.device("cuda", dist.local_rank() % torch.cuda.device_count())
-    torch.cuda.set_device(dev)
-    numa_cpus = dist.bind_numa(dev.index)  # before any pinned allocation
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but the job has {world} ranks; reporting {world}", file=sys.stderr)
+    if use_gpu:
+        assert torch.cuda.is_available(), "bench.py needs a GPU (or --device cpu)"
+        dev = torch.device("cuda", dist.local_rank() % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        numa_cpus = dist.bind_numa(dev.index)  # before any pinned allocation
+    else:
+        dev, numa_cpus = torch.device("cpu"), []
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize()
 
     nparts = world * args.parts_per_gpu
     schema = StructType([tfs.tensor_field("x", tf.float32, [DIM])])
@@ -71,7 +108,7 @@ def main():
 
     def make(p):
         a, b = (p * args.rows) // nparts, ((p + 1) * args.rows) // nparts
-        host = _C.empty_pinned([b - a, DIM], torch.float32)
+        host = _C.empty_pinned([b - a, DIM], torch.float32) if use_gpu else torch.empty((b - a, DIM))
         gen = torch.Generator(device=dev).manual_seed(1000 + p)
         step = 1 << 20
         for s in range(0, b - a, step):
@@ -95,14 +132,14 @@ def main():
     def timed(fn, steps, warmup):
         for _ in range(warmup):
             fn()
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
         t0 = time.perf_counter()
         res = None
         for _ in range(steps):
             res = None  # a step's output frame is dropped before the next step (like a loop body)
             res = fn()
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
         dt = time.perf_counter() - t0
         if dist.is_distributed():
@@ -122,7 +159,7 @@ def main():
     results["host"] = dt
 
     dev_rows_per_s = None
-    if args.mode in ("device", "both"):
+    if args.mode in ("device", "both") and use_gpu:
         base_dev = base.cache_on_device(dev)
 
         def step_dev():
@@ -147,6 +184,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
             "dtype": "fp32",
+            "device": args.device,
             "data": "synthetic (random normal float32[512] rows in page-locked host memory; random-init W)",
             "config": {
                 "model": "map_blocks relu(matmul(x[?,512], W[512,512])) float32",

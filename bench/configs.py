@@ -6,9 +6,12 @@
     python bench/configs.py reduce              # 4: 10M x float32[1024] reduce_blocks Sum
     python bench/configs.py inception           # 5: N x 224x224x3 Inception-v3 scoring
     python bench/configs.py kmeans              # reference demo workload
+    python bench/configs.py reduce --gpus N     # N ranks, one per GPU (spawned here)
     torchrun --nproc-per-node N bench/configs.py reduce|inception ...
 
 Each prints one JSON line (rank 0). Data is synthetic, weights random-init.
+With `--gpus N > 1` outside torchrun the parent process starts N fresh ranks
+(tensorframes_amd/parallel/launch.py) and never touches the GPU itself.
 """
 import argparse
 import json
@@ -16,18 +19,28 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-import tensorframes_amd as tfs  # noqa: E402
-from tensorframes_amd import engine, tf  # noqa: E402
-from tensorframes_amd._native import _C  # noqa: E402
-from tensorframes_amd.frame.block import Block  # noqa: E402
-from tensorframes_amd.frame.types import ArrayType, FloatType, StructField, StructType  # noqa: E402
-from tensorframes_amd.parallel import dist  # noqa: E402
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+# the package (and its HIP runtime) is imported by the ranks only: see main()
+tfs = tf = engine = _C = Block = dist = None
+ArrayType = FloatType = StructField = StructType = None
+
+
+def _import_package():
+    global tfs, tf, engine, _C, Block, dist, ArrayType, FloatType, StructField, StructType
+    import tensorframes_amd as _tfs
+    from tensorframes_amd import engine as _engine, tf as _tf
+    from tensorframes_amd._native import _C as __C
+    from tensorframes_amd.frame.block import Block as _Block
+    from tensorframes_amd.frame import types as _types
+    from tensorframes_amd.parallel import dist as _dist
+    tfs, tf, engine, _C, Block, dist = _tfs, _tf, _engine, __C, _Block, _dist
+    ArrayType, FloatType, StructField, StructType = (_types.ArrayType, _types.FloatType, _types.StructField,
+                                                     _types.StructType)
 
 
 def sync():
@@ -260,6 +273,20 @@ def cfg_kmeans(a):
           **{f"{k}_ms": v for k, v in out.items()}})
 
 
+
+def _launcher():
+    """parallel/launch.py loaded by path: the launcher parent imports neither
+    the package nor its HIP runtime (it never touches the GPU)."""
+    import importlib.util
+    root = os.path.dirname(os.path.abspath(__file__))
+    if os.path.basename(root) == "bench":
+        root = os.path.dirname(root)
+    spec = importlib.util.spec_from_file_location(
+        "_tfa_launch", os.path.join(root, "tensorframes_amd", "parallel", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config", choices=["plumbing", "add", "reduce", "inception", "kmeans", "refperf"])
@@ -271,7 +298,13 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--precision", choices=["f32", "bf16x3", "bf16"], default="f32",
                     help="float32 MatMul/Conv2D compute mode (Config.precision); f32 = exact")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks to spawn (one per GPU) outside torchrun")
     a = ap.parse_args()
+    spawn_if_needed = _launcher().spawn_if_needed
+    rc = spawn_if_needed(a.gpus)
+    if rc is not None:
+        sys.exit(rc)
+    _import_package()
     tfs.set_config(precision=a.precision)
     dist.init()
     if torch.cuda.is_available():

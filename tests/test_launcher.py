@@ -1,0 +1,63 @@
+"""The multi-GPU entry point: `python bench.py --gpus N` runs N ranks.
+
+Rehearsed on the CPU with gloo (the launcher parent spawns fresh child
+processes with RANK/LOCAL_RANK/WORLD_SIZE set; rank 0 prints the slowest
+rank's time). On the GPU box the same launcher starts one rank per GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(n, rows=4096, extra=()):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--device", "cpu",
+                        "--rows", str(rows), "--steps", "2", "--warmup", "1", *extra],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_bench_spawns_n_ranks(n):
+    out = _run_bench(n)
+    assert out["n_gpus"] == n
+    assert out["config"]["parallelism"] == f"dp{n}"
+    assert out["config"]["rows"] == 4096 and out["config"]["partitions"] == 4 * n
+    assert out["steps"] == 2 and out["warmup"] == 1
+    assert out["value"] > 0 and out["max_abs_err"] < 1e-3
+    assert out["scaling"] == "strong"
+
+
+def test_launcher_propagates_failure(tmp_path):
+    sys.path.insert(0, REPO)
+    from tensorframes_amd.parallel import launch
+    script = tmp_path / "fail.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "sys.exit(3) if r == 1 else time.sleep(60)\n")
+    rc = launch.spawn([str(script)], 3)
+    assert rc == 3  # the failing rank's code; the sleeping ranks were taken down
+
+
+def test_launcher_sets_rank_env(tmp_path):
+    sys.path.insert(0, REPO)
+    from tensorframes_amd.parallel import launch
+    out = tmp_path / "out"
+    out.mkdir()
+    script = tmp_path / "env.py"
+    script.write_text("import os\n"
+                      f"open(os.path.join({str(out)!r}, os.environ['RANK']), 'w').write(\n"
+                      "  ','.join(os.environ[k] for k in ('LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR')))\n")
+    assert launch.spawn([str(script)], 4) == 0
+    got = {p.name: p.read_text() for p in out.iterdir()}
+    assert got == {str(r): f"{r},4,127.0.0.1" for r in range(4)}
