@@ -198,7 +198,11 @@ def cfg_reduce(a):
             res[mode] = timed(step, a.steps, a.warmup)
         del df
         torch.cuda.empty_cache()
-    emit({"config": "4: 10M-row float32[1024] reduce_blocks ReduceSum, partitions pinned to GPUs, RCCL all-reduce",
+    comb = ("RCCL all-reduce" if dist.is_distributed() and dist.gpu_collectives() else
+            "gloo all-reduce" if dist.is_distributed() else "none (1 rank, no collective)")
+    emit({"config": f"4: {rows}-row float32[1024] reduce_blocks ReduceSum, {nparts} partitions on "
+                    f"{dist.world_size()} GPU rank(s); cross-rank combine: {comb}",
+          "collective_device_ms_total": dist.collective_device_ms() if dist.is_distributed() else 0.0,
           "metric": "rows/sec", "value": rows / res["host"], "unit": "rows/s", "higher_is_better": True,
           "ms_per_step": res["host"] * 1e3, "device_resident_rows_per_sec": rows / res["device"],
           "device_resident_ms_per_step": res["device"] * 1e3, "rows": rows,
@@ -299,6 +303,8 @@ def main():
     ap.add_argument("--precision", choices=["f32", "bf16x3", "bf16"], default="f32",
                     help="float32 MatMul/Conv2D compute mode (Config.precision); f32 = exact")
     ap.add_argument("--gpus", type=int, default=1, help="ranks to spawn (one per GPU) outside torchrun")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="run the cross-rank collectives even with one rank (RCCL group of size 1)")
     a = ap.parse_args()
     spawn_if_needed = _launcher().spawn_if_needed
     rc = spawn_if_needed(a.gpus)
@@ -306,7 +312,7 @@ def main():
         sys.exit(rc)
     _import_package()
     tfs.set_config(precision=a.precision)
-    dist.init()
+    dist.init(force=a.force_collectives)
     if torch.cuda.is_available():
         torch.cuda.set_device(dist.local_rank() % torch.cuda.device_count())
         dist.bind_numa()

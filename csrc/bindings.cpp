@@ -261,6 +261,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("registered_ops", [] { return OpRegistry::get().names(); });
   // float32 MatMul/Conv2D compute mode: 0 exact f32, 1 bf16, 2 bf16x3 (kernels/gemm_bf16.hip)
   m.def("set_f32_precision", [](int mode) { k::set_f32_precision(mode); });
+  m.def("set_debug_sync", &set_debug_sync, "synchronise + check after every kernel (read per launch)");
+  m.def("get_debug_sync", &get_debug_sync);
   m.def("f32_precision", [] { return k::f32_precision(); });
   m.def("set_gemm_tile", [](int cfg) { k::set_gemm_tile(cfg); });
   m.def("gemm_tile_count", [] { return k::gemm_tile_count(); });

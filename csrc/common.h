@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdlib>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -30,6 +31,17 @@ enum class DType : int {
   BF16 = 14,
   F16 = 19,
 };
+
+// A positive integer from the environment; unset, unparsable or < 1 values
+// fall back to `dflt` (a bad override must never produce a 0-block grid).
+inline int64_t env_positive(const char* name, int64_t dflt) {
+  const char* e = std::getenv(name);
+  if (!e || !*e) return dflt;
+  char* end = nullptr;
+  long long v = std::strtoll(e, &end, 10);
+  if (end == e || *end != '\0' || v < 1) return dflt;
+  return static_cast<int64_t>(v);
+}
 
 const char* dtype_name(DType d);
 int64_t dtype_size(DType d);

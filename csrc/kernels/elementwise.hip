@@ -182,10 +182,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 // 2048 blocks (grid-stride) 5.0 TB/s, 16384 5.3, uncapped 5.7 (ATen 6.1); 1M x 128:
 // 5.6 / 5.8 / 5.8 (ATen 6.0). TFA_EW_MAX_BLOCKS overrides.
 int ew_max_blocks() {
-  static const int v = [] {
-    const char* e = std::getenv("TFA_EW_MAX_BLOCKS");
-    return e ? std::atoi(e) : (1 << 22);
-  }();
+  static const int v = static_cast<int>(std::min<int64_t>(env_positive("TFA_EW_MAX_BLOCKS", 1 << 22), 1 << 30));
   return v;
 }
 

@@ -267,10 +267,7 @@ RedPlan plan_reduce(int64_t outer, int64_t r, int64_t inner) {
   int64_t cols = (inner + p.vec - 1) / p.vec;
   p.col_blocks = (cols + 255) / 256;
   int64_t blocks = p.col_blocks * outer;
-  static const int64_t target = [] {
-    const char* e = std::getenv("TFA_RED_TARGET_BLOCKS");
-    return e ? std::atoll(e) : int64_t(2048);
-  }();
+  static const int64_t target = env_positive("TFA_RED_TARGET_BLOCKS", 2048);
   int64_t S = blocks >= target ? 1 : (target + blocks - 1) / blocks;
   int64_t max_s = std::max<int64_t>(1, r / 64);
   p.S = std::min<int64_t>(std::min<int64_t>(S, max_s), 65535);

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <set>
@@ -31,12 +32,19 @@ namespace {
     TFA_CHECK(_e == hipSuccess, "HIP error ", hipGetErrorString(_e), " at ", #expr); \
   } while (0)
 
+// -1: not set yet (TFA_DEBUG_SYNC decides on first use); set_debug_sync()
+// (Config.debug_sync) overrides it at any time, read on every launch
+std::atomic<int> g_debug_sync{-1};
+
 bool debug_sync() {
-  static bool v = [] {
+  int v = g_debug_sync.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = std::getenv("TFA_DEBUG_SYNC");
-    return e && e[0] == '1';
-  }();
-  return v;
+    int want = (e && e[0] == '1') ? 1 : 0;
+    g_debug_sync.compare_exchange_strong(v, want);
+    v = g_debug_sync.load(std::memory_order_relaxed);
+  }
+  return v == 1;
 }
 
 struct RangeGuard {
@@ -51,6 +59,9 @@ std::string strip0(const std::string& s) {
 
 }  // namespace
 
+void set_debug_sync(bool on) { g_debug_sync.store(on ? 1 : 0); }
+bool get_debug_sync() { return debug_sync(); }
+
 struct Program::Step {
   enum Kind { OP, GEMM, CONV } kind = OP;
   int node = -1;         // node whose op runs (for GEMM/CONV: the MatMul/Conv2D node)
@@ -61,6 +72,7 @@ struct Program::Step {
   std::vector<const TensorInfo*> in_info;
   int bias_slot = -1;
   int act = 0;
+  Shape gemm_shape;  // GEMM/CONV: the MatMul/Conv2D's own output shape (out_info may be a view of it)
   std::vector<int> release;  // slots dropped after the step
   // write-into-slice (GPU): a GEMM/CONV step whose only consumer is a
   // last-axis ConcatV2 writes straight into its channel range of the concat
@@ -313,22 +325,46 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     Step st;
     st.node = n;
     st.out_node = n;
-    // ---- fusion: MatMul/Conv2D -> (BiasAdd | Add const-vector) -> (Relu | Relu6)
+    // ---- fusion: MatMul/Conv2D -> (BiasAdd | Add const-vector) -> (Relu | Relu6),
+    // looking through single-consumer view ops (Reshape/Squeeze/ExpandDims/
+    // Identity: same elements, same order) between them, e.g. the lifted
+    // row-wise MatMul of map_rows: [B*1,k]x[k,n] -> Reshape [B,1,n] -> Squeeze -> Relu
     bool gemm = nd.op == "MatMul" &&
                 (infos[n][0].dtype == DType::F32 || infos[n][0].dtype == DType::F64);
     bool conv = nd.op == "Conv2D" && infos[n][0].dtype == DType::F32;
     if (gemm || conv) {
       st.kind = gemm ? Step::GEMM : Step::CONV;
       int cur = n;
-      TensorRef cur_ref{n, 0};
       int64_t ncols = infos[n][0].shape.dims.back();
       auto single = [&](int node) -> int {
         TensorRef r{node, 0};
         if (fetched.count(r) || uses[r] != 1 || !consumer.count(node)) return -1;
         return consumer[node];
       };
-      int c1 = single(cur);
+      auto is_view = [&](int node) {
+        const std::string& op = g_->node(node).op;
+        return (op == "Reshape" || op == "Squeeze" || op == "ExpandDims" || op == "Identity") &&
+               g_->node(node).inputs.size() >= 1 && infos[node][0].shape.fully_known() &&
+               !infos[node][0].shape.dims.empty() && infos[node][0].shape.dims.back() == ncols;
+      };
+      // follows views from `from`; returns the first non-view single consumer (or -1)
+      // and the last view passed (== from when none)
+      auto next_op = [&](int from, int* last_view) -> int {
+        int at = from;
+        for (int guard = 0; guard < 8; ++guard) {
+          int c = single(at);
+          if (c < 0) { *last_view = at; return -1; }
+          if (is_view(c) && g_->node(c).inputs[0] == TensorRef{at, 0}) { at = c; continue; }
+          *last_view = at;
+          return c;
+        }
+        *last_view = at;
+        return -1;
+      };
+      int lv = cur;
+      int c1 = next_op(cur, &lv);
       if (c1 >= 0) {
+        const TensorRef cur_ref{lv, 0};
         const Node& cn = g_->node(c1);
         int other = -1;
         if (cn.op == "BiasAdd" && cn.inputs[0] == cur_ref &&
@@ -340,26 +376,28 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
           const TensorRef& br = cn.inputs[other];
           const TensorInfo& bi = infos[br.node][br.index];
           bool ok = bi.shape.rank() == 1 && bi.shape.dims[0] == ncols && bi.dtype == infos[n][0].dtype &&
-                    infos[c1][0].shape == infos[n][0].shape;
+                    infos[c1][0].shape == infos[lv][0].shape;
           if (ok) {
-            st.bias_slot = -2 - static_cast<int>(br.node);  // resolved below
             st.bias_slot = slot_for(br);
+            for (int v = lv; v != cur; v = g_->node(v).inputs[0].node) absorbed.insert(v);
             absorbed.insert(c1);
             cur = c1;
-            cur_ref = {c1, 0};
           }
         }
       }
-      int c2 = single(cur);
+      int lv2 = cur;
+      int c2 = next_op(cur, &lv2);
       if (c2 >= 0) {
         const Node& cn = g_->node(c2);
-        if ((cn.op == "Relu" || cn.op == "Relu6") && cn.inputs[0] == cur_ref) {
+        if ((cn.op == "Relu" || cn.op == "Relu6") && cn.inputs[0] == TensorRef{lv2, 0}) {
           st.act = cn.op == "Relu" ? 1 : 2;
+          for (int v = lv2; v != cur; v = g_->node(v).inputs[0].node) absorbed.insert(v);
           absorbed.insert(c2);
           cur = c2;
         }
       }
       st.out_node = cur;
+      st.gemm_shape = infos[n][0].shape;
       if (cur != n) p->fused++;
     }
     const OpDef* od = reg.find(nd.op);
@@ -405,7 +443,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
           const TensorRef out_ref{ps.out_node, 0};
           const bool single_use = uses[out_ref] == 1 && !fetched.count(out_ref);
           if ((ps.kind == Step::CONV || ps.kind == Step::GEMM) && single_use && ps.alias_slot < 0 &&
-              ps.out_info[0].dtype == DType::F32) {
+              ps.out_info[0].dtype == DType::F32 && ps.out_info[0].shape == ps.gemm_shape) {
             ps.alias_slot = cs.out_slots[0];
             ps.alias_offset = off;
             ps.alias_info = &cs.out_info[0];
@@ -509,22 +547,34 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           c.out[0] = out;
         } else {
           at::Tensor out = gpu ? c.alloc_out(0) : at::Tensor();
+          // absorbed views: the kernel writes the MatMul/Conv2D shape, the step
+          // hands out the same elements in the view's shape
+          const bool viewed = !(st.out_info[0].shape == st.gemm_shape);
+          at::Tensor kout = (gpu && viewed) ? out.view(st.gemm_shape.dims) : out;
           at::Tensor bias;
           if (st.bias_slot >= 0) bias = slots[st.bias_slot];
           const at::Tensor* bp = st.bias_slot >= 0 ? &bias : nullptr;
           if (st.kind == Step::GEMM)
-            run_gemm(c, c.in[0], c.in[1], nd.attr_b("transpose_a", false), nd.attr_b("transpose_b", false), bp, st.act, out);
+            run_gemm(c, c.in[0], c.in[1], nd.attr_b("transpose_a", false), nd.attr_b("transpose_b", false), bp, st.act, kout);
           else
-            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out);
-          c.out[0] = out;
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout);
+          c.out[0] = viewed ? kout.reshape(st.out_info[0].shape.dims) : kout;
         }
       } catch (const GraphError& e) {
         throw GraphError(str_cat("while executing node '", nd.name, "' (", nd.op, "): ", e.what()));
       }
     }
-    if (gpu && debug_sync()) {
-      HIP_OK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-      HIP_OK(hipGetLastError());
+    if (gpu) {
+      // launch errors are reported with the node that caused them (a HIP fault
+      // is sticky: the caller must not retry in this process); debug_sync also
+      // waits for the kernel so asynchronous faults are attributed too
+      hipError_t le = hipGetLastError();
+      if (le == hipSuccess && debug_sync()) {
+        le = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+        if (le == hipSuccess) le = hipGetLastError();
+      }
+      TFA_CHECK(le == hipSuccess, "HIP error ", hipGetErrorString(le), " (", hipGetErrorName(le),
+                ") in node '", nd.name, "' (", nd.op, ")");
     }
     for (size_t k = 0; k < st.out_slots.size(); ++k) {
       at::Tensor& o = c.out[k];
@@ -572,10 +622,7 @@ int64_t now_ns() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 int64_t hip_graph_max_bytes() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("TFA_HIP_GRAPH_MAX_BYTES");
-    return e ? std::atoll(e) : (int64_t(16) << 20);
-  }();
+  static const int64_t v = env_positive("TFA_HIP_GRAPH_MAX_BYTES", int64_t(16) << 20);
   return v;
 }
 }  // namespace
@@ -893,8 +940,7 @@ class PinnedPool {
 
  private:
   PinnedPool() {
-    const char* e = std::getenv("TFA_PINNED_POOL_MB");
-    limit_ = (e ? std::strtoull(e, nullptr, 10) : 65536ull) << 20;
+    limit_ = static_cast<size_t>(env_positive("TFA_PINNED_POOL_MB", 65536)) << 20;
   }
   static constexpr size_t kGran = size_t(2) << 20;
   std::mutex mu_;

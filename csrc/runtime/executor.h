@@ -98,5 +98,8 @@ size_t pinned_pool_cached_bytes();
 // page-lock an existing host tensor's memory in place (hipHostRegister)
 void pin_host_tensor(const at::Tensor& t);
 void unpin_host_tensor(const at::Tensor& t);
+// Config.debug_sync: synchronise + check after every kernel (read per launch)
+void set_debug_sync(bool on);
+bool get_debug_sync();
 
 }  // namespace tfa

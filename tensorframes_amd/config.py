@@ -49,6 +49,9 @@ class Config:
     # "bf16" (bf16 operands) or "bf16x3" (hi/lo bf16 split, ~16-bit operands);
     # f32 accumulation and f32 tensors in every mode (kernels/gemm_bf16.hip)
     precision: str = dataclasses.field(default_factory=lambda: _env("TFA_PRECISION", "f32", str))
+    # run the cross-rank collectives even in a 1-rank job (an RCCL/gloo group of
+    # world size 1): exercises the collective path on a single GPU
+    force_collectives: bool = dataclasses.field(default_factory=lambda: _env("TFA_FORCE_COLLECTIVES", False, bool))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 
@@ -67,6 +70,8 @@ def set_config(**kw):
         setattr(config, k, v)
     if "debug_sync" in kw:
         os.environ["TFA_DEBUG_SYNC"] = "1" if kw["debug_sync"] else "0"
+        from ._native import _C
+        _C.set_debug_sync(bool(kw["debug_sync"]))  # read by the executor on every launch
     if "precision" in kw:
         apply_precision()
 

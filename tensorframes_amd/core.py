@@ -446,33 +446,36 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
         res = {}
         for pid in sorted(blocks):
             b = blocks[pid]
-            per_out: List[List[Optional[torch.Tensor]]] = [[None] * b.nrows for _ in outputs]
-            cell_views = [_cells(b.columns[c]) for c in feed_cols]
+            cell_views = [_CellView(b.columns[c]) for c in feed_cols]
             host_views = [_decoded_cells(hf, b) for hf in host]
             dev = _rows_device(cell_views + host_views)
-            # rows are enqueued back to back; device outputs stay on the GPU until
-            # the partition is done (one D2H per column instead of a sync per row)
-            done = vec.run_groups(b, feed_cols, cell_views, dev, per_out) if vec is not None and not host \
-                else [None] * b.nrows
-            if bcut is not None and b.nrows >= 2 and any(d is None for d in done):
-                todo = [i for i in range(b.nrows) if done[i] is None]
-                sub = [[None] * len(todo) for _ in outputs]
-                bcut.run(len(todo), lambda k: [cv[todo[k]] for cv in cell_views] + [hv[todo[k]] for hv in host_views],
-                         dev, sub)
-                for j in range(len(outputs)):
-                    for k, i in enumerate(todo):
-                        per_out[j][i] = sub[j][k]
-                done = [True] * b.nrows
-            for i in range(b.nrows):
-                if done[i] is not None:
-                    continue
-                with metrics.timer("map_rows_inputs"):
-                    ins = [cv[i] for cv in cell_views] + [hv[i] for hv in host_views]
-                with metrics.timer("map_rows_run"):
-                    outs = engine.run_program(prog, ins, dev)
-                for j, o in enumerate(outs):
-                    per_out[j][i] = o
-            host_rows = not any(len(cv) and cv[0].is_cuda for cv in cell_views)
+            per_out: List[Any] = [None for _ in outputs]
+            whole = vec.run_whole_block(b, feed_cols, per_out) if vec is not None and not host else False
+            if not whole:
+                per_out = [[None] * b.nrows for _ in outputs]
+                # rows are enqueued back to back; device outputs stay on the GPU until
+                # the partition is done (one D2H per column instead of a sync per row)
+                done = vec.run_groups(b, feed_cols, cell_views, dev, per_out) if vec is not None and not host \
+                    else [None] * b.nrows
+                if bcut is not None and b.nrows >= 2 and any(d is None for d in done):
+                    todo = [i for i in range(b.nrows) if done[i] is None]
+                    sub = [[None] * len(todo) for _ in outputs]
+                    bcut.run(len(todo), lambda k: [cv[todo[k]] for cv in cell_views] +
+                             [hv[todo[k]] for hv in host_views], dev, sub)
+                    for j in range(len(outputs)):
+                        for k, i in enumerate(todo):
+                            per_out[j][i] = sub[j][k]
+                    done = [True] * b.nrows
+                for i in range(b.nrows):
+                    if done[i] is not None:
+                        continue
+                    with metrics.timer("map_rows_inputs"):
+                        ins = [cv[i] for cv in cell_views] + [hv[i] for hv in host_views]
+                    with metrics.timer("map_rows_run"):
+                        outs = engine.run_program(prog, ins, dev)
+                    for j, o in enumerate(outs):
+                        per_out[j][i] = o
+            host_rows = not any(len(cv) and cv.is_cuda for cv in cell_views)
             cols_out = {}
             for (name, dt, shp), vals in zip(out_meta, per_out):
                 col = vals if isinstance(vals, torch.Tensor) else _stack_cells(vals, dt, shp)
@@ -703,6 +706,9 @@ class _BatchCut:
         metrics.add("map_rows_batch_cut_post_ms", t_post * 1e3)
 
 
+_LIFT_CACHE: Dict[tuple, tuple] = {}  # (graph, fetches, feeds, cell ranks) -> (lifted bytes, program)
+
+
 class _RowVectorizer:
     """map_rows fast path: rows with identical cell shapes run as ONE block
     through the lifted (batched) form of the row graph
@@ -715,9 +721,13 @@ class _RowVectorizer:
         self.feed_names = list(feed_names)
         self.feed_dtypes = list(feed_dtypes)
         self._progs: Dict[tuple, Any] = {}  # cell ranks -> lifted program (or None)
+        self._lifted: Dict[tuple, bytes] = {}  # cell ranks -> lifted graph bytes
 
     def _program(self, cell_shapes: tuple):
         key = tuple(len(s) for s in cell_shapes)
+        gkey = (engine._key(self.graph_bytes), tuple(self.fetch_refs), tuple(self.feed_names), key)
+        if key not in self._progs and gkey in _LIFT_CACHE:  # lifted by an earlier map_rows call
+            self._lifted[key], self._progs[key] = _LIFT_CACHE[gkey]
         if key not in self._progs:
             from .graph import vectorize
             g = engine.native_graph(self.graph_bytes)
@@ -730,41 +740,75 @@ class _RowVectorizer:
                 patch = vectorize.lift(light, self.fetch_refs, self.feed_names, infos, patch_only=True)
             except ValueError:
                 patch = None
-            self._progs[key] = None if patch is None else engine.program(
-                _C.patch_graphdef(self.graph_bytes, P.serialize_graphdef(patch)), self.fetch_refs, self.feed_names)
+            if patch is None:
+                self._progs[key] = None
+            else:
+                lifted = _C.patch_graphdef(self.graph_bytes, P.serialize_graphdef(patch))
+                self._lifted[key] = lifted
+                self._progs[key] = engine.program(lifted, self.fetch_refs, self.feed_names)
             metrics.add("map_rows_vectorized_graphs" if patch is not None else "map_rows_unliftable_graphs")
+            _LIFT_CACHE[gkey] = (self._lifted.get(key), self._progs[key])
+            while len(_LIFT_CACHE) > 64:
+                _LIFT_CACHE.pop(next(iter(_LIFT_CACHE)))
         return self._progs[key]
 
+    def _run_block(self, prog, cell_shapes: tuple, ins: List[torch.Tensor]) -> List[torch.Tensor]:
+        if all(t.is_cuda for t in ins):
+            return engine.run_program(prog, ins, ins[0].device)
+        if not engine.gpu_available():
+            return engine.run_program(prog, ins, torch.device("cpu"))
+        lifted = self._lifted[tuple(len(s) for s in cell_shapes)]
+        if ins[0].shape[0] >= config.min_chunked_rows:
+            shapes = _concrete_output_shapes(lifted, self.fetch_refs, self.feed_names, ins)
+            specs = [(tuple(s), o.dtype) for s, o in zip(shapes, self._out_dtypes(lifted))]
+            metrics.add("map_rows_pipelined_rows", ins[0].shape[0])
+            return engine.run_segments_pipelined(prog, [ins], [specs])[0]
+        return engine.run_block_host(prog, ins, False)
+
+    def _out_dtypes(self, lifted: bytes):
+        g = engine.native_graph(lifted)
+        infos = _C.analyze_fetches(g, self.fetch_refs, self.feed_names, {})
+        return [torch.empty((), dtype=D.torch_dtype(infos[r]["dtype"])) for r in self.fetch_refs]
+
+    def run_whole_block(self, b: Block, feed_cols: List[str], per_out: list) -> bool:
+        """Dense feed columns: the whole block runs as ONE lifted program (no
+        per-row Python work at all); per_out[j] becomes output column j.
+        False when the block is not dense or the graph cannot be lifted."""
+        cols = [b.columns[c] for c in feed_cols]
+        if b.nrows == 0 or not all(is_dense(c) for c in cols):
+            return False
+        shapes = tuple(tuple(c.shape[1:]) for c in cols)
+        prog = self._program(shapes)
+        if prog is None:
+            return False
+        outs = self._run_block(prog, shapes, cols)
+        if any(o.dim() == 0 or o.shape[0] != b.nrows for o in outs):
+            return False  # lifted graph did not keep the row dim: per-row loop
+        for j, o in enumerate(outs):
+            per_out[j] = o
+        metrics.add("map_rows_vectorized_rows", b.nrows)
+        return True
+
     def run_groups(self, b: Block, feed_cols: List[str], cell_views, dev, per_out) -> list:
+        """Ragged blocks: rows grouped by cell shapes, each group of >= 2 rows
+        run as one lifted block. Returns per-row done flags."""
         done = [None] * b.nrows
         if b.nrows == 0:
             return done
-        cols = [b.columns[c] for c in feed_cols]
-        if all(is_dense(c) for c in cols):
-            groups = {tuple(tuple(c.shape[1:]) for c in cols): None}  # one group: the whole block
-        else:
-            groups = {}
-            for i in range(b.nrows):
-                groups.setdefault(tuple(tuple(cv[i].shape) for cv in cell_views), []).append(i)
+        groups: Dict[tuple, List[int]] = {}
+        for i in range(b.nrows):
+            groups.setdefault(tuple(tuple(cv[i].shape) for cv in cell_views), []).append(i)
         for shapes, rows in groups.items():
             prog = self._program(shapes)
             if prog is None:
                 return done
-            if rows is None:
-                ins, idx, n = cols, None, b.nrows
-            else:
-                if len(rows) < 2:
-                    continue
-                ins = [torch.stack([cv[i] for i in rows], 0) for cv in cell_views]
-                idx, n = rows, len(rows)
+            if len(rows) < 2:
+                continue
+            ins = [torch.stack([cv[i] for i in rows], 0) for cv in cell_views]
+            idx, n = rows, len(rows)
             outs = engine.run_program(prog, ins, dev)
             if any(o.dim() == 0 or o.shape[0] != n for o in outs):
                 return done  # lifted graph did not keep the row dim: per-row loop
-            if idx is None:  # the whole block in one go: outputs are the columns
-                for j, o in enumerate(outs):
-                    per_out[j] = o
-                metrics.add("map_rows_vectorized_rows", n)
-                return [True] * n
             for j, o in enumerate(outs):
                 for k, i in enumerate(idx):
                     per_out[j][i] = o[k]
@@ -806,12 +850,37 @@ def _decoded_cells(hf, b: Block):
     return _LazyDecoded(hf, cells)
 
 
-def _cells(col) -> List[torch.Tensor]:
-    if is_dense(col):
-        return list(col.unbind(0)) if col.shape[0] else []
-    if isinstance(col, RaggedColumn):
-        return [torch.from_numpy(np.asarray(c, order="C")) for c in col.cells]
-    raise TensorFramesError("map_rows: only numeric columns can be fed to a graph")
+class _CellView:
+    """The cells of one column, built on access: a dense block is never
+    unbound row by row up front (the vectorised path runs the whole block and
+    touches no cell; the per-row loop builds only the rows it runs)."""
+
+    __slots__ = ("_dense", "_ragged")
+
+    def __init__(self, col):
+        self._dense = self._ragged = None
+        if is_dense(col):
+            self._dense = col
+        elif isinstance(col, RaggedColumn):
+            self._ragged = col.cells
+        else:
+            raise TensorFramesError("map_rows: only numeric columns can be fed to a graph")
+
+    def __len__(self):
+        return self._dense.shape[0] if self._dense is not None else len(self._ragged)
+
+    def __getitem__(self, i) -> torch.Tensor:
+        if self._dense is not None:
+            return self._dense[i]
+        return torch.from_numpy(np.asarray(self._ragged[i], order="C"))
+
+    @property
+    def is_cuda(self) -> bool:
+        return self._dense is not None and self._dense.is_cuda
+
+
+def _cells(col):
+    return _CellView(col)
 
 
 def _rows_device(cell_views) -> torch.device:
@@ -887,27 +956,123 @@ def _monoid_reduce(op: str, t: torch.Tensor, dev: Optional[torch.device] = None)
     return engine.run_program(prog, [t], dev)[0]
 
 
-def _combine_across(partials: List[torch.Tensor], op: str) -> torch.Tensor:
-    """Monoid combine of per-partition partial cells: locally with the native
-    reduction, then across ranks with one all-reduce (RCCL for device tensors)."""
+# One flag element rides along with every monoid all-reduce so that ranks
+# without data contribute the identity and an all-empty frame is detected in
+# the same collective: encode(has) reduces to "some rank had data" under op.
+_FLAG_ENCODE = {"Sum": lambda has: has, "Max": lambda has: has, "Min": lambda has: -has,
+                "Prod": lambda has: 1 - has}
+_FLAG_ANY = {"Sum": lambda v: v > 0, "Max": lambda v: v > 0, "Min": lambda v: v < 0, "Prod": lambda v: v == 0}
+
+
+def _agree_shapes(local: Dict[str, Optional[torch.Tensor]], static: Dict[str, Optional[tuple]],
+                  dev: torch.device) -> Dict[str, tuple]:
+    """Cell shape of every fetch on every rank. Statically known shapes need no
+    communication; otherwise ONE small device all-reduce (MAX) of
+    [has, rank, dims...] per fetch settles them. The decision depends on
+    static information only, so every rank makes the same collective calls."""
+    names = list(local)
+    out = {n: tuple(static[n]) for n in names if static.get(n) is not None}
+    todo = [n for n in names if n not in out]
+    if not todo:
+        return out
+    if not dist.is_distributed():
+        for n in todo:
+            _check(local[n] is not None, "Cannot reduce an empty DataFrame")
+            out[n] = tuple(local[n].shape)
+        return out
+    width = 2 + 8
+    desc = torch.zeros((len(todo), width), dtype=torch.int64)
+    for i, n in enumerate(todo):
+        if local[n] is not None:
+            shp = tuple(local[n].shape)
+            _check(len(shp) <= 8, "reduction outputs of rank > 8 are not supported")
+            desc[i, 0], desc[i, 1] = 1, len(shp)
+            desc[i, 2:2 + len(shp)] = torch.tensor(shp, dtype=torch.int64)
+    desc = desc.to(dev)
+    dist.all_reduce_(desc, "Max")
+    desc = desc.cpu()
+    for i, n in enumerate(todo):
+        _check(int(desc[i, 0]) == 1, "Cannot reduce an empty DataFrame")
+        shp = tuple(int(d) for d in desc[i, 2:2 + int(desc[i, 1])])
+        _check(local[n] is None or tuple(local[n].shape) == shp,
+               f"reduction output '{n}' has shape {tuple(local[n].shape) if local[n] is not None else None} "
+               f"on this rank but {shp} on another")
+        out[n] = shp
+    return out
+
+
+def _combine_monoids(partials: Dict[str, List[torch.Tensor]], ops: Dict[str, str],
+                     static: Dict[str, Optional[tuple]], dtypes: Dict[str, int]) -> Dict[str, torch.Tensor]:
+    """Monoid combine of per-partition partial cells: each fetch is reduced
+    locally with the native reduction, then fetches sharing (op, dtype) cross
+    the ranks in ONE all-reduce (RCCL for device tensors) that also carries
+    the has-data flag. No host-object (gloo) exchange is made."""
     dev = engine.compute_device()
-    if partials:
-        local = _monoid_reduce(op, torch.stack([p.to(dev) for p in partials], 0), dev)
-        has = 1
-    else:
-        local, has = None, 0
-    if dist.is_distributed():
-        counts = dist.all_gather_object((has, None if local is None else (tuple(local.shape), str(local.dtype))))
-        if not any(c[0] for c in counts):
-            raise TensorFramesError("Cannot reduce an empty DataFrame")
-        shape, dt = next(c[1] for c in counts if c[0])
-        if local is None:  # identity element for ranks without data
-            local = _identity(op, shape, getattr(torch, dt.split(".")[-1]), dev)
+    local: Dict[str, Optional[torch.Tensor]] = {}
+    for n, ps in partials.items():
+        local[n] = _monoid_reduce(ops[n], torch.stack([p.to(dev) for p in ps], 0), dev) if ps else None
+    if not dist.is_distributed():
+        _check(all(v is not None for v in local.values()), "Cannot reduce an empty DataFrame")
+        return local
+    shapes = _agree_shapes(local, static, dev)
+    groups: Dict[tuple, List[str]] = {}
+    for n in partials:
+        groups.setdefault((ops[n], int(dtypes[n])), []).append(n)
+    out: Dict[str, torch.Tensor] = {}
+    for (op, tfd), names in sorted(groups.items()):
+        tdt = D.torch_dtype(tfd)
+        has = int(any(local[n] is not None for n in names))
+        pieces = []
+        for n in names:
+            v = local[n] if local[n] is not None else _identity(op, shapes[n], tdt, dev)
+            pieces.append(v.reshape(-1).to(tdt))
+        pieces.append(torch.tensor([_FLAG_ENCODE[op](has)], dtype=tdt, device=dev))
+        buf = torch.cat(pieces)
         with metrics.timer("allreduce"):
-            local = dist.all_reduce_(local.contiguous(), op)
-    elif local is None:
-        raise TensorFramesError("Cannot reduce an empty DataFrame")
-    return local
+            dist.all_reduce_(buf, op)
+        _check(bool(_FLAG_ANY[op](buf[-1].item())), "Cannot reduce an empty DataFrame")
+        off = 0
+        for n in names:
+            k = int(np.prod(shapes[n])) if shapes[n] else 1
+            out[n] = buf[off:off + k].reshape(shapes[n])
+            off += k
+    return out
+
+
+def _gather_rank_values(local: Dict[str, Optional[torch.Tensor]], static: Dict[str, Optional[tuple]],
+                        dtypes: Dict[str, int]) -> Dict[str, List[torch.Tensor]]:
+    """Generic (non-monoid) combine: every rank's partial of every fetch, in
+    rank order, from the ranks that had data. One all-gather of the has-flags
+    and one per fetch (RCCL for device tensors)."""
+    names = list(local)
+    if not dist.is_distributed():
+        return {n: [local[n]] if local[n] is not None else [] for n in names}
+    dev = engine.compute_device()
+    shapes = _agree_shapes(local, static, dev)
+    has = any(v is not None for v in local.values())
+    flags = dist.all_gather_tensor(torch.tensor([int(has)], dtype=torch.int64, device=dev)).reshape(-1).cpu()
+    _check(int(flags.sum()) > 0, "Cannot reduce an empty DataFrame")
+    out = {}
+    for n in names:
+        tdt = D.torch_dtype(dtypes[n])
+        v = local[n].to(dev) if local[n] is not None else torch.zeros(shapes[n], dtype=tdt, device=dev)
+        allv = dist.all_gather_tensor(v.to(tdt).contiguous())
+        out[n] = [allv[r] for r in range(allv.shape[0]) if int(flags[r])]
+    return out
+
+
+def _static_shapes(spec_bytes: bytes, fetch_refs: List[str], names: List[str], feed_names: List[str],
+                   hints: Dict[str, tuple]) -> Dict[str, Optional[tuple]]:
+    """Fetch shapes inferred from the column schema alone (unknown -> None)."""
+    try:
+        infos = _C.analyze_fetches(engine.native_graph(spec_bytes), list(fetch_refs), list(feed_names), hints)
+    except ValueError:
+        return {n: None for n in names}
+    out = {}
+    for n, r in zip(names, fetch_refs):
+        shp = infos[r]["shape"]
+        out[n] = tuple(shp) if shp is not None and all(d is not None and d >= 0 for d in shp) else None
+    return out
 
 
 def _identity(op: str, shape, dtype, dev) -> torch.Tensor:
@@ -965,19 +1130,32 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
         for j, o in enumerate(per_part[pid]):
             partials[j].append(o)
 
+    fetch_refs = [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names]
+    col_hints = {n + "_input": (summary[n].tf_dtype, list(_col_info(dframe.schema[n]).shape.tail().prepend(UNKNOWN).dims))
+                 for n in out_names}
+    static = _static_shapes(spec.graph_bytes, fetch_refs, out_names, in_names, col_hints)
+    dtypes = {n: summary[n].tf_dtype for n in out_names}
     if uniform:
-        # partials reduced on device, then one all-reduce per fetch over RCCL
-        results = {name: _combine_across(partials[j], uniform[name]).cpu().numpy()
-                   for j, name in enumerate(out_names)}
+        # partials reduced on device, then one all-reduce per (op, dtype) over RCCL
+        comb = _combine_monoids({n: partials[j] for j, n in enumerate(out_names)}, uniform, static, dtypes)
+        results = {n: comb[n].cpu().numpy() for n in out_names}
     else:
-        # generic associative graph: gather every partition's partial row and
-        # run the graph once on the stacked [P, ...] block
-        rows = [[partials[k][i].cpu() for k in range(len(out_names))] for i in range(len(partials[0]))]
-        allp = [x for chunk in dist.all_gather_object(rows) for x in chunk]
-        _check(len(allp) > 0, "Cannot reduce an empty DataFrame")
-        stacks = [torch.stack([r[k] for r in allp], 0) for k in range(len(out_names))]
-        outs = engine.run_program(prog, stacks)
-        results = {n: o.cpu().numpy() for n, o in zip(out_names, outs)}
+        # generic associative graph: this rank's partials are folded by the graph
+        # on their stacked [P, ...] block, the per-rank partials are all-gathered
+        # and the graph runs once more on the stacked [ranks, ...] block
+        local: Dict[str, Optional[torch.Tensor]] = {n: None for n in out_names}
+        if partials[0]:
+            stacks = [torch.stack(partials[k], 0) for k in range(len(out_names))]
+            outs = engine.run_program(prog, stacks) if len(partials[0]) > 1 else [p[0] for p in partials]
+            local = dict(zip(out_names, outs))
+        allp = _gather_rank_values(local, static, dtypes)
+        if not dist.is_distributed():
+            _check(all(allp[n] for n in out_names), "Cannot reduce an empty DataFrame")
+        if len(allp[out_names[0]]) == 1:
+            results = {n: allp[n][0].cpu().numpy() for n in out_names}
+        else:
+            outs = engine.run_program(prog, [torch.stack(allp[n], 0) for n in out_names])
+            results = {n: o.cpu().numpy() for n, o in zip(out_names, outs)}
     metrics.add("reduce_blocks_calls")
     return _unpack(results, spec, summary)
 
@@ -1042,20 +1220,26 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
                 if b.nrows == 0:
                     continue
                 row = {}
+                folded = None  # ragged columns: one pairwise fold of the block serves every column
                 for n in names:
                     col = b.columns[n]
                     if is_dense(col):
                         row[n] = _monoid_reduce(monoid[n], col)
                     else:
-                        row[n] = _fold_rows(prog, names, [_cells(b.columns[m]) for m in names])[names.index(n)]
+                        if folded is None:
+                            folded = _fold_rows(prog, names, [_cells(b.columns[m]) for m in names])
+                        row[n] = folded[names.index(n)]
                 res[pid] = row
             return res
         per_part = faults.with_retries("reduce_rows", task)(dframe.local_blocks())
         for pid in sorted(per_part):
             for n in names:
                 partials[n].append(per_part[pid][n])
+        static = {n: (tuple(_col_info(dframe.schema[n]).shape.tail().dims)
+                      if _col_info(dframe.schema[n]).shape.tail().has_unknown() is False else None) for n in names}
+        comb = _combine_monoids(partials, monoid, static, {n: summary[n].tf_dtype for n in names})
         for n in names:
-            results[n] = _combine_across(partials[n], monoid[n]).cpu().numpy()
+            results[n] = comb[n].cpu().numpy()
         return _unpack(results, spec, summary)
     # generic: sequential fold per partition, then fold the partials
     def fold_task(blocks):
@@ -1063,11 +1247,19 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
                 for pid, b in sorted(blocks.items()) if b.nrows > 0}
     per_part = faults.with_retries("reduce_rows", fold_task)(dframe.local_blocks())
     partials_rows = [per_part[pid] for pid in sorted(per_part)]
-    allp = [x for chunk in dist.all_gather_object(partials_rows) for x in chunk]
-    _check(len(allp) > 0, "Cannot reduce an empty DataFrame")
-    acc = allp[0]
-    for r in allp[1:]:
-        acc = engine.run_program(prog, list(acc) + list(r), torch.device("cpu"))
+    # this rank's partials folded pairwise, then the per-rank partials gathered
+    local: Dict[str, Optional[torch.Tensor]] = {n: None for n in names}
+    if partials_rows:
+        acc = partials_rows[0]
+        for r in partials_rows[1:]:
+            acc = engine.run_program(prog, list(acc) + list(r), torch.device("cpu"))
+        local = dict(zip(names, acc))
+    static = {n: None for n in names}  # generic pair graphs: shapes agreed at run time
+    allp = _gather_rank_values(local, static, {n: summary[n].tf_dtype for n in names})
+    _check(all(allp[n] for n in names), "Cannot reduce an empty DataFrame")
+    acc = [allp[n][0].cpu() for n in names]
+    for r in range(1, len(allp[names[0]])):
+        acc = engine.run_program(prog, acc + [allp[n][r].cpu() for n in names], torch.device("cpu"))
     return _unpack({n: a.cpu().numpy() for n, a in zip(names, acc)}, spec, summary)
 
 
@@ -1159,7 +1351,7 @@ def _shuffle_blocks(send: List[List[Block]], names: List[str], tf_types: Dict[st
     rank) travel as tensors in one all_to_all per column, device-resident
     ones over RCCL; other columns (strings, ragged cells) as pickled values."""
     w = dist.world_size()
-    if w == 1:
+    if not dist.is_distributed():
         return list(send[0])
     per = [concat_blocks(s, names) if s else None for s in send]
     recv_rows = dist.all_to_all_counts([0 if p is None else p.nrows for p in per])
@@ -1234,9 +1426,9 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 ids = torch.from_numpy(codes).to(dev)
                 red = _C.unsorted_segment_reduce(monoid[n], xd.contiguous(), ids, ng)
                 # partials stay in HBM when the shuffle can move them over RCCL
-                cols[n] = red if (w > 1 and red.is_cuda and dist.gpu_collectives()) else red.cpu()
+                cols[n] = red if (dist.is_distributed() and red.is_cuda and dist.gpu_collectives()) else red.cpu()
             part = Block(ng, cols)
-            if w == 1:
+            if not dist.is_distributed():
                 send[0].append(part)
                 continue
             dest = (_key_hash([_key_array(part.columns[k]) for k in keys]) % np.uint64(w)).astype(np.int64)
@@ -1269,7 +1461,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             if b.nrows == 0:
                 continue
             host = b.select(all_cols).to(torch.device("cpu"))
-            if w == 1:
+            if not dist.is_distributed():
                 send[0].append(host)
                 continue
             dest = (_key_hash([_key_array(host.columns[k]) for k in keys]) % np.uint64(w)).astype(np.int64)

@@ -239,12 +239,22 @@ def _lift(gdef, fetches, feeds, infos, patch_only=False):
                 raise _Refuse("data-dependent split")
             m.input = shifted_const(nd, ax_i, lambda a: shift_axes(a, 0))
         elif op == "MatMul":
-            # cell [m,k] x const [k,n] -> batched [B,m,k] x [k,n]
+            # cell [m,k] x const [k,n]: the batch [B,m,k] is flattened to ONE
+            # [B*m,k] x [k,n] GEMM (the MFMA kernel, fusable epilogue) and the
+            # result viewed back as [B,m,n]
             if bflags[1] or rank(*data_ins[0]) != 2 or nd.attr.get("transpose_a") and nd.attr["transpose_a"].value:
                 raise _Refuse("MatMul form not liftable")
-            tb = bool(nd.attr["transpose_b"].value) if "transpose_b" in nd.attr else False
-            m = P.NodeDef(nd.name, "BatchMatMulV2", list(nd.input),
-                          {"T": nd.attr["T"], "adj_x": P.AttrValue.b(False), "adj_y": P.AttrValue.b(tb)}, nd.device)
+            a_shape = infos[data_ins[0][0]][data_ins[0][1]]["shape"]
+            o_shape = infos[name][0]["shape"]
+            if any(d is None or d < 0 for d in list(a_shape) + list(o_shape)):
+                raise _Refuse("MatMul with unknown cell dims")
+            flat, mm = f"{name}/_tfa_vec_flat", f"{name}/_tfa_vec_mm"
+            tattr = {"T": nd.attr["T"], "Tshape": P.AttrValue.type(D.DT_INT32)}
+            extra.append(_const_node(flat + "/shape", np.asarray([-1, a_shape[1]], np.int32)))
+            extra.append(P.NodeDef(flat, "Reshape", [nd.input[0], flat + "/shape"], dict(tattr)))
+            extra.append(P.NodeDef(mm, "MatMul", [flat, nd.input[1]], dict(nd.attr), nd.device))
+            extra.append(_const_node(name + "/_tfa_vec_shape", np.asarray([-1] + list(o_shape), np.int32)))
+            m = P.NodeDef(nd.name, "Reshape", [mm, name + "/_tfa_vec_shape"], dict(tattr), nd.device)
         else:
             raise _Refuse(f"no lifting rule for {op}")
         out_nodes[name] = m

@@ -26,8 +26,18 @@ def env_world_size() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
+def _forced() -> bool:
+    from ..config import config
+    return bool(config.force_collectives)
+
+
 def is_distributed() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    """True when cross-rank collectives run: a process group of world size > 1,
+    or any group with `Config.force_collectives` (a 1-rank RCCL group on one
+    GPU executes exactly the collective calls an 8-rank job makes)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or _forced()
 
 
 def rank() -> int:
@@ -42,22 +52,35 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", str(rank())))
 
 
-def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> bool:
+def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, force: bool = False) -> bool:
     """Initialise the default process group from torchrun's env (idempotent).
 
     Collectives time out after `Config.collective_timeout_s`; RCCL errors and
     timeouts abort the communicator instead of hanging (async error handling).
-    Returns True when running with world_size > 1.
+    With `force` (or `Config.force_collectives`) a single process builds a
+    world-size-1 group, so RCCL runs even on one GPU.
+    Returns True when collectives are active (`is_distributed()`).
     """
     from ..config import config
     if timeout_s is None:
         timeout_s = config.collective_timeout_s
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    if force:
+        config.force_collectives = True
     if dist.is_initialized():
         _ensure_groups()
-        return dist.get_world_size() > 1
-    if env_world_size() <= 1:
+        return is_distributed()
+    if env_world_size() <= 1 and not _forced():
         return False
+    if env_world_size() <= 1:
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("LOCAL_RANK", "0")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     use_gpu = torch.cuda.is_available()
@@ -73,7 +96,7 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> bo
     dist.init_process_group(**kwargs)
     _state["initialized_here"] = True
     _ensure_groups()
-    return dist.get_world_size() > 1
+    return is_distributed()
 
 
 def _parse_cpulist(text: str) -> List[int]:
@@ -162,15 +185,21 @@ def barrier():
         dist.barrier(group=_state["cpu_group"])
 
 
+_pending_events: List[tuple] = []  # (name, start, end) device events not yet read
+
+
 class _traced:
     """Observability for one collective: a roctx range
     (`rocprofv3 --marker-trace` shows it next to the kernels) and metrics
     counters `collective_<name>` (calls), `collective_bytes`,
     `collective_ms` (host time: RCCL calls return once enqueued, gloo ones
-    when done)."""
+    when done). Device collectives also record a hipEvent pair on the current
+    stream; `collective_device_ms()` reads their elapsed device time (the
+    RCCL kernel's own duration, not the enqueue time)."""
 
-    def __init__(self, name: str, nbytes: int = 0):
+    def __init__(self, name: str, nbytes: int = 0, device: Optional[torch.device] = None):
         self.name, self.nbytes = name, int(nbytes)
+        self.device = device if device is not None and device.type == "cuda" else None
 
     def __enter__(self):
         self.t0 = time.perf_counter()
@@ -180,9 +209,18 @@ class _traced:
                 torch.cuda.nvtx.range_push(f"tfa.collective.{self.name}")
             except Exception:  # no roctx in this build
                 self.rng = False
+        self.ev = None
+        if self.device is not None:
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record(torch.cuda.current_stream(self.device))
         return self
 
     def __exit__(self, *exc):
+        if self.ev is not None:
+            self.ev[1].record(torch.cuda.current_stream(self.device))
+            _pending_events.append((self.name,) + self.ev)
+            if len(_pending_events) > 4096:
+                collective_device_ms()
         if self.rng:
             torch.cuda.nvtx.range_pop()
         from ..utils.logging import metrics
@@ -190,6 +228,22 @@ class _traced:
         metrics.add("collective_bytes", self.nbytes)
         metrics.add("collective_ms", (time.perf_counter() - self.t0) * 1e3)
         return False
+
+
+def collective_device_ms() -> float:
+    """Device time of the device collectives issued so far (waits for them);
+    also accumulated into metrics `collective_device_ms` and
+    `collective_<name>_device_ms`."""
+    from ..utils.logging import metrics
+    total = 0.0
+    while _pending_events:
+        name, a, b = _pending_events.pop(0)
+        b.synchronize()
+        ms = a.elapsed_time(b)
+        total += ms
+        metrics.add("collective_device_ms", ms)
+        metrics.add(f"collective_{name}_device_ms", ms)
+    return metrics.snapshot().get("collective_device_ms", 0.0)
 
 
 def _nbytes(t: torch.Tensor) -> int:
@@ -267,7 +321,7 @@ def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torc
         return all_to_all_tensors([c.cpu() for c in chunks], recv_rows).to(x.device)
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
     out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    with _traced("all_to_all", _nbytes(x)):
+    with _traced("all_to_all", _nbytes(x), x.device):
         dist.all_to_all_single(out, x, [int(r) for r in recv_rows], [int(c.shape[0]) for c in chunks],
                                group=group)
     return out
@@ -285,7 +339,7 @@ def all_reduce_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
     if t.is_cuda and not gpu_collectives():  # gloo rehearsal: stage through the host
         return t.copy_(all_reduce_(t.cpu(), op))
     group = _state["device_group"] if t.is_cuda else _state["cpu_group"]
-    with _traced("all_reduce", _nbytes(t)):
+    with _traced("all_reduce", _nbytes(t), t.device):
         dist.all_reduce(t, op=_OPS[op], group=group)
     return t
 
@@ -300,7 +354,7 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
         return all_gather_tensor(t.cpu()).to(t.device)
     if t.is_cuda:
         out = torch.empty((world_size(),) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        with _traced("all_gather", _nbytes(t)):
+        with _traced("all_gather", _nbytes(t), t.device):
             dist.all_gather_into_tensor(out, t, group=_state["device_group"])
         return out
     parts = [torch.empty_like(t) for _ in range(world_size())]

@@ -11,7 +11,14 @@ for tests, e.g. "the map_blocks task of partition 3 fails once":
         df2.collect()          # retried when config.task_retries >= 1
 
 Validation errors (TensorFramesError and other ValueError/TypeError that do
-not come from the device runtime) are never retried.
+not come from the device runtime) are never retried. Device errors are
+sorted: running out of memory is recoverable (cached blocks are released and
+the partition re-run); a HIP fault (illegal address, kernel abort, ECC...)
+leaves the process's GPU context unusable, so it is NEVER retried in-process:
+it is re-raised at once as `DeviceFaultError`, naming the node and kernel the
+executor was running (csrc/runtime/executor.cpp checks every launch). Other
+HIP errors (an invalid launch configuration, ...) are deterministic and not
+retried either.
 """
 from __future__ import annotations
 
@@ -25,6 +32,44 @@ from .logging import logger, metrics
 
 class InjectedFault(RuntimeError):
     """Raised by an armed injection site."""
+
+
+class DeviceFaultError(RuntimeError):
+    """A sticky GPU fault: the HIP context of this process is lost. The job
+    must fail (or be re-run in a fresh process); retrying here would fail
+    again or hang."""
+
+
+# substrings of HIP/HSA errors after which the context cannot be used again
+_STICKY = ("illegal address", "illegaladdress", "memory access fault", "launch failure", "launchfailure",
+           "device-side assert", "hiperrorassert", "illegal instruction", "illegalinstruction", "ecc",
+           "hardware exception", "hsa_status_error", "launch timed out", "launchtimeout", "misaligned address",
+           "context is destroyed", "contextisdestroyed", "unspecified launch")
+_OOM = ("out of memory", "outofmemory", "hiperroroutofmemory", "memoryallocation")
+
+
+def classify(e: BaseException) -> str:
+    """'validation', 'oom', 'sticky', 'device' (other deterministic HIP errors),
+    'transient' (injected faults, I/O, other runtime errors)."""
+    from ..core import TensorFramesError
+    if isinstance(e, DeviceFaultError):
+        return "sticky"
+    if isinstance(e, MemoryError):
+        return "oom"
+    msg = str(e).lower()
+    if any(k in msg for k in _STICKY):
+        return "sticky"
+    if any(k in msg for k in _OOM):
+        return "oom"
+    if isinstance(e, (TensorFramesError, TypeError, KeyError)):
+        return "validation"
+    if "hip error" in msg or "hiperror" in msg:
+        return "device"
+    if isinstance(e, ValueError):
+        return "validation"
+    if isinstance(e, InjectedFault):
+        return "transient"
+    return "transient" if isinstance(e, (RuntimeError, OSError)) else "validation"
 
 
 @dataclass
@@ -75,15 +120,24 @@ def check(site: str, partitions: Iterable[int]):
 
 
 def is_retryable(e: BaseException) -> bool:
-    from ..core import TensorFramesError
-    if isinstance(e, (TensorFramesError, TypeError, KeyError)):
-        return False
-    if isinstance(e, ValueError):
-        # native runtime errors surface as GraphError (a ValueError); only the
-        # device-side ones (HIP launch/runtime failures) are transient
-        msg = str(e).lower()
-        return "hip" in msg or "device" in msg
-    return isinstance(e, (RuntimeError, OSError, MemoryError))
+    return classify(e) in ("oom", "transient")
+
+
+def _raise_sticky(site: str, e: BaseException):
+    metrics.add("device_faults")
+    if isinstance(e, DeviceFaultError):
+        raise e
+    raise DeviceFaultError(f"{site}: GPU fault, the device context of this process is lost and the task is "
+                           f"not retried in-process: {e}") from e
+
+
+def _release_device_memory():
+    try:
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.empty_cache()
+    except Exception:  # noqa: BLE001 - best effort before a retry
+        pass
 
 
 def with_retries(site: str, fn: Callable[[Dict[int, object]], Dict[int, object]]):
@@ -97,8 +151,12 @@ def with_retries(site: str, fn: Callable[[Dict[int, object]], Dict[int, object]]
             check(site, blocks.keys())
             return fn(blocks)
         except Exception as e:  # noqa: BLE001
+            if classify(e) == "sticky":
+                _raise_sticky(site, e)
             if config.task_retries <= 0 or not is_retryable(e):
                 raise
+            if classify(e) == "oom":
+                _release_device_memory()
             first = e
         logger.warning("%s: task failed (%s); retrying %d partition(s) one by one", site, first, len(blocks))
         res = {}
@@ -110,8 +168,12 @@ def with_retries(site: str, fn: Callable[[Dict[int, object]], Dict[int, object]]
                     metrics.add("task_retries")
                     break
                 except Exception as e:  # noqa: BLE001
+                    if classify(e) == "sticky":
+                        _raise_sticky(site, e)
                     if attempt >= config.task_retries or not is_retryable(e):
                         raise
+                    if classify(e) == "oom":
+                        _release_device_memory()
                     logger.warning("%s: partition %d attempt %d failed: %s", site, pid, attempt, e)
         return res
 

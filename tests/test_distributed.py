@@ -79,6 +79,22 @@ def _worker(rank, world, port, outdir, device="cpu"):
         one = tfs.create_dataframe([Row(c="a", x=float(i)) for i in range(20)], num_partitions=5)
         agg = tfs.aggregate(tf.reduce_min(xi, [0], name="x"), one.groupBy("c"))
         res["agg_one"] = [list(r) for r in agg.collect()]
+    # reductions make no host-object (pickled gloo) exchange; ranks without
+    # data contribute identities (1 partition: only rank 0 has rows), also
+    # when the output shape is only known at run time (unanalysed [?,?] column)
+    from tensorframes_amd.utils.logging import metrics as _m
+    ago0 = _m.snapshot().get("collective_all_gather_object", 0)
+    one_part = tfs.create_dataframe([Row(x=float(i), v=[float(i), 1.0]) for i in range(7)], num_partitions=1)
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        res["sum_one_part"] = tfs.reduce_blocks(tf.reduce_sum(xi, [0], name="x"), one_part.select("x"))
+    with tf.Graph().as_default():
+        vi = tf.placeholder(tf.double, shape=[None, None], name="v_input")
+        res["vmin_one_part"] = tfs.reduce_blocks(tf.reduce_min(vi, [0], name="v"), one_part.select("v")).tolist()
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        res["gen_one_part"] = tfs.reduce_blocks(tf.identity(tf.reduce_max(xi, [0]), name="x"), one_part.select("x"))
+    res["ago_delta"] = _m.snapshot().get("collective_all_gather_object", 0) - ago0
     res["repart"] = [r.x for r in df.repartition(4).select("x").collect()]
     # checkpoint: every rank writes its own partitions, reads them back
     ck = os.path.join(outdir, "ck")
@@ -141,6 +157,8 @@ def _check_results(tmp_path, world, device):
                                 for k in range(4)]
         assert o["agg_gen"] == [[k, sum(x * x for x in xs if int(x) % 4 == k)] for k in range(4)]
         assert o["agg_one"] == [["a", 0.0]]
+        assert o["sum_one_part"] == 21.0 and o["vmin_one_part"] == [0.0, 1.0] and o["gen_one_part"] == 6.0
+        assert o["ago_delta"] == 0
         assert o["repart"] == xs
         assert o["ck_parts"] == o["local_parts"] and o["ck_x"] == xs
         assert o["retry_z"] == [x + 1.0 for x in xs]

@@ -69,5 +69,51 @@ def test_validation_errors_are_not_retried(df):
     tfs.set_config(task_retries=3)
     assert not faults.is_retryable(tfs.TensorFramesError("bad shape"))
     assert not faults.is_retryable(ValueError("while executing node 'x': bad attr"))
-    assert faults.is_retryable(ValueError("gemm: hipErrorLaunchFailure"))
-    assert faults.is_retryable(RuntimeError("HIP error: an illegal memory access"))
+    # sticky device faults: the context is lost, never retried in-process
+    assert not faults.is_retryable(ValueError("gemm: hipErrorLaunchFailure"))
+    assert not faults.is_retryable(RuntimeError("HIP error: an illegal memory access was encountered"))
+    assert faults.classify(RuntimeError("Memory access fault by GPU node-2")) == "sticky"
+    # deterministic HIP errors are not transient either; running out of memory is
+    assert faults.classify(ValueError("HIP error invalid configuration argument in node 'y'")) == "device"
+    assert not faults.is_retryable(ValueError("HIP error invalid configuration argument in node 'y'"))
+    assert faults.is_retryable(RuntimeError("HIP out of memory. Tried to allocate 2.00 GiB"))
+    assert faults.classify(faults.InjectedFault("x")) == "transient"
+
+
+def test_sticky_fault_is_not_retried_in_process(df):
+    tfs.set_config(task_retries=5)
+    calls = []
+
+    def task(blocks):
+        calls.append(sorted(blocks))
+        raise RuntimeError("HIP error an illegal memory access was encountered (hipErrorIllegalAddress) "
+                           "in node 'y' (MatMul)")
+    with pytest.raises(faults.DeviceFaultError, match="not retried in-process.*node 'y'"):
+        faults.with_retries("map_blocks", task)({0: None, 1: None})
+    assert len(calls) == 1  # one attempt, no per-partition re-runs
+
+
+def test_oom_is_retried(df):
+    tfs.set_config(task_retries=2)
+    calls = []
+
+    def task(blocks):
+        calls.append(sorted(blocks))
+        if len(calls) == 1:
+            raise RuntimeError("HIP out of memory. Tried to allocate 64.00 GiB")
+        return {p: p for p in blocks}
+    assert faults.with_retries("map_blocks", task)({0: None, 1: None}) == {0: 0, 1: 1}
+    assert calls == [[0, 1], [0], [1]]
+
+
+def test_debug_sync_can_be_toggled_after_a_run(df):
+    from tensorframes_amd._native import _C
+    old = tfs.config.debug_sync
+    try:
+        assert [r.z for r in _plus3(df).collect()][0] == 3.0  # a program has run
+        tfs.set_config(debug_sync=True)
+        assert _C.get_debug_sync()
+        tfs.set_config(debug_sync=False)
+        assert not _C.get_debug_sync()
+    finally:
+        tfs.set_config(debug_sync=old)
