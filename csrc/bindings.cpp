@@ -10,6 +10,7 @@
 #include "ir/graph.h"
 #include "kernels/kernels.h"
 #include "runtime/executor.h"
+#include "runtime/jit.h"
 
 namespace py = pybind11;
 using namespace tfa;
@@ -171,7 +172,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("run_chunked", &Program::run_chunked, py::arg("seg_inputs"), py::arg("seg_outputs"),
            py::arg("chunk_rows"), py::arg("device"), py::arg("depth") = 3,
            py::call_guard<py::gil_scoped_release>())
-      .def("describe", &Program::describe_plan)
+      .def("describe", &Program::describe_plan, py::arg("inputs"), py::arg("as_gpu") = false)
+      .def("fused_sources", &Program::fused_sources)
       .def("reset_stats", &Program::reset_stats)
       .def("stats", [](const Program& p) {
         ExecStats s = p.stats();
@@ -261,6 +263,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("registered_ops", [] { return OpRegistry::get().names(); });
   // float32 MatMul/Conv2D compute mode: 0 exact f32, 1 bf16, 2 bf16x3 (kernels/gemm_bf16.hip)
   m.def("set_f32_precision", [](int mode) { k::set_f32_precision(mode); });
+  m.def("jit_compile", [](const std::string& src) { return jit::compile_only(src); },
+        "compile a generated kernel with hiprtc for gfx950 (no device needed); returns the code-object size");
+  m.def("jit_stats", []() {
+    auto s = jit::stats();
+    py::dict d;
+    d["compiled"] = s.compiled;
+    d["disk_hits"] = s.disk_hits;
+    d["memory_hits"] = s.memory_hits;
+    d["compile_ms"] = s.compile_ms;
+    return d;
+  });
   m.def("set_debug_sync", &set_debug_sync, "synchronise + check after every kernel (read per launch)");
   m.def("get_debug_sync", &get_debug_sync);
   m.def("f32_precision", [] { return k::f32_precision(); });

@@ -16,6 +16,8 @@
 #include <sstream>
 
 #include "../ir/ops_common.h"
+#include "fusion.h"
+#include "jit.h"
 
 namespace tfa {
 
@@ -63,7 +65,8 @@ void set_debug_sync(bool on) { g_debug_sync.store(on ? 1 : 0); }
 bool get_debug_sync() { return debug_sync(); }
 
 struct Program::Step {
-  enum Kind { OP, GEMM, CONV } kind = OP;
+  enum Kind { OP, GEMM, CONV, FUSED } kind = OP;
+  int fused = -1;        // FUSED: index into Plan::fused
   int node = -1;         // node whose op runs (for GEMM/CONV: the MatMul/Conv2D node)
   int out_node = -1;     // node whose outputs this step produces
   std::vector<int> in_slots;
@@ -93,6 +96,13 @@ struct Program::Plan {
   std::vector<int> fetch_slots;
   std::map<int, std::map<int, at::Tensor>> dev_consts;  // device index -> slot -> tensor
   int fused = 0;
+  // fused elementwise regions (GPU plans): generated source + loaded kernel per device
+  struct Fused {
+    FusedRegion region;
+    std::mutex mu;
+    std::map<int, jit::Kernel> kernels;
+  };
+  std::vector<std::unique_ptr<Fused>> fused_regions;
   // HIP-graph replay of this plan (small, repeated launches): static input
   // buffers the inputs are copied into, the captured graph, its outputs
   struct Captured {
@@ -243,15 +253,16 @@ std::shared_ptr<Program::Plan> Program::plan_for(const std::vector<at::Tensor>& 
   std::lock_guard<std::mutex> lk(mu_);
   auto it = plans_.find(key);
   if (it != plans_.end()) return it->second;
-  auto p = build_plan(inputs);
+  auto p = build_plan(inputs, false);
   if (plans_.size() >= kMaxPlans) plans_.erase(plans_.begin());  // bounded (e.g. many image sizes)
   plans_[key] = p;
   stats_.plans_built++;
   return p;
 }
 
-std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>& inputs) {
+std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>& inputs, bool force_gpu) {
   auto p = std::make_shared<Plan>();
+  const bool gpu_plan = force_gpu || (!inputs.empty() && inputs[0].is_cuda());
   std::map<int, TensorInfo> feeds;
   for (size_t i = 0; i < inputs.size(); ++i) {
     TensorInfo ti;
@@ -414,6 +425,61 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     }
     p->steps.push_back(std::move(st));
   }
+  // ---- elementwise-region fusion (GPU plans): regions replace their member steps
+  if (gpu_plan && fusion_enabled()) {
+    FusionInput fi;
+    fi.g = g_.get();
+    fi.infos = &p->infos;
+    fi.runtime = runtime;
+    fi.fetched = fetched;
+    fi.excluded = absorbed;
+    for (auto& st : p->steps)
+      if (st.kind != Step::OP) fi.excluded.insert(st.node);
+    for (int n : runtime)
+      for (auto& r : g_->node(n).inputs) fi.consumers[r.node].push_back(n);
+    std::vector<FusedRegion> regions = find_fused_regions(fi);
+    if (!regions.empty()) {
+      std::map<int, int> first_out;  // first output node -> region index
+      std::set<int> covered;         // prologue members and outputs: their steps are replaced
+      for (size_t i = 0; i < regions.size(); ++i) {
+        first_out[regions[i].outputs.front()] = static_cast<int>(i);
+        covered.insert(regions[i].nodes.begin(), regions[i].nodes.end());
+        covered.insert(regions[i].outputs.begin(), regions[i].outputs.end());
+      }
+      std::map<int, const Step*> step_of;
+      for (auto& st : p->steps)
+        if (st.kind == Step::OP) step_of[st.node] = &st;
+      std::vector<Step> steps;
+      for (auto& st : p->steps) {
+        if (st.kind != Step::OP || !covered.count(st.node)) {
+          steps.push_back(std::move(st));
+          continue;
+        }
+        auto rit = first_out.find(st.node);
+        if (rit == first_out.end()) continue;  // evaluated inside a region's kernel
+        const FusedRegion& rg = regions[rit->second];
+        Step fs;
+        fs.kind = Step::FUSED;
+        fs.node = fs.out_node = st.node;
+        fs.fused = static_cast<int>(p->fused_regions.size());
+        for (auto& l : rg.leaves) {
+          fs.in_slots.push_back(slot_for(l.ref));
+          fs.in_info.push_back(&infos[l.ref.node][l.ref.index]);
+        }
+        for (int o : rg.outputs) {
+          const Step* os = step_of.at(o);
+          TFA_CHECK(os->out_slots.size() == 1, "internal: fused output with several outputs");
+          fs.out_slots.push_back(os->out_slots[0]);
+          fs.out_info.push_back(os->out_info[0]);
+        }
+        auto fe = std::make_unique<Plan::Fused>();
+        fe->region = rg;
+        p->fused_regions.push_back(std::move(fe));
+        steps.push_back(std::move(fs));
+      }
+      p->steps = std::move(steps);
+    }
+  }
   for (auto& f : fetches_) p->fetch_slots.push_back(slot_for(f));
 
   // write-into-slice for last-axis ConcatV2 of f32 GEMM/CONV outputs
@@ -517,7 +583,37 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
       std::unique_ptr<RangeGuard> rg;
       if (gpu) rg = std::make_unique<RangeGuard>(nd.op + ":" + nd.name);
       try {
-        if (st.kind == Step::OP && gpu && !st.preplaced.empty()) {
+        if (st.kind == Step::FUSED) {
+          TFA_CHECK(gpu, "internal: fused step in a host plan");
+          Plan::Fused& fe = *p.fused_regions[st.fused];
+          const int di = dev.index();
+          jit::Kernel kern;
+          {
+            std::lock_guard<std::mutex> lk(fe.mu);
+            auto kit = fe.kernels.find(di);
+            if (kit == fe.kernels.end()) {
+              hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+              (void)hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cs);
+              TFA_CHECK(cs == hipStreamCaptureStatusNone, "fused kernel not loaded before graph capture");
+              kit = fe.kernels.emplace(di, jit::get(fe.region.source, fe.region.entry)).first;
+            }
+            kern = kit->second;
+          }
+          std::vector<void*> outs;
+          for (size_t k = 0; k < st.out_slots.size(); ++k) {
+            c.out[k] = c.alloc_out(static_cast<int>(k));
+            outs.push_back(c.out[k].data_ptr());
+          }
+          std::vector<const void*> ptrs;
+          for (size_t k = 0; k < c.in.size(); ++k) {
+            if (!c.in[k].is_contiguous()) c.in[k] = materialize(c, c.in[k]);
+            ptrs.push_back(c.in[k].data_ptr());
+          }
+          std::vector<int64_t> w = fused_args(fe.region, ptrs, outs);
+          TFA_CHECK(fe.region.grid >= 1 && fe.region.grid < (int64_t(1) << 31), "fused kernel: grid out of range");
+          jit::launch(kern, static_cast<unsigned>(fe.region.grid), fe.region.block, w.data(),
+                      w.size() * sizeof(int64_t), static_cast<hipStream_t>(stream));
+        } else if (st.kind == Step::OP && gpu && !st.preplaced.empty()) {
           // concat whose producers wrote in place: copy only the other inputs
           at::Tensor& out = slots[st.out_slots[0]];
           TFA_CHECK(out.defined(), "internal: concat output not allocated by its producers");
@@ -858,16 +954,29 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
   stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
 }
 
+std::vector<std::string> Program::fused_sources(const std::vector<at::Tensor>& inputs) {
+  auto p = build_plan(inputs, true);
+  std::vector<std::string> out;
+  for (auto& f : p->fused_regions) out.push_back(f->region.source);
+  return out;
+}
+
 ExecStats Program::stats() const { return stats_; }
 void Program::reset_stats() { stats_ = ExecStats(); }
 
-std::string Program::describe_plan(const std::vector<at::Tensor>& inputs) {
-  auto p = plan_for(inputs);
+std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool as_gpu) {
+  auto p = as_gpu ? build_plan(inputs, true) : plan_for(inputs);
   std::ostringstream os;
   os << "plan: " << p->steps.size() << " steps, " << p->const_slots.size() << " constants, "
-     << p->fused << " fused epilogues\n";
+     << p->fused << " fused epilogues, " << p->fused_regions.size() << " fused regions\n";
   for (auto& st : p->steps) {
     const Node& nd = g_->node(st.node);
+    if (st.kind == Step::FUSED) {
+      const FusedRegion& rg = p->fused_regions[st.fused]->region;
+      os << "  FUSED" << (rg.kind == 1 ? "-ROWRED " : " ") << nd.name << " [" << rg.expr << "] "
+         << rg.leaves.size() << " inputs " << rg.outputs.size() << " outputs " << st.out_info[0].shape.str() << '\n';
+      continue;
+    }
     os << "  " << (st.kind == Step::GEMM ? "GEMM" : st.kind == Step::CONV ? "CONV" : "OP  ") << ' '
        << nd.op << ' ' << nd.name;
     if (st.out_node != st.node) os << " -> " << g_->node(st.out_node).name;

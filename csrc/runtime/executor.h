@@ -65,14 +65,17 @@ class Program {
 
   ExecStats stats() const;
   void reset_stats();
-  std::string describe_plan(const std::vector<at::Tensor>& inputs);
+  // as_gpu: describe the plan a GPU run would use (fusion included), from host tensors
+  std::string describe_plan(const std::vector<at::Tensor>& inputs, bool as_gpu = false);
+  // generated sources of the fused regions of the GPU plan for these input shapes
+  std::vector<std::string> fused_sources(const std::vector<at::Tensor>& inputs);
 
  private:
   std::string host_op_error_;  // set when a host-only op is reachable (analysis ok, running not)
   struct Step;
   struct Plan;
   std::shared_ptr<Plan> plan_for(const std::vector<at::Tensor>& inputs);
-  std::shared_ptr<Plan> build_plan(const std::vector<at::Tensor>& inputs);
+  std::shared_ptr<Plan> build_plan(const std::vector<at::Tensor>& inputs, bool force_gpu);
   std::vector<at::Tensor> execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream);
   at::Tensor device_const(Plan& p, int slot, const at::Device& dev);
   bool graphable(const Plan& p) const;
