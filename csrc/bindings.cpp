@@ -263,6 +263,47 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("registered_ops", [] { return OpRegistry::get().names(); });
   // float32 MatMul/Conv2D compute mode: 0 exact f32, 1 bf16, 2 bf16x3 (kernels/gemm_bf16.hip)
   m.def("set_f32_precision", [](int mode) { k::set_f32_precision(mode); });
+  // device groupBy segmentation (kernels/groupby.hip); host tensors use the ATen oracle
+  m.def("factorize", [](const at::Tensor& keys0) {
+    TFA_CHECK(keys0.dim() == 1, "factorize: keys must be 1-D");
+    at::Tensor keys = keys0.contiguous();
+    const int64_t n = keys.size(0);
+    if (!keys.is_cuda()) {
+      auto r = at::_unique2(keys, /*sorted=*/true, /*return_inverse=*/true, /*return_counts=*/false);
+      return py::make_tuple(std::get<1>(r).to(at::kLong), std::get<0>(r));
+    }
+    c10::hip::HIPGuard guard(keys.device().index());
+    auto opts = keys.options();
+    if (n == 0) return py::make_tuple(at::empty({0}, opts.dtype(at::kLong)), at::empty({0}, opts));
+    hipStream_t s = c10::hip::getCurrentHIPStream(keys.device().index()).stream();
+    const DType dt = from_scalar_type(keys.scalar_type());
+    const size_t wsb = k::factorize_workspace_bytes(dt, n);
+    at::Tensor ws = at::empty({static_cast<int64_t>(wsb)}, opts.dtype(at::kByte));
+    at::Tensor ids = at::empty({n}, opts.dtype(at::kLong));
+    at::Tensor uniq = at::empty({n}, opts);
+    int64_t nseg = 0;
+    {
+      py::gil_scoped_release nogil;
+      nseg = k::factorize(dt, keys.data_ptr(), n, ids.data_ptr<int64_t>(), uniq.data_ptr(), ws.data_ptr(), wsb, s);
+    }
+    return py::make_tuple(ids, uniq.narrow(0, 0, nseg));
+  }, "keys [n] -> (group id per row int64, distinct keys ascending)");
+  m.def("key_dest", [](const std::vector<at::Tensor>& keys, int64_t world) {
+    TFA_CHECK(!keys.empty() && keys[0].is_cuda(), "key_dest: device key columns expected");
+    c10::hip::HIPGuard guard(keys[0].device().index());
+    const int64_t n = keys[0].size(0);
+    hipStream_t s = c10::hip::getCurrentHIPStream(keys[0].device().index()).stream();
+    at::Tensor h = at::empty({n}, keys[0].options().dtype(at::kLong));
+    for (size_t i = 0; i < keys.size(); ++i) {
+      at::Tensor kc = keys[i].contiguous();
+      TFA_CHECK(kc.dim() == 1 && kc.size(0) == n, "key_dest: key columns must be 1-D of equal length");
+      k::key_hash(from_scalar_type(kc.scalar_type()), kc.data_ptr(), n,
+                  reinterpret_cast<uint64_t*>(h.data_ptr<int64_t>()), i > 0, s);
+    }
+    at::Tensor dest = at::empty({n}, h.options());
+    k::hash_mod(reinterpret_cast<const uint64_t*>(h.data_ptr<int64_t>()), n, world, dest.data_ptr<int64_t>(), s);
+    return dest;
+  }, "destination rank of every row: hash(keys) % world (same on every rank)");
   m.def("jit_compile", [](const std::string& src) { return jit::compile_only(src); },
         "compile a generated kernel with hiprtc for gfx950 (no device needed); returns the code-object size");
   m.def("jit_stats", []() {

@@ -74,6 +74,17 @@ void unsorted_segment_reduce(RedOp op, DType dt, DType idt, const void* x, const
 void segment_reduce_csr(RedOp op, DType dt, const void* x, const int64_t* offsets, void* y,
                         int64_t nseg, int64_t inner, hipStream_t s);
 
+// ------------------------------------------------------------ groupBy (groupby.hip)
+// keys [n] -> ids [n] (group of each row, groups in ascending key order) and
+// uniq (first nseg entries: the distinct keys, ascending); returns nseg
+// (synchronises the stream once to read it).
+size_t factorize_workspace_bytes(DType dt, int64_t n);
+int64_t factorize(DType dt, const void* keys, int64_t n, int64_t* ids, void* uniq, void* workspace,
+                  size_t workspace_size, hipStream_t s);
+// per-row 64-bit key hash (accumulate: combine with the hash already in h)
+void key_hash(DType dt, const void* keys, int64_t n, uint64_t* h, bool accumulate, hipStream_t s);
+void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s);
+
 // ------------------------------------------------------------ data movement
 // dst[idx] = src[idx] over `dims`, both operands addressed by element strides
 // (src strides may be 0 or negative; pointers already include the offsets).

@@ -193,13 +193,14 @@ def chunk_rows_for(inputs: List[torch.Tensor], total_rows: Optional[int] = None)
     """Rows per pipelined chunk: at most `chunk_bytes` of the widest input,
     and small enough that a job yields >= `min_pipeline_chunks` chunks (a
     3-stage pipeline only overlaps once it has several chunks in flight),
-    but not below 4 MB per DMA."""
+    but not below 4 MB per DMA (or one row, for rows bigger than that:
+    images)."""
     row_bytes = max((t[0].numel() * t.element_size() if t.shape[0] else 1) for t in inputs) if inputs else 1
     row_bytes = max(row_bytes, 1)
     rows = int(config.chunk_bytes // row_bytes)
     if total_rows:
         rows = min(rows, -(-total_rows // max(1, config.min_pipeline_chunks)))
-    return max(1024, (4 << 20) // row_bytes, rows)
+    return max(1, (4 << 20) // row_bytes, rows)
 
 
 def run_segments_pipelined(prog, segments: List[List[torch.Tensor]],

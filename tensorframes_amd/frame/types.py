@@ -64,6 +64,19 @@ class LongType(NumericType):
         return "bigint"
 
 
+class UByteType(NumericType):
+    """uint8 cells (decoded image pixels). An extension of the reference's
+    four numeric types (its images entered as binary JPEG cells and were
+    decoded to uint8 inside the graph: src/main/python/tensorframes_snippets/read_image.py:42);
+    here a decoded uint8 column can be fed to a graph directly."""
+
+    type_name = "ubyte"
+    tf_dtype = D.DT_UINT8
+
+    def simpleString(self):  # noqa: N802
+        return "ubyte"
+
+
 class BooleanType(DataType):
     type_name = "boolean"
 
@@ -100,7 +113,7 @@ class ArrayType(DataType):
 
 # the scalar types tensors can hold, in the reference's lookup order
 # (reference: src/main/scala/org/tensorframes/impl/datatypes.scala:267)
-SUPPORTED_SCALARS = [DoubleType(), FloatType(), IntegerType(), LongType()]
+SUPPORTED_SCALARS = [DoubleType(), FloatType(), IntegerType(), LongType(), UByteType()]
 
 _BY_TF = {t.tf_dtype: t for t in SUPPORTED_SCALARS}
 _BY_STR = {str(t): t for t in SUPPORTED_SCALARS}
@@ -112,7 +125,7 @@ _BY_STR["bigint"] = LongType()
 def sql_type_for_tf(enum: int) -> NumericType:
     if enum not in _BY_TF:
         raise TypeError(f"TF dtype {D.dtype_name(enum)} has no supported SQL type "
-                        f"(supported: double, float, int32, int64)")
+                        f"(supported: double, float, int32, int64, uint8)")
     return _BY_TF[enum]
 
 
