@@ -304,6 +304,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     k::hash_mod(reinterpret_cast<const uint64_t*>(h.data_ptr<int64_t>()), n, world, dest.data_ptr<int64_t>(), s);
     return dest;
   }, "destination rank of every row: hash(keys) % world (same on every rank)");
+  m.def("group_representatives", [](const at::Tensor& ids, int64_t nseg) {
+    TFA_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.dim() == 1, "group_representatives: device int64 ids");
+    c10::hip::HIPGuard guard(ids.device().index());
+    at::Tensor rep = at::empty({nseg}, ids.options());
+    k::group_representatives(ids.contiguous().data_ptr<int64_t>(), ids.size(0), rep.data_ptr<int64_t>(),
+                             c10::hip::getCurrentHIPStream(ids.device().index()).stream());
+    return rep;
+  }, "one row index per group (device)");
+  m.def("partition_rows", [](const at::Tensor& dest0, int64_t world) {
+    TFA_CHECK(dest0.is_cuda() && dest0.scalar_type() == at::kLong && dest0.dim() == 1, "partition_rows: device int64 dest");
+    c10::hip::HIPGuard guard(dest0.device().index());
+    at::Tensor dest = dest0.contiguous();
+    const int64_t n = dest.size(0);
+    hipStream_t s = c10::hip::getCurrentHIPStream(dest.device().index()).stream();
+    const size_t wsb = k::partition_workspace_bytes(n);
+    at::Tensor ws = at::empty({static_cast<int64_t>(wsb)}, dest.options().dtype(at::kByte));
+    at::Tensor perm = at::empty({n}, dest.options());
+    at::Tensor counts = at::empty({world}, dest.options());
+    k::partition_rows(dest.data_ptr<int64_t>(), n, world, perm.data_ptr<int64_t>(), counts.data_ptr<int64_t>(),
+                      ws.data_ptr(), wsb, s);
+    return py::make_tuple(perm, counts);
+  }, "rows ordered by destination rank (stable) + rows per destination (device)");
+  m.def("gather_rows", [](const at::Tensor& x0, const at::Tensor& idx) {
+    TFA_CHECK(x0.is_cuda() && idx.is_cuda() && idx.scalar_type() == at::kLong, "gather_rows: device tensors");
+    c10::hip::HIPGuard guard(x0.device().index());
+    at::Tensor x = x0.contiguous();
+    auto sizes = x.sizes().vec();
+    sizes[0] = idx.size(0);
+    at::Tensor out = at::empty(sizes, x.options());
+    const int64_t inner = x.size(0) ? x.numel() / x.size(0) : 0;
+    if (out.numel())
+      k::gather(x.element_size(), DType::I64, x.data_ptr(), idx.contiguous().data_ptr(), out.data_ptr(), 1, x.size(0),
+                idx.size(0), inner, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    return out;
+  }, "out[j] = x[idx[j]] along dim 0 (device gather kernel)");
   m.def("jit_compile", [](const std::string& src) { return jit::compile_only(src); },
         "compile a generated kernel with hiprtc for gfx950 (no device needed); returns the code-object size");
   m.def("jit_stats", []() {

@@ -84,6 +84,20 @@ int64_t factorize(DType dt, const void* keys, int64_t n, int64_t* ids, void* uni
 // per-row 64-bit key hash (accumulate: combine with the hash already in h)
 void key_hash(DType dt, const void* keys, int64_t n, uint64_t* h, bool accumulate, hipStream_t s);
 void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s);
+// ids [n] in [0, nseg) -> rows ordered by segment (stable) perm [n] and CSR
+// offsets [nseg + 1]; out-of-range ids are dropped
+size_t segment_csr_workspace_bytes(int64_t n, int64_t nseg);
+void segment_csr(DType idt, const void* ids, int64_t n, int64_t nseg, int64_t* perm, int64_t* offsets,
+                 void* workspace, size_t workspace_size, hipStream_t s);
+// segment g = rows perm[offsets[g] .. offsets[g+1]) of x [*, inner] -> y [nseg, inner] (deterministic)
+void segment_reduce_perm(RedOp op, DType dt, const void* x, const int64_t* perm, const int64_t* offsets, void* y,
+                         int64_t nseg, int64_t inner, hipStream_t s);
+// rep[g] = some row of group g (ids in [0, nseg))
+void group_representatives(const int64_t* ids, int64_t n, int64_t* rep, hipStream_t s);
+// rows ordered by destination (stable): perm [n]; counts [world] rows per destination
+size_t partition_workspace_bytes(int64_t n);
+void partition_rows(const int64_t* dest, int64_t n, int64_t world, int64_t* perm, int64_t* counts, void* workspace,
+                    size_t workspace_size, hipStream_t s);
 
 // ------------------------------------------------------------ data movement
 // dst[idx] = src[idx] over `dims`, both operands addressed by element strides

@@ -532,6 +532,49 @@ __global__ __launch_bounds__(256) void seg_csr(const T* __restrict__ x, const in
   y[sg * inner + col] = finish<OP, T, A>(acc, off[sg + 1] - off[sg]);
 }
 
+// ---- segment reduce over permuted rows: segment g = rows perm[off[g] .. off[g+1]),
+// one wave per segment; for inner <= 64 the wave reads 64/inner_pad rows at
+// once (lane = row slot x column) and folds them with a fixed xor tree
+// (deterministic); wider rows loop over 64-column chunks
+// TF: an empty segment of a Min/Max gets the type's highest / lowest value
+template <typename T, int OP, typename A>
+__device__ __forceinline__ T seg_empty_or(A acc, int64_t count) {
+  if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
+    if (count == 0) {
+      if constexpr (std::is_floating_point<T>::value)
+        return OP == (int)RedOp::MAX ? -std::numeric_limits<T>::max() : std::numeric_limits<T>::max();
+      else
+        return OP == (int)RedOp::MAX ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
+    }
+  }
+  return finish<OP, T, A>(acc, count);
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void seg_perm(const T* __restrict__ x, const int64_t* __restrict__ perm,
+                                                const int64_t* __restrict__ off, T* __restrict__ y, int64_t nseg,
+                                                int64_t inner, int inner_pad) {
+  using A = typename AccT<T>::type;
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nseg) return;  // the whole wave leaves together
+  const int64_t b = off[g], e = off[g + 1];
+  if (inner <= 64) {
+    const int c = lane % inner_pad, rs = lane / inner_pad, R = 64 / inner_pad;
+    A acc = ident<OP, A>();
+    if (c < inner)
+      for (int64_t j = b + rs; j < e; j += R) acc = combine<OP, A>(acc, A(x[perm[j] * inner + c]));
+    for (int s = 32; s >= inner_pad; s >>= 1) acc = combine<OP, A>(acc, __shfl_xor(acc, s, 64));
+    if (rs == 0 && c < inner) y[g * inner + c] = seg_empty_or<T, OP, A>(acc, e - b);
+  } else {
+    for (int64_t c = lane; c < inner; c += 64) {
+      A acc = ident<OP, A>();
+      for (int64_t j = b; j < e; ++j) acc = combine<OP, A>(acc, A(x[perm[j] * inner + c]));
+      y[g * inner + c] = seg_empty_or<T, OP, A>(acc, e - b);
+    }
+  }
+}
+
 constexpr int64_t kUsegTile = 256;
 constexpr int64_t kUsegLds = 64 * 1024;
 
@@ -625,8 +668,49 @@ void topk(DType dt, const void* x, void* vals, int32_t* idx, int64_t rows, int64
   TFA_LAUNCH_CHECK("topk");
 }
 
+// many segments (the LDS-private histograms do not fit): rows are ordered by
+// segment with one radix sort (groupby.hip) and reduced per segment
+static bool useg_fits_lds(int64_t inner, int64_t nseg) {
+  return static_cast<size_t>(nseg * useg_tile(inner) * 8) <= static_cast<size_t>(kUsegLds);
+}
+
+static size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
+
 size_t unsorted_segment_workspace_bytes(RedOp, DType, int64_t n, int64_t inner, int64_t nseg) {
-  return static_cast<size_t>(useg_blocks(n)) * nseg * inner * 8;
+  if (useg_fits_lds(inner, nseg)) return static_cast<size_t>(useg_blocks(n)) * nseg * inner * 8;
+  return align256(n * 8) + align256((nseg + 1) * 8) + segment_csr_workspace_bytes(n, nseg);
+}
+
+template <typename T>
+static void seg_perm_op(RedOp op, const void* x, const int64_t* perm, const int64_t* off, void* y, int64_t nseg,
+                        int64_t inner, hipStream_t s) {
+  int inner_pad = 1;
+  while (inner_pad < inner && inner_pad < 64) inner_pad <<= 1;
+  dim3 grid((unsigned)((nseg + 3) / 4));
+  switch (op) {
+#define TFA_SP(OPV) hipLaunchKernelGGL((seg_perm<T, (int)OPV>), grid, dim3(256), 0, s, (const T*)x, perm, off, (T*)y, nseg, inner, inner_pad); break;
+    case RedOp::SUM: TFA_SP(RedOp::SUM)
+    case RedOp::PROD: TFA_SP(RedOp::PROD)
+    case RedOp::MIN: TFA_SP(RedOp::MIN)
+    case RedOp::MAX: TFA_SP(RedOp::MAX)
+    case RedOp::MEAN: TFA_SP(RedOp::MEAN)
+#undef TFA_SP
+    default: TFA_CHECK(false, "segment reduce: unsupported op");
+  }
+}
+
+void segment_reduce_perm(RedOp op, DType dt, const void* x, const int64_t* perm, const int64_t* offsets, void* y,
+                         int64_t nseg, int64_t inner, hipStream_t s) {
+  if (nseg * inner <= 0) return;
+  TFA_CHECK((nseg + 3) / 4 <= 0x7fffffff, "segment reduce: too many segments");
+  switch (dt) {
+    case DType::F32: seg_perm_op<float>(op, x, perm, offsets, y, nseg, inner, s); break;
+    case DType::F64: seg_perm_op<double>(op, x, perm, offsets, y, nseg, inner, s); break;
+    case DType::I32: seg_perm_op<int32_t>(op, x, perm, offsets, y, nseg, inner, s); break;
+    case DType::I64: seg_perm_op<int64_t>(op, x, perm, offsets, y, nseg, inner, s); break;
+    default: TFA_CHECK(false, "segment reduce: dtype not supported");
+  }
+  TFA_LAUNCH_CHECK("segment_reduce_perm");
 }
 
 template <typename T, typename I, int OP>
@@ -668,6 +752,15 @@ void unsorted_segment_reduce(RedOp op, DType dt, DType idt, const void* x, const
   }
   TFA_CHECK(workspace != nullptr, "unsorted segment reduce: missing workspace");
   TFA_CHECK(idt == DType::I32 || idt == DType::I64, "segment ids must be int32/int64");
+  if (!useg_fits_lds(inner, nseg)) {
+    char* p = static_cast<char*>(workspace);
+    int64_t* perm = reinterpret_cast<int64_t*>(p);
+    int64_t* off = reinterpret_cast<int64_t*>(p + align256(n * 8));
+    void* rest = p + align256(n * 8) + align256((nseg + 1) * 8);
+    segment_csr(idt, ids, n, nseg, perm, off, rest, segment_csr_workspace_bytes(n, nseg), s);
+    segment_reduce_perm(op, dt, x, perm, off, y, nseg, inner, s);
+    return;
+  }
   bool i64 = idt == DType::I64;
   switch (dt) {
     case DType::F32: i64 ? useg_op<float, int64_t>(op, x, ids, y, n, inner, nseg, workspace, s) : useg_op<float, int32_t>(op, x, ids, y, n, inner, nseg, workspace, s); break;

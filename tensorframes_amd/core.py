@@ -752,6 +752,29 @@ class _RowVectorizer:
                 _LIFT_CACHE.pop(next(iter(_LIFT_CACHE)))
         return self._progs[key]
 
+    def program_for(self, cell_shapes: tuple):
+        """Lifted program for exactly these cell shapes (the lifting may bake
+        cell sizes into reshapes, e.g. of a MatMul): keyed by the shapes."""
+        key = ("shapes",) + tuple(tuple(s) for s in cell_shapes)
+        gkey = (engine._key(self.graph_bytes), tuple(self.fetch_refs), tuple(self.feed_names), key)
+        if gkey in _LIFT_CACHE:
+            return _LIFT_CACHE[gkey][1]
+        from .graph import vectorize
+        g = engine.native_graph(self.graph_bytes)
+        hints = {n: (dt, list(s)) for n, dt, s in zip(self.feed_names, self.feed_dtypes, cell_shapes)}
+        try:
+            infos = _C.infer_fed(g, self.fetch_refs, self.feed_names, hints)
+            light = P.parse_graphdef(_C.light_graphdef(self.graph_bytes, 4096))
+            patch = vectorize.lift(light, self.fetch_refs, self.feed_names, infos, patch_only=True)
+        except ValueError:
+            patch = None
+        prog = None
+        if patch is not None:
+            prog = engine.program(_C.patch_graphdef(self.graph_bytes, P.serialize_graphdef(patch)),
+                                  self.fetch_refs, self.feed_names)
+        _LIFT_CACHE[gkey] = (None, prog)
+        return prog
+
     def _run_block(self, prog, cell_shapes: tuple, ins: List[torch.Tensor]) -> List[torch.Tensor]:
         if all(t.is_cuda for t in ins):
             return engine.run_program(prog, ins, ins[0].device)
@@ -891,6 +914,8 @@ def _rows_device(cell_views) -> torch.device:
     if cell_views and len(cell_views[0]) and cell_views[0][0].is_cuda:
         return cell_views[0][0].device
     biggest = max((cv[0].numel() for cv in cell_views if len(cv)), default=0)
+    if config.device == "cuda":
+        return engine.compute_device()
     return engine.compute_device() if biggest >= config.map_rows_gpu_min_elems else torch.device("cpu")
 
 
@@ -1252,21 +1277,21 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     if partials_rows:
         acc = partials_rows[0]
         for r in partials_rows[1:]:
-            acc = engine.run_program(prog, list(acc) + list(r), torch.device("cpu"))
+            acc = engine.run_program(prog, list(acc) + list(r), engine.small_work_device())
         local = dict(zip(names, acc))
     static = {n: None for n in names}  # generic pair graphs: shapes agreed at run time
     allp = _gather_rank_values(local, static, {n: summary[n].tf_dtype for n in names})
     _check(all(allp[n] for n in names), "Cannot reduce an empty DataFrame")
-    acc = [allp[n][0].cpu() for n in names]
+    acc = [allp[n][0] for n in names]
     for r in range(1, len(allp[names[0]])):
-        acc = engine.run_program(prog, acc + [allp[n][r].cpu() for n in names], torch.device("cpu"))
+        acc = engine.run_program(prog, acc + [allp[n][r] for n in names], engine.small_work_device())
     return _unpack({n: a.cpu().numpy() for n, a in zip(names, acc)}, spec, summary)
 
 
 def _fold_rows(prog, names, cells_per_col) -> List[torch.Tensor]:
     n = len(cells_per_col[0])
     acc = [cv[0] for cv in cells_per_col]
-    dev = torch.device("cpu")
+    dev = engine.small_work_device()
     for i in range(1, n):
         acc = engine.run_program(prog, list(acc) + [cv[i] for cv in cells_per_col], dev)
     return acc
@@ -1406,8 +1431,65 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
 
     def combine(blocks):
         """Monoid graphs: map-side combine. Each partition is reduced per key on
-        its own device (unsorted segmented reduction), only the per-key partials
-        (one row per key and partition) are shuffled, then reduced again."""
+        its own device (keys factorised by the groupBy kernels, values by the
+        unsorted segmented reduction), only the per-key partials cross ranks
+        (hash-routed all-to-all over RCCL), and are reduced again per key."""
+        from .ops import groupby as G
+        # decided from the schema, so every rank takes the same (collective) path
+        if not numeric_keys:
+            return combine_host(blocks)
+        dev = engine.compute_device()
+        on_device = any(b.columns[n].is_cuda for b in blocks.values() if b.nrows for n in out_names) or \
+            dev.type == "cuda"
+        kparts: List[List[torch.Tensor]] = []
+        vparts: Dict[str, List[torch.Tensor]] = {n: [] for n in out_names}
+        for pid, b in sorted(blocks.items()):
+            if b.nrows == 0:
+                continue
+            ids, uniq, ng = G.group_ids([b.columns[k].to(dev) for k in keys])
+            kparts.append(uniq)
+            for n in out_names:
+                vparts[n].append(_C.unsorted_segment_reduce(monoid[n], b.columns[n].to(dev).contiguous(), ids, ng))
+        kdt = [D.torch_dtype(tf_types[k]) for k in keys]
+        if kparts:
+            K = [torch.cat([p[i] for p in kparts]) if len(kparts) > 1 else kparts[0][i] for i in range(len(keys))]
+            V = {n: torch.cat(vparts[n]) if len(vparts[n]) > 1 else vparts[n][0] for n in out_names}
+        else:
+            K = [torch.empty(0, dtype=t, device=dev) for t in kdt]
+            V = {n: None for n in out_names}
+        if dist.is_distributed():
+            cells = _agree_shapes({n: (V[n][0] if V[n] is not None and V[n].shape[0] else None) for n in out_names},
+                                  {n: agg_static.get(n) for n in out_names}, dev) if any(
+                agg_static.get(n) is None for n in out_names) or any(V[n] is None for n in out_names) else \
+                {n: tuple(V[n].shape[1:]) for n in out_names}
+            for n in out_names:
+                if V[n] is None:
+                    V[n] = torch.empty((0,) + tuple(cells[n]), dtype=D.torch_dtype(summary[n].tf_dtype), device=dev)
+            recv = G.route(K, [V[n] for n in out_names])
+            K, V = recv[:len(keys)], dict(zip(out_names, recv[len(keys):]))
+        if K[0].shape[0] == 0:
+            return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, dist.world_size()))}
+        ids, uniq, ng = G.group_ids(K)
+        out_cols: Dict[str, Any] = dict(zip(keys, uniq))
+        for n in out_names:
+            out_cols[n] = _C.unsorted_segment_reduce(monoid[n], V[n].contiguous(), ids, ng)
+        if not on_device or not keep_on_device:
+            out_cols = {k: v.cpu() for k, v in out_cols.items()}
+        metrics.add("aggregate_device_groupby" if dev.type == "cuda" else "aggregate_host_groupby")
+        return {dist.rank(): Block(ng, out_cols)}
+
+    numeric_keys = all(tf_types[k] in (D.DT_FLOAT, D.DT_DOUBLE, D.DT_INT32, D.DT_INT64) and
+                       (ColumnInformation(df.schema[k]).stf is not None and
+                        ColumnInformation(df.schema[k]).stf.shape.num_dims == 1) for k in keys)
+    # static cell shapes of the reduced columns (from the schema), for ranks without rows
+    agg_static = {}
+    for n in out_names:
+        cell = _col_info(df.schema[n]).shape.tail()
+        agg_static[n] = None if cell.has_unknown() else tuple(cell.dims)
+    keep_on_device = any(b.columns[n].is_cuda for b in (df._cached or {}).values() if b.nrows for n in out_names)
+
+    def combine_host(blocks):
+        """String / non-scalar keys: keys dictionary-encoded on the host."""
         w = dist.world_size()
         send = [[] for _ in range(w)]
         for pid, b in sorted(blocks.items()):
@@ -1451,6 +1533,9 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             out_cols[n] = _C.unsorted_segment_reduce(monoid[n], x, ids.to(x.device), ng).cpu()
         return {dist.rank(): Block(ng, out_cols)}
 
+    lifter = _RowVectorizer(spec.graph_bytes, [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names],
+                            in_names, [summary[n].tf_dtype for n in out_names])
+
     def compute(blocks):
         if uniform and all(is_dense(b.columns[n]) for b in blocks.values() for n in out_names):
             return combine(blocks)
@@ -1484,13 +1569,40 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         out_cols: Dict[str, Any] = {}
         for i, k in enumerate(keys):
             out_cols[k] = build_column([u[i] for u in uniq], _tf_of_field(df.schema[k]))
-        per = {n: [] for n in out_names}
-        for g in range(len(uniq)):
-            seg = sorted_blk.slice(int(offsets[g]), int(offsets[g + 1]))
-            ins = _dense_inputs(seg, out_names, "aggregate")
-            outs = engine.run_program(prog, ins)
-            for n, o in zip(out_names, outs):
-                per[n].append(o.cpu())
+        per: Dict[str, List[Optional[torch.Tensor]]] = {n: [None] * ngroups for n in out_names}
+        # groups of equal size run together: the reducer graph lifted over a new
+        # leading group axis ([G, size, ...] -> [G, ...], graph/vectorize.py)
+        # is evaluated once per size; graphs that cannot be lifted, and sizes
+        # that occur once, run group by group
+        by_size: Dict[int, List[int]] = {}
+        for g in range(ngroups):
+            by_size.setdefault(int(counts[g]), []).append(g)
+        vals = _dense_inputs(sorted_blk, out_names, "aggregate")
+        dev = engine.compute_device()
+        batched = 0
+        for size, gl in sorted(by_size.items()):
+            lifted = None
+            if len(gl) >= 2 and size > 0:
+                lifted = lifter.program_for(tuple((size,) + tuple(v.shape[1:]) for v in vals))
+            if lifted is not None:
+                rows = np.concatenate([np.arange(offsets[g], offsets[g + 1]) for g in gl])
+                ridx = torch.from_numpy(rows)
+                ins = [v[ridx].reshape((len(gl), size) + tuple(v.shape[1:])) for v in vals]
+                outs = engine.run_program(lifted, ins, dev)
+                if all(o.dim() >= 1 and o.shape[0] == len(gl) for o in outs):
+                    for n, o in zip(out_names, outs):
+                        o = o.cpu()
+                        for j, g in enumerate(gl):
+                            per[n][g] = o[j]
+                    batched += len(gl)
+                    continue
+            for g in gl:
+                seg = sorted_blk.slice(int(offsets[g]), int(offsets[g + 1]))
+                outs = engine.run_program(prog, _dense_inputs(seg, out_names, "aggregate"))
+                for n, o in zip(out_names, outs):
+                    per[n][g] = o.cpu()
+        metrics.add("aggregate_batched_groups", batched)
+        metrics.add("aggregate_single_groups", ngroups - batched)
         for n in out_names:
             out_cols[n] = torch.stack(per[n], 0)
         return {dist.rank(): Block(len(uniq), out_cols)}

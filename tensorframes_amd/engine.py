@@ -109,6 +109,15 @@ def compute_device() -> torch.device:
     return torch.device("cpu")
 
 
+def small_work_device() -> torch.device:
+    """Where tiny host work (per-row folds, small map_rows cells) runs: the
+    host executor, unless `Config.device == "cuda"` forces every op onto the
+    GPU (e.g. the GPU run of the acceptance corpus)."""
+    if config.device == "cuda":
+        return compute_device()
+    return torch.device("cpu")
+
+
 def to_device(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
     if t.device == dev:
         return t

@@ -198,21 +198,37 @@ class DataFrame:
         return self._blocks()
 
     # -- actions
-    def _local_rows(self) -> List[tuple]:
-        out = []
+    @staticmethod
+    def _column_payload(col, a: int = 0, b: Optional[int] = None):
+        """A column slice in a cheap-to-pickle form: dense columns as one numpy
+        array (a buffer, not one object per cell), others as value lists."""
+        if is_dense(col):
+            t = col[a:b]
+            return t.detach().cpu().numpy()
+        return column_values(col)[a:b]
+
+    def _rows_of(self, nrows: int, payload: Dict[str, Any]) -> List[Row]:
         names = self._schema.names
+        if not names:
+            return [Row.from_fields([], []) for _ in range(nrows)]
+        cols = []
+        for n in names:
+            v = payload[n]
+            cols.append(column_values(torch.from_numpy(np.ascontiguousarray(v))) if isinstance(v, np.ndarray) else v)
+        return [Row.from_fields(names, vals) for vals in zip(*cols)]
+
+    def _local_columns(self) -> List[tuple]:
+        out = []
         for pid, b in self._iter_blocks():  # evaluated once, partition by partition
-            cols = [column_values(b.columns[n]) for n in names]
-            out.append((pid, [Row.from_fields(names, vals) for vals in zip(*cols)] if cols else
-                        [Row.from_fields([], []) for _ in range(b.nrows)]))
+            out.append((pid, b.nrows, {n: self._column_payload(b.columns[n]) for n in self._schema.names}))
         return out
 
     def collect(self) -> List[Row]:
-        parts = []
-        for chunk in dist.all_gather_object(self._local_rows()):
-            parts.extend(chunk)
+        """All rows, in partition order. Ranks exchange column payloads (dense
+        columns as arrays), and every rank builds the Row objects once."""
+        parts = [x for chunk in dist.all_gather_object(self._local_columns()) for x in chunk]
         parts.sort(key=lambda x: x[0])
-        return [r for _, rows in parts for r in rows]
+        return [r for _, nrows, payload in parts for r in self._rows_of(nrows, payload)]
 
     def count(self) -> int:
         n = sum(b.nrows for _, b in self._iter_blocks())
@@ -225,7 +241,42 @@ class DataFrame:
     head = first
 
     def take(self, n: int) -> List[Row]:
-        return self.collect()[:n]
+        """The first n rows in partition order. Partitions are evaluated in
+        order and evaluation stops once n rows are in hand (later partitions
+        are never computed); across ranks, each partition's owner sends only
+        the rows still needed."""
+        if n <= 0:
+            return []
+        out: List[Row] = []
+        local = iter(self._iter_blocks())
+        buffered: Dict[int, Block] = {}
+
+        def local_block(p: int) -> Optional[Block]:
+            while p not in buffered:
+                try:
+                    pid, b = next(local)
+                except StopIteration:
+                    return None
+                buffered[pid] = b
+            return buffered.pop(p)
+
+        w = dist.world_size()
+        for p in range(self._nparts):
+            need = n - len(out)
+            owner = p % w if dist.is_distributed() else 0
+            payload = None
+            if owner == dist.rank():
+                b = local_block(p)
+                if b is not None and b.nrows:
+                    k = min(need, b.nrows)
+                    payload = (k, {c: self._column_payload(b.columns[c], 0, k) for c in self._schema.names})
+            if dist.is_distributed():
+                payload = dist.broadcast_object(payload, src=owner)
+            if payload is not None:
+                out.extend(self._rows_of(*payload))
+            if len(out) >= n:
+                break
+        return out[:n]
 
     def show(self, n: int = 20):
         rows = self.take(n)

@@ -1,0 +1,87 @@
+"""groupBy segmentation and the keyed shuffle, on the device.
+
+Keys of a block are factorised where they live: on a GPU by the radix-sort
+kernels of csrc/kernels/groupby.hip (`_C.factorize`), on the host by the ATen
+oracle. Groups come out in ascending key order (lexicographic for several
+key columns), the order the reference's Spark groupBy results are compared in
+(reference: src/test/scala/org/tensorframes/BasicOperationsSuite.scala:200-210
+via compareRows). String keys are dictionary-encoded on the host once.
+
+The cross-rank shuffle of per-key partials hashes the keys on the device
+(`_C.key_dest`: the same 64-bit hash on every rank), orders the rows by
+destination with one radix sort (`_C.partition_rows`), gathers every column
+in that order (`_C.gather_rows`) and exchanges them with one all-to-all per
+column (RCCL for device tensors). Reference counterpart: the UDAF shuffle
+(src/main/scala/org/tensorframes/impl/DebugRowOps.scala:573-576).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .._native import _C
+from ..parallel import dist
+
+_KEY_DTYPES = (torch.float32, torch.float64, torch.int32, torch.int64)
+
+
+def device_keys(cols: Sequence) -> bool:
+    """All key columns are dense 1-D numeric tensors the kernels can factorise."""
+    return all(isinstance(c, torch.Tensor) and c.dim() == 1 and c.dtype in _KEY_DTYPES for c in cols)
+
+
+def group_ids(keys: List[torch.Tensor]) -> Tuple[torch.Tensor, List[torch.Tensor], int]:
+    """(group id of every row [n] int64, distinct key columns [ngroups], ngroups).
+
+    One key: a single factorisation. Several keys: each column is factorised,
+    the codes are combined lexicographically (code * n_next + id_next) and
+    re-factorised after every column, so codes stay below n and the group
+    order stays lexicographic; the key values of each group are read from one
+    representative row."""
+    n = keys[0].shape[0]
+    if n == 0:
+        return (torch.empty(0, dtype=torch.int64, device=keys[0].device),
+                [k[:0] for k in keys], 0)
+    if len(keys) == 1:
+        ids, uniq = _C.factorize(keys[0])
+        return ids, [uniq], int(uniq.shape[0])
+    code, _ = _C.factorize(keys[0])
+    for k in keys[1:]:
+        ids_k, uniq_k = _C.factorize(k)
+        code, _ = _C.factorize(code * int(uniq_k.shape[0]) + ids_k)
+    ids, ucode = _C.factorize(code)
+    ng = int(ucode.shape[0])
+    if ids.is_cuda:
+        rep = _C.group_representatives(ids, ng)
+        uniq = [_C.gather_rows(k.contiguous(), rep) for k in keys]
+    else:
+        rep = torch.empty(ng, dtype=torch.int64)
+        rep[ids] = torch.arange(n, dtype=torch.int64)
+        uniq = [k[rep] for k in keys]
+    return ids, uniq, ng
+
+
+def route(keys: List[torch.Tensor], cols: List[torch.Tensor]) -> List[torch.Tensor]:
+    """Keyed all-to-all: rows go to rank hash(keys) % world; returns the
+    received columns (keys first, then `cols`), concatenated in source-rank
+    order. Device columns: hash, partition and gather on the GPU, exchange
+    over RCCL; every rank takes part even with no rows."""
+    w = dist.world_size()
+    allc = list(keys) + list(cols)
+    dev = allc[0].device
+    n = allc[0].shape[0]
+    if dev.type == "cuda":
+        dest = _C.key_dest([k.contiguous() for k in keys], w) if n else torch.empty(0, dtype=torch.int64, device=dev)
+        perm, counts = _C.partition_rows(dest, w)
+        send_rows = [int(c) for c in counts.cpu().tolist()]
+        ordered = [_C.gather_rows(c.contiguous(), perm) if n else c for c in allc]
+    else:
+        from ..core import _key_hash
+        dest = (_key_hash([k.numpy() for k in keys]) % np.uint64(w)).astype(np.int64) if n else np.zeros(0, np.int64)
+        perm = torch.from_numpy(np.argsort(dest, kind="stable"))
+        send_rows = np.bincount(dest, minlength=w).tolist()
+        ordered = [c[perm] for c in allc]
+    recv_rows = dist.all_to_all_counts(send_rows)
+    return [dist.all_to_all_rows(c, send_rows, recv_rows) for c in ordered]

@@ -327,6 +327,23 @@ def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torc
     return out
 
 
+def all_to_all_rows(x: torch.Tensor, send_rows: List[int], recv_rows: List[int]) -> torch.Tensor:
+    """Rows of x, already ordered by destination (send_rows[r] rows for rank
+    r), exchanged in one all_to_all (no concatenation copy); returns the
+    received rows in source-rank order."""
+    if not is_distributed():
+        return x
+    _ensure_groups()
+    x = x.contiguous()
+    if x.is_cuda and not gpu_collectives():
+        return all_to_all_rows(x.cpu(), send_rows, recv_rows).to(x.device)
+    group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
+    out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    with _traced("all_to_all", _nbytes(x), x.device):
+        dist.all_to_all_single(out, x, [int(r) for r in recv_rows], [int(c) for c in send_rows], group=group)
+    return out
+
+
 # -- tensor collectives: device tensors over RCCL, host tensors over gloo
 _OPS = {"Sum": dist.ReduceOp.SUM, "Min": dist.ReduceOp.MIN, "Max": dist.ReduceOp.MAX,
         "Prod": dist.ReduceOp.PRODUCT}

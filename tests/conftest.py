@@ -23,3 +23,18 @@ def _fresh_default_graph():
 def gpu_available():
     import torch
     return torch.cuda.is_available()
+
+
+@pytest.fixture(params=["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def on_device(request):
+    """Runs a test once on the host executor and once (gpu-marked) with every
+    op forced onto the GPU (`Config.device = "cuda"`): the reference's
+    acceptance corpus then executes the HIP kernels."""
+    import torch
+    from tensorframes_amd.config import config
+    if request.param == "cuda" and not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    old = config.device
+    config.device = request.param
+    yield request.param
+    config.device = old

@@ -5,6 +5,11 @@ TensorFlow import replaced by `tensorframes_amd.tf` and Spark by our frame.
 import tensorframes_amd as tfs
 from tensorframes_amd import Row, tf
 
+import pytest as _pytest
+
+# every test runs on the host executor and, gpu-marked, on the GPU (conftest.on_device)
+pytestmark = _pytest.mark.usefixtures("on_device")
+
 
 def test_schema(capsys):
     data = [Row(x=float(x)) for x in range(100)]

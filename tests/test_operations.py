@@ -8,6 +8,11 @@ import tensorframes_amd as tfs
 from tensorframes_amd import Row, tf
 from tensorframes_amd.frame.types import IntegerType, StringType, StructField, StructType, DoubleType
 
+import pytest as _pytest
+
+# every test runs on the host executor and, gpu-marked, on the GPU (conftest.on_device)
+pytestmark = _pytest.mark.usefixtures("on_device")
+
 
 def make1(xs, col="x", num_partitions=1):
     return tfs.create_dataframe([(x,) for x in xs], [col], num_partitions=num_partitions)

@@ -9,6 +9,11 @@ from tensorframes_amd import tf
 from tensorframes_amd.frame.types import (ArrayType, DoubleType, FloatType, IntegerType, LongType,
                                           StringType, StructField, StructType)
 
+import pytest as _pytest
+
+# every test runs on the host executor and, gpu-marked, on the GPU (conftest.on_device)
+pytestmark = _pytest.mark.usefixtures("on_device")
+
 TYPES = [
     (IntegerType(), tf.int32, int),
     (LongType(), tf.int64, int),
