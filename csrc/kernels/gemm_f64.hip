@@ -30,64 +30,118 @@ __device__ __forceinline__ T act_apply(T v, int act) {
   return v;
 }
 
-constexpr int D_BM = 64, D_BN = 64, D_BK = 16, D_PAD = 2;
-constexpr int D_LDS = D_BM + D_PAD;
+constexpr int D_BK = 16, D_PAD = 2;
 
-template <bool TA, bool TB>
+// Block tile BM x BN (64x64 or 128x128), 4 waves as 2x2, each wave owning
+// (BM/2)x(BN/2) as TMxTN 16x16 MFMA tiles. Interior blocks load 2 doubles per
+// 16-byte access without bounds checks; edge blocks take the checked path.
+template <int BM, int BN, int WM, int WN, bool TA, bool TB>
 __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) double As[2][D_BK][D_LDS];
-  __shared__ __attribute__((aligned(16))) double Bs[2][D_BK][D_LDS];
+  constexpr int LDA = BM + D_PAD, LDB = BN + D_PAD;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves, >= one 16x16 tile each");
+  constexpr int AE = BM * D_BK / 256, BE = BN * D_BK / 256;  // doubles per thread per K tile
+  static_assert(AE % 2 == 0 && (BE % 2 == 0 || BE == 1), "pairs of doubles (or one B element)");
+  __shared__ __attribute__((aligned(16))) double As[2][D_BK][LDA];
+  __shared__ __attribute__((aligned(16))) double Bs[2][D_BK][LDB];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int nwg = tiles_m * tiles_n;
   const int wg = xcd_remap64(blockIdx.x, nwg);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * D_BM;
-  const int64_t n0 = (int64_t)(wg % tiles_n) * D_BN;
+  const int64_t m0 = (int64_t)(wg / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * BN;
   const int64_t bz = blockIdx.z;
   const double* A = static_cast<const double*>(g.A) + bz * g.strideA;
   const double* B = static_cast<const double*>(g.B) + bz * g.strideB;
   double* C = static_cast<double*>(g.C) + bz * g.strideC;
   const int64_t M = g.M, N = g.N, K = g.K;
+  // A and B take the unchecked 16-byte path independently (a skinny N edge
+  // tile still streams A unchecked)
+  const bool a_rows = m0 + BM <= M && (reinterpret_cast<uintptr_t>(A) & 15) == 0 && g.lda % 2 == 0;
+  const bool b_cols = n0 + BN <= N && (reinterpret_cast<uintptr_t>(B) & 15) == 0 && g.ldb % 2 == 0;
 
-  // each thread moves 4 doubles of A and 4 of B per K tile
-  double ra[4], rb[4];
+  // element e (pairs e, e+1 are adjacent along the contiguous dim) of this
+  // thread's share: A [M][K] -> (row, k) with k contiguous; A^T [K][M] -> (k, m)
+  double ra[AE], rb[BE];
+  auto a_coord = [&](int e, int& r, int& c) {  // r = m, c = k (tile-local)
+    const int idx = tid * AE + e;
+    if (!TA) { r = idx / D_BK; c = idx % D_BK; }
+    else { c = idx / BM; r = idx % BM; }
+  };
+  auto b_coord = [&](int e, int& r, int& c) {  // r = k, c = n
+    const int idx = tid * BE + e;
+    if (!TB) { r = idx / BN; c = idx % BN; }
+    else { c = idx / D_BK; r = idx % D_BK; }
+  };
   auto load = [&](int64_t k0) {
+    const bool kfull = k0 + D_BK <= K;  // only the K tail tile is checked
+    const bool a_fast = a_rows && kfull, b_fast = b_cols && kfull;
+    if (a_fast) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int idx = tid + 256 * p;  // 0..1023
-      if (!TA) {  // A [M][K]: idx -> (row = idx>>4, k = idx&15)
-        const int64_t gm = m0 + (idx >> 4), gk = k0 + (idx & 15);
-        ra[p] = (gm < M && gk < K) ? A[gm * g.lda + gk] : 0.0;
-      } else {  // A [K][M]: idx -> (k = idx>>6, m = idx&63)
-        const int64_t gk = k0 + (idx >> 6), gm = m0 + (idx & 63);
-        ra[p] = (gm < M && gk < K) ? A[gk * g.lda + gm] : 0.0;
+      for (int e = 0; e < AE; e += 2) {
+        int r, c;
+        a_coord(e, r, c);
+        const double* p = !TA ? A + (m0 + r) * g.lda + (k0 + c) : A + (k0 + c) * g.lda + (m0 + r);
+        const double2 v = *reinterpret_cast<const double2*>(p);
+        ra[e] = v.x;
+        ra[e + 1] = v.y;
       }
-      if (!TB) {  // B [K][N]
-        const int64_t gk = k0 + (idx >> 6), gn = n0 + (idx & 63);
-        rb[p] = (gn < N && gk < K) ? B[gk * g.ldb + gn] : 0.0;
-      } else {  // B [N][K]
-        const int64_t gn = n0 + (idx >> 4), gk = k0 + (idx & 15);
-        rb[p] = (gn < N && gk < K) ? B[gn * g.ldb + gk] : 0.0;
+    } else {
+#pragma unroll
+      for (int e = 0; e < AE; ++e) {
+        int r, c;
+        a_coord(e, r, c);
+        const int64_t gm = m0 + r, gk = k0 + c;
+        ra[e] = (gm < M && gk < K) ? (!TA ? A[gm * g.lda + gk] : A[gk * g.lda + gm]) : 0.0;
+      }
+    }
+    if (b_fast) {
+      if constexpr (BE == 1) {
+        int r, c;
+        b_coord(0, r, c);
+        rb[0] = !TB ? B[(k0 + r) * g.ldb + (n0 + c)] : B[(n0 + c) * g.ldb + (k0 + r)];
+      } else {
+#pragma unroll
+        for (int e = 0; e < BE; e += 2) {
+          int r, c;
+          b_coord(e, r, c);
+          const double* p = !TB ? B + (k0 + r) * g.ldb + (n0 + c) : B + (n0 + c) * g.ldb + (k0 + r);
+          const double2 v = *reinterpret_cast<const double2*>(p);
+          rb[e] = v.x;
+          rb[e + 1] = v.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < BE; ++e) {
+        int r, c;
+        b_coord(e, r, c);
+        const int64_t gk = k0 + r, gn = n0 + c;
+        rb[e] = (gn < N && gk < K) ? (!TB ? B[gk * g.ldb + gn] : B[gn * g.ldb + gk]) : 0.0;
       }
     }
   };
   auto store = [&](int st) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int idx = tid + 256 * p;
-      if (!TA) As[st][idx & 15][idx >> 4] = ra[p];
-      else As[st][idx >> 6][idx & 63] = ra[p];
-      if (!TB) Bs[st][idx >> 6][idx & 63] = rb[p];
-      else Bs[st][idx & 15][idx >> 4] = rb[p];
+    for (int e = 0; e < AE; ++e) {
+      int r, c;
+      a_coord(e, r, c);
+      As[st][c][r] = ra[e];
+    }
+#pragma unroll
+    for (int e = 0; e < BE; ++e) {
+      int r, c;
+      b_coord(e, r, c);
+      Bs[st][r][c] = rb[e];
     }
   };
 
-  f64x4 acc[2][2];
+  f64x4 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
 
   const int64_t ktiles = (K + D_BK - 1) / D_BK;
   load(0);
@@ -100,14 +154,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
 #pragma unroll
     for (int kk = 0; kk < D_BK; kk += 4) {
       const int kr = kk + (lane >> 4);
-      double a0 = As[cur][kr][wm * 32 + (lane & 15)];
-      double a1 = As[cur][kr][wm * 32 + 16 + (lane & 15)];
-      double b0 = Bs[cur][kr][wn * 32 + (lane & 15)];
-      double b1 = Bs[cur][kr][wn * 32 + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      double a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[cur][kr][wm * (BM / WM) + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = Bs[cur][kr][wn * (BN / WN) + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     if (has_next) store(cur ^ 1);
     __syncthreads();
@@ -116,14 +171,14 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
   // f64 C/D layout: col = lane&15, row = (lane>>4) + 4*r
   const double* bias = static_cast<const double*>(g.bias);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t col = n0 + wn * 32 + j * 16 + (lane & 15);
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
     const double bv = (bias && col < N) ? bias[col] : 0.0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
+        const int64_t row = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) + 4 * r;
         if (row < M && col < N) C[row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
       }
     }
@@ -218,15 +273,27 @@ void pool2d_launch(const PoolArgs& a, hipStream_t s) {
 
 }  // namespace
 
-void gemm_f64_launch(const GemmArgs& g, hipStream_t s) {
-  const int64_t tm = (g.M + D_BM - 1) / D_BM, tn = (g.N + D_BN - 1) / D_BN;
+template <int BM, int BN, int WM, int WN>
+static void gemm_f64_tile_launch(const GemmArgs& g, hipStream_t s) {
+  const int64_t tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
   TFA_CHECK(g.batch <= 65535, "gemm: batch too large");
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)g.batch);
-  if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<false, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
-  else if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_f64_mfma<false, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
-  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<true, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
-  else hipLaunchKernelGGL((gemm_f64_mfma<true, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+  if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+  else if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_f64_mfma<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_f64_mfma<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+  else hipLaunchKernelGGL((gemm_f64_mfma<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, s, g, (int)tm, (int)tn);
+}
+
+void gemm_f64_launch(const GemmArgs& g, hipStream_t s) {
+  // 128x128 tiles halve operand traffic per FLOP; used when they still give
+  // >= 2 blocks per CU (256 CUs), else 64x64
+  // skinny N (K-Means: points x k centres): 64x16 tiles, A streamed once by
+  // many blocks (the shape is HBM-bound)
+  const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128) * g.batch;
+  if (g.N <= 16) gemm_f64_tile_launch<64, 16, 4, 1>(g, s);
+  else if (g.N > 64 && big >= 512) gemm_f64_tile_launch<128, 128, 2, 2>(g, s);
+  else gemm_f64_tile_launch<64, 64, 2, 2>(g, s);
 }
 
 void gemm_int_launch(DType dt, const GemmArgs& g, hipStream_t s) {

@@ -23,6 +23,14 @@ GEMMS = [  # M, N, K, bias+relu
     (1_000_000, 64, 256, True),
     (100_000, 10, 100, False),
 ]
+GEMMS_F64 = [  # M, N, K, transpose_b (K-Means shapes: points x centres^T; BASELINE config 3 in f64)
+    (100_000, 10, 100, True),
+    (1_000_000, 10, 100, True),
+    (10_000_000, 512, 512, False),
+    (4096, 4096, 4096, False),
+    (262_144, 512, 512, False),
+]
+F64_PEAK_TF = 78.6  # MI355X FP64 matrix peak (spec)
 CONVS = [  # N, H, W, C, KH, KW, OC, stride, padding (Inception-v3 @224, batch 512)
     (512, 111, 111, 32, 3, 3, 32, 1, "VALID"),
     (512, 109, 109, 32, 3, 3, 64, 1, "SAME"),
@@ -53,11 +61,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--f64-only", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
     res = []
-    for m, n, k, br in GEMMS:
+    for m, n, k, br in ([] if a.f64_only else GEMMS):
         g = tf.Graph()
         with g.as_default():
             x = tf.placeholder(tf.float32, [None, k], name="x")
@@ -72,6 +81,23 @@ def main():
         print(json.dumps(r), flush=True)
         res.append(r)
         del xin
+    for m, n, k, tb in GEMMS_F64:
+        g = tf.Graph()
+        with g.as_default():
+            x = tf.placeholder(tf.float64, [None, k], name="x")
+            wv = rng.standard_normal((n, k) if tb else (k, n))
+            tf.identity(tf.matmul(x, tf.constant(wv), transpose_b=tb), name="y")
+        prog = engine.program(g.serialize(), ["y"], ["x"])
+        xin = torch.randn((m, k), device=dev, dtype=torch.float64)
+        ms = timeit(prog, [xin], a.iters)
+        tfl = 2 * m * n * k / ms / 1e9
+        r = {"kind": "gemm_f64", "M": m, "N": n, "K": k, "transpose_b": tb, "ms": ms, "tflops": tfl,
+             "fraction_of_f64_peak": tfl / F64_PEAK_TF}
+        print(json.dumps(r), flush=True)
+        res.append(r)
+        del xin
+    if a.f64_only:
+        CONVS.clear()
     for nb, h, w, c, kh, kw, oc, s, pad in CONVS:
         g = tf.Graph()
         with g.as_default():
