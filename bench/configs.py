@@ -144,16 +144,18 @@ def cfg_refperf(a):
     back = tfs.from_columns({"x": np.arange(cells, dtype=np.int32)}, num_partitions=1).cache()
     back.local_blocks()
     t_back = timed(lambda: back.to_arrow(), a.steps, a.warmup)
-    # boxed path: 1M Python Row objects -> frame
-    rows = [tfs.Row(x=i) for i in range(1_000_000)]
-    t_rows = timed(lambda: tfs.create_dataframe(rows, num_partitions=1).local_blocks(), 1, 0)
+    # boxed path (the reference's ConvertPerformanceSuite:19-39 case): 10M Row(int)
+    # objects -> an int column, through the native packer (runtime/packer.cpp)
+    rows = [tfs.Row(x=i) for i in range(10_000_000)]
+    t_rows = timed(lambda: tfs.create_dataframe(rows, num_partitions=1).local_blocks(), 3, 1)
     emit({"config": "reference perf suites (PerformanceSuite / Convert / ConvertBack)",
           "map_blocks_x_plus_x_then_sum_20M_rows_ms": t_map * 1e3,
           "map_blocks_x_plus_x_then_sum_rows_per_sec": n / t_map,
-          "convert_10M_int_cells_arrow_ms": t_conv * 1e3,
-          "convert_one_10M_vector_arrow_ms": t_conv_vec * 1e3,
-          "convert_back_10M_int_cells_arrow_ms": t_back * 1e3,
-          "convert_1M_python_rows_ms": t_rows * 1e3,
+          "convert_10M_int_cells_arrow_zero_copy_view_ms": t_conv * 1e3,
+          "convert_one_10M_vector_arrow_zero_copy_view_ms": t_conv_vec * 1e3,
+          "convert_back_10M_int_cells_to_arrow_ms": t_back * 1e3,
+          "convert_10M_python_Row_int_cells_ms": t_rows * 1e3,
+          "convert_10M_python_Row_int_cells_rows_per_sec": 10_000_000 / t_rows,
           "device": str(engine.compute_device()), "data": "synthetic"})
 
 

@@ -15,6 +15,10 @@
 namespace py = pybind11;
 using namespace tfa;
 
+namespace tfa {
+void register_packer(py::module& m);  // runtime/packer.cpp
+}
+
 namespace {
 
 py::object shape_to_py(const Shape& s) {
@@ -339,6 +343,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                 idx.size(0), inner, c10::hip::getCurrentHIPStream(x.device().index()).stream());
     return out;
   }, "out[j] = x[idx[j]] along dim 0 (device gather kernel)");
+  register_packer(m);
   m.def("jit_compile", [](const std::string& src) { return jit::compile_only(src); },
         "compile a generated kernel with hiprtc for gfx950 (no device needed); returns the code-object size");
   m.def("jit_stats", []() {

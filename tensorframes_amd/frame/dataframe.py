@@ -462,17 +462,20 @@ def _tf_of(dt: DataType) -> Optional[int]:
 
 
 def _normalize_rows(data: Sequence[Any], names: Optional[List[str]]):
-    rows = list(data)
+    rows = data if isinstance(data, list) else list(data)
     if not rows:
         return [], names or []
     r0 = rows[0]
     if isinstance(r0, Row) and r0.__fields__:
         names = names or list(r0.__fields__)
-        return [tuple(r) for r in rows], names
+        return rows, names  # Rows are tuples already: no per-row copy
     if isinstance(r0, dict):
         names = names or list(r0.keys())
         return [tuple(r[n] for n in names) for r in rows], names
-    if isinstance(r0, (tuple, list, Row)):
+    if isinstance(r0, tuple):
+        names = names or [f"_{i + 1}" for i in range(len(r0))]
+        return rows, names
+    if isinstance(r0, list):
         names = names or [f"_{i + 1}" for i in range(len(r0))]
         return [tuple(r) for r in rows], names
     names = names or ["value"]
@@ -485,13 +488,12 @@ def create_dataframe(data, schema=None, num_partitions: Optional[int] = None) ->
     nparts = num_partitions or max(1, dist.world_size())
     if isinstance(data, dict):
         return from_columns(data, num_partitions=nparts, schema=schema if isinstance(schema, StructType) else None)
-    try:
-        import pandas as pd
+    import sys
+    pd = sys.modules.get("pandas")  # a pandas frame can only exist if pandas is loaded
+    if pd is not None:
         if isinstance(data, pd.DataFrame):
             return from_columns({c: data[c].to_numpy() if data[c].dtype != object else list(data[c])
                                  for c in data.columns}, num_partitions=nparts)
-    except ImportError:  # pragma: no cover
-        pass
     names = schema if isinstance(schema, (list, tuple)) else None
     rows, names = _normalize_rows(data, list(names) if names else None)
     if isinstance(schema, StructType):
@@ -509,20 +511,39 @@ def create_dataframe(data, schema=None, num_partitions: Optional[int] = None) ->
                 t = StringType()
             fields.append(StructField(n, t, True))
         st = StructType(fields)
-    for r in rows:
-        if len(r) != len(names):
-            raise ValueError(f"row {r} has {len(r)} values, schema has {len(names)} columns")
+    if not isinstance(rows, list):
+        rows = list(rows)
+    ncols = len(names)
     blocks = {}
     n = len(rows)
+    from .._native import _C
     for p in dist.local_partitions(nparts):
         a, b = _bounds(n, nparts, p)
         cols = {}
         for i, f in enumerate(st.fields):
+            tf = _tf_of(f.dataType)
+            packed = None
+            if tf is not None:
+                # native pass over the row tuples (also checks widths and nulls)
+                try:
+                    packed = _C.pack_column(rows, i, ncols, a, b, tf)
+                except ValueError as e:
+                    if "wrong width" in str(e):
+                        bad = next(r for r in rows[a:b] if len(r) != ncols)
+                        raise ValueError(f"row {bad} has {len(bad)} values, schema has {ncols} columns")
+                    raise ValueError(f"column '{f.name}' contains null values; tensorframes_amd requires "
+                                     f"non-null columns (the reference silently accepted them)")
+            if packed is not None:
+                cols[f.name] = packed
+                continue
+            for r in rows[a:b]:
+                if len(r) != ncols:
+                    raise ValueError(f"row {r} has {len(r)} values, schema has {ncols} columns")
             vals = [r[i] for r in rows[a:b]]
             if any(v is None for v in vals):
                 raise ValueError(f"column '{f.name}' contains null values; tensorframes_amd requires "
                                  f"non-null columns (the reference silently accepted them)")
-            cols[f.name] = build_column(vals, _tf_of(f.dataType))
+            cols[f.name] = build_column(vals, tf)
         blocks[p] = Block(b - a, cols)
     return DataFrame(st, _Materialized(blocks), nparts)
 
