@@ -1,7 +1,6 @@
 // Planner + executor (see executor.h).
 #include "executor.h"
 
-#include <ATen/hip/HIPGraph.h>
 
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
@@ -17,6 +16,7 @@
 
 #include "../ir/ops_common.h"
 #include "fusion.h"
+#include "hip_graph.h"
 #include "jit.h"
 
 namespace tfa {
@@ -62,6 +62,24 @@ std::string strip0(const std::string& s) {
 }  // namespace
 
 void set_debug_sync(bool on) { g_debug_sync.store(on ? 1 : 0); }
+
+// Persistent non-blocking copy streams, created on first use: [device][0 = H2D, 1 = D2H]
+hipStream_t copy_stream(int device, int which) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams.find({device, which});
+  if (it != streams.end()) return it->second;
+  int cur = 0;
+  TFA_CHECK(hipGetDevice(&cur) == hipSuccess, "hipGetDevice failed");
+  TFA_CHECK(hipSetDevice(device) == hipSuccess, "hipSetDevice failed");
+  hipStream_t st = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  (void)hipSetDevice(cur);
+  TFA_CHECK(e == hipSuccess, "hipStreamCreate failed: ", hipGetErrorString(e));
+  streams[{device, which}] = st;
+  return st;
+}
 bool get_debug_sync() { return debug_sync(); }
 
 struct Program::Step {
@@ -115,7 +133,7 @@ struct Program::Plan {
     bool declined = false;
     int device = -1;
     hipStream_t stream = nullptr;  // our own capture stream (never shared)
-    std::unique_ptr<at::cuda::CUDAGraph> graph;
+    std::unique_ptr<HipGraph> graph;
     std::vector<at::Tensor> static_in, static_out;
     ~Captured() {
       graph.reset();
@@ -763,18 +781,19 @@ std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor
     (void)hipEventRecord(ev, cur);
     (void)hipStreamWaitEvent(c.stream, ev, 0);
     (void)hipEventDestroy(ev);
-    auto g = std::make_unique<at::cuda::CUDAGraph>();
+    auto g = std::make_unique<HipGraph>();
     try {
       c10::hip::HIPStreamGuard sg(side);
-      g->capture_begin({0, 0}, hipStreamCaptureModeThreadLocal);
+      g->begin(c.stream, dev);
       c.static_out = execute(p, c.static_in, c.stream);
-      g->capture_end();
+      g->end();
     } catch (const std::exception& e) {
-      // the capture stream is abandoned (never reused); run normally from now on
+      // the capture is discarded and the plan runs eagerly from now on
+      g->abort();
       c.failed = true;
       c.static_in.clear();
       c.static_out.clear();
-      g.release();  // a half-captured graph cannot be safely destroyed; leak it
+      g.release();  // its pool may still back tensors of the failed capture; leak it
       stats_.graph_failures++;
       return execute(p, inputs, cur);
     }
@@ -783,7 +802,8 @@ std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor
     stats_.graphs_captured++;
   }
   for (size_t i = 0; i < inputs.size(); ++i) c.static_in[i].copy_(inputs[i], true);
-  c.graph->replay();
+  // the replay is ordered after the input copies on the caller's stream
+  c.graph->replay(cur);
   std::vector<at::Tensor> outs;
   outs.reserve(c.static_out.size());
   for (auto& o : c.static_out) outs.push_back(o.clone());
@@ -848,8 +868,10 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
   c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
   at::Device dev(at::kCUDA, static_cast<c10::DeviceIndex>(device));
   auto compute = c10::hip::getCurrentHIPStream(device);
-  auto h2d = c10::hip::getStreamFromPool(false, device);
-  auto d2h = c10::hip::getStreamFromPool(false, device);
+  // the runtime's own copy streams (one per direction per device): the DMA
+  // engines run both directions concurrently, overlapped with compute
+  auto h2d = c10::hip::getStreamFromExternal(copy_stream(device, 0), static_cast<c10::DeviceIndex>(device));
+  auto d2h = c10::hip::getStreamFromExternal(copy_stream(device, 1), static_cast<c10::DeviceIndex>(device));
   auto t0 = std::chrono::steady_clock::now();
 
   struct Chunk {

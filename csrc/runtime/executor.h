@@ -9,6 +9,7 @@
 #pragma once
 
 #include <ATen/ATen.h>
+#include <hip/hip_runtime.h>
 
 #include <map>
 #include <tuple>
@@ -101,6 +102,8 @@ size_t pinned_pool_cached_bytes();
 // page-lock an existing host tensor's memory in place (hipHostRegister)
 void pin_host_tensor(const at::Tensor& t);
 void unpin_host_tensor(const at::Tensor& t);
+// the runtime's persistent copy streams: which = 0 host->device, 1 device->host
+hipStream_t copy_stream(int device, int which);
 // Config.debug_sync: synchronise + check after every kernel (read per launch)
 void set_debug_sync(bool on);
 bool get_debug_sync();
