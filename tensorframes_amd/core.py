@@ -1646,11 +1646,7 @@ def analyze(dframe: DataFrame) -> DataFrame:
             if is_dense(col):
                 shapes[f.name] = list(col.shape)
             elif isinstance(col, RaggedColumn):
-                cell = None
-                for c in col.cells:
-                    s = Shape(tuple(c.shape))
-                    cell = s if cell is None else (cell.merge(s) or Shape(tuple([UNKNOWN] * max(cell.num_dims, s.num_dims))))
-                shapes[f.name] = [b.nrows] + list(cell.dims)
+                shapes[f.name] = [b.nrows] + _merged_cell_dims(col.cells)
         local[pid] = shapes
     merged: Dict[str, Optional[Shape]] = {}
     for chunk in dist.all_gather_object(local):
@@ -1669,6 +1665,23 @@ def analyze(dframe: DataFrame) -> DataFrame:
         else:
             fields.append(f)
     return dframe.with_schema(StructType(fields))
+
+
+def _merged_cell_dims(cells) -> List[int]:
+    """Per-dim merge of the cell shapes of a ragged column, vectorised: the
+    shapes form an [ncells, rank] array and a dim is kept where every cell
+    agrees, else unknown (reference: ExperimentalOperations.scala:147-157).
+    Cells of different ranks merge to all-unknown of the largest rank."""
+    ranks = {c.ndim for c in cells}
+    if len(ranks) != 1:
+        return [UNKNOWN] * max(ranks)
+    rank = ranks.pop()
+    if rank == 0:
+        return []
+    dims = np.fromiter((d for c in cells for d in c.shape), dtype=np.int64, count=len(cells) * rank)
+    dims = dims.reshape(len(cells), rank)
+    same = (dims == dims[0]).all(axis=0)
+    return [int(d) if ok else UNKNOWN for d, ok in zip(dims[0], same)]
 
 
 def print_schema(dframe: DataFrame):
