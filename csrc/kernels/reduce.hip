@@ -487,25 +487,48 @@ __global__ __launch_bounds__(256) void useg_private(const T* __restrict__ x, con
   const int64_t r0 = blockIdx.x * rows_per_block;
   const int64_t r1 = min(n, r0 + rows_per_block);
   if (col < inner) {
-    for (int64_t i = r0; i < r1; ++i) {
-      int64_t sg = (int64_t)ids[i];
-      if (sg < 0 || sg >= nseg) continue;
-      A* a = &acc[sg * tile + threadIdx.x];
-      *a = combine<OP, A>(*a, A(x[i * inner + col]));
+    // 8 rows of ids and values are loaded before they are folded, so the
+    // global loads overlap instead of one latency per row; the fold itself
+    // keeps the row order (deterministic)
+    constexpr int U = 8;
+    for (int64_t i = r0; i < r1; i += U) {
+      int64_t sg[U];
+      A v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = i + u < r1;
+        sg[u] = ok ? (int64_t)ids[i + u] : -1;
+        v[u] = ok ? A(x[(i + u) * inner + col]) : A(0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (sg[u] < 0 || sg[u] >= nseg) continue;
+        A* a = &acc[sg[u] * tile + threadIdx.x];
+        *a = combine<OP, A>(*a, v[u]);
+      }
     }
     for (int64_t sgi = 0; sgi < nseg; ++sgi)
       part[((int64_t)blockIdx.x * nseg + sgi) * inner + col] = acc[sgi * tile + threadIdx.x];
   }
 }
 
+// folds the B partial slabs: a group of G lanes (G = pow2 <= 64) per output
+// element strides over the slabs, then a fixed xor tree (deterministic)
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void useg_final(const typename AccT<T>::type* __restrict__ part,
-                                                  T* __restrict__ y, int64_t m, int64_t B) {
+                                                  T* __restrict__ y, int64_t m, int64_t B, int G) {
   using A = typename AccT<T>::type;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % G;
+  const int per_wave = 64 / G;
+  const int64_t waves = (int64_t)gridDim.x * 4;
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * per_wave; base < m; base += waves * per_wave) {
+    const int64_t i = base + lane / G;
     A acc = ident<OP, A>();
-    for (int64_t b = 0; b < B; ++b) acc = combine<OP, A>(acc, part[b * m + i]);
+    if (i < m)
+      for (int64_t b = sub; b < B; b += G) acc = combine<OP, A>(acc, part[b * m + i]);
+    for (int s = G / 2; s >= 1; s >>= 1) acc = combine<OP, A>(acc, __shfl_xor(acc, s, 64));
+    if (i >= m || sub != 0) continue;
     if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
       // TF: empty segments get the type's lowest (max) / highest (min) value
       if (acc == ident<OP, A>()) {
@@ -583,7 +606,18 @@ int64_t useg_tile(int64_t inner) {
   return std::min<int64_t>(t, kUsegTile);
 }
 
-int64_t useg_blocks(int64_t n) { return std::max<int64_t>(1, std::min<int64_t>(1024, (n + 127) / 128)); }
+// row blocks of the LDS-private pass: at least 4 rows per segment and 32 per
+// block, so the partial slabs (B x nseg x inner) stay well below the input
+// they summarise, and at most 8192 blocks
+int64_t useg_rows_per_block(int64_t n, int64_t nseg) {
+  int64_t rpb = std::max<int64_t>(32, 4 * nseg);
+  rpb = std::max<int64_t>(rpb, (n + 8191) / 8192);
+  return (rpb + 7) / 8 * 8;
+}
+
+int64_t useg_blocks(int64_t n, int64_t nseg) {
+  return std::max<int64_t>(1, (n + useg_rows_per_block(n, nseg) - 1) / useg_rows_per_block(n, nseg));
+}
 
 }  // namespace
 
@@ -677,7 +711,7 @@ static bool useg_fits_lds(int64_t inner, int64_t nseg) {
 static size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
 size_t unsorted_segment_workspace_bytes(RedOp, DType, int64_t n, int64_t inner, int64_t nseg) {
-  if (useg_fits_lds(inner, nseg)) return static_cast<size_t>(useg_blocks(n)) * nseg * inner * 8;
+  if (useg_fits_lds(inner, nseg)) return static_cast<size_t>(useg_blocks(n, nseg)) * nseg * inner * 8;
   return align256(n * 8) + align256((nseg + 1) * 8) + segment_csr_workspace_bytes(n, nseg);
 }
 
@@ -721,13 +755,17 @@ static void useg_typed(const void* x, const void* ids, void* y, int64_t n, int64
   size_t lds = static_cast<size_t>(nseg * tile * sizeof(A));
   TFA_CHECK(lds <= kUsegLds, "unsorted segment reduce: ", nseg, " segments x ", tile,
             " columns exceed the LDS budget");
-  int64_t B = useg_blocks(n);
-  int64_t rpb = (n + B - 1) / B;
+  const int64_t rpb = useg_rows_per_block(n, nseg);
+  const int64_t B = useg_blocks(n, nseg);
   dim3 grid((unsigned)B, (unsigned)((inner + tile - 1) / tile));
   hipLaunchKernelGGL((useg_private<T, I, OP>), grid, dim3((unsigned)tile), lds, s, (const T*)x, (const I*)ids,
                      (A*)ws, n, inner, nseg, rpb);
-  int64_t m = nseg * inner;
-  hipLaunchKernelGGL((useg_final<T, OP>), dim3(ew_grid(m)), dim3(256), 0, s, (const A*)ws, (T*)y, m, B);
+  const int64_t m = nseg * inner;
+  int G = 1;
+  while (G < 64 && G < B) G <<= 1;
+  const int64_t groups = (m + 64 / G - 1) / (64 / G);  // waves
+  const unsigned fgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 3) / 4, 65536));
+  hipLaunchKernelGGL((useg_final<T, OP>), dim3(fgrid), dim3(256), 0, s, (const A*)ws, (T*)y, m, B, G);
 }
 
 template <typename T, typename I>

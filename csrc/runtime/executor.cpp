@@ -561,6 +561,11 @@ at::Tensor Program::device_const(Plan& p, int slot, const at::Device& dev) {
   auto& m = p.dev_consts[di];
   auto it = m.find(slot);
   if (it != m.end()) return it->second;
+  if (dev.is_cuda() && m.empty()) {
+    upload_consts(p, m, dev);
+    it = m.find(slot);
+    if (it != m.end()) return it->second;
+  }
   TensorRef r{};
   for (auto& cs : p.const_slots)
     if (cs.first == slot) r = cs.second;
@@ -581,6 +586,55 @@ at::Tensor Program::device_const(Plan& p, int slot, const at::Device& dev) {
   m[slot] = t;
   if (graph_const) graph_consts_[gkey] = t;
   return t;
+}
+
+// All constants of a plan that are not already on the device go up in ONE
+// host->device copy: they are packed (256-byte aligned) into a pinned staging
+// buffer and the device arena is sliced into typed views. A program built per
+// iteration (K-Means rebuilds its graph with new centres) then pays one
+// transfer instead of one synchronous copy per constant.
+void Program::upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Device& dev) {
+  const int di = dev.index();
+  struct Item {
+    int slot;
+    at::Tensor v;
+    size_t off;
+    bool graph_const;
+    std::tuple<int, int, int> gkey;
+  };
+  std::vector<Item> items;
+  size_t total = 0;
+  for (auto& cs : p.const_slots) {
+    const TensorRef& r = cs.second;
+    const bool graph_const = g_->node(r.node).op == "Const";
+    auto gkey = std::make_tuple(r.node, r.index, di);
+    if (graph_const) {
+      auto git = graph_consts_.find(gkey);
+      if (git != graph_consts_.end()) {
+        m[cs.first] = git->second;
+        continue;
+      }
+    }
+    const at::Tensor& v = *p.infos[r.node][r.index].value;
+    if (v.numel() == 0) continue;  // the per-slot path makes the empty tensor
+    at::Tensor c = v.contiguous();
+    const size_t off = (total + 255) & ~size_t(255);
+    total = off + c.nbytes();
+    items.push_back({cs.first, c, off, graph_const, gkey});
+  }
+  if (items.empty()) return;
+  at::Tensor host = at::empty({static_cast<int64_t>(total)},
+                              at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  auto* hp = static_cast<uint8_t*>(host.data_ptr());
+  for (auto& it : items) std::memcpy(hp + it.off, it.v.data_ptr(), it.v.nbytes());
+  at::Tensor arena = host.to(dev, /*non_blocking=*/false);
+  for (auto& it : items) {
+    at::Tensor t = arena.narrow(0, static_cast<int64_t>(it.off), static_cast<int64_t>(it.v.nbytes()))
+                       .view(it.v.scalar_type())
+                       .view(it.v.sizes());
+    m[it.slot] = t;
+    if (it.graph_const) graph_consts_[it.gkey] = t;
+  }
 }
 
 std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream) {

@@ -79,6 +79,7 @@ class Program {
   std::shared_ptr<Plan> build_plan(const std::vector<at::Tensor>& inputs, bool force_gpu);
   std::vector<at::Tensor> execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream);
   at::Tensor device_const(Plan& p, int slot, const at::Device& dev);
+  void upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Device& dev);
   bool graphable(const Plan& p) const;
   std::vector<at::Tensor> run_graph(Plan& p, const std::vector<at::Tensor>& inputs);
 

@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--variant", choices=["in_graph", "aggregate"], default="in_graph")
 ap.add_argument("--points", type=int, default=100_000)
+ap.add_argument("--cprofile", action="store_true", help="print the top host functions by own time")
 a = ap.parse_args()
 rng = np.random.default_rng(2)
 pts = rng.uniform(0.0, 1.0, size=(a.points, 100))
@@ -28,12 +29,21 @@ c0 = np.random.default_rng(2).standard_normal((10, 100))
 agg = a.variant == "in_graph"
 kmeans.kmeans(df, c0, num_iters=1, tf_aggregate=agg)  # warm: plans, JIT, tile tuning
 torch.cuda.synchronize()
+prof = None
+if a.cprofile:
+    import cProfile
+    prof = cProfile.Profile()
+    prof.enable()
 t0 = time.perf_counter()
 c = c0
 for _ in range(a.iters):
     c, _d = (kmeans.run_one_step2 if agg else kmeans.run_one_step)(df, c)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / a.iters
+if prof is not None:
+    import pstats
+    prof.disable()
+    pstats.Stats(prof).sort_stats("tottime").print_stats(30)
 from tensorframes_amd._native import _C  # noqa: E402
 print(json.dumps({"variant": a.variant, "iters": a.iters, "ms_per_iter": dt * 1e3,
                   "fusion": os.environ.get("TFA_FUSION", "1"), "jit": _C.jit_stats()}))

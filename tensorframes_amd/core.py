@@ -1035,7 +1035,10 @@ def _combine_monoids(partials: Dict[str, List[torch.Tensor]], ops: Dict[str, str
     dev = engine.compute_device()
     local: Dict[str, Optional[torch.Tensor]] = {}
     for n, ps in partials.items():
-        local[n] = _monoid_reduce(ops[n], torch.stack([p.to(dev) for p in ps], 0), dev) if ps else None
+        if len(ps) == 1:
+            local[n] = ps[0].to(dev)
+        else:
+            local[n] = _monoid_reduce(ops[n], torch.stack([p.to(dev) for p in ps], 0), dev) if ps else None
     if not dist.is_distributed():
         _check(all(v is not None for v in local.values()), "Cannot reduce an empty DataFrame")
         return local
@@ -1100,6 +1103,29 @@ def _static_shapes(spec_bytes: bytes, fetch_refs: List[str], names: List[str], f
     return out
 
 
+def _to_host_batched(vals: Dict[str, torch.Tensor]) -> Dict[str, np.ndarray]:
+    """Device results to numpy with one device->host copy per dtype (each copy
+    is a synchronisation) instead of one per fetch."""
+    out: Dict[str, np.ndarray] = {}
+    by_dtype: Dict[Any, List[str]] = {}
+    for n, v in vals.items():
+        if v.is_cuda:
+            by_dtype.setdefault(v.dtype, []).append(n)
+        else:
+            out[n] = v.numpy()
+    for names in by_dtype.values():
+        if len(names) == 1:
+            out[names[0]] = vals[names[0]].cpu().numpy()
+            continue
+        flat = torch.cat([vals[n].reshape(-1) for n in names]).cpu().numpy()
+        off = 0
+        for n in names:
+            k = vals[n].numel()
+            out[n] = flat[off:off + k].reshape(tuple(vals[n].shape))
+            off += k
+    return out
+
+
 def _identity(op: str, shape, dtype, dev) -> torch.Tensor:
     if op == "Sum":
         return torch.zeros(shape, dtype=dtype, device=dev)
@@ -1129,10 +1155,26 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
 
     def task(blocks):
         res = {}
+        dense_of = {}
+        if uniform and len(blocks) > 1:
+            # every fetch is op(x_input, axis=0): this rank's device-resident
+            # partitions are one block for the graph, so a concatenation per
+            # column replaces a reduction per partition per fetch plus a stack
+            dense = [(pid, _dense_inputs(b, cols, "reduce_blocks")) for pid, b in sorted(blocks.items())
+                     if b.nrows > 0]
+            dense_of = dict(dense)
+            devs = {t.device for _, ins in dense for t in ins}
+            nbytes = sum(t.numel() * t.element_size() for _, ins in dense for t in ins)
+            if (len(dense) > 1 and len(devs) == 1 and next(iter(devs)).type == "cuda"
+                    and nbytes <= config.chunk_bytes):
+                ins = [torch.cat([d[1][j] for d in dense], 0) for j in range(len(cols))]
+                res[dense[0][0]] = engine.run_program(prog, ins, ins[0].device)
+                metrics.add("reduce_blocks_merged_partitions", len(dense))
+                return res
         for pid, b in sorted(blocks.items()):
             if b.nrows == 0:
                 continue
-            ins = _dense_inputs(b, cols, "reduce_blocks")
+            ins = dense_of.get(pid) or _dense_inputs(b, cols, "reduce_blocks")
             on_device = all(t.is_cuda for t in ins)
             # reductions stage 8 pipeline chunks at a time: per-chunk overhead stays
             # negligible and device memory bounded (1 GiB at the default chunk_bytes)
@@ -1163,7 +1205,7 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     if uniform:
         # partials reduced on device, then one all-reduce per (op, dtype) over RCCL
         comb = _combine_monoids({n: partials[j] for j, n in enumerate(out_names)}, uniform, static, dtypes)
-        results = {n: comb[n].cpu().numpy() for n in out_names}
+        results = _to_host_batched(comb)
     else:
         # generic associative graph: this rank's partials are folded by the graph
         # on their stacked [P, ...] block, the per-rank partials are all-gathered

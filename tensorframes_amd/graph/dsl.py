@@ -234,9 +234,16 @@ class Graph:
         the nodes added since the last call."""
         with self._lock:
             cache = self._enc_view if view else self._enc_full
-            for n in self._nodes[len(cache):]:
-                e = P._ld(1, P.serialize_node(self._view_node(n) if view else n))
-                cache.append(list(e.parts) if isinstance(e, P._Rope) else [e])
+            other = self._enc_full if view else self._enc_view
+            i = len(cache)  # (no range(): this module defines the tf.range op)
+            for n in self._nodes[i:]:
+                vn = self._view_node(n)
+                if vn is n and i < len(other):  # same node in both views: encode once
+                    cache.append(other[i])
+                else:
+                    e = P._ld(1, P.serialize_node(vn if view else n))
+                    cache.append(list(e.parts) if isinstance(e, P._Rope) else [e])
+                i += 1
             return cache[:len(self._nodes)]
 
     def _shape_view(self) -> bytes:

@@ -299,6 +299,25 @@ def _enc_attr(a: AttrValue) -> bytes:
     raise ValueError(f"unknown attr kind {k}")
 
 
+# encoded `attr` map entries of small hashable values (dtype, int, bool,
+# string attrs repeat across nodes and graphs): built once
+_ATTR_ENTRIES: Dict[tuple, bytes] = {}
+
+
+def _attr_entry(k: str, a: AttrValue) -> bytes:
+    v = a.value
+    # (floats stay out: -0.0 == 0.0 would share one encoding)
+    if a.kind in ("type", "i", "b", "s") and isinstance(v, (int, bool, bytes, str)):
+        key = (k, a.kind, v)
+        e = _ATTR_ENTRIES.get(key)
+        if e is None:
+            e = _ld(5, _ld(1, k.encode()) + _ld(2, _enc_attr(a)))
+            if len(_ATTR_ENTRIES) < 65536:
+                _ATTR_ENTRIES[key] = e
+        return e
+    return _ld(5, _ld(1, k.encode()) + _ld(2, _enc_attr(a)))
+
+
 def serialize_node(n: NodeDef) -> bytes:
     out = _ld(1, n.name.encode()) + _ld(2, n.op.encode())
     for i in n.input:
@@ -306,7 +325,7 @@ def serialize_node(n: NodeDef) -> bytes:
     if n.device:
         out += _ld(4, n.device.encode())
     for k in sorted(n.attr):
-        out += _ld(5, _ld(1, k.encode()) + _ld(2, _enc_attr(n.attr[k])))
+        out += _attr_entry(k, n.attr[k])
     return out
 
 
