@@ -43,7 +43,8 @@ dt = (time.perf_counter() - t0) / a.iters
 if prof is not None:
     import pstats
     prof.disable()
-    pstats.Stats(prof).sort_stats("tottime").print_stats(30)
+    pstats.Stats(prof).sort_stats("tottime").print_stats(25)
+    pstats.Stats(prof).sort_stats("cumulative").print_stats(60)
 from tensorframes_amd._native import _C  # noqa: E402
 print(json.dumps({"variant": a.variant, "iters": a.iters, "ms_per_iter": dt * 1e3,
                   "fusion": os.environ.get("TFA_FUSION", "1"), "jit": _C.jit_stats()}))
