@@ -17,6 +17,21 @@
 namespace tfa {
 
 inline hipStream_t stream_of(const ExecCtx& c) { return static_cast<hipStream_t>(c.stream); }
+
+// host (ATen) form of a fused epilogue activation (k::Act codes); same
+// formulas as the standalone ops
+inline at::Tensor apply_act_host(const at::Tensor& r, int act) {
+  switch (act) {
+    case k::ACT_RELU: return at::clamp_min(r, 0);
+    case k::ACT_RELU6: return at::clamp(r, 0, 6);
+    case k::ACT_SIGMOID: return at::sigmoid(r);
+    case k::ACT_TANH: return at::tanh(r);
+    case k::ACT_ELU: return at::where(r > 0, r, at::expm1(r));
+    case k::ACT_SELU: return at::selu(r);
+    case k::ACT_SOFTPLUS: return at::where(r > 20, r, at::log1p(at::exp(r)));
+    default: return r;
+  }
+}
 inline DType dt_of(const at::Tensor& t) { return from_scalar_type(t.scalar_type()); }
 
 inline int64_t norm_axis(int64_t a, int64_t rank, const char* what = "axis") {

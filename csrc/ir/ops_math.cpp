@@ -394,9 +394,7 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
     at::Tensor b = tb ? b0.transpose(-1, -2) : b0;
     at::Tensor r = at::matmul(a, b);
     if (bias) r = r + *bias;
-    if (act == 1) r = at::clamp_min(r, 0);
-    if (act == 2) r = at::clamp(r, 0, 6);
-    out = r.contiguous();
+    out = apply_act_host(r, act).contiguous();
     return;
   }
   require_gpu_dtype(a0, {at::kFloat, at::kDouble, at::kInt, at::kLong}, "MatMul");

@@ -102,9 +102,7 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
                               at::IntArrayRef(pad), at::IntArrayRef(dil), 1);
     y = y.permute({0, 2, 3, 1});
     if (bias) y = y + *bias;
-    if (act == 1) y = at::clamp_min(y, 0);
-    if (act == 2) y = at::clamp(y, 0, 6);
-    out = y.contiguous();
+    out = apply_act_host(y, act).contiguous();
     return;
   }
   require_gpu_dtype(x0, {at::kFloat}, "Conv2D");

@@ -448,10 +448,7 @@ __global__ __launch_bounds__(256) void channel_affine_kernel(const T* __restrict
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     int64_t c = i % C;
-    T v = x[i] * sc[c] + sh[c];
-    if (act == 1) v = v > T(0) ? v : T(0);
-    else if (act == 2) v = v > T(0) ? (v < T(6) ? v : T(6)) : T(0);
-    y[i] = v;
+    y[i] = act_apply<T>(x[i] * sc[c] + sh[c], act);
   }
 }
 

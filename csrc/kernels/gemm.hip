@@ -40,11 +40,6 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-__device__ __forceinline__ float act_apply(float v, int act) {
-  if (act == 1) return v > 0.f ? v : 0.f;
-  if (act == 2) return v > 0.f ? (v < 6.f ? v : 6.f) : 0.f;
-  return v;
-}
 
 enum ALoad { A_KCONTIG = 0, A_MCONTIG = 1, A_CONV = 2 };
 

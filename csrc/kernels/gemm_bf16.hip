@@ -60,11 +60,6 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-__device__ __forceinline__ float act_apply(float v, int act) {
-  if (act == 1) return v > 0.f ? v : 0.f;
-  if (act == 2) return v > 0.f ? (v < 6.f ? v : 6.f) : 0.f;
-  return v;
-}
 
 // B f32 ([K][N] or [N][K]) -> hi/lo bf16 images [N][Kp], zero-padded to Kp
 __global__ __launch_bounds__(256) void prep_b(const float* __restrict__ B, int64_t ldb, bool tb, int64_t N,

@@ -23,12 +23,6 @@ __device__ __forceinline__ int xcd_remap64(int b, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <typename T>
-__device__ __forceinline__ T act_apply(T v, int act) {
-  if (act == 1) return v > T(0) ? v : T(0);
-  if (act == 2) return v > T(0) ? (v < T(6) ? v : T(6)) : T(0);
-  return v;
-}
 
 constexpr int D_BK = 16, D_PAD = 2;
 

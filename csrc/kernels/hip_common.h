@@ -22,6 +22,25 @@ inline int ew_grid(int64_t work_items, int block = 256, int max_blocks = 256 * 8
   return static_cast<int>(b);
 }
 
+// epilogue activation (codes: enum Act in kernels.h); `act` is uniform per
+// launch, so the switch is a scalar branch
+template <typename T>
+__device__ __forceinline__ T act_apply(T v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > T(0) ? v : T(0);
+    case ACT_RELU6: return v > T(0) ? (v < T(6) ? v : T(6)) : T(0);
+    case ACT_SIGMOID: return T(1) / (T(1) + exp(-v));
+    case ACT_TANH: return tanh(v);
+    case ACT_ELU: return v > T(0) ? v : expm1(v);
+    case ACT_SELU: {
+      const T alpha = T(1.6732632423543772848170429916717), scale = T(1.0507009873554804934193349852946);
+      return v > T(0) ? scale * v : scale * alpha * expm1(v);
+    }
+    case ACT_SOFTPLUS: return v > T(20) ? v : log1p(exp(v));
+    default: return v;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

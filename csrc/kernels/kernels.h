@@ -112,6 +112,11 @@ void one_hot(DType dt, DType idt, const void* idx, void* out, int64_t n, int64_t
              double on, double off, hipStream_t s);
 
 // ------------------------------------------------------------ GEMM (MFMA)
+// GEMM/conv epilogue activations (planner-fused unary op after the product
+// and its bias); the formulas match the standalone elementwise kernels
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2, ACT_SIGMOID = 3, ACT_TANH = 4, ACT_ELU = 5,
+                 ACT_SELU = 6, ACT_SOFTPLUS = 7 };
+
 // C[b] = op(A[b]) @ op(B[b]) (+ bias[N]) (relu); row-major, leading dims in elements.
 struct GemmArgs {
   int64_t M, N, K;
@@ -120,7 +125,7 @@ struct GemmArgs {
   void* C; int64_t ldc; int64_t strideC;
   bool ta, tb;
   const void* bias;  // nullable, length N
-  int act;           // 0 none, 1 relu, 2 relu6
+  int act;           // epilogue activation: an Act code
   int64_t batch;
   void* workspace = nullptr;  // split-K partials (gemm_workspace_bytes)
 };

@@ -54,6 +54,20 @@ struct RangeGuard {
   ~RangeGuard() { roctxRangePop(); }
 };
 
+// unary ops a GEMM/conv epilogue absorbs (k::Act code; ACT_NONE = not fusible)
+int epilogue_act(const std::string& op) {
+  static const std::map<std::string, int> m = {
+      {"Relu", k::ACT_RELU},   {"Relu6", k::ACT_RELU6}, {"Sigmoid", k::ACT_SIGMOID}, {"Tanh", k::ACT_TANH},
+      {"Elu", k::ACT_ELU},     {"Selu", k::ACT_SELU},   {"Softplus", k::ACT_SOFTPLUS}};
+  auto it = m.find(op);
+  return it == m.end() ? k::ACT_NONE : it->second;
+}
+
+const char* act_name(int act) {
+  static const char* names[] = {"none", "relu", "relu6", "sigmoid", "tanh", "elu", "selu", "softplus"};
+  return act >= 0 && act < 8 ? names[act] : "?";
+}
+
 std::string strip0(const std::string& s) {
   if (s.size() > 2 && s.compare(s.size() - 2, 2, ":0") == 0) return s.substr(0, s.size() - 2);
   return s;
@@ -418,8 +432,9 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
       int c2 = next_op(cur, &lv2);
       if (c2 >= 0) {
         const Node& cn = g_->node(c2);
-        if ((cn.op == "Relu" || cn.op == "Relu6") && cn.inputs[0] == TensorRef{lv2, 0}) {
-          st.act = cn.op == "Relu" ? 1 : 2;
+        const int act = epilogue_act(cn.op);
+        if (act != k::ACT_NONE && cn.inputs[0] == TensorRef{lv2, 0}) {
+          st.act = act;
           for (int v = lv2; v != cur; v = g_->node(v).inputs[0].node) absorbed.insert(v);
           absorbed.insert(c2);
           cur = c2;
@@ -1057,7 +1072,7 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
        << nd.op << ' ' << nd.name;
     if (st.out_node != st.node) os << " -> " << g_->node(st.out_node).name;
     if (st.bias_slot >= 0) os << " +bias";
-    if (st.act) os << (st.act == 1 ? " +relu" : " +relu6");
+    if (st.act) os << " +" << act_name(st.act);
     if (st.alias_slot >= 0) os << " ->concat-slice@" << st.alias_offset;
     if (!st.preplaced.empty()) {
       int n = 0;
