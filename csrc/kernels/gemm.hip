@@ -327,24 +327,30 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* ws = static_cast<float*>(g.workspace);
   const float* bias = static_cast<const float*>(g.bias);
+  auto epilogue = [&](auto act) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
-    if (col >= N) continue;
-    const float bv = (!ws && bias) ? bias[col] : 0.f;
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
+      if (col >= N) continue;
+      const float bv = (!ws && bias) ? bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= M) continue;
-        if (ws)  // split-K partial slab [split][batch][M][N]
-          ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = acc[i][j][r];
-        else
-          static_cast<float*>(g.C)[bz * g.strideC + row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row >= M) continue;
+          if (ws)  // split-K partial slab [split][batch][M][N]
+            ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = acc[i][j][r];
+          else
+            static_cast<float*>(g.C)[bz * g.strideC + row * g.ldc + col] = act(acc[i][j][r] + bv);
+        }
       }
     }
-  }
+  };
+  if (ws || g.act <= ACT_RELU6)
+    epilogue([&](float v) { return act_fast(v, g.act); });
+  else
+    epilogue([&](float v) { return act_apply(v, g.act); });
 }
 
 // split-K combine: fixed summation order over the splits (deterministic)

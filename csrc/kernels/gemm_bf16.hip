@@ -277,21 +277,27 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
   }
 
   const float* bias = static_cast<const float*>(g.bias);
+  auto epilogue = [&](auto act) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int64_t col = n0 + wn * (BN / WN) + j * 32 + li;
-    if (col >= N) continue;
-    const float bv = bias ? bias[col] : 0.f;
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = n0 + wn * (BN / WN) + j * 32 + li;
+      if (col >= N) continue;
+      const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= M) continue;
-        static_cast<float*>(g.C)[row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row >= M) continue;
+          static_cast<float*>(g.C)[row * g.ldc + col] = act(acc[i][j][r] + bv);
+        }
       }
     }
-  }
+  };
+  if (g.act <= ACT_RELU6)
+    epilogue([&](float v) { return act_fast(v, g.act); });
+  else
+    epilogue([&](float v) { return act_apply(v, g.act); });
 }
 
 int64_t padded_k(int64_t K) { return (K + kBK - 1) / kBK * kBK; }

@@ -164,19 +164,25 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
   }
   // f64 C/D layout: col = lane&15, row = (lane>>4) + 4*r
   const double* bias = static_cast<const double*>(g.bias);
+  auto epilogue = [&](auto act) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int64_t col = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-    const double bv = (bias && col < N) ? bias[col] : 0.0;
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+      const double bv = (bias && col < N) ? bias[col] : 0.0;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) + 4 * r;
-        if (row < M && col < N) C[row * g.ldc + col] = act_apply(acc[i][j][r] + bv, g.act);
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) + 4 * r;
+          if (row < M && col < N) C[row * g.ldc + col] = act(acc[i][j][r] + bv);
+        }
       }
     }
-  }
+  };
+  if (g.act <= ACT_RELU6)
+    epilogue([&](double v) { return act_fast(v, g.act); });
+  else
+    epilogue([&](double v) { return act_apply(v, g.act); });
 }
 
 // ============================================================== integer GEMM (VALU)
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(256) void gemm_int(GemmArgs g) {
   if (row < g.M && col < g.N) {
     T v = T(acc);
     if (g.bias) v += static_cast<const T*>(g.bias)[col];
-    C[row * g.ldc + col] = act_apply(v, g.act);
+    C[row * g.ldc + col] = act_fast(v, g.act);
   }
 }
 

@@ -22,6 +22,16 @@ inline int ew_grid(int64_t work_items, int block = 256, int max_blocks = 256 * 8
   return static_cast<int>(b);
 }
 
+// the cheap epilogue activations (none / relu / relu6): kernels branch once
+// on `act` between an epilogue built from this and one built from act_apply,
+// so the transcendental forms do not bloat the common hot epilogue
+template <typename T>
+__device__ __forceinline__ T act_fast(T v, int act) {
+  if (act == ACT_RELU) return v > T(0) ? v : T(0);
+  if (act == ACT_RELU6) return v > T(0) ? (v < T(6) ? v : T(6)) : T(0);
+  return v;
+}
+
 // epilogue activation (codes: enum Act in kernels.h); `act` is uniform per
 // launch, so the switch is a scalar branch
 template <typename T>
