@@ -189,6 +189,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["d2h_bytes"] = s.d2h_bytes;
         d["chunks"] = s.chunks;
         d["wall_ms"] = s.wall_ms;
+        d["h2d_ms"] = s.h2d_ms;        // device time of the host->device copies (hipEvents)
+        d["compute_ms"] = s.compute_ms;
+        d["d2h_ms"] = s.d2h_ms;
         d["graphs_captured"] = s.graphs_captured;
         d["graph_replays"] = s.graph_replays;
         d["graph_failures"] = s.graph_failures;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -53,6 +54,15 @@ struct RangeGuard {
   explicit RangeGuard(const std::string& name) { roctxRangePushA(name.c_str()); }
   ~RangeGuard() { roctxRangePop(); }
 };
+
+// TFA_STAGE_TIMERS=0 turns off the per-chunk hipEvent stage timers of run_chunked
+bool stage_timers_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TFA_STAGE_TIMERS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // unary ops a GEMM/conv epilogue absorbs (k::Act code; ACT_NONE = not fusible)
 int epilogue_act(const std::string& op) {
@@ -982,6 +992,16 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
   }
   std::vector<bool> used(depth, false);
   int64_t h2d_bytes = 0, d2h_bytes = 0;
+  // per-stage device time (hipEvent pairs bracketing each chunk's H2D, compute
+  // and D2H on their streams; read once after the final synchronisation)
+  const bool timed = stage_timers_enabled();
+  std::vector<std::array<hipEvent_t, 6>> tev;
+  auto stamp = [&](size_t ci, int k, hipStream_t s) {
+    if (!timed) return;
+    HIP_OK(hipEventCreate(&tev[ci][k]));
+    HIP_OK(hipEventRecord(tev[ci][k], s));
+  };
+  if (timed) tev.assign(chunks.size(), std::array<hipEvent_t, 6>{});
   for (size_t ci = 0; ci < chunks.size(); ++ci) {
     const Chunk& ch = chunks[ci];
     int slot = static_cast<int>(ci % depth);
@@ -991,6 +1011,7 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
       HIP_OK(hipStreamWaitEvent(h2d.stream(), ev_d2h[slot], 0));
     }
     std::vector<at::Tensor> dev_in;
+    stamp(ci, 0, h2d.stream());
     for (size_t i = 0; i < nin; ++i) {
       const at::Tensor& src = seg_inputs[ch.seg][i];
       int64_t row_bytes = src.numel() / std::max<int64_t>(src.size(0), 1) * src.element_size();
@@ -1001,18 +1022,22 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
       h2d_bytes += ch.rows * row_bytes;
       dev_in.push_back(dst);
     }
+    stamp(ci, 1, h2d.stream());
     HIP_OK(hipEventRecord(ev_h2d[slot], h2d.stream()));
     // compute
     HIP_OK(hipStreamWaitEvent(compute.stream(), ev_h2d[slot], 0));
     std::vector<at::Tensor> outs;
+    stamp(ci, 2, compute.stream());
     {
       RangeGuard rg("chunk_compute");
       auto p = plan_for(dev_in);
       outs = execute(*p, dev_in, compute.stream());
     }
+    stamp(ci, 3, compute.stream());
     HIP_OK(hipEventRecord(ev_comp[slot], compute.stream()));
     // D2H
     HIP_OK(hipStreamWaitEvent(d2h.stream(), ev_comp[slot], 0));
+    stamp(ci, 4, d2h.stream());
     for (size_t j = 0; j < outs.size(); ++j) {
       at::Tensor o = outs[j];
       const at::Tensor& dst = seg_outputs[ch.seg][j];
@@ -1026,6 +1051,7 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
       c10::hip::HIPCachingAllocator::recordStream(o.storage().data_ptr(), d2h);
       d2h_bytes += ch.rows * row_bytes;
     }
+    stamp(ci, 5, d2h.stream());
     HIP_OK(hipEventRecord(ev_d2h[slot], d2h.stream()));
     used[slot] = true;
     stats_.chunks++;
@@ -1038,11 +1064,22 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
     hipEventDestroy(ev_comp[d]);
     hipEventDestroy(ev_d2h[d]);
   }
+  double stage_ms[3] = {0, 0, 0};
+  for (auto& e : tev) {
+    for (int k = 0; k < 3; ++k) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, e[2 * k], e[2 * k + 1]) == hipSuccess) stage_ms[k] += ms;
+    }
+    for (hipEvent_t ev : e) hipEventDestroy(ev);
+  }
   auto t1 = std::chrono::steady_clock::now();
   stats_.runs++;
   stats_.h2d_bytes += h2d_bytes;
   stats_.d2h_bytes += d2h_bytes;
   stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  stats_.h2d_ms += stage_ms[0];
+  stats_.compute_ms += stage_ms[1];
+  stats_.d2h_ms += stage_ms[2];
 }
 
 std::vector<std::string> Program::fused_sources(const std::vector<at::Tensor>& inputs) {

@@ -223,10 +223,15 @@ def run_segments_pipelined(prog, segments: List[List[torch.Tensor]],
     outs = [[empty_host(shape, dt, True) for (shape, dt) in spec] for spec in out_specs]
     total = sum(seg[0].shape[0] for seg in segs if seg)
     chunk = chunk_rows_for(segs[0], total) if segs and segs[0] else 1 << 16
+    before = prog.stats()
     with metrics.timer("pipelined"):
         prog.run_chunked(segs, outs, chunk, dev.index or 0, config.pipeline_depth)
     st = prog.stats()
-    metrics.add("chunks", st["chunks"])
+    # this call's share of the program's cumulative counters; the *_device_ms
+    # stage times come from hipEvent pairs around each chunk's copies/kernels
+    metrics.add("chunks", st["chunks"] - before["chunks"])
+    for k in ("h2d_ms", "compute_ms", "d2h_ms"):
+        metrics.add("pipeline_" + k.replace("_ms", "_device_ms"), st[k] - before[k])
     return outs
 
 

@@ -114,6 +114,33 @@ def test_hip_graph_replay_matches_eager_and_outputs_do_not_alias():
             torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-4)
 
 
+def test_pipeline_stage_device_timers():
+    """run_chunked brackets every chunk's H2D, compute and D2H with hipEvent
+    pairs: the stage device times are positive, each below the wall time of
+    the call, and exported as metrics for this call only."""
+    import numpy as np
+    from tensorframes_amd import engine, tf
+    from tensorframes_amd.utils.logging import metrics
+    g = tf.Graph()
+    w = np.random.default_rng(4).standard_normal((256, 256)).astype(np.float32)
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 256], name="x")
+        tf.nn.relu(tf.matmul(x, tf.constant(w)), name="y")
+    prog = engine.program(g.serialize(), ["y"], ["x"])
+    xin = torch.randn((400_000, 256))
+    m0 = metrics.snapshot()
+    out = engine.run_segments_pipelined(prog, [[xin]], [[((400_000, 256), torch.float32)]])
+    m1 = metrics.snapshot()
+    st = prog.stats()
+    assert st["chunks"] >= 2
+    for k in ("h2d_ms", "compute_ms", "d2h_ms"):
+        assert 0 < st[k] < st["wall_ms"], (k, st)
+        key = "pipeline_" + k.replace("_ms", "_device_ms")
+        assert abs((m1.get(key, 0) - m0.get(key, 0)) - st[k]) < 1e-6
+    assert m1["chunks"] - m0.get("chunks", 0) == st["chunks"]
+    torch.testing.assert_close(out[0][0][:100], torch.relu(xin[:100] @ torch.as_tensor(w)), rtol=1e-4, atol=1e-4)
+
+
 def test_concat_write_into_slice_matches_cpu():
     """Inception-style block: conv branches (+bias+relu) concatenated on the
     channel axis write straight into the concat output; a pooled branch and
