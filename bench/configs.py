@@ -361,7 +361,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512, help="rows per partition")
     ap.add_argument("--source", choices=["host", "device"], default="host", help="inception: where the column lives")
     ap.add_argument("--input-dtype", choices=["float32", "uint8"], default="float32", help="inception image dtype")
-    ap.add_argument("--chunk-images", type=int, default=256, help="inception (host): images per pipelined chunk")
+    ap.add_argument("--chunk-images", type=int, default=512, help="inception (host): images per pipelined chunk")
     ap.add_argument("--ring", type=int, default=3, help="inception (host): distinct synthetic partitions")
     ap.add_argument("--precision", choices=["f32", "bf16x3", "bf16"], default="f32",
                     help="float32 MatMul/Conv2D compute mode (Config.precision); f32 = exact")

@@ -30,6 +30,12 @@ class Config:
     pipeline_depth: int = dataclasses.field(default_factory=lambda: _env("TFA_PIPELINE_DEPTH", 3, int))
     # partitions smaller than this run in one shot (no chunking)
     min_chunked_rows: int = dataclasses.field(default_factory=lambda: _env("TFA_MIN_CHUNKED_ROWS", 65536, int))
+    # ... or at least this many input bytes (a partition of 2048 images is 1.2 GB:
+    # one-shot it would copy in, compute, copy out with nothing overlapped)
+    min_chunked_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_MIN_CHUNKED_BYTES", 32 << 20, int))
+    # streaming actions hand derived operators groups of partitions of up to
+    # this many input bytes (one pipeline ramp per group; memory bound)
+    stream_group_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_STREAM_GROUP_BYTES", 4 << 30, int))
     # allocate map_blocks outputs in page-locked host memory (DMA target)
     pinned_outputs: bool = dataclasses.field(default_factory=lambda: _env("TFA_PINNED_OUTPUTS", True, bool))
     pinned_min_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_PINNED_MIN_BYTES", 1 << 20, int))

@@ -332,7 +332,7 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
         return res
 
     def _run_host_jobs(jobs, res):
-        big = [j for j in jobs if separable and j[1].nrows >= config.min_chunked_rows]
+        big = [j for j in jobs if separable and engine.worth_pipelining(j[2])]
         small = [j for j in jobs if j not in big]
         if big:
             specs = []
@@ -781,7 +781,7 @@ class _RowVectorizer:
         if not engine.gpu_available():
             return engine.run_program(prog, ins, torch.device("cpu"))
         lifted = self._lifted[tuple(len(s) for s in cell_shapes)]
-        if ins[0].shape[0] >= config.min_chunked_rows:
+        if engine.worth_pipelining(ins):
             shapes = _concrete_output_shapes(lifted, self.fetch_refs, self.feed_names, ins)
             specs = [(tuple(s), o.dtype) for s, o in zip(shapes, self._out_dtypes(lifted))]
             metrics.add("map_rows_pipelined_rows", ins[0].shape[0])

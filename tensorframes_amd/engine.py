@@ -178,6 +178,16 @@ class _single_threaded:
         _thread_lock.release()
 
 
+def worth_pipelining(inputs: List[torch.Tensor]) -> bool:
+    """A host partition streams through the chunked H2D/compute/D2H pipeline
+    when it has many rows or many bytes; smaller ones run in one shot."""
+    if not inputs:
+        return False
+    rows = inputs[0].shape[0]
+    nbytes = sum(t.numel() * t.element_size() for t in inputs)
+    return rows >= 2 and (rows >= config.min_chunked_rows or nbytes >= config.min_chunked_bytes)
+
+
 def run_block_host(prog, inputs: List[torch.Tensor], separable: bool,
                    out_specs: Optional[List[Tuple[tuple, torch.dtype]]] = None) -> List[torch.Tensor]:
     """Host-resident block -> host-resident outputs, on the compute device."""
@@ -185,7 +195,7 @@ def run_block_host(prog, inputs: List[torch.Tensor], separable: bool,
     rows = inputs[0].shape[0] if inputs else 0
     if dev.type != "cuda":
         return [o.contiguous() for o in prog.run([t.contiguous() for t in inputs])]
-    if separable and out_specs is not None and rows >= config.min_chunked_rows:
+    if separable and out_specs is not None and worth_pipelining(inputs):
         return run_segments_pipelined(prog, [inputs], [out_specs])[0]
     outs = run_program(prog, inputs, dev)
     res = []

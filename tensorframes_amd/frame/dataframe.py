@@ -71,8 +71,30 @@ class _Derived(_Source):
         return self._fn(self._parent._blocks())
 
     def iterate(self):
+        """Streams the parent's partitions through fn in small groups: up to
+        `Config.stream_group_bytes` of input per call, so a pipelined engine
+        call spans several partitions (one H2D ramp-up per group, not per
+        partition) while memory stays bounded."""
+        from ..config import config
+        group: Dict[int, Block] = {}
+        nbytes = 0
         for pid, b in self._parent._iter_blocks():
-            yield pid, self._fn({pid: b})[pid]
+            group[pid] = b
+            nbytes += _block_bytes(b)
+            if nbytes >= config.stream_group_bytes:
+                yield from self._run_group(group)
+                group, nbytes = {}, 0
+        if group:
+            yield from self._run_group(group)
+
+    def _run_group(self, group: Dict[int, Block]):
+        res = self._fn(group)
+        for pid in sorted(group):
+            yield pid, res[pid]
+
+
+def _block_bytes(b: Block) -> int:
+    return sum(c.numel() * c.element_size() for c in b.columns.values() if isinstance(c, torch.Tensor))
 
 
 # ------------------------------------------------------------------ DataFrame
@@ -131,7 +153,8 @@ class DataFrame:
 
     def _iter_blocks(self):
         """Local (pid, block) pairs in pid order, streamed through generated and
-        streamable derived sources so only one partition is alive at a time."""
+        streamable derived sources so only a bounded group of partitions
+        (`Config.stream_group_bytes`) is alive at a time."""
         if self._cached is not None or self._persist:
             blocks = self._blocks()
             for pid in sorted(blocks):
