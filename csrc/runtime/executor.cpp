@@ -974,7 +974,6 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
     for (int64_t st = 0; st < rows; st += chunk_rows) chunks.push_back({s, st, std::min(chunk_rows, rows - st)});
   }
   if (chunks.empty()) return;
-
   // device input ring
   size_t nin = feed_nodes_.size();
   std::vector<std::vector<at::Tensor>> ring(depth);
