@@ -77,6 +77,13 @@ def main():
         sys.exit(rc)
     if args.device == "cpu":
         os.environ["TFA_DEVICE"] = "cpu"
+    from tensorframes_amd.utils import faults
+    # a rank that loses its GPU context exits with EXIT_DEVICE_FAULT, so the
+    # launcher can re-run the job in fresh processes (TFA_MAX_RESTARTS)
+    faults.exit_on_device_fault(rank_main)(args)
+
+
+def rank_main(args):
     import tensorframes_amd as tfs
     from tensorframes_amd import tf
     from tensorframes_amd.frame.block import Block

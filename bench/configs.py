@@ -374,6 +374,11 @@ def main():
     if rc is not None:
         sys.exit(rc)
     _import_package()
+    from tensorframes_amd.utils import faults
+    faults.exit_on_device_fault(_rank_main)(a)
+
+
+def _rank_main(a):
     tfs.set_config(precision=a.precision)
     dist.init(force=a.force_collectives)
     if torch.cuda.is_available():

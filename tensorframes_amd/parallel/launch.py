@@ -37,11 +37,34 @@ def under_launcher() -> bool:
     return "WORLD_SIZE" in os.environ and "RANK" in os.environ
 
 
+EXIT_DEVICE_FAULT = 75  # == utils.faults.EXIT_DEVICE_FAULT (not imported: no package import here)
+
+
 def spawn(argv: Sequence[str], nprocs: int, extra_env: Optional[Dict[str, str]] = None,
-          timeout_s: Optional[float] = None) -> int:
+          timeout_s: Optional[float] = None, max_restarts: Optional[int] = None) -> int:
     """Run `python argv...` as `nprocs` ranks on this node; returns the first
     non-zero exit code (0 when every rank succeeded). A failing rank takes
-    the others down (they would block in a collective otherwise)."""
+    the others down (they would block in a collective otherwise).
+
+    When a rank exits with EXIT_DEVICE_FAULT (it lost its GPU context, see
+    `faults.exit_on_device_fault`) the whole job is re-run in fresh processes,
+    up to `max_restarts` times (default: TFA_MAX_RESTARTS, else 0); each
+    attempt sees TFA_RESTART_COUNT."""
+    if max_restarts is None:
+        max_restarts = int(os.environ.get("TFA_MAX_RESTARTS", "0"))
+    attempt = 0
+    while True:
+        env = dict(extra_env or {})
+        env["TFA_RESTART_COUNT"] = str(attempt)
+        rc = _spawn_once(argv, nprocs, env, timeout_s)
+        if rc != EXIT_DEVICE_FAULT or attempt >= max_restarts:
+            return rc
+        attempt += 1
+        print(f"[launch] a rank lost its GPU context (exit {rc}); restarting the job "
+              f"({attempt}/{max_restarts})", file=sys.stderr, flush=True)
+
+
+def _spawn_once(argv: Sequence[str], nprocs: int, extra_env: Dict[str, str], timeout_s: Optional[float]) -> int:
     port = free_port()
     procs: List[subprocess.Popen] = []
     for r in range(nprocs):

@@ -19,6 +19,14 @@ it is re-raised at once as `DeviceFaultError`, naming the node and kernel the
 executor was running (csrc/runtime/executor.cpp checks every launch). Other
 HIP errors (an invalid launch configuration, ...) are deterministic and not
 retried either.
+
+Recovery from a sticky fault happens one level up, in a fresh process: a rank
+whose entry point is wrapped in `exit_on_device_fault` exits with
+`EXIT_DEVICE_FAULT`, and the launcher (`parallel/launch.py`, `max_restarts` /
+`TFA_MAX_RESTARTS`) re-runs the whole job in new processes with new HIP
+contexts. Partition tasks are deterministic functions of their input
+partitions, so the re-run recomputes the same results (the reference's
+counterpart is Spark's task re-execution from lineage).
 """
 from __future__ import annotations
 
@@ -117,6 +125,35 @@ def check(site: str, partitions: Iterable[int]):
                 f.times -= 1
                 metrics.add("faults_injected")
                 raise f.exc(f"injected fault at {site} (partition {hit[0]}, rank {r})")
+
+
+EXIT_DEVICE_FAULT = 75  # exit status of a rank that lost its GPU context
+
+
+def exit_on_device_fault(fn: Callable):
+    """Decorator for a rank's entry point: a sticky GPU fault ends the process
+    with `EXIT_DEVICE_FAULT` (after logging it), so a supervising launcher can
+    re-run the job in fresh processes; other errors propagate unchanged."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(*a, **kw):
+        try:
+            return fn(*a, **kw)
+        except Exception as e:  # noqa: BLE001
+            if classify(e) != "sticky":
+                raise
+            logger.error("device fault, exiting for a fresh-process restart: %s", e)
+            import sys
+            sys.stderr.flush()
+            raise SystemExit(EXIT_DEVICE_FAULT) from e
+    return run
+
+
+def restart_count() -> int:
+    """How many times the launcher has re-run this job (0 = first attempt)."""
+    import os
+    return int(os.environ.get("TFA_RESTART_COUNT", "0"))
 
 
 def is_retryable(e: BaseException) -> bool:

@@ -61,3 +61,62 @@ def test_launcher_sets_rank_env(tmp_path):
     assert launch.spawn([str(script)], 4) == 0
     got = {p.name: p.read_text() for p in out.iterdir()}
     assert got == {str(r): f"{r},4,127.0.0.1" for r in range(4)}
+
+
+def _fault_script(tmp_path, fail_attempts):
+    """Rank 1 loses its 'GPU context' (a sticky-classified error) on the first
+    `fail_attempts` attempts of the job; every rank records its attempt."""
+    script = tmp_path / "sticky.py"
+    script.write_text(
+        "import os, sys\n"
+        f"sys.path.insert(0, {REPO!r})\n"
+        "from tensorframes_amd.utils import faults\n"
+        "@faults.exit_on_device_fault\n"
+        "def main():\n"
+        "    k = faults.restart_count()\n"
+        f"    open(os.path.join({str(tmp_path)!r}, f\"r{{os.environ['RANK']}}_a{{k}}\"), 'w').close()\n"
+        f"    if os.environ['RANK'] == '1' and k < {fail_attempts}:\n"
+        "        raise RuntimeError('HIP error: an illegal memory access was encountered (illegal address)')\n"
+        "main()\n")
+    return script
+
+
+def test_launcher_restarts_job_after_device_fault(tmp_path):
+    """A sticky GPU fault is never retried in-process: the rank exits with
+    EXIT_DEVICE_FAULT and the launcher re-runs the whole job in fresh
+    processes (new HIP contexts), up to max_restarts times."""
+    sys.path.insert(0, REPO)
+    from tensorframes_amd.parallel import launch
+    from tensorframes_amd.utils import faults
+    assert launch.EXIT_DEVICE_FAULT == faults.EXIT_DEVICE_FAULT
+    script = _fault_script(tmp_path, fail_attempts=1)
+    assert launch.spawn([str(script)], 2, max_restarts=1) == 0
+    names = {p.name for p in tmp_path.iterdir() if p.name.startswith("r")}
+    assert {"r0_a0", "r1_a0", "r0_a1", "r1_a1"} <= names
+
+
+def test_launcher_gives_up_after_max_restarts(tmp_path):
+    sys.path.insert(0, REPO)
+    from tensorframes_amd.parallel import launch
+    from tensorframes_amd.utils import faults
+    script = _fault_script(tmp_path, fail_attempts=5)
+    assert launch.spawn([str(script)], 2, max_restarts=1) == faults.EXIT_DEVICE_FAULT
+    assert launch.spawn([str(script)], 2, max_restarts=0) == faults.EXIT_DEVICE_FAULT
+
+
+def test_non_sticky_errors_are_not_turned_into_restarts(tmp_path):
+    sys.path.insert(0, REPO)
+    from tensorframes_amd.utils import faults
+
+    @faults.exit_on_device_fault
+    def bad():
+        raise ValueError("a validation error")
+    with pytest.raises(ValueError):
+        bad()
+
+    @faults.exit_on_device_fault
+    def sticky():
+        raise faults.DeviceFaultError("context lost")
+    with pytest.raises(SystemExit) as ei:
+        sticky()
+    assert ei.value.code == faults.EXIT_DEVICE_FAULT
