@@ -91,7 +91,10 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, force
     if use_gpu:
         torch.cuda.set_device(local_rank() % max(torch.cuda.device_count(), 1))
     kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
-    if backend == "nccl":
+    if backend == "nccl" and os.environ.get("TFA_NCCL_EAGER", "0") == "1":
+        # eager RCCL communicator creation (errors surface at init); by default
+        # the communicator is built at the first device collective, so jobs
+        # that never issue one (the map_blocks benchmark) never create it
         kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
     dist.init_process_group(**kwargs)
     _state["initialized_here"] = True
