@@ -18,6 +18,76 @@ namespace tfa {
 
 inline hipStream_t stream_of(const ExecCtx& c) { return static_cast<hipStream_t>(c.stream); }
 
+// one op of an elementwise chain absorbed into a GEMM/conv epilogue (the
+// planner's match; k::EpiCode / k::EpiOperand): `t` holds the tensor operand
+// (per-column [N], per-row [M,1], full, or a 1-element runtime scalar)
+struct EpiStep {
+  int code = k::EPI_ADD, kind = k::EPO_NONE, act = k::ACT_NONE;
+  double s = 0;
+  at::Tensor t;
+};
+
+// fills the kernel-side program (device pointers of contiguous operands)
+inline k::EpiProg epi_prog(const std::vector<EpiStep>* epi) {
+  k::EpiProg p;
+  if (!epi) return p;
+  TFA_CHECK(static_cast<int>(epi->size()) <= k::kMaxEpi, "epilogue chain too long");
+  for (const EpiStep& e : *epi) {
+    k::EpiOp& o = p.op[p.n++];
+    o.code = e.code;
+    o.kind = e.kind;
+    o.act = e.act;
+    o.s = e.s;
+    if (e.t.defined()) {
+      TFA_CHECK(e.t.is_contiguous(), "epilogue operand must be contiguous");
+      o.p = e.t.data_ptr();
+    }
+  }
+  return p;
+}
+
+inline at::Tensor apply_act_host(const at::Tensor& r, int act);
+
+// host (ATen) form of the chain over a result r (2-D view [rows, N])
+inline at::Tensor apply_epi_host(at::Tensor r, const std::vector<EpiStep>* epi) {
+  if (!epi) return r;
+  const int64_t N = r.size(-1);
+  for (const EpiStep& e : *epi) {
+    at::Tensor x;
+    switch (e.kind) {
+      case k::EPO_SCALAR: x = at::scalar_tensor(e.s, r.options()); break;
+      case k::EPO_SCALAR_PTR: x = e.t.reshape({}); break;
+      case k::EPO_COL: x = e.t.reshape({N}); break;
+      case k::EPO_ROW: x = e.t.reshape({r.numel() / N, 1}); break;
+      case k::EPO_FULL: x = e.t.reshape(r.sizes()); break;
+      default: break;
+    }
+    switch (e.code) {
+      case k::EPI_ADD: r = r + x; break;
+      case k::EPI_SUB: r = r - x; break;
+      case k::EPI_RSUB: r = x - r; break;
+      case k::EPI_MUL: r = r * x; break;
+      case k::EPI_DIV: r = r / x; break;
+      case k::EPI_RDIV: r = x / r; break;
+      case k::EPI_MAX: r = at::maximum(r, x.expand_as(r)); break;
+      case k::EPI_MIN: r = at::minimum(r, x.expand_as(r)); break;
+      case k::EPI_ACT: r = apply_act_host(r, e.act); break;
+      case k::EPI_NEG: r = -r; break;
+      case k::EPI_SQUARE: r = r * r; break;
+      case k::EPI_ABS: r = at::abs(r); break;
+      default: break;
+    }
+  }
+  return r;
+}
+
+// MatMul / Conv2D with a fused epilogue (bias [N], activation, absorbed chain);
+// shared by the ops and the planner's fused steps
+void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, bool tb,
+              const at::Tensor* bias, int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
+void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
+                int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
+
 // host (ATen) form of a fused epilogue activation (k::Act codes); same
 // formulas as the standalone ops
 inline at::Tensor apply_act_host(const at::Tensor& r, int act) {

@@ -388,13 +388,15 @@ void infer_matmul(InferCtx& c, bool batch) {
 
 // shared with the planner's fused GEMM epilogue
 void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, bool tb,
-              const at::Tensor* bias, int act, at::Tensor& out) {
+              const at::Tensor* bias, int act, at::Tensor& out, const std::vector<EpiStep>* epi) {
   if (!c.gpu) {
     at::Tensor a = ta ? a0.transpose(-1, -2) : a0;
     at::Tensor b = tb ? b0.transpose(-1, -2) : b0;
     at::Tensor r = at::matmul(a, b);
     if (bias) r = r + *bias;
-    out = apply_act_host(r, act).contiguous();
+    r = apply_act_host(r, act);
+    if (epi) r = apply_epi_host(r.reshape({-1, r.size(-1)}), epi).reshape(r.sizes());
+    out = r.contiguous();
     return;
   }
   require_gpu_dtype(a0, {at::kFloat, at::kDouble, at::kInt, at::kLong}, "MatMul");
@@ -422,6 +424,7 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
   g.ta = ta; g.tb = tb;
   g.bias = bias ? bias->data_ptr() : nullptr;
   g.act = act;
+  g.epi = epi_prog(epi);
   g.batch = batch;
   if (M == 0 || N == 0) return;
   if (K == 0) {

@@ -10,8 +10,6 @@
 
 namespace tfa {
 
-void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, bool tb,
-              const at::Tensor* bias, int act, at::Tensor& out);
 
 namespace {
 
@@ -91,7 +89,7 @@ void rows_batch(InferCtx& c) {
 
 // shared with the planner's fused conv epilogue
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
-                int act, at::Tensor& out) {
+                int act, at::Tensor& out, const std::vector<EpiStep>* epi) {
   Conv2DGeom g = conv_geom(c.node, x0.sizes().vec(), w0.sizes().vec());
   if (!c.gpu) {
     at::Tensor x = x0.permute({0, 3, 1, 2});
@@ -102,7 +100,9 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
                               at::IntArrayRef(pad), at::IntArrayRef(dil), 1);
     y = y.permute({0, 2, 3, 1});
     if (bias) y = y + *bias;
-    out = apply_act_host(y, act).contiguous();
+    y = apply_act_host(y, act);
+    if (epi) y = apply_epi_host(y.reshape({-1, g.OC}), epi).reshape(y.sizes());
+    out = y.contiguous();
     return;
   }
   require_gpu_dtype(x0, {at::kFloat}, "Conv2D");
@@ -115,6 +115,7 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
   a.x = x.data_ptr(); a.w = w.data_ptr(); a.y = out.data_ptr();
   a.bias = bias ? bias->data_ptr() : nullptr;
   a.act = act;
+  a.epi = epi_prog(epi);
   // `out` may be a channel slice of a wider NHWC tensor (concat write-into-slice)
   TFA_CHECK(out.stride(3) == 1 && out.stride(1) == out.size(2) * out.stride(2) &&
                 out.stride(0) == out.size(1) * out.stride(1),

@@ -342,22 +342,24 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
           if (ws)  // split-K partial slab [split][batch][M][N]
             ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = acc[i][j][r];
           else
-            static_cast<float*>(g.C)[bz * g.strideC + row * g.ldc + col] = act(acc[i][j][r] + bv);
+            static_cast<float*>(g.C)[bz * g.strideC + row * g.ldc + col] = act(acc[i][j][r] + bv, row, col);
         }
       }
     }
   };
-  if (ws || g.act <= ACT_RELU6)
-    epilogue([&](float v) { return act_fast(v, g.act); });
+  if (ws || (g.act <= ACT_RELU6 && g.epi.n == 0))
+    epilogue([&](float v, int64_t, int64_t) { return act_fast(v, g.act); });
   else
-    epilogue([&](float v) { return act_apply(v, g.act); });
+    epilogue([&](float v, int64_t row, int64_t col) {
+      return epi_apply(g.epi, act_apply(v, g.act), row, col, N, bz * M * N);
+    });
 }
 
 // split-K combine: fixed summation order over the splits (deterministic)
 __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ ws, float* __restrict__ C,
                                                      const float* __restrict__ bias, int64_t M, int64_t N,
                                                      int64_t ldc, int64_t strideC, int64_t batch,
-                                                     int splits, int act) {
+                                                     int splits, int act, EpiProg epi) {
   const int64_t total = batch * M * N;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
@@ -367,7 +369,7 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
     const int64_t row = (i / N) % M;
     const int64_t b = i / (M * N);
     if (bias) s += bias[col];
-    C[b * strideC + row * ldc + col] = act_apply(s, act);
+    C[b * strideC + row * ldc + col] = epi_apply(epi, act_apply(s, act), row, col, N, b * M * N);
   }
 }
 
@@ -559,7 +561,7 @@ void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream
     int64_t total = g.batch * g.M * g.N;
     hipLaunchKernelGGL(splitk_reduce, dim3(ew_grid(total)), dim3(256), 0, s, static_cast<const float*>(g.workspace),
                        static_cast<float*>(g.C), static_cast<const float*>(g.bias), g.M, g.N, g.ldc, g.strideC,
-                       g.batch, p.splits, g.act);
+                       g.batch, p.splits, g.act, g.epi);
   }
 }
 
@@ -603,6 +605,7 @@ GemmArgs conv_as_gemm(const ConvArgs& a) {
   g.act = a.act;
   g.batch = 1;
   g.workspace = a.workspace;
+  g.epi = a.epi;
   return g;
 }
 

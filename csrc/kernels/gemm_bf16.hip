@@ -289,15 +289,15 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
         for (int r = 0; r < 16; ++r) {
           const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           if (row >= M) continue;
-          static_cast<float*>(g.C)[row * g.ldc + col] = act(acc[i][j][r] + bv);
+          static_cast<float*>(g.C)[row * g.ldc + col] = act(acc[i][j][r] + bv, row, col);
         }
       }
     }
   };
-  if (g.act <= ACT_RELU6)
-    epilogue([&](float v) { return act_fast(v, g.act); });
+  if (g.act <= ACT_RELU6 && g.epi.n == 0)
+    epilogue([&](float v, int64_t, int64_t) { return act_fast(v, g.act); });
   else
-    epilogue([&](float v) { return act_apply(v, g.act); });
+    epilogue([&](float v, int64_t row, int64_t col) { return epi_apply(g.epi, act_apply(v, g.act), row, col, N, 0); });
 }
 
 int64_t padded_k(int64_t K) { return (K + kBK - 1) / kBK * kBK; }

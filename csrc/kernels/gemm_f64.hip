@@ -174,15 +174,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t row = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) + 4 * r;
-          if (row < M && col < N) C[row * g.ldc + col] = act(acc[i][j][r] + bv);
+          if (row < M && col < N) C[row * g.ldc + col] = act(acc[i][j][r] + bv, row, col);
         }
       }
     }
   };
-  if (g.act <= ACT_RELU6)
-    epilogue([&](double v) { return act_fast(v, g.act); });
+  if (g.act <= ACT_RELU6 && g.epi.n == 0)
+    epilogue([&](double v, int64_t, int64_t) { return act_fast(v, g.act); });
   else
-    epilogue([&](double v) { return act_apply(v, g.act); });
+    epilogue([&](double v, int64_t row, int64_t col) {
+      return epi_apply(g.epi, act_apply(v, g.act), row, col, N, bz * M * N);
+    });
 }
 
 // ============================================================== integer GEMM (VALU)

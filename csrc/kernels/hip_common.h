@@ -51,6 +51,41 @@ __device__ __forceinline__ T act_apply(T v, int act) {
   }
 }
 
+// the absorbed elementwise chain of a GEMM/conv epilogue at output (row, col)
+// of batch offset `boff` (elements); operands are contiguous [.., M, N]
+template <typename T>
+__device__ __forceinline__ T epi_apply(const EpiProg& e, T v, int64_t row, int64_t col, int64_t N, int64_t boff) {
+  for (int k = 0; k < e.n; ++k) {
+    const EpiOp& o = e.op[k];
+    const T* p = static_cast<const T*>(o.p);
+    T x = T(0);
+    switch (o.kind) {
+      case EPO_SCALAR: x = T(o.s); break;
+      case EPO_SCALAR_PTR: x = p[0]; break;
+      case EPO_COL: x = p[col]; break;
+      case EPO_ROW: x = p[row]; break;
+      case EPO_FULL: x = p[boff + row * N + col]; break;
+      default: break;
+    }
+    switch (o.code) {
+      case EPI_ADD: v = v + x; break;
+      case EPI_SUB: v = v - x; break;
+      case EPI_RSUB: v = x - v; break;
+      case EPI_MUL: v = v * x; break;
+      case EPI_DIV: v = v / x; break;
+      case EPI_RDIV: v = x / v; break;
+      case EPI_MAX: v = v > x ? v : x; break;
+      case EPI_MIN: v = v < x ? v : x; break;
+      case EPI_ACT: v = act_apply(v, o.act); break;
+      case EPI_NEG: v = -v; break;
+      case EPI_SQUARE: v = v * v; break;
+      case EPI_ABS: v = v < T(0) ? -v : v; break;
+      default: break;
+    }
+  }
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -117,6 +117,25 @@ void one_hot(DType dt, DType idt, const void* idx, void* out, int64_t n, int64_t
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2, ACT_SIGMOID = 3, ACT_TANH = 4, ACT_ELU = 5,
                  ACT_SELU = 6, ACT_SOFTPLUS = 7 };
 
+// Elementwise chain absorbed into the GEMM/conv epilogue: after bias and
+// activation, v = op_k(v, x_k) for k < n, where x_k is a scalar, a per-column
+// [N] vector, a per-row [M] vector or a full [batch, M, N] tensor (the
+// planner's match of ops that follow the product; formulas as the
+// standalone elementwise kernels)
+enum EpiCode : int { EPI_ADD = 0, EPI_SUB, EPI_RSUB, EPI_MUL, EPI_DIV, EPI_RDIV, EPI_MAX, EPI_MIN, EPI_ACT, EPI_NEG,
+                     EPI_SQUARE, EPI_ABS };
+enum EpiOperand : int { EPO_NONE = 0, EPO_SCALAR, EPO_SCALAR_PTR, EPO_COL, EPO_ROW, EPO_FULL };
+struct EpiOp {
+  int code = EPI_ADD, kind = EPO_NONE, act = ACT_NONE;
+  double s = 0;              // EPO_SCALAR value
+  const void* p = nullptr;   // device operand (same dtype as the output)
+};
+constexpr int kMaxEpi = 6;
+struct EpiProg {
+  int n = 0;
+  EpiOp op[kMaxEpi];
+};
+
 // C[b] = op(A[b]) @ op(B[b]) (+ bias[N]) (relu); row-major, leading dims in elements.
 struct GemmArgs {
   int64_t M, N, K;
@@ -128,6 +147,7 @@ struct GemmArgs {
   int act;           // epilogue activation: an Act code
   int64_t batch;
   void* workspace = nullptr;  // split-K partials (gemm_workspace_bytes)
+  EpiProg epi;                // absorbed elementwise chain (epi.n == 0: none)
 };
 // bytes of scratch the launch needs (0 = none); allocate before the launch
 size_t gemm_workspace_bytes(DType dt, const GemmArgs& g);
@@ -152,6 +172,7 @@ struct ConvArgs {
   const void* bias; int act;
   void* workspace = nullptr;
   int64_t ldc = 0;  // output pixel stride in elements (0 = OC; > OC writes a channel slice)
+  EpiProg epi;      // absorbed elementwise chain over the [N*OH*OW, OC] output
 };
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a);
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s);

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -22,10 +23,6 @@
 
 namespace tfa {
 
-void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, bool tb,
-              const at::Tensor* bias, int act, at::Tensor& out);
-void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
-                int act, at::Tensor& out);
 
 namespace {
 
@@ -78,6 +75,14 @@ const char* act_name(int act) {
   return act >= 0 && act < 8 ? names[act] : "?";
 }
 
+// transposition flags of MatMul (transpose_a/b) and BatchMatMul (adj_x/y)
+bool gemm_ta(const Node& nd) {
+  return nd.op == "MatMul" ? nd.attr_b("transpose_a", false) : nd.attr_b("adj_x", false);
+}
+bool gemm_tb(const Node& nd) {
+  return nd.op == "MatMul" ? nd.attr_b("transpose_b", false) : nd.attr_b("adj_y", false);
+}
+
 std::string strip0(const std::string& s) {
   if (s.size() > 2 && s.compare(s.size() - 2, 2, ":0") == 0) return s.substr(0, s.size() - 2);
   return s;
@@ -117,6 +122,13 @@ struct Program::Step {
   std::vector<const TensorInfo*> in_info;
   int bias_slot = -1;
   int act = 0;
+  // absorbed elementwise chain after bias/act (GEMM/CONV steps)
+  struct Epi {
+    int code, kind, act;
+    double s;
+    int slot;  // tensor operand slot (-1: none / constant scalar)
+  };
+  std::vector<Epi> epi;
   Shape gemm_shape;  // GEMM/CONV: the MatMul/Conv2D's own output shape (out_info may be a view of it)
   std::vector<int> release;  // slots dropped after the step
   // write-into-slice (GPU): a GEMM/CONV step whose only consumer is a
@@ -382,17 +394,25 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     // looking through single-consumer view ops (Reshape/Squeeze/ExpandDims/
     // Identity: same elements, same order) between them, e.g. the lifted
     // row-wise MatMul of map_rows: [B*1,k]x[k,n] -> Reshape [B,1,n] -> Squeeze -> Relu
-    bool gemm = nd.op == "MatMul" &&
+    bool gemm = (nd.op == "MatMul" || nd.op == "BatchMatMul" || nd.op == "BatchMatMulV2") &&
                 (infos[n][0].dtype == DType::F32 || infos[n][0].dtype == DType::F64);
     bool conv = nd.op == "Conv2D" && infos[n][0].dtype == DType::F32;
     if (gemm || conv) {
       st.kind = gemm ? Step::GEMM : Step::CONV;
       int cur = n;
       int64_t ncols = infos[n][0].shape.dims.back();
+      // the only consumer node of output 0 (it may read it twice: x * x)
       auto single = [&](int node) -> int {
         TensorRef r{node, 0};
-        if (fetched.count(r) || uses[r] != 1 || !consumer.count(node)) return -1;
-        return consumer[node];
+        if (fetched.count(r)) return -1;
+        if (uses[r] == 1 && consumer.count(node)) return consumer[node];
+        if (uses[r] == 2) {
+          for (int m : runtime) {
+            const auto& ins = g_->node(m).inputs;
+            if (std::count(ins.begin(), ins.end(), r) == 2) return m;
+          }
+        }
+        return -1;
       };
       auto is_view = [&](int node) {
         const std::string& op = g_->node(node).op;
@@ -449,6 +469,83 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
           absorbed.insert(c2);
           cur = c2;
         }
+      }
+      // ---- absorbed elementwise chain: ops that follow the product (and its
+      // bias / activation) one by one, each with a scalar, per-column [N],
+      // per-row or same-shaped operand, become the epilogue's program
+      const DType gdt = infos[n][0].dtype;
+      const bool batched = gemm && infos[n][0].shape.rank() > 2;
+      for (int k = 0; k < k::kMaxEpi; ++k) {
+        int lvk = cur;
+        int ck = next_op(cur, &lvk);
+        if (ck < 0) break;
+        const Node& cn = g_->node(ck);
+        const TensorRef cref{lvk, 0};
+        const TensorInfo& vin = infos[lvk][0];
+        const TensorInfo& oinf = infos[ck][0];
+        if (oinf.dtype != gdt || !oinf.shape.fully_known() || !(oinf.shape == vin.shape)) break;
+        Step::Epi e{k::EPI_ADD, k::EPO_NONE, k::ACT_NONE, 0.0, -1};
+        const int uact = epilogue_act(cn.op);
+        static const std::map<std::string, int> unary = {{"Neg", k::EPI_NEG}, {"Square", k::EPI_SQUARE},
+                                                         {"Abs", k::EPI_ABS}};
+        static const std::map<std::string, std::pair<int, int>> binary = {
+            {"Add", {k::EPI_ADD, k::EPI_ADD}},     {"AddV2", {k::EPI_ADD, k::EPI_ADD}},
+            {"Sub", {k::EPI_SUB, k::EPI_RSUB}},    {"Mul", {k::EPI_MUL, k::EPI_MUL}},
+            {"RealDiv", {k::EPI_DIV, k::EPI_RDIV}}, {"Div", {k::EPI_DIV, k::EPI_RDIV}},
+            {"Maximum", {k::EPI_MAX, k::EPI_MAX}}, {"Minimum", {k::EPI_MIN, k::EPI_MIN}}};
+        if (uact != k::ACT_NONE || unary.count(cn.op)) {
+          if (cn.inputs.empty() || !(cn.inputs[0] == cref)) break;
+          e.code = uact != k::ACT_NONE ? k::EPI_ACT : unary.at(cn.op);
+          e.act = uact;
+        } else if (binary.count(cn.op) && cn.inputs.size() == 2) {
+          const bool first = cn.inputs[0] == cref, second = cn.inputs[1] == cref;
+          if (first && second) {
+            if (cn.op != "Mul") break;
+            e.code = k::EPI_SQUARE;
+          } else if (first || second) {
+            e.code = first ? binary.at(cn.op).first : binary.at(cn.op).second;
+            const TensorRef& oref = cn.inputs[first ? 1 : 0];
+            const TensorInfo& oi = infos[oref.node][oref.index];
+            if (oi.dtype != gdt || !oi.shape.fully_known()) break;
+            const auto& od = oi.shape.dims;
+            const auto& vd = vin.shape.dims;
+            int64_t numel = 1;
+            for (int64_t d : od) numel *= d;
+            bool col = !od.empty() && od.back() == ncols && numel == ncols;
+            bool row = !batched && od.size() == vd.size() && !od.empty() && od.back() == 1 &&
+                       std::equal(od.begin(), od.end() - 1, vd.begin());
+            if (numel == 1) {
+              if (oi.value) {
+                e.kind = k::EPO_SCALAR;
+                e.s = oi.value->to(at::kDouble).reshape({}).item<double>();
+              } else {
+                e.kind = k::EPO_SCALAR_PTR;
+              }
+            } else if (col) {
+              e.kind = k::EPO_COL;
+            } else if (row) {
+              e.kind = k::EPO_ROW;
+            } else if (oi.shape == vin.shape) {
+              // a full-size operand that the elementwise fusion would compute
+              // on the fly (a Tile/broadcast/elementwise producer) stays
+              // there: reading it here would materialise it in HBM
+              const std::string& pop = g_->node(oref.node).op;
+              if (gpu_plan && fusion_enabled() && fusible_op(pop) && pop != "Identity") break;
+              e.kind = k::EPO_FULL;
+            } else {
+              break;
+            }
+            if (e.kind != k::EPO_SCALAR) e.slot = slot_for(oref);
+          } else {
+            break;
+          }
+        } else {
+          break;
+        }
+        st.epi.push_back(e);
+        for (int v = lvk; v != cur; v = g_->node(v).inputs[0].node) absorbed.insert(v);
+        absorbed.insert(ck);
+        cur = ck;
       }
       st.out_node = cur;
       st.gemm_shape = infos[n][0].shape;
@@ -572,6 +669,8 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
   for (size_t i = 0; i < p->steps.size(); ++i) {
     for (int s : p->steps[i].in_slots) last[s] = static_cast<int>(i);
     if (p->steps[i].bias_slot >= 0) last[p->steps[i].bias_slot] = static_cast<int>(i);
+    for (auto& e : p->steps[i].epi)
+      if (e.slot >= 0) last[e.slot] = static_cast<int>(i);
   }
   std::set<int> keep(p->fetch_slots.begin(), p->fetch_slots.end());
   for (auto& cs : p->const_slots) keep.insert(cs.first);
@@ -663,6 +762,20 @@ void Program::upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Dev
 }
 
 std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream) {
+  // operands of a step's absorbed epilogue chain (contiguous, on the step's device)
+  auto epi_steps = [](const Step& st, const std::vector<at::Tensor>& slots) {
+    std::vector<EpiStep> ep;
+    for (const auto& e : st.epi) {
+      EpiStep x;
+      x.code = e.code;
+      x.kind = e.kind;
+      x.act = e.act;
+      x.s = e.s;
+      if (e.slot >= 0) x.t = slots[e.slot].contiguous();
+      ep.push_back(std::move(x));
+    }
+    return ep;
+  };
   const OpRegistry& reg = OpRegistry::get();
   at::Device dev = inputs.empty() ? at::Device(at::kCPU) : inputs[0].device();
   bool gpu = dev.is_cuda();
@@ -733,10 +846,13 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           at::Tensor bias;
           if (st.bias_slot >= 0) bias = slots[st.bias_slot];
           const at::Tensor* bp = st.bias_slot >= 0 ? &bias : nullptr;
+          std::vector<EpiStep> ep = epi_steps(st, slots);
+          const std::vector<EpiStep>* epp = ep.empty() ? nullptr : &ep;
           if (st.kind == Step::GEMM)
-            run_gemm(c, c.in[0], c.in[1], nd.attr_b("transpose_a", false), nd.attr_b("transpose_b", false), bp, st.act, out);
+            run_gemm(c, c.in[0], c.in[1], gemm_ta(nd), gemm_tb(nd), bp, st.act, out,
+                     epp);
           else
-            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out);
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out, epp);
           c.out[0] = out;
         } else {
           at::Tensor out = gpu ? c.alloc_out(0) : at::Tensor();
@@ -747,10 +863,13 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           at::Tensor bias;
           if (st.bias_slot >= 0) bias = slots[st.bias_slot];
           const at::Tensor* bp = st.bias_slot >= 0 ? &bias : nullptr;
+          std::vector<EpiStep> ep = epi_steps(st, slots);
+          const std::vector<EpiStep>* epp = ep.empty() ? nullptr : &ep;
           if (st.kind == Step::GEMM)
-            run_gemm(c, c.in[0], c.in[1], nd.attr_b("transpose_a", false), nd.attr_b("transpose_b", false), bp, st.act, kout);
+            run_gemm(c, c.in[0], c.in[1], gemm_ta(nd), gemm_tb(nd), bp, st.act,
+                     kout, epp);
           else
-            run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout);
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout, epp);
           c.out[0] = viewed ? kout.reshape(st.out_info[0].shape.dims) : kout;
         }
       } catch (const GraphError& e) {
@@ -1109,6 +1228,17 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
     if (st.out_node != st.node) os << " -> " << g_->node(st.out_node).name;
     if (st.bias_slot >= 0) os << " +bias";
     if (st.act) os << " +" << act_name(st.act);
+    if (!st.epi.empty()) {
+      static const char* codes[] = {"add", "sub", "rsub", "mul", "div", "rdiv", "max", "min", "act", "neg", "square", "abs"};
+      static const char* kinds[] = {"", "scalar", "scalar", "col", "row", "full"};
+      os << " +epi[";
+      for (size_t k = 0; k < st.epi.size(); ++k) {
+        const auto& e = st.epi[k];
+        os << (k ? "," : "") << (e.code == k::EPI_ACT ? act_name(e.act) : codes[e.code]);
+        if (e.kind != k::EPO_NONE) os << ":" << kinds[e.kind];
+      }
+      os << "]";
+    }
     if (st.alias_slot >= 0) os << " ->concat-slice@" << st.alias_offset;
     if (!st.preplaced.empty()) {
       int n = 0;

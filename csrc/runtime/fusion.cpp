@@ -528,6 +528,8 @@ bool is_reduction_op(const std::string& op) {
 
 }  // namespace
 
+bool fusible_op(const std::string& op) { return op_table().count(op) > 0; }
+
 bool fusion_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("TFA_FUSION");

@@ -85,5 +85,7 @@ constexpr int kFusedEPT = 4;  // elements per thread
 
 // Disable with TFA_FUSION=0.
 bool fusion_enabled();
+// the op can be evaluated inside a fused elementwise region (no HBM value)
+bool fusible_op(const std::string& op);
 
 }  // namespace tfa

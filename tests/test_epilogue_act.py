@@ -73,3 +73,117 @@ def test_conv_bias_act_fused(dev, act):
     conv = torch.nn.functional.conv2d(xt, wt, padding=1).permute(0, 2, 3, 1) + torch.as_tensor(b).double()
     want = torch.as_tensor(ref(conv.numpy()))
     torch.testing.assert_close(got, want, rtol=2e-5, atol=2e-5)
+
+
+def _run(dev, g, fetch, feeds):
+    names = list(feeds)
+    prog = engine.program(g.serialize(), [fetch], names)
+    ins = [torch.as_tensor(feeds[n]).to(dev) for n in names]
+    plan = prog.describe(ins, dev.type == "cuda")
+    return plan, engine.run_program(prog, ins, dev)[0].cpu().double().numpy()
+
+
+@pytest.mark.parametrize("dtype,m,n,k", [(np.float32, 3000, 96, 128), (np.float32, 300, 32, 2048),
+                                         (np.float64, 1000, 64, 100)])
+def test_matmul_absorbs_elementwise_chain(dev, dtype, m, n, k):
+    """relu(x@W + b) * 0.5 + c[N] - z[M,N] (z a feed) , then max with r[M,1]
+    and a square: ONE GEMM step whose epilogue runs the whole chain."""
+    rng = np.random.default_rng(7)
+    tdt = tf.float32 if dtype == np.float32 else tf.float64
+    w = (rng.standard_normal((k, n)) / np.sqrt(k)).astype(dtype)
+    b, c = rng.uniform(-1, 1, n).astype(dtype), rng.uniform(-1, 1, n).astype(dtype)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tdt, [None, k], name="x")
+        z = tf.placeholder(tdt, [None, n], name="z")
+        r = tf.placeholder(tdt, [None, 1], name="r")
+        h = tf.nn.relu(tf.nn.bias_add(tf.matmul(x, tf.constant(w)), tf.constant(b)))
+        h = (h * 0.5 + tf.constant(c)) - z
+        h = tf.maximum(h, r)
+        tf.multiply(h, h, name="y")
+    x_ = rng.uniform(-2, 2, (m, k)).astype(dtype)
+    z_ = rng.uniform(-1, 1, (m, n)).astype(dtype)
+    r_ = rng.uniform(-1, 1, (m, 1)).astype(dtype)
+    plan, got = _run(dev, g, "y", {"x": x_, "z": z_, "r": r_})
+    assert "+bias +relu +epi[mul:scalar,add:col,sub:full,max:row,square]" in plan, plan
+    assert "plan: 1 steps" in plan, plan
+    h = np.maximum(x_.astype(np.float64) @ w.astype(np.float64) + b, 0) * 0.5 + c - z_
+    want = np.maximum(h, r_) ** 2
+    tol = (4e-7 * 3 * k + 1e-5) if dtype == np.float32 else 1e-10
+    np.testing.assert_allclose(got, want, rtol=tol, atol=tol)
+
+
+def test_matmul_chain_reversed_operands_and_runtime_scalar(dev):
+    """2 / (x@W) style reversed operands (rdiv, rsub) and a 1-element runtime
+    tensor operand."""
+    rng = np.random.default_rng(8)
+    w = (rng.standard_normal((64, 48)) / 8).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 64], name="x")
+        s = tf.placeholder(tf.float32, [], name="s")
+        h = tf.matmul(x, tf.constant(w))
+        h = 3.0 - tf.abs(h)                 # rsub:scalar after abs
+        h = tf.constant(2.0, tf.float32) / h  # rdiv:scalar
+        tf.multiply(s, tf.tanh(h), name="y")  # tanh, mul by runtime scalar
+    x_ = rng.uniform(-0.2, 0.2, (500, 64)).astype(np.float32)
+    plan, got = _run(dev, g, "y", {"x": x_, "s": np.float32(1.5)})
+    assert "+epi[abs,rsub:scalar,rdiv:scalar,tanh,mul:scalar]" in plan, plan
+    want = 1.5 * np.tanh(2.0 / (3.0 - np.abs(x_.astype(np.float64) @ w)))
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-5)
+
+
+def test_batch_matmul_chain_full_and_col(dev):
+    rng = np.random.default_rng(9)
+    g = tf.Graph()
+    c = rng.uniform(-1, 1, 24).astype(np.float32)
+    with g.as_default():
+        a = tf.placeholder(tf.float32, [None, 40, 32], name="a")
+        bm = tf.placeholder(tf.float32, [None, 32, 24], name="b")
+        z = tf.placeholder(tf.float32, [None, 40, 24], name="z")
+        tf.add(tf.matmul(a, bm) * tf.constant(c), z, name="y")
+    a_ = rng.uniform(-1, 1, (3, 40, 32)).astype(np.float32)
+    b_ = rng.uniform(-1, 1, (3, 32, 24)).astype(np.float32)
+    z_ = rng.uniform(-1, 1, (3, 40, 24)).astype(np.float32)
+    plan, got = _run(dev, g, "y", {"a": a_, "b": b_, "z": z_})
+    assert "+epi[mul:col,add:full]" in plan, plan
+    want = (a_.astype(np.float64) @ b_.astype(np.float64)) * c + z_
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-5)
+
+
+def test_conv_absorbs_chain(dev):
+    rng = np.random.default_rng(10)
+    w = (rng.standard_normal((3, 3, 8, 16)) * 0.1).astype(np.float32)
+    b = rng.uniform(-1, 1, 16).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 10, 10, 8], name="x")
+        z = tf.placeholder(tf.float32, [None, 10, 10, 16], name="z")
+        h = tf.nn.relu(tf.nn.bias_add(tf.nn.conv2d(x, tf.constant(w), [1, 1, 1, 1], "SAME"), tf.constant(b)))
+        tf.add(h * 2.0, z, name="y")  # residual add
+    x_ = rng.uniform(-1, 1, (2, 10, 10, 8)).astype(np.float32)
+    z_ = rng.uniform(-1, 1, (2, 10, 10, 16)).astype(np.float32)
+    plan, got = _run(dev, g, "y", {"x": x_, "z": z_})
+    assert "+bias +relu +epi[mul:scalar,add:full]" in plan, plan
+    xt = torch.as_tensor(x_).double().permute(0, 3, 1, 2)
+    wt = torch.as_tensor(w).double().permute(3, 2, 0, 1)
+    conv = torch.nn.functional.conv2d(xt, wt, padding=1).permute(0, 2, 3, 1) + torch.as_tensor(b).double()
+    want = torch.clamp_min(conv, 0).numpy() * 2.0 + z_
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-5)
+
+
+def test_chain_stops_at_fetched_intermediate(dev):
+    """An intermediate that is also fetched stays materialised: the chain ends there."""
+    rng = np.random.default_rng(11)
+    w = rng.standard_normal((16, 8)).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 16], name="x")
+        h = tf.multiply(tf.matmul(x, tf.constant(w)), 2.0, name="h")
+        tf.add(h, 1.0, name="y")
+    prog = engine.program(g.serialize(), ["h", "y"], ["x"])
+    x_ = torch.as_tensor(rng.uniform(-1, 1, (64, 16)).astype(np.float32)).to(dev)
+    plan = prog.describe([x_], dev.type == "cuda")
+    assert "+epi[mul:scalar]" in plan and "add" not in plan.split("+epi[mul:scalar]")[1].split("\n")[0], plan
+    h_, y_ = [o.cpu().numpy() for o in engine.run_program(prog, [x_], dev)]
+    np.testing.assert_allclose(y_, h_ + 1.0, rtol=1e-6)

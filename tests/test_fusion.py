@@ -32,11 +32,12 @@ def test_kmeans_distance_chain_is_one_kernel():
     prog = engine.program(gb, ["indexes", "min_distances"], ["features"])
     x = [torch.zeros(25000, 100, dtype=torch.float64)]
     plan = prog.describe(x, True)
-    # t1 + t2 - 2 * prods (two Tiles, ExpandDims, Add, Mul, Sub) evaluated inside the
-    # ArgMin/Min row reduction; Square -> Sum as one row reduction; GEMM kept
-    assert "FUSED-ROWRED indexes [Tile ExpandDims Tile Add Mul Sub -> ArgMin Min]" in plan, plan
+    # 2 * prods runs in the GEMM epilogue; t1 + t2 - (2 * prods) (two Tiles,
+    # ExpandDims, Add, Sub) is evaluated inside the ArgMin/Min row reduction;
+    # Square -> Sum as one row reduction
+    assert "FUSED-ROWRED indexes [Tile ExpandDims Tile Add Sub -> ArgMin Min]" in plan, plan
     assert "FUSED-ROWRED distances/Sum [Square -> Sum]" in plan, plan
-    assert "GEMM MatMul distances/MatMul" in plan
+    assert "GEMM MatMul distances/MatMul -> distances/mul +epi[mul:scalar]" in plan, plan
     assert plan.startswith("plan: 3 steps"), plan  # was 9 unfused kernels
     # the host plan is unfused (ATen oracle path)
     assert "FUSED" not in prog.describe(x)
@@ -47,7 +48,7 @@ def test_distance_chain_fetched_is_an_elementwise_region():
     prog = engine.program(gb, ["d"], ["features"])
     plan = prog.describe([torch.zeros(1000, 100, dtype=torch.float64)], True)
     # (the constant t1 = tile(center_squares) is folded on the host at this size)
-    assert "FUSED d [ExpandDims Tile Add Mul Sub Identity]" in plan, plan
+    assert "FUSED d [ExpandDims Tile Add Sub Identity]" in plan, plan
 
 
 def test_generated_sources_compile_for_gfx950():
