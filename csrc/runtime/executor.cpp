@@ -75,6 +75,15 @@ const char* act_name(int act) {
   return act >= 0 && act < 8 ? names[act] : "?";
 }
 
+// TFA_EPI_CHAIN=0: GEMM/conv epilogues absorb bias and one activation only
+bool epi_chain_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TFA_EPI_CHAIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // transposition flags of MatMul (transpose_a/b) and BatchMatMul (adj_x/y)
 bool gemm_ta(const Node& nd) {
   return nd.op == "MatMul" ? nd.attr_b("transpose_a", false) : nd.attr_b("adj_x", false);
@@ -475,7 +484,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
       // per-row or same-shaped operand, become the epilogue's program
       const DType gdt = infos[n][0].dtype;
       const bool batched = gemm && infos[n][0].shape.rank() > 2;
-      for (int k = 0; k < k::kMaxEpi; ++k) {
+      for (int k = 0; k < (epi_chain_enabled() ? k::kMaxEpi : 0); ++k) {
         int lvk = cur;
         int ck = next_op(cur, &lvk);
         if (ck < 0) break;
