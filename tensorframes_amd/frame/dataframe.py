@@ -81,7 +81,7 @@ class _Derived(_Source):
         for pid, b in self._parent._iter_blocks():
             group[pid] = b
             nbytes += _block_bytes(b)
-            if nbytes >= config.stream_group_bytes:
+            if nbytes >= config.stream_group_bytes or len(group) >= _MAX_GROUP_PARTITIONS:
                 yield from self._run_group(group)
                 group, nbytes = {}, 0
         if group:
@@ -93,8 +93,16 @@ class _Derived(_Source):
             yield pid, res[pid]
 
 
+_MAX_GROUP_PARTITIONS = 16  # bound for columns whose size is only estimated
+
+
 def _block_bytes(b: Block) -> int:
-    return sum(c.numel() * c.element_size() for c in b.columns.values() if isinstance(c, torch.Tensor))
+    """Bytes of the block's tensor columns; other columns (strings, ragged
+    cells) count 64 bytes per row."""
+    n = 0
+    for c in b.columns.values():
+        n += c.numel() * c.element_size() if isinstance(c, torch.Tensor) else 64 * b.nrows
+    return n
 
 
 # ------------------------------------------------------------------ DataFrame
