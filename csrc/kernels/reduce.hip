@@ -608,15 +608,18 @@ int64_t useg_tile(int64_t inner) {
 
 // row blocks of the LDS-private pass: at least 4 rows per segment and 32 per
 // block, so the partial slabs (B x nseg x inner) stay well below the input
-// they summarise, and at most 8192 blocks
-int64_t useg_rows_per_block(int64_t n, int64_t nseg) {
+// they summarise; at most 8192 blocks and 256 MB of slabs
+int64_t useg_rows_per_block(int64_t n, int64_t nseg, int64_t inner) {
   int64_t rpb = std::max<int64_t>(32, 4 * nseg);
   rpb = std::max<int64_t>(rpb, (n + 8191) / 8192);
+  const int64_t max_blocks = std::max<int64_t>(1, (int64_t(256) << 20) / std::max<int64_t>(1, nseg * inner * 8));
+  rpb = std::max<int64_t>(rpb, (n + max_blocks - 1) / max_blocks);
   return (rpb + 7) / 8 * 8;
 }
 
-int64_t useg_blocks(int64_t n, int64_t nseg) {
-  return std::max<int64_t>(1, (n + useg_rows_per_block(n, nseg) - 1) / useg_rows_per_block(n, nseg));
+int64_t useg_blocks(int64_t n, int64_t nseg, int64_t inner) {
+  const int64_t rpb = useg_rows_per_block(n, nseg, inner);
+  return std::max<int64_t>(1, (n + rpb - 1) / rpb);
 }
 
 }  // namespace
@@ -711,7 +714,7 @@ static bool useg_fits_lds(int64_t inner, int64_t nseg) {
 static size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
 size_t unsorted_segment_workspace_bytes(RedOp, DType, int64_t n, int64_t inner, int64_t nseg) {
-  if (useg_fits_lds(inner, nseg)) return static_cast<size_t>(useg_blocks(n, nseg)) * nseg * inner * 8;
+  if (useg_fits_lds(inner, nseg)) return static_cast<size_t>(useg_blocks(n, nseg, inner)) * nseg * inner * 8;
   return align256(n * 8) + align256((nseg + 1) * 8) + segment_csr_workspace_bytes(n, nseg);
 }
 
@@ -755,8 +758,8 @@ static void useg_typed(const void* x, const void* ids, void* y, int64_t n, int64
   size_t lds = static_cast<size_t>(nseg * tile * sizeof(A));
   TFA_CHECK(lds <= kUsegLds, "unsorted segment reduce: ", nseg, " segments x ", tile,
             " columns exceed the LDS budget");
-  const int64_t rpb = useg_rows_per_block(n, nseg);
-  const int64_t B = useg_blocks(n, nseg);
+  const int64_t rpb = useg_rows_per_block(n, nseg, inner);
+  const int64_t B = useg_blocks(n, nseg, inner);
   dim3 grid((unsigned)B, (unsigned)((inner + tile - 1) / tile));
   hipLaunchKernelGGL((useg_private<T, I, OP>), grid, dim3((unsigned)tile), lds, s, (const T*)x, (const I*)ids,
                      (A*)ws, n, inner, nseg, rpb);
