@@ -130,12 +130,14 @@ struct Program::Step {
   std::vector<TensorInfo> out_info;
   std::vector<const TensorInfo*> in_info;
   int bias_slot = -1;
+  TensorRef bias_ref{-1, 0};  // planning: resolved to bias_slot when the step is placed
   int act = 0;
   // absorbed elementwise chain after bias/act (GEMM/CONV steps)
   struct Epi {
     int code, kind, act;
     double s;
-    int slot;  // tensor operand slot (-1: none / constant scalar)
+    int slot;       // tensor operand slot (-1: none / constant scalar)
+    TensorRef ref;  // planning: the operand, resolved to `slot` when the step is placed
   };
   std::vector<Epi> epi;
   Shape gemm_shape;  // GEMM/CONV: the MatMul/Conv2D's own output shape (out_info may be a view of it)
@@ -393,7 +395,36 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
 
   const OpRegistry& reg = OpRegistry::get();
   std::set<int> absorbed;
+  // a fused GEMM/CONV step is placed at its LAST absorbed node: the operands of
+  // its bias / epilogue chain may be produced by nodes that come after the
+  // MatMul in topological order (they all come before the chain's last op)
+  auto place = [&](Step& st) {
+    if (st.bias_ref.node >= 0) st.bias_slot = slot_for(st.bias_ref);
+    for (auto& e : st.epi)
+      if (e.ref.node >= 0) e.slot = slot_for(e.ref);
+    const Node& nd = g_->node(st.node);
+    const OpDef* od = reg.find(nd.op);
+    TFA_CHECK(od && od->compute, "op '", nd.op, "' has no compute function");
+    for (auto& r : nd.inputs) {
+      st.in_slots.push_back(slot_for(r));
+      st.in_info.push_back(&infos[r.node][r.index]);
+    }
+    st.out_info = infos[st.out_node];
+    for (size_t k = 0; k < infos[st.out_node].size(); ++k) {
+      int s = new_slot();
+      slot_of[{st.out_node, static_cast<int>(k)}] = s;
+      st.out_slots.push_back(s);
+    }
+    p->steps.push_back(std::move(st));
+  };
+  std::map<int, Step> deferred;  // out_node -> fused step waiting for its placement
   for (int n : runtime) {
+    auto dit = deferred.find(n);
+    if (dit != deferred.end()) {
+      place(dit->second);
+      deferred.erase(dit);
+      continue;
+    }
     if (absorbed.count(n)) continue;
     const Node& nd = g_->node(n);
     Step st;
@@ -460,7 +491,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
           bool ok = bi.shape.rank() == 1 && bi.shape.dims[0] == ncols && bi.dtype == infos[n][0].dtype &&
                     infos[c1][0].shape == infos[lv][0].shape;
           if (ok) {
-            st.bias_slot = slot_for(br);
+            st.bias_ref = br;
             for (int v = lv; v != cur; v = g_->node(v).inputs[0].node) absorbed.insert(v);
             absorbed.insert(c1);
             cur = c1;
@@ -493,7 +524,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
         const TensorInfo& vin = infos[lvk][0];
         const TensorInfo& oinf = infos[ck][0];
         if (oinf.dtype != gdt || !oinf.shape.fully_known() || !(oinf.shape == vin.shape)) break;
-        Step::Epi e{k::EPI_ADD, k::EPO_NONE, k::ACT_NONE, 0.0, -1};
+        Step::Epi e{k::EPI_ADD, k::EPO_NONE, k::ACT_NONE, 0.0, -1, TensorRef{-1, 0}};
         const int uact = epilogue_act(cn.op);
         static const std::map<std::string, int> unary = {{"Neg", k::EPI_NEG}, {"Square", k::EPI_SQUARE},
                                                          {"Abs", k::EPI_ABS}};
@@ -544,7 +575,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
             } else {
               break;
             }
-            if (e.kind != k::EPO_SCALAR) e.slot = slot_for(oref);
+            if (e.kind != k::EPO_SCALAR) e.ref = oref;
           } else {
             break;
           }
@@ -560,20 +591,13 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
       st.gemm_shape = infos[n][0].shape;
       if (cur != n) p->fused++;
     }
-    const OpDef* od = reg.find(nd.op);
-    TFA_CHECK(od && od->compute, "op '", nd.op, "' has no compute function");
-    for (auto& r : nd.inputs) {
-      st.in_slots.push_back(slot_for(r));
-      st.in_info.push_back(&infos[r.node][r.index]);
+    if (st.out_node != n) {
+      deferred.emplace(st.out_node, std::move(st));
+      continue;
     }
-    st.out_info = infos[st.out_node];
-    for (size_t k = 0; k < infos[st.out_node].size(); ++k) {
-      int s = new_slot();
-      slot_of[{st.out_node, static_cast<int>(k)}] = s;
-      st.out_slots.push_back(s);
-    }
-    p->steps.push_back(std::move(st));
+    place(st);
   }
+  TFA_CHECK(deferred.empty(), "internal: a fused step was never placed");
   // ---- elementwise-region fusion (GPU plans): regions replace their member steps
   if (gpu_plan && fusion_enabled()) {
     FusionInput fi;

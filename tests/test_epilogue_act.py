@@ -187,3 +187,26 @@ def test_chain_stops_at_fetched_intermediate(dev):
     assert "+epi[mul:scalar]" in plan and "add" not in plan.split("+epi[mul:scalar]")[1].split("\n")[0], plan
     h_, y_ = [o.cpu().numpy() for o in engine.run_program(prog, [x_], dev)]
     np.testing.assert_allclose(y_, h_ + 1.0, rtol=1e-6)
+
+
+def test_chain_operand_produced_after_the_matmul(dev):
+    """The chain's full-size operand is computed by a node that follows the
+    MatMul in topological order: the fused step runs at the chain's last op."""
+    rng = np.random.default_rng(12)
+    w = rng.standard_normal((16, 8)).astype(np.float32)
+    b = rng.standard_normal(8).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 16], name="x")
+        x3 = tf.placeholder(tf.float32, [None, 8, 4], name="x3")
+        h = tf.nn.bias_add(tf.matmul(x, tf.constant(w)), tf.constant(b))
+        z = tf.reduce_sum(x3, [2])          # produced after the MatMul
+        c = tf.reduce_max(x3, [1, 2])        # per-row [M] -> [M, 1]
+        tf.subtract(h, z) * tf.reshape(c, [-1, 1])
+        tf.identity(tf.subtract(h, z) * tf.reshape(c, [-1, 1]), name="y")
+    x_ = rng.uniform(-1, 1, (64, 16)).astype(np.float32)
+    x3_ = rng.uniform(-1, 1, (64, 8, 4)).astype(np.float32)
+    plan, got = _run(dev, g, "y", {"x": x_, "x3": x3_})
+    assert "+bias +epi[sub:full" in plan, plan
+    want = (x_.astype(np.float64) @ w + b - x3_.sum(2)) * x3_.max((1, 2))[:, None]
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
