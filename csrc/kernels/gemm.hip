@@ -8,8 +8,9 @@
 //
 //  * k-major LDS images (As[k][m], Bs[k][n]): every MFMA operand read is 32
 //    consecutive floats per half-wave (conflict-free ds_read_b32);
-//  * two LDS stages; the next K tile's global loads are issued before the
-//    current tile's MFMAs (register-staged pipeline, one barrier per tile);
+//  * two LDS stages; the next K tile's global loads are issued during the
+//    current tile's MFMAs (register-staged pipeline, one barrier per tile),
+//    with every memory op interleaved between MFMAs (sched_group_barrier);
 //  * bias + ReLU/ReLU6 fused into the epilogue (or into the split-K reducer);
 //  * XCD-aware bijective block->tile remap: blocks sharing an A row panel
 //    run on one XCD and share its L2.
@@ -63,8 +64,31 @@ __device__ __forceinline__ float4 ld4_fast(const float* p) {
   return make_float4(p[0], p[1], p[2], p[3]);
 }
 
+// sched_group_barrier masks (LLVM AMDGPU): MFMA, VMEM read, DS read, DS write
+constexpr int kSchedMfma = 0x008, kSchedVmemRead = 0x020, kSchedDsRead = 0x100, kSchedDsWrite = 0x200;
+
+// ops [J, END) of a k-step whose first O1 ops have mask M1 and the rest M2
+template <int J, int END, int O1, int M1, int M2>
+__device__ __forceinline__ void sched_ops() {
+  if constexpr (J < END) {
+    __builtin_amdgcn_sched_group_barrier(J < O1 ? M1 : M2, 1, 0);
+    sched_ops<J + 1, END, O1, M1, M2>();
+  }
+}
+// a k-step of NM MFMAs and O memory ops: slot I gets ops [I*O/NM, (I+1)*O/NM)
+// (rounded up), then one MFMA
+template <int I, int NM, int O, int O1, int M1, int M2>
+__device__ __forceinline__ void sched_interleave() {
+  if constexpr (I < NM) {
+    constexpr int lo = (I * O + NM - 1) / NM, hi = ((I + 1) * O + NM - 1) / NM;
+    sched_ops<lo, hi, O1, M1, M2>();
+    __builtin_amdgcn_sched_group_barrier(kSchedMfma, 1, 0);
+    sched_interleave<I + 1, NM, O, O1, M1, M2>();
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
-__global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
+__global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
                                                          int64_t k_per_split) {
   constexpr int LDA = BM + 4, LDB = BN + 4;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -280,6 +304,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int ktiles = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+  // instructions per tile, for the interleaved schedule: global loads (a
+  // non-vector piece is 4 scalar loads), LDS writes (a k-major image of a
+  // k-contiguous operand is 4 scalar stores per piece), LDS reads per k-step
+  constexpr int S = BK / 2, NM = TM * TN, R = TM + TN;
+  constexpr int L = (VEC ? 1 : 4) * (AP + BP);
+  constexpr int W = AP * (AL == A_MCONTIG ? 1 : 4) + BP * (TB ? 4 : 1);
   auto mainloop = [&](auto chk) {
     if (ktiles > 0) {
       load(kbeg, chk);
@@ -287,12 +317,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
     }
     __syncthreads();
     int cur = 0;
-    for (int kt = 0; kt < ktiles; ++kt) {
-      const bool has_next = kt + 1 < ktiles;
-      if (has_next) load(kbeg + (int64_t)(kt + 1) * BK, chk);
-      // LDS operand reads run one k-step ahead of the MFMAs that use them
-      // (software pipelined; sched_barriers keep the compiler from sinking the
-      // reads next to their consumers, which exposed the LDS latency per step)
+    // One k tile. The next tile's global loads (first k-step), the next
+    // k-step's LDS operand reads (every k-step) and the next stage's LDS
+    // writes (last k-step) are spread between the MFMAs with
+    // sched_group_barrier instead of being issued as a block: each wave keeps
+    // the MFMA pipe fed while its memory ops are in flight (measured +5% on
+    // 128x128, and what makes the 256x128 tile pay; scripts/bigtile_lab.hip).
+    // The last tile is peeled off so the loop body has no branch.
+    auto tile = [&](int64_t knext, auto more) {
+      constexpr bool NEXT = decltype(more)::value;
       float a[2][TM], b[2][TN];
       auto rd = [&](int buf, int kk) {
         const int kr = kk + (lane >> 5);
@@ -302,21 +335,31 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_tile(GemmArgs g, int tiles_m,
         for (int j = 0; j < TN; ++j) b[buf][j] = Bs[cur][kr][wn * (BN / WN) + j * 32 + (lane & 31)];
       };
       rd(0, 0);
+      __builtin_amdgcn_sched_group_barrier(kSchedDsRead, R, 0);
+      if constexpr (NEXT) load(knext, chk);
 #pragma unroll
-      for (int kk = 0; kk < BK / 2; ++kk) {
-        if (kk + 1 < BK / 2) rd((kk + 1) & 1, 2 * (kk + 1));
-        __builtin_amdgcn_sched_barrier(0);
+      for (int kk = 0; kk < S; ++kk) {
+        if (kk + 1 < S) rd((kk + 1) & 1, 2 * (kk + 1));
+        if (NEXT && kk == S - 1) store(cur ^ 1);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk & 1][i], b[kk & 1][j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+        if (kk == 0 && NEXT)
+          sched_interleave<0, NM, L + R, L, kSchedVmemRead, kSchedDsRead>();
+        else if (kk == S - 1 && NEXT)
+          sched_interleave<0, NM, W, W, kSchedDsWrite, kSchedDsWrite>();
+        else if (kk + 1 < S)
+          sched_interleave<0, NM, R, R, kSchedDsRead, kSchedDsRead>();
+        else
+          __builtin_amdgcn_sched_group_barrier(kSchedMfma, NM, 0);
       }
-      if (has_next) store(cur ^ 1);
       __syncthreads();
       cur ^= 1;
-    }
+    };
+    for (int kt = 0; kt + 1 < ktiles; ++kt) tile(kbeg + (int64_t)(kt + 1) * BK, std::true_type{});
+    if (ktiles > 0) tile(0, std::false_type{});
   };
   const bool interior = m0 + BM <= M && n0 + BN <= N && (kend - kbeg) % BK == 0;
   if (interior)
@@ -381,12 +424,14 @@ struct F32Plan {
   int64_t k_per_split;
 };
 
-// measured (scripts/gemm_bench.py): 256x128 / 128x256 and BK=32 variants were slower on every shape
+// measured (scripts/gemm_bench.py, scripts/bigtile_lab.hip): 128x256 and BK=32 variants were slower on every
+// shape; 256x128 (wave tile 128x64) pays only with the interleaved schedule (+8-12% on big GEMMs) and
+// loses on grids of a few hundred blocks
 // {BM, BN}; the N-widths 96/160/192 fit Inception-style channel counts without
 // padding a 128-wide tile (a 128 tile on N=96 computes 25% zeros)
-constexpr int kNumTiles = 9;
+constexpr int kNumTiles = 10;
 constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
-                                      {128, 96}, {128, 192}, {128, 160}, {64, 192}};
+                                      {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128}};
 
 int64_t tile_blocks(int c, int64_t M, int64_t N, int64_t batch) {
   return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
@@ -421,6 +466,7 @@ int tile_env() { return forced_tile().load(); }
 F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
   // narrow N picks a narrow tile (a 128-wide tile on N=32 wastes 3/4 of the MFMAs)
   int cfg = N <= 32 ? 4 : (N <= 64 ? 1 : 0);
+  if (cfg == 0 && N >= 256 && tile_blocks(9, M, N, batch) >= 2048) cfg = 9;  // big GEMMs: 256x128
   // too few blocks to fill 256 CUs twice: shrink the tile
   if (tile_blocks(cfg, M, N, batch) < 512) {
     if (cfg == 0) cfg = N > 96 ? 2 : 3;
@@ -448,7 +494,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 5: TFA_LAUNCH_TILE(128, 96, 4, 1); break;
     case 6: TFA_LAUNCH_TILE(128, 192, 2, 2); break;
     case 7: TFA_LAUNCH_TILE(128, 160, 4, 1); break;
-    default: TFA_LAUNCH_TILE(64, 192, 2, 2); break;
+    case 8: TFA_LAUNCH_TILE(64, 192, 2, 2); break;
+    default: TFA_LAUNCH_TILE(256, 128, 2, 2); break;
   }
 #undef TFA_LAUNCH_TILE
 }

@@ -57,12 +57,30 @@ def timeit(prog, ins, iters):
     return s.elapsed_time(e) / iters
 
 
+def vendor_time(fn, iters):
+    for _ in range(2):  # library heuristics / MIOpen find on the first calls
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default=None)
     ap.add_argument("--f64-only", action="store_true")
+    ap.add_argument("--vendor", action="store_true",
+                    help="also time the same op through the ROCm libraries (torch.matmul -> hipBLASLt/rocBLAS, "
+                         "F.conv2d -> MIOpen), exact f32 (no TF32/xf32), same bias+ReLU epilogue")
     a = ap.parse_args()
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
     res = []
@@ -78,6 +96,13 @@ def main():
         xin = torch.randn((m, k), device=dev)
         ms = timeit(prog, [xin], a.iters)
         r = {"kind": "gemm", "M": m, "N": n, "K": k, "ms": ms, "tflops": 2 * m * n * k / ms / 1e9}
+        if a.vendor:
+            wt = torch.randn((k, n), device=dev)
+            bt = torch.randn((n,), device=dev)
+            fn = (lambda: torch.relu(torch.addmm(bt, xin, wt))) if br else (lambda: xin @ wt)
+            vms = vendor_time(fn, a.iters)
+            r.update(vendor_ms=vms, vendor_tflops=2 * m * n * k / vms / 1e9, speedup_vs_vendor=vms / ms)
+            del wt, bt
         print(json.dumps(r), flush=True)
         res.append(r)
         del xin
@@ -112,6 +137,18 @@ def main():
         ow = (w - kw) // s + 1 if pad == "VALID" else (w + s - 1) // s
         fl = 2 * nb * oh * ow * oc * kh * kw * c
         r = {"kind": "conv", "shape": [nb, h, w, c, kh, kw, oc, s, pad], "ms": ms, "tflops": fl / ms / 1e9}
+        if a.vendor:
+            import torch.nn.functional as F
+            xn = xin.permute(0, 3, 1, 2)  # NHWC storage viewed as NCHW: channels_last for MIOpen
+            wt = torch.randn((oc, c, kh, kw), device=dev).contiguous(memory_format=torch.channels_last)
+            bt = torch.zeros((oc,), device=dev)
+            if pad == "SAME":
+                ph, pw = max((oh - 1) * s + kh - h, 0), max((ow - 1) * s + kw - w, 0)
+                xn = F.pad(xn, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2)).contiguous(
+                    memory_format=torch.channels_last)
+            vms = vendor_time(lambda: torch.relu(F.conv2d(xn, wt, bt, stride=s)), a.iters)
+            r.update(vendor_ms=vms, vendor_tflops=fl / vms / 1e9, speedup_vs_vendor=vms / ms)
+            del xn, wt, bt
         print(json.dumps(r), flush=True)
         res.append(r)
         del xin
