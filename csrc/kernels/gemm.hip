@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
   constexpr int S = BK / 2, NM = TM * TN, R = TM + TN;
   constexpr int L = (VEC ? 1 : 4) * (AP + BP);
   constexpr int W = AP * (AL == A_MCONTIG ? 1 : 4) + BP * (TB ? 4 : 1);
-  auto mainloop = [&](auto chk) {
+  auto mainloop = [&](auto chk) __attribute__((always_inline)) {
     if (ktiles > 0) {
       load(kbeg, chk);
       store(0);
@@ -370,32 +370,44 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* ws = static_cast<float*>(g.workspace);
   const float* bias = static_cast<const float*>(g.bias);
-  auto epilogue = [&](auto act) {
+  // Accumulators are only ever indexed with constants (static_for), so they stay
+  // in registers. The cheap epilogue (bias + none/ReLU/ReLU6) is applied while
+  // storing; a transcendental activation or an absorbed elementwise chain is
+  // applied afterwards by a runtime loop over the elements this thread just
+  // wrote (re-read from its own stores: small code, no dynamic acc index).
+  const bool heavy = !ws && !(g.act <= ACT_RELU6 && g.epi.n == 0);
+  const int cheap_act = heavy ? ACT_NONE : g.act;
+  float* Cb = static_cast<float*>(g.C) + bz * g.strideC;
+  static_for<TN>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
+    if (col >= N) return;
+    const float bv = (!ws && bias) ? bias[col] : 0.f;
+    static_for<TM>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      const f32x16 v = acc[i][j];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
-      if (col >= N) continue;
-      const float bv = (!ws && bias) ? bias[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (row >= M) continue;
-          if (ws)  // split-K partial slab [split][batch][M][N]
-            ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = acc[i][j][r];
-          else
-            static_cast<float*>(g.C)[bz * g.strideC + row * g.ldc + col] = act(acc[i][j][r] + bv, row, col);
-        }
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= M) continue;
+        if (ws)  // split-K partial slab [split][batch][M][N]
+          ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = v[r];
+        else
+          Cb[row * g.ldc + col] = act_fast(v[r] + bv, cheap_act);
       }
-    }
-  };
-  if (ws || (g.act <= ACT_RELU6 && g.epi.n == 0))
-    epilogue([&](float v, int64_t, int64_t) { return act_fast(v, g.act); });
-  else
-    epilogue([&](float v, int64_t row, int64_t col) {
-      return epi_apply(g.epi, act_apply(v, g.act), row, col, N, bz * M * N);
     });
+  });
+  if (heavy) {
+#pragma nounroll
+    for (int e = 0; e < TN * TM * 16; ++e) {
+      const int j = e / (TM * 16), i = (e / 16) % TM, r = e % 16;
+      const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
+      const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (col >= N || row >= M) continue;
+      float* p = Cb + row * g.ldc + col;
+      *p = epi_apply(g.epi, act_apply(*p, g.act), row, col, N, bz * M * N);
+    }
+  }
 }
 
 // split-K combine: fixed summation order over the splits (deterministic)

@@ -277,27 +277,38 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tile(GemmArgs g, int tiles_m
   }
 
   const float* bias = static_cast<const float*>(g.bias);
-  auto epilogue = [&](auto act) {
+  // constant acc indices only (see gemm.hip): cheap epilogue while storing,
+  // transcendental activations / absorbed chains in a fix-up loop
+  const bool heavy = !(g.act <= ACT_RELU6 && g.epi.n == 0);
+  const int cheap_act = heavy ? ACT_NONE : g.act;
+  float* Cf = static_cast<float*>(g.C);
+  static_for<TN>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    const int64_t col = n0 + wn * (BN / WN) + j * 32 + li;
+    if (col >= N) return;
+    const float bv = bias ? bias[col] : 0.f;
+    static_for<TM>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      const auto v = acc[i][j];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = n0 + wn * (BN / WN) + j * 32 + li;
-      if (col >= N) continue;
-      const float bv = bias ? bias[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row >= M) continue;
-          static_cast<float*>(g.C)[row * g.ldc + col] = act(acc[i][j][r] + bv, row, col);
-        }
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= M) continue;
+        Cf[row * g.ldc + col] = act_fast(v[r] + bv, cheap_act);
       }
+    });
+  });
+  if (heavy) {
+#pragma nounroll
+    for (int e = 0; e < TN * TM * 16; ++e) {
+      const int j = e / (TM * 16), i = (e / 16) % TM, r = e % 16;
+      const int64_t col = n0 + wn * (BN / WN) + j * 32 + li;
+      const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (col >= N || row >= M) continue;
+      float* p = Cf + row * g.ldc + col;
+      *p = epi_apply(g.epi, act_apply(*p, g.act), row, col, N, 0);
     }
-  };
-  if (g.act <= ACT_RELU6 && g.epi.n == 0)
-    epilogue([&](float v, int64_t, int64_t) { return act_fast(v, g.act); });
-  else
-    epilogue([&](float v, int64_t row, int64_t col) { return epi_apply(g.epi, act_apply(v, g.act), row, col, N, 0); });
+  }
 }
 
 int64_t padded_k(int64_t K) { return (K + kBK - 1) / kBK * kBK; }

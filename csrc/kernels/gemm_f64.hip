@@ -164,27 +164,36 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
   }
   // f64 C/D layout: col = lane&15, row = (lane>>4) + 4*r
   const double* bias = static_cast<const double*>(g.bias);
-  auto epilogue = [&](auto act) {
+  // constant acc indices only (see gemm.hip): cheap epilogue while storing,
+  // transcendental activations / absorbed chains in a fix-up loop over the
+  // elements this thread wrote
+  const bool heavy = !(g.act <= ACT_RELU6 && g.epi.n == 0);
+  const int cheap_act = heavy ? ACT_NONE : g.act;
+  static_for<TN>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    const int64_t col = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+    const double bv = (bias && col < N) ? bias[col] : 0.0;
+    static_for<TM>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      const f64x4 v = acc[i][j];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-      const double bv = (bias && col < N) ? bias[col] : 0.0;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) + 4 * r;
-          if (row < M && col < N) C[row * g.ldc + col] = act(acc[i][j][r] + bv, row, col);
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) + 4 * r;
+        if (row < M && col < N) C[row * g.ldc + col] = act_fast(v[r] + bv, cheap_act);
       }
-    }
-  };
-  if (g.act <= ACT_RELU6 && g.epi.n == 0)
-    epilogue([&](double v, int64_t, int64_t) { return act_fast(v, g.act); });
-  else
-    epilogue([&](double v, int64_t row, int64_t col) {
-      return epi_apply(g.epi, act_apply(v, g.act), row, col, N, bz * M * N);
     });
+  });
+  if (heavy) {
+#pragma nounroll
+    for (int e = 0; e < TN * TM * 4; ++e) {
+      const int j = e / (TM * 4), i = (e / 4) % TM, r = e % 4;
+      const int64_t col = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+      const int64_t row = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) + 4 * r;
+      if (col >= N || row >= M) continue;
+      double* p = C + row * g.ldc + col;
+      *p = epi_apply(g.epi, act_apply(*p, g.act), row, col, N, bz * M * N);
+    }
+  }
 }
 
 // ============================================================== integer GEMM (VALU)

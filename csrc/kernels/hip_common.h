@@ -5,6 +5,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <type_traits>
+#include <utility>
 
 #include "kernels.h"
 
@@ -49,6 +51,19 @@ __device__ __forceinline__ T act_apply(T v, int act) {
     case ACT_SOFTPLUS: return v > T(20) ? v : log1p(exp(v));
     default: return v;
   }
+}
+
+// f(std::integral_constant<int, I>) for I = 0..N-1, expanded at compile time.
+// Accumulator tiles must be indexed with constants: one loop the unroller gives
+// up on (a big epilogue body) demotes the whole accumulator array to scratch,
+// and the k loop then stores every accumulator to scratch once per k tile.
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // the absorbed elementwise chain of a GEMM/conv epilogue at output (row, col)
