@@ -26,6 +26,27 @@ __device__ __forceinline__ int xcd_remap64(int b, int nwg) {
 
 constexpr int D_BK = 16, D_PAD = 2;
 
+// sched_group_barrier masks (LLVM AMDGPU): MFMA, VMEM read, DS read, DS write
+constexpr int kSchedMfma64 = 0x008, kSchedVmemRead64 = 0x020, kSchedDsRead64 = 0x100, kSchedDsWrite64 = 0x200;
+
+template <int J, int END, int O1, int M1, int M2>
+__device__ __forceinline__ void sched_ops64() {
+  if constexpr (J < END) {
+    __builtin_amdgcn_sched_group_barrier(J < O1 ? M1 : M2, 1, 0);
+    sched_ops64<J + 1, END, O1, M1, M2>();
+  }
+}
+// NM MFMAs with O memory ops spread between them (slot I: ops [I*O/NM, (I+1)*O/NM))
+template <int I, int NM, int O, int O1, int M1, int M2>
+__device__ __forceinline__ void sched_interleave64() {
+  if constexpr (I < NM) {
+    constexpr int lo = (I * O + NM - 1) / NM, hi = ((I + 1) * O + NM - 1) / NM;
+    sched_ops64<lo, hi, O1, M1, M2>();
+    __builtin_amdgcn_sched_group_barrier(kSchedMfma64, 1, 0);
+    sched_interleave64<I + 1, NM, O, O1, M1, M2>();
+  }
+}
+
 // Block tile BM x BN (64x64 or 128x128), 4 waves as 2x2, each wave owning
 // (BM/2)x(BN/2) as TMxTN 16x16 MFMA tiles. Interior blocks load 2 doubles per
 // 16-byte access without bounds checks; edge blocks take the checked path.
@@ -68,9 +89,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
     if (!TB) { r = idx / BN; c = idx % BN; }
     else { c = idx / D_BK; r = idx % D_BK; }
   };
-  auto load = [&](int64_t k0) {
-    const bool kfull = k0 + D_BK <= K;  // only the K tail tile is checked
-    const bool a_fast = a_rows && kfull, b_fast = b_cols && kfull;
+  // FAST: interior block (A rows and B columns in range, 16-byte aligned,
+  // K a multiple of D_BK): unconditional 16-byte loads, no branch in the loop
+  auto load = [&](int64_t k0, auto fast_t) __attribute__((always_inline)) {
+    constexpr bool FAST = decltype(fast_t)::value;
+    const bool kfull = FAST || k0 + D_BK <= K;  // only the K tail tile is checked
+    const bool a_fast = FAST || (a_rows && kfull), b_fast = FAST || (b_cols && kfull);
     if (a_fast) {
 #pragma unroll
       for (int e = 0; e < AE; e += 2) {
@@ -116,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
       }
     }
   };
-  auto store = [&](int st) {
+  auto store = [&](int st) __attribute__((always_inline)) {
 #pragma unroll
     for (int e = 0; e < AE; ++e) {
       int r, c;
@@ -137,31 +161,62 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_mfma(GemmArgs g, int tiles_m,
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
 
+  // per K tile: S k-steps of NM MFMAs; R LDS reads per k-step; L global loads
+  // and W LDS writes per tile. Interior blocks use the interleaved schedule of
+  // gemm.hip (memory ops spread between the MFMAs with sched_group_barrier,
+  // operands read one k-step ahead, last tile peeled: no branch in the loop).
+  constexpr int S = D_BK / 4, NM = TM * TN, R = TM + TN;
+  constexpr int L = AE / 2 + (BE == 1 ? 1 : BE / 2), W = AE + BE;
   const int64_t ktiles = (K + D_BK - 1) / D_BK;
-  load(0);
-  store(0);
-  __syncthreads();
-  int cur = 0;
-  for (int64_t kt = 0; kt < ktiles; ++kt) {
-    const bool has_next = kt + 1 < ktiles;
-    if (has_next) load((kt + 1) * D_BK);
-#pragma unroll
-    for (int kk = 0; kk < D_BK; kk += 4) {
-      const int kr = kk + (lane >> 4);
-      double a[TM], b[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[cur][kr][wm * (BM / WM) + i * 16 + (lane & 15)];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[cur][kr][wn * (BN / WN) + j * 16 + (lane & 15)];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (has_next) store(cur ^ 1);
+  auto mainloop = [&](auto fast_t) __attribute__((always_inline)) {
+    constexpr bool FAST = decltype(fast_t)::value;
+    load(0, fast_t);
+    store(0);
     __syncthreads();
-    cur ^= 1;
-  }
+    int cur = 0;
+    auto tile = [&](int64_t knext, auto more) __attribute__((always_inline)) {
+      constexpr bool NEXT = decltype(more)::value;
+      double a[2][TM], b[2][TN];
+      auto rd = [&](int buf, int kk) __attribute__((always_inline)) {
+        const int kr = kk + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[buf][i] = As[cur][kr][wm * (BM / WM) + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[buf][j] = Bs[cur][kr][wn * (BN / WN) + j * 16 + (lane & 15)];
+      };
+      rd(0, 0);
+      if constexpr (FAST) __builtin_amdgcn_sched_group_barrier(kSchedDsRead64, R, 0);
+      if constexpr (NEXT) load(knext, fast_t);
+#pragma unroll
+      for (int kk = 0; kk < S; ++kk) {
+        if (kk + 1 < S) rd((kk + 1) & 1, 4 * (kk + 1));
+        if (NEXT && kk == S - 1) store(cur ^ 1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk & 1][i], b[kk & 1][j], acc[i][j], 0, 0, 0);
+        if constexpr (FAST) {
+          if (kk == 0 && NEXT)
+            sched_interleave64<0, NM, L + R, L, kSchedVmemRead64, kSchedDsRead64>();
+          else if (kk == S - 1 && NEXT)
+            sched_interleave64<0, NM, W, W, kSchedDsWrite64, kSchedDsWrite64>();
+          else if (kk + 1 < S)
+            sched_interleave64<0, NM, R, R, kSchedDsRead64, kSchedDsRead64>();
+          else
+            __builtin_amdgcn_sched_group_barrier(kSchedMfma64, NM, 0);
+        }
+      }
+      __syncthreads();
+      cur ^= 1;
+    };
+    for (int64_t kt = 0; kt + 1 < ktiles; ++kt) tile((kt + 1) * D_BK, std::true_type{});
+    tile(0, std::false_type{});
+  };
+  if (a_rows && b_cols && K > 0 && K % D_BK == 0)
+    mainloop(std::true_type{});
+  else
+    mainloop(std::false_type{});
   // f64 C/D layout: col = lane&15, row = (lane>>4) + 4*r
   const double* bias = static_cast<const double*>(g.bias);
   // constant acc indices only (see gemm.hip): cheap epilogue while storing,
