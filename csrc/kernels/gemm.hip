@@ -441,9 +441,10 @@ struct F32Plan {
 // loses on grids of a few hundred blocks
 // {BM, BN}; the N-widths 96/160/192 fit Inception-style channel counts without
 // padding a 128-wide tile (a 128 tile on N=96 computes 25% zeros)
-constexpr int kNumTiles = 10;
+constexpr int kNumTiles = 13;
 constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
-                                      {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128}};
+                                      {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128},
+                                      {256, 64}, {256, 32}, {256, 96}};
 
 int64_t tile_blocks(int c, int64_t M, int64_t N, int64_t batch) {
   return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
@@ -507,7 +508,12 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 6: TFA_LAUNCH_TILE(128, 192, 2, 2); break;
     case 7: TFA_LAUNCH_TILE(128, 160, 4, 1); break;
     case 8: TFA_LAUNCH_TILE(64, 192, 2, 2); break;
-    default: TFA_LAUNCH_TILE(256, 128, 2, 2); break;
+    case 9: TFA_LAUNCH_TILE(256, 128, 2, 2); break;
+    // tall tiles for narrow-N convs: 4 waves stacked along M, so each wave
+    // runs 2 x TN MFMAs per k-step instead of 1 x TN (128x32 / 128x64 / 128x96)
+    case 10: TFA_LAUNCH_TILE(256, 64, 4, 1); break;
+    case 11: TFA_LAUNCH_TILE(256, 32, 4, 1); break;
+    default: TFA_LAUNCH_TILE(256, 96, 4, 1); break;
   }
 #undef TFA_LAUNCH_TILE
 }
