@@ -157,7 +157,7 @@ __device__ __forceinline__ void emit_slots() {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int MINB>
+template <int BM, int BN, int WM, int WN, int BK, int MINB, int VAR = 0>
 __global__ __launch_bounds__(256, MINB) void tile_gemm_il(const float* __restrict__ A, const float* __restrict__ B,
                                                           const float* __restrict__ bias, float* __restrict__ C,
                                                           int M, int N, int K, int tiles_n) {
@@ -203,6 +203,23 @@ __global__ __launch_bounds__(256, MINB) void tile_gemm_il(const float* __restric
       *reinterpret_cast<float4*>(&Bs[st][kr][4 * nq]) = rb[p];
     }
   };
+  auto storeA = [&](int st) {
+#pragma unroll
+    for (int p = 0; p < AP; ++p) {
+      const int idx = tid + 256 * p, row = idx / KQ, kq = idx % KQ;
+      As[st][4 * kq + 0][row] = ra[p].x;
+      As[st][4 * kq + 1][row] = ra[p].y;
+      As[st][4 * kq + 2][row] = ra[p].z;
+      As[st][4 * kq + 3][row] = ra[p].w;
+    }
+  };
+  auto storeB = [&](int st) {
+#pragma unroll
+    for (int p = 0; p < BP; ++p) {
+      const int idx = tid + 256 * p, kr = idx / (BN / 4), nq = idx % (BN / 4);
+      *reinterpret_cast<float4*>(&Bs[st][kr][4 * nq]) = rb[p];
+    }
+  };
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -231,14 +248,23 @@ __global__ __launch_bounds__(256, MINB) void tile_gemm_il(const float* __restric
 #pragma unroll
     for (int kk = 0; kk < S; ++kk) {
       if (kk + 1 < S) rd((kk + 1) & 1, 2 * (kk + 1));
-      if (NEXT && kk == S - 1) store(cur ^ 1);
+      if constexpr (VAR == 1) {  // A image written one k-step earlier than B
+        if (NEXT && kk == S - 2) storeA(cur ^ 1);
+        if (NEXT && kk == S - 1) storeB(cur ^ 1);
+      } else {
+        if (NEXT && kk == S - 1) store(cur ^ 1);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk & 1][i], b[kk & 1][j], acc[i][j], 0, 0, 0);
       // this step's MFMAs with its memory ops spread between them
-      if (kk == 0 && NEXT) {
+      if (VAR == 1 && NEXT && kk == S - 2) {
+        emit_slots<0, NM, R + 4 * AP, R, kDS_R, kDS_W>();
+      } else if (VAR == 1 && NEXT && kk == S - 1) {
+        emit_slots<0, NM, BP, BP, kDS_W, kDS_W>();
+      } else if (kk == 0 && NEXT) {
         emit_slots<0, NM, L + R, L, kVMEM_R, kDS_R>();
       } else if (kk == S - 1 && NEXT) {
         emit_slots<0, NM, W, W, kDS_W, kDS_W>();
@@ -429,6 +455,9 @@ void run(const char* name, const Shape& s, const float* A, const float* B, const
     if constexpr (IL == 2)
       hipLaunchKernelGGL((tile_gemm_kp<BM, BN, WM, WN, BK, MINB>), dim3(nwg), dim3(256), 0, 0, A, Bt, bias, C, s.M,
                          s.N, s.K, tn);
+    else if constexpr (IL == 3)
+      hipLaunchKernelGGL((tile_gemm_il<BM, BN, WM, WN, BK, MINB, 1>), dim3(nwg), dim3(256), 0, 0, A, B, bias, C, s.M,
+                         s.N, s.K, tn);
     else if constexpr (IL == 1)
       hipLaunchKernelGGL((tile_gemm_il<BM, BN, WM, WN, BK, MINB>), dim3(nwg), dim3(256), 0, 0, A, B, bias, C, s.M,
                          s.N, s.K, tn);
@@ -495,14 +524,15 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&Bt, (size_t)s.K * s.N * 4));
     hipLaunchKernelGGL(transpose, dim3(1024), dim3(256), 0, 0, B, Bt, s.K, s.N);
     CHECK(hipDeviceSynchronize());
-    run<128, 128, 2, 2, 16, 2>("128x128 w64x64 bk16 occ2 (shipped)", s, A, B, bias, C, iters);
-    run<256, 128, 2, 2, 16, 2, 1>("IL 256x128 w128x64 bk16 occ2", s, A, B, bias, C, iters);
-    run<128, 128, 2, 2, 16, 2, 2>("KP 128x128 w64x64 bk16 occ2", s, A, B, bias, C, iters, Bt);
-    run<128, 128, 2, 2, 32, 2, 2>("KP 128x128 w64x64 bk32 occ2", s, A, B, bias, C, iters, Bt);
-    run<256, 128, 2, 2, 16, 2, 2>("KP 256x128 w128x64 bk16 occ2", s, A, B, bias, C, iters, Bt);
-    run<256, 128, 2, 2, 32, 1, 2>("KP 256x128 w128x64 bk32 occ1", s, A, B, bias, C, iters, Bt);
-    run<256, 256, 2, 2, 16, 1, 2>("KP 256x256 w128x128 bk16 occ1", s, A, B, bias, C, iters, Bt);
-    run<256, 256, 2, 2, 32, 1, 2>("KP 256x256 w128x128 bk32 occ1", s, A, B, bias, C, iters, Bt);
+    run<128, 128, 2, 2, 16, 2>("128x128 w64x64 bk16 occ2 (walls)", s, A, B, bias, C, iters);
+    run<128, 128, 2, 2, 16, 2, 1>("IL 128x128 occ2", s, A, B, bias, C, iters);
+    run<128, 128, 2, 2, 16, 3, 1>("IL 128x128 occ3", s, A, B, bias, C, iters);
+    run<128, 128, 2, 2, 16, 2, 3>("IL+splitW 128x128 occ2", s, A, B, bias, C, iters);
+    run<256, 128, 2, 2, 16, 2, 1>("IL 256x128 occ2", s, A, B, bias, C, iters);
+    run<256, 128, 2, 2, 16, 1, 1>("IL 256x128 occ1", s, A, B, bias, C, iters);
+    run<256, 128, 2, 2, 16, 2, 3>("IL+splitW 256x128 occ2", s, A, B, bias, C, iters);
+    run<256, 64, 4, 1, 16, 2, 1>("IL 256x64 w64x64 occ2", s, A, B, bias, C, iters);
+    run<256, 64, 4, 1, 16, 3, 1>("IL 256x64 w64x64 occ3", s, A, B, bias, C, iters);
     CHECK(hipFree(Bt));
     CHECK(hipFree(A));
     CHECK(hipFree(B));
