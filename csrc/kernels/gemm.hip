@@ -479,7 +479,9 @@ int tile_env() { return forced_tile().load(); }
 F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
   // narrow N picks a narrow tile (a 128-wide tile on N=32 wastes 3/4 of the MFMAs)
   int cfg = N <= 32 ? 4 : (N <= 64 ? 1 : 0);
-  if (cfg == 0 && N >= 256 && tile_blocks(9, M, N, batch) >= 2048) cfg = 9;  // big GEMMs: 256x128
+  // big GEMMs: 256x64 with the 4 waves stacked along M (each 64x64, B fragments shared);
+  // measured best on 2.5Mx512x512, 262kx512x512, 4096^3 and 8192x1024^2 (scripts/bigtile_lab.hip)
+  if (cfg == 0 && tile_blocks(10, M, N, batch) >= 512) cfg = 10;
   // too few blocks to fill 256 CUs twice: shrink the tile
   if (tile_blocks(cfg, M, N, batch) < 512) {
     if (cfg == 0) cfg = N > 96 ? 2 : 3;
