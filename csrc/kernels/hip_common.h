@@ -89,8 +89,9 @@ __device__ __forceinline__ T epi_apply(const EpiProg& e, T v, int64_t row, int64
       case EPI_MUL: v = v * x; break;
       case EPI_DIV: v = v / x; break;
       case EPI_RDIV: v = x / v; break;
-      case EPI_MAX: v = v > x ? v : x; break;
-      case EPI_MIN: v = v < x ? v : x; break;
+      // NaN-propagating, like the unfused Maximum/Minimum kernels
+      case EPI_MAX: v = (v != v || x != x) ? v + x : (v > x ? v : x); break;
+      case EPI_MIN: v = (v != v || x != x) ? v + x : (v < x ? v : x); break;
       case EPI_ACT: v = act_apply(v, o.act); break;
       case EPI_NEG: v = -v; break;
       case EPI_SQUARE: v = v * v; break;

@@ -723,9 +723,21 @@ class _RowVectorizer:
         self._progs: Dict[tuple, Any] = {}  # cell ranks -> lifted program (or None)
         self._lifted: Dict[tuple, bytes] = {}  # cell ranks -> lifted graph bytes
 
+    def _cache_key(self, cell_shapes: tuple) -> tuple:
+        """Programs are shared by every cell shape of the same ranks unless the
+        lifting baked cell sizes into the graph (a lifted MatMul reshapes to
+        [-1, m, n]); those are keyed by the full shapes."""
+        rkey = tuple(len(s) for s in cell_shapes)
+        if rkey in self._progs or self._gkey(rkey) in _LIFT_CACHE:
+            return rkey
+        return ("shapes",) + tuple(tuple(s) for s in cell_shapes)
+
+    def _gkey(self, key: tuple) -> tuple:
+        return (engine._key(self.graph_bytes), tuple(self.fetch_refs), tuple(self.feed_names), key)
+
     def _program(self, cell_shapes: tuple):
-        key = tuple(len(s) for s in cell_shapes)
-        gkey = (engine._key(self.graph_bytes), tuple(self.fetch_refs), tuple(self.feed_names), key)
+        key = self._cache_key(cell_shapes)
+        gkey = self._gkey(key)
         if key not in self._progs and gkey in _LIFT_CACHE:  # lifted by an earlier map_rows call
             self._lifted[key], self._progs[key] = _LIFT_CACHE[gkey]
         if key not in self._progs:
@@ -740,6 +752,9 @@ class _RowVectorizer:
                 patch = vectorize.lift(light, self.fetch_refs, self.feed_names, infos, patch_only=True)
             except ValueError:
                 patch = None
+            if patch is None or not vectorize.bakes_cell_sizes(patch):
+                key = tuple(len(s) for s in cell_shapes)  # valid for every shape of these ranks
+                gkey = self._gkey(key)
             if patch is None:
                 self._progs[key] = None
             else:
@@ -780,7 +795,7 @@ class _RowVectorizer:
             return engine.run_program(prog, ins, ins[0].device)
         if not engine.gpu_available():
             return engine.run_program(prog, ins, torch.device("cpu"))
-        lifted = self._lifted[tuple(len(s) for s in cell_shapes)]
+        lifted = self._lifted[self._cache_key(cell_shapes)]
         if engine.worth_pipelining(ins):
             shapes = _concrete_output_shapes(lifted, self.fetch_refs, self.feed_names, ins)
             specs = [(tuple(s), o.dtype) for s, o in zip(shapes, self._out_dtypes(lifted))]

@@ -279,4 +279,11 @@ def _lift(gdef, fetches, feeds, infos, patch_only=False):
     return P.GraphDef(new, gdef.producer)
 
 
-__all__ = ["lift"]
+def bakes_cell_sizes(gdef: "P.GraphDef") -> bool:
+    """True when the lifted graph hard-codes cell dims (a lifted MatMul's
+    [-1, m, n] reshape), so it is valid only for the cell shapes it was
+    lifted for."""
+    return any(n.name.endswith("/_tfa_vec_shape") for n in gdef.node)
+
+
+__all__ = ["lift", "bakes_cell_sizes"]

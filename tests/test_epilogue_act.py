@@ -210,3 +210,27 @@ def test_chain_operand_produced_after_the_matmul(dev):
     assert "+bias +epi[sub:full" in plan, plan
     want = (x_.astype(np.float64) @ w + b - x3_.sum(2)) * x3_.max((1, 2))[:, None]
     np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
+
+
+def test_matmul_chain_max_min_propagate_nan(dev):
+    """An absorbed Maximum/Minimum propagates NaN from either side, exactly as
+    the unfused elementwise kernels (and np.maximum / np.minimum) do."""
+    rng = np.random.default_rng(9)
+    w = (rng.standard_normal((32, 16)) / 6).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 32], name="x")
+        r = tf.placeholder(tf.float32, [None, 1], name="r")
+        z = tf.placeholder(tf.float32, [None, 16], name="z")
+        tf.minimum(tf.maximum(tf.matmul(x, tf.constant(w)), r), z, name="y")
+    x_ = rng.uniform(-1, 1, (300, 32)).astype(np.float32)
+    r_ = rng.uniform(-1, 1, (300, 1)).astype(np.float32)
+    z_ = rng.uniform(-1, 1, (300, 16)).astype(np.float32)
+    x_[0, 3] = np.nan   # NaN accumulator
+    r_[1, 0] = np.nan   # NaN max operand
+    z_[2, 5] = np.nan   # NaN min operand
+    plan, got = _run(dev, g, "y", {"x": x_, "r": r_, "z": z_})
+    assert "+epi[max:row,min:full]" in plan, plan
+    want = np.minimum(np.maximum(x_.astype(np.float64) @ w, r_), z_)
+    assert np.isnan(got[0]).all() and np.isnan(got[1]).all() and np.isnan(got[2, 5])
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-5)

@@ -116,3 +116,30 @@ def test_unliftable_graphs_fall_back(builder):
         got = [np.asarray(r.out) for r in tfs.map_rows(o, df).collect()]
     assert metrics.snapshot().get("map_rows_vectorized_rows", 0) == before
     assert len(got) == 9
+
+
+def _matrix_frame(ms):
+    rows = [Row(x=[[float(v) for v in rng.standard_normal(4)] for _ in range(m)]) for m in ms]
+    return tfs.analyze(tfs.create_dataframe(rows, num_partitions=2))
+
+
+def _matrix_rows(df):
+    with tf.Graph().as_default():
+        x = tf.placeholder(tf.float64, [None, 4], name="x")
+        out = tfs.map_rows(tf.nn.relu(tf.matmul(x, tf.constant(W)), name="o"), df)
+        return out.collect()
+
+
+def test_lifted_matmul_keys_programs_by_cell_shape():
+    # the lifted MatMul bakes the cell's row count m into a reshape: rows of
+    # two different m in one call, and a second call with a third m, must each
+    # get their own program (not the first one lifted for these ranks)
+    for ms in ([2, 3] * 4, [5] * 4):
+        df = _matrix_frame(ms)
+        before = metrics.snapshot().get("map_rows_vectorized_rows", 0)
+        got = _matrix_rows(df)
+        assert metrics.snapshot().get("map_rows_vectorized_rows", 0) - before == len(ms)
+        assert len(got) == len(ms)
+        for r in got:
+            x = np.asarray(r.x)
+            np.testing.assert_allclose(np.asarray(r.o), np.maximum(x @ W, 0), rtol=1e-12, atol=1e-12)
