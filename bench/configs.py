@@ -144,6 +144,9 @@ def cfg_refperf(a):
     back = tfs.from_columns({"x": np.arange(cells, dtype=np.int32)}, num_partitions=1).cache()
     back.local_blocks()
     t_back = timed(lambda: back.to_arrow(), a.steps, a.warmup)
+    # tensor -> Row objects (the reference's ConvertBackPerformanceSuite:22-43 case,
+    # a real Row per cell: native build_rows, runtime/packer.cpp)
+    t_back_rows = timed(lambda: back.collect(), 3, 1)
     # boxed path (the reference's ConvertPerformanceSuite:19-39 case): 10M Row(int)
     # objects -> an int column, through the native packer (runtime/packer.cpp)
     rows = [tfs.Row(x=i) for i in range(10_000_000)]
@@ -154,6 +157,8 @@ def cfg_refperf(a):
           "convert_10M_int_cells_arrow_zero_copy_view_ms": t_conv * 1e3,
           "convert_one_10M_vector_arrow_zero_copy_view_ms": t_conv_vec * 1e3,
           "convert_back_10M_int_cells_to_arrow_ms": t_back * 1e3,
+          "convert_back_10M_int_cells_to_python_Rows_ms": t_back_rows * 1e3,
+          "convert_back_10M_int_cells_to_python_Rows_rows_per_sec": cells / t_back_rows,
           "convert_10M_python_Row_int_cells_ms": t_rows * 1e3,
           "convert_10M_python_Row_int_cells_rows_per_sec": 10_000_000 / t_rows,
           "device": str(engine.compute_device()), "data": "synthetic"})

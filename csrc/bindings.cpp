@@ -82,6 +82,48 @@ py::dict infer_all(const std::string& bytes) {
   return out;
 }
 
+// order-preserving integer image of float keys, the host twin of
+// key_image in kernels/groupby.hip: NaNs -> one canonical NaN (sorted last),
+// -0.0 -> +0.0, negative values' magnitude bits flipped
+template <typename F, typename S>
+at::Tensor key_image_typed(const at::Tensor& keys, at::ScalarType st) {
+  at::Tensor out = at::empty({keys.size(0)}, keys.options().dtype(st));
+  const F* in = keys.data_ptr<F>();
+  S* o = out.data_ptr<S>();
+  const S flip = std::numeric_limits<S>::max();
+  for (int64_t i = 0; i < keys.size(0); ++i) {
+    F v = in[i];
+    if (v != v) v = std::numeric_limits<F>::quiet_NaN();
+    if (v == F(0)) v = F(0);
+    S b;
+    std::memcpy(&b, &v, sizeof(b));
+    o[i] = b < 0 ? S(b ^ flip) : b;
+  }
+  return out;
+}
+
+template <typename F, typename S>
+at::Tensor key_from_image_typed(const at::Tensor& img, at::ScalarType st) {
+  at::Tensor out = at::empty({img.size(0)}, img.options().dtype(st));
+  const S* in = img.data_ptr<S>();
+  F* o = out.data_ptr<F>();
+  const S flip = std::numeric_limits<S>::max();
+  for (int64_t i = 0; i < img.size(0); ++i) {
+    S b = in[i] < 0 ? S(in[i] ^ flip) : in[i];
+    std::memcpy(&o[i], &b, sizeof(b));
+  }
+  return out;
+}
+
+at::Tensor host_key_image(const at::Tensor& keys) {
+  return keys.scalar_type() == at::kDouble ? key_image_typed<double, int64_t>(keys, at::kLong)
+                                           : key_image_typed<float, int32_t>(keys, at::kInt);
+}
+
+at::Tensor host_key_from_image(const at::Tensor& img, at::ScalarType st) {
+  return st == at::kDouble ? key_from_image_typed<double, int64_t>(img, st) : key_from_image_typed<float, int32_t>(img, st);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -176,6 +218,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("run_chunked", &Program::run_chunked, py::arg("seg_inputs"), py::arg("seg_outputs"),
            py::arg("chunk_rows"), py::arg("device"), py::arg("depth") = 3,
            py::call_guard<py::gil_scoped_release>())
+      .def("run_chunked_reduce", &Program::run_chunked_reduce, py::arg("seg_inputs"), py::arg("chunk_rows"),
+           py::arg("device"), py::arg("depth") = 3, py::call_guard<py::gil_scoped_release>())
       .def("describe", &Program::describe_plan, py::arg("inputs"), py::arg("as_gpu") = false)
       .def("fused_sources", &Program::fused_sources)
       .def("reset_stats", &Program::reset_stats)
@@ -276,8 +320,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     at::Tensor keys = keys0.contiguous();
     const int64_t n = keys.size(0);
     if (!keys.is_cuda()) {
-      auto r = at::_unique2(keys, /*sorted=*/true, /*return_inverse=*/true, /*return_counts=*/false);
-      return py::make_tuple(std::get<1>(r).to(at::kLong), std::get<0>(r));
+      // float keys through their order image (groupby.hip): every NaN is one
+      // key sorted last, -0.0 and 0.0 are one key
+      const bool fl = keys.scalar_type() == at::kFloat || keys.scalar_type() == at::kDouble;
+      at::Tensor img = fl ? host_key_image(keys) : keys;
+      auto r = at::_unique2(img, /*sorted=*/true, /*return_inverse=*/true, /*return_counts=*/false);
+      at::Tensor uniq = fl ? host_key_from_image(std::get<0>(r), keys.scalar_type()) : std::get<0>(r);
+      return py::make_tuple(std::get<1>(r).to(at::kLong), uniq);
     }
     c10::hip::HIPGuard guard(keys.device().index());
     auto opts = keys.options();
@@ -380,7 +429,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // Unsorted segmented reduction: out[ids[i]] op= x[i] (rows in any order),
   // the map-side combine of groupBy/aggregate. ids int32/int64 on x's device.
   m.def("unsorted_segment_reduce", [](const std::string& op, const at::Tensor& x, const at::Tensor& ids,
-                                      int64_t nseg) {
+                                      int64_t nseg, std::optional<at::Tensor> out_opt) {
     TFA_CHECK(x.dim() >= 1 && ids.dim() == 1 && ids.size(0) == x.size(0), "unsorted_segment_reduce: ids must be [rows]");
     TFA_CHECK(ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt, "unsorted_segment_reduce: int ids");
     TFA_CHECK(ids.device() == x.device(), "unsorted_segment_reduce: ids and x on different devices");
@@ -403,11 +452,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         out = at::empty({nseg, xs.size(1)}, x.options());
         out = out.index_reduce_(0, is, xs, mx ? "amax" : "amin", false);
       }
-      return out.reshape(osz).contiguous();
+      out = out.reshape(osz).contiguous();
+      if (out_opt) return out_opt->copy_(out);
+      return out;
     }
     c10::hip::HIPGuard guard(x.device().index());
     at::Tensor xc = x.contiguous(), ic = ids.contiguous();
-    at::Tensor out = at::empty(osz, xc.options());
+    at::Tensor out;
+    if (out_opt) {  // write into a caller's slice (e.g. one partition's row of a stacked buffer)
+      out = *out_opt;
+      TFA_CHECK(out.is_cuda() && out.is_contiguous() && out.sizes().vec() == osz && out.scalar_type() == xc.scalar_type(),
+                "unsorted_segment_reduce: out must be a contiguous device tensor of the result shape and dtype");
+    } else {
+      out = at::empty(osz, xc.options());
+    }
     if (!out.numel()) return out;
     const int64_t inner = out.numel() / nseg;
     const DType dt = from_scalar_type(xc.scalar_type());
@@ -418,7 +476,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                out.data_ptr(), nrows, inner, nseg, ws ? work.data_ptr() : nullptr,
                                c10::hip::getCurrentHIPStream(x.device().index()).stream());
     return out;
-  });
+  }, py::arg("op"), py::arg("x"), py::arg("ids"), py::arg("nseg"), py::arg("out") = py::none());
   m.def("segment_reduce", [](const std::string& op, const at::Tensor& x, const at::Tensor& offsets) {
     TFA_CHECK(x.dim() >= 1, "segment_reduce needs rank >= 1");
     TFA_CHECK(offsets.scalar_type() == at::kLong && offsets.dim() == 1, "offsets must be int64[nseg+1]");

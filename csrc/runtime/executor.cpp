@@ -1233,6 +1233,103 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
   stats_.d2h_ms += stage_ms[2];
 }
 
+std::vector<at::Tensor> Program::run_chunked_reduce(const std::vector<std::vector<at::Tensor>>& seg_inputs,
+                                                    int64_t chunk_rows, int device, int depth) {
+  TFA_CHECK(host_op_error_.empty(), host_op_error_);
+  TFA_CHECK(chunk_rows > 0, "chunk_rows must be > 0");
+  depth = std::max(2, std::min(depth, 4));
+  c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+  at::Device dev(at::kCUDA, static_cast<c10::DeviceIndex>(device));
+  auto compute = c10::hip::getCurrentHIPStream(device);
+  auto h2d = c10::hip::getStreamFromExternal(copy_stream(device, 0), static_cast<c10::DeviceIndex>(device));
+  auto t0 = std::chrono::steady_clock::now();
+  struct Chunk {
+    size_t seg;
+    int64_t start, rows;
+  };
+  std::vector<Chunk> chunks;
+  for (size_t s = 0; s < seg_inputs.size(); ++s) {
+    TFA_CHECK(seg_inputs[s].size() == feed_nodes_.size(), "segment ", s, ": expected ", feed_nodes_.size(), " inputs");
+    const int64_t rows = seg_inputs[s].empty() ? 0 : seg_inputs[s][0].size(0);
+    for (auto& t : seg_inputs[s]) {
+      TFA_CHECK(t.size(0) == rows, "segment inputs disagree on rows");
+      TFA_CHECK(!t.is_cuda() && t.is_contiguous(), "run_chunked_reduce inputs must be contiguous host tensors");
+    }
+    for (int64_t st = 0; st < rows; st += chunk_rows) chunks.push_back({s, st, std::min(chunk_rows, rows - st)});
+  }
+  TFA_CHECK(!chunks.empty(), "run_chunked_reduce: no rows");
+  const size_t nin = feed_nodes_.size();
+  std::vector<std::vector<at::Tensor>> ring(depth);
+  for (int d = 0; d < depth; ++d)
+    for (size_t i = 0; i < nin; ++i) {
+      auto sz = seg_inputs[0][i].sizes().vec();
+      sz[0] = chunk_rows;
+      ring[d].push_back(at::empty(sz, seg_inputs[0][i].options().device(dev).pinned_memory(false)));
+    }
+  std::vector<hipEvent_t> ev_h2d(depth), ev_comp(depth);
+  for (int d = 0; d < depth; ++d) {
+    HIP_OK(hipEventCreateWithFlags(&ev_h2d[d], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_comp[d], hipEventDisableTiming));
+  }
+  std::vector<bool> used(depth, false);
+  std::vector<at::Tensor> acc;  // [nchunks, *fetch shape] per fetch, on the device
+  int64_t h2d_bytes = 0;
+  for (size_t ci = 0; ci < chunks.size(); ++ci) {
+    const Chunk& ch = chunks[ci];
+    const int slot = static_cast<int>(ci % depth);
+    if (used[slot]) HIP_OK(hipStreamWaitEvent(h2d.stream(), ev_comp[slot], 0));
+    std::vector<at::Tensor> dev_in;
+    for (size_t i = 0; i < nin; ++i) {
+      const at::Tensor& src = seg_inputs[ch.seg][i];
+      const int64_t row_bytes = src.numel() / std::max<int64_t>(src.size(0), 1) * src.element_size();
+      at::Tensor dst = ring[slot][i].narrow(0, 0, ch.rows);
+      const char* sp = static_cast<const char*>(src.data_ptr()) + ch.start * row_bytes;
+      if (ch.rows * row_bytes)
+        HIP_OK(hipMemcpyAsync(dst.data_ptr(), sp, ch.rows * row_bytes, hipMemcpyHostToDevice, h2d.stream()));
+      h2d_bytes += ch.rows * row_bytes;
+      dev_in.push_back(dst);
+    }
+    HIP_OK(hipEventRecord(ev_h2d[slot], h2d.stream()));
+    HIP_OK(hipStreamWaitEvent(compute.stream(), ev_h2d[slot], 0));
+    std::vector<at::Tensor> outs;
+    {
+      RangeGuard rg("chunk_reduce");
+      auto p = plan_for(dev_in);
+      outs = execute(*p, dev_in, compute.stream());
+    }
+    if (acc.empty()) {
+      for (auto& o : outs) {
+        auto sz = o.sizes().vec();
+        sz.insert(sz.begin(), static_cast<int64_t>(chunks.size()));
+        acc.push_back(at::empty(sz, o.options().device(dev)));
+      }
+    }
+    for (size_t j = 0; j < outs.size(); ++j) {
+      at::Tensor o = outs[j].is_cuda() ? outs[j].contiguous() : outs[j].to(dev);
+      at::Tensor dst = acc[j].select(0, static_cast<int64_t>(ci));
+      TFA_CHECK(o.numel() == dst.numel(), "fetch '", fetch_names_[j], "' changed shape between chunks");
+      const int64_t nb = o.numel() * o.element_size();
+      if (nb) HIP_OK(hipMemcpyAsync(dst.data_ptr(), o.data_ptr(), nb, hipMemcpyDeviceToDevice, compute.stream()));
+    }
+    HIP_OK(hipEventRecord(ev_comp[slot], compute.stream()));
+    used[slot] = true;
+    stats_.chunks++;
+  }
+  // the ring's last readers are on the compute stream: the caller's stream
+  // orders every later use of acc; the copy stream must finish before the
+  // ring is freed
+  HIP_OK(hipStreamSynchronize(h2d.stream()));
+  for (int d = 0; d < depth; ++d) {
+    hipEventDestroy(ev_h2d[d]);
+    hipEventDestroy(ev_comp[d]);
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  stats_.runs++;
+  stats_.h2d_bytes += h2d_bytes;
+  stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  return acc;
+}
+
 std::vector<std::string> Program::fused_sources(const std::vector<at::Tensor>& inputs) {
   auto p = build_plan(inputs, true);
   std::vector<std::string> out;

@@ -64,6 +64,15 @@ class Program {
                    const std::vector<std::vector<at::Tensor>>& seg_outputs, int64_t chunk_rows,
                    int device, int depth);
 
+  // Pipelined host->device reduction over row chunks (reduce_blocks of host
+  // partitions): every chunk's fetches are copied into slot c of a device
+  // buffer [nchunks, *fetch shape] on the compute stream while the next chunk's
+  // H2D runs on the copy stream; nothing comes back to the host. Returns the
+  // stacked per-chunk partials (device), which the caller folds with the same
+  // (associative) graph.
+  std::vector<at::Tensor> run_chunked_reduce(const std::vector<std::vector<at::Tensor>>& seg_inputs,
+                                             int64_t chunk_rows, int device, int depth);
+
   ExecStats stats() const;
   void reset_stats();
   // as_gpu: describe the plan a GPU run would use (fusion included), from host tensors

@@ -24,6 +24,8 @@ for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 1200 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    groupby) run groupby 600 python -u -m pytest tests/test_groupby.py -x -v --timeout 120 --timeout-method thread ;;
+    gbprof) export TMPDIR=/tmp; run gbprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/gbprof" -o run -- python scripts/groupby_profile.py ;;
     kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -x -q ;;
     bench) run bench 900 python bench.py --steps ${BENCH_STEPS:-5} --warmup ${BENCH_WARMUP:-2} ${BENCH_ARGS:-} ;;
     benchsmall) run benchsmall 600 python bench.py --steps 3 --warmup 1 --rows 1000000 ;;

@@ -694,7 +694,7 @@ class _BatchCut:
             t0 = time.perf_counter()
             if side is not None:
                 main.wait_stream(side)
-            outs = engine.run_program(self.post, [torch.cat(cut, 0)], dev)
+            outs = engine.run_program(self.post, [engine.cat_rows(cut)], dev)
             for j, (o, mode) in enumerate(zip(outs, self.modes)):
                 for k, i in enumerate(rows):
                     per_out[j][i] = o[k] if mode == "index" else o[k:k + 1]
@@ -1053,7 +1053,7 @@ def _combine_monoids(partials: Dict[str, List[torch.Tensor]], ops: Dict[str, str
         if len(ps) == 1:
             local[n] = ps[0].to(dev)
         else:
-            local[n] = _monoid_reduce(ops[n], torch.stack([p.to(dev) for p in ps], 0), dev) if ps else None
+            local[n] = _monoid_reduce(ops[n], engine.stack_rows([p.to(dev) for p in ps]), dev) if ps else None
     if not dist.is_distributed():
         _check(all(v is not None for v in local.values()), "Cannot reduce an empty DataFrame")
         return local
@@ -1062,23 +1062,36 @@ def _combine_monoids(partials: Dict[str, List[torch.Tensor]], ops: Dict[str, str
     for n in partials:
         groups.setdefault((ops[n], int(dtypes[n])), []).append(n)
     out: Dict[str, torch.Tensor] = {}
+    flags = []
     for (op, tfd), names in sorted(groups.items()):
         tdt = D.torch_dtype(tfd)
         has = int(any(local[n] is not None for n in names))
-        pieces = []
-        for n in names:
-            v = local[n] if local[n] is not None else _identity(op, shapes[n], tdt, dev)
-            pieces.append(v.reshape(-1).to(tdt))
-        pieces.append(torch.tensor([_FLAG_ENCODE[op](has)], dtype=tdt, device=dev))
-        buf = torch.cat(pieces)
+        sizes = [int(np.prod(shapes[n])) if shapes[n] else 1 for n in names]
+        # one buffer per (op, dtype): the partials by device DMA, the has-data
+        # flag (and a data-less rank's identities) by one small host copy
+        buf = torch.empty(sum(sizes) + 1, dtype=tdt, device=dev)
+        off = 0
+        for n, k in zip(names, sizes):
+            v = local[n]
+            if v is None:
+                buf[off:off + k].copy_(_identity(op, (k,), tdt, torch.device("cpu")))
+            else:
+                buf[off:off + k].copy_(v.reshape(-1).to(tdt))
+            off += k
+        buf[off:].copy_(torch.tensor([_FLAG_ENCODE[op](has)], dtype=tdt))
         with metrics.timer("allreduce"):
             dist.all_reduce_(buf, op)
-        _check(bool(_FLAG_ANY[op](buf[-1].item())), "Cannot reduce an empty DataFrame")
+        flags.append((op, buf[off:]))
         off = 0
-        for n in names:
-            k = int(np.prod(shapes[n])) if shapes[n] else 1
+        for n, k in zip(names, sizes):
             out[n] = buf[off:off + k].reshape(shapes[n])
             off += k
+    # every group's flag comes back to the host in one synchronisation
+    host = [f.to("cpu", non_blocking=True) if f.is_cuda else f for _, f in flags]
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
+    for (op, _), h in zip(flags, host):
+        _check(bool(_FLAG_ANY[op](h[0].item())), "Cannot reduce an empty DataFrame")
     return out
 
 
@@ -1182,7 +1195,7 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
             nbytes = sum(t.numel() * t.element_size() for _, ins in dense for t in ins)
             if (len(dense) > 1 and len(devs) == 1 and next(iter(devs)).type == "cuda"
                     and nbytes <= config.chunk_bytes):
-                ins = [torch.cat([d[1][j] for d in dense], 0) for j in range(len(cols))]
+                ins = [engine.cat_rows([d[1][j] for d in dense]) for j in range(len(cols))]
                 res[dense[0][0]] = engine.run_program(prog, ins, ins[0].device)
                 metrics.add("reduce_blocks_merged_partitions", len(dense))
                 return res
@@ -1191,19 +1204,18 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
                 continue
             ins = dense_of.get(pid) or _dense_inputs(b, cols, "reduce_blocks")
             on_device = all(t.is_cuda for t in ins)
-            # reductions stage 8 pipeline chunks at a time: per-chunk overhead stays
-            # negligible and device memory bounded (1 GiB at the default chunk_bytes)
-            chunk = 8 * engine.chunk_rows_for(ins)
+            chunk = engine.chunk_rows_for(ins)
             if not on_device and engine.gpu_available() and b.nrows > 2 * chunk:
                 # a host partition bigger than the staging budget streams through
-                # HBM chunk by chunk; the partials are folded by the same graph
-                # (the associativity contract of reduce_blocks)
+                # HBM chunk by chunk: H2D on the copy stream overlapped with the
+                # chunk reductions, every chunk's partial kept on the device;
+                # the stacked partials are folded by the same graph (the
+                # associativity contract of reduce_blocks)
                 dev = engine.compute_device()
-                parts = [engine.run_program(prog, [t[a:a + chunk] for t in ins], dev)
-                         for a in range(0, b.nrows, chunk)]
-                stacked = [torch.stack([p[j] for p in parts], 0) for j in range(len(parts[0]))]
-                res[pid] = engine.run_program(prog, stacked, dev)
-                metrics.add("reduce_blocks_chunks", len(parts))
+                seg = [t.contiguous() for t in ins]  # pinned frames DMA directly; pageable ones are staged by HIP
+                stacked = prog.run_chunked_reduce([seg], chunk, dev.index or 0, config.pipeline_depth)
+                res[pid] = engine.run_program(prog, list(stacked), dev)
+                metrics.add("reduce_blocks_chunks", int(stacked[0].shape[0]))
             else:
                 res[pid] = engine.run_program(prog, ins, ins[0].device if on_device else None)
         return res
@@ -1227,7 +1239,7 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
         # and the graph runs once more on the stacked [ranks, ...] block
         local: Dict[str, Optional[torch.Tensor]] = {n: None for n in out_names}
         if partials[0]:
-            stacks = [torch.stack(partials[k], 0) for k in range(len(out_names))]
+            stacks = [engine.stack_rows(partials[k]) for k in range(len(out_names))]
             outs = engine.run_program(prog, stacks) if len(partials[0]) > 1 else [p[0] for p in partials]
             local = dict(zip(out_names, outs))
         allp = _gather_rank_values(local, static, dtypes)
@@ -1236,7 +1248,7 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
         if len(allp[out_names[0]]) == 1:
             results = {n: allp[n][0].cpu().numpy() for n in out_names}
         else:
-            outs = engine.run_program(prog, [torch.stack(allp[n], 0) for n in out_names])
+            outs = engine.run_program(prog, [engine.stack_rows(allp[n]) for n in out_names])
             results = {n: o.cpu().numpy() for n, o in zip(out_names, outs)}
     metrics.add("reduce_blocks_calls")
     return _unpack(results, spec, summary)
@@ -1408,6 +1420,8 @@ def _key_hash(arrays: List[np.ndarray]) -> np.ndarray:
     import pandas as pd
     h = np.zeros(len(arrays[0]), dtype=np.uint64)
     for a in arrays:
+        if a.dtype.kind == "f":  # equal keys hash alike: one NaN, -0.0 == 0.0
+            a = np.where(np.isnan(a), np.nan, a) + a.dtype.type(0)
         h = h * np.uint64(1000003) ^ pd.util.hash_array(a)
     return h
 
@@ -1498,22 +1512,36 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         dev = engine.compute_device()
         on_device = any(b.columns[n].is_cuda for b in blocks.values() if b.nrows for n in out_names) or \
             dev.type == "cuda"
-        kparts: List[List[torch.Tensor]] = []
-        vparts: Dict[str, List[torch.Tensor]] = {n: [] for n in out_names}
-        for pid, b in sorted(blocks.items()):
-            if b.nrows == 0:
-                continue
-            ids, uniq, ng = G.group_ids([b.columns[k].to(dev) for k in keys])
-            kparts.append(uniq)
-            for n in out_names:
-                vparts[n].append(_C.unsorted_segment_reduce(monoid[n], b.columns[n].to(dev).contiguous(), ids, ng))
+        parts = [b for _, b in sorted(blocks.items()) if b.nrows]
         kdt = [D.torch_dtype(tf_types[k]) for k in keys]
-        if kparts:
-            K = [torch.cat([p[i] for p in kparts]) if len(kparts) > 1 else kparts[0][i] for i in range(len(keys))]
-            V = {n: torch.cat(vparts[n]) if len(vparts[n]) > 1 else vparts[n][0] for n in out_names}
-        else:
-            K = [torch.empty(0, dtype=t, device=dev) for t in kdt]
-            V = {n: None for n in out_names}
+        K: List[torch.Tensor] = [torch.empty(0, dtype=t, device=dev) for t in kdt]
+        V: Dict[str, Optional[torch.Tensor]] = {n: None for n in out_names}
+        if parts:
+            # this rank's keys are factorised ONCE over all its partitions
+            # (one id space), so every partition reduces straight into its
+            # row of a [P, groups, ...] buffer and the partitions combine by an
+            # elementwise fold: no second factorisation on a single rank
+            ids, K, ng = G.group_ids([engine.cat_rows([b.columns[k].to(dev) for b in parts]) for k in keys])
+            bounds = np.cumsum([0] + [b.nrows for b in parts])
+            for n in out_names:
+                vals = [b.columns[n].to(dev).contiguous() for b in parts]
+                if len(parts) == 1:
+                    V[n] = _C.unsorted_segment_reduce(monoid[n], vals[0], ids, ng)
+                    continue
+                stacked = torch.empty((len(parts), ng) + tuple(vals[0].shape[1:]), dtype=vals[0].dtype, device=dev)
+                for p, v in enumerate(vals):
+                    _C.unsorted_segment_reduce(monoid[n], v, ids[int(bounds[p]):int(bounds[p + 1])], ng,
+                                               out=stacked[p])
+                V[n] = _monoid_reduce(monoid[n], stacked, dev)
+        if not dist.is_distributed():
+            if K[0].shape[0] == 0:
+                return {0: Block(0, _empty_agg_cols(df, keys, out_names))}
+            out_cols: Dict[str, Any] = dict(zip(keys, K))
+            out_cols.update(V)
+            if not on_device or not keep_on_device:
+                out_cols = {k: v.cpu() for k, v in out_cols.items()}
+            metrics.add("aggregate_device_groupby" if dev.type == "cuda" else "aggregate_host_groupby")
+            return {0: Block(int(K[0].shape[0]), out_cols)}
         if dist.is_distributed():
             cells = _agree_shapes({n: (V[n][0] if V[n] is not None and V[n].shape[0] else None) for n in out_names},
                                   {n: agg_static.get(n) for n in out_names}, dev) if any(

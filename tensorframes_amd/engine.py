@@ -131,6 +131,31 @@ def empty_host(shape, dtype: torch.dtype, pinned: bool) -> torch.Tensor:
     return torch.empty(tuple(shape), dtype=dtype)
 
 
+def cat_rows(ts: Sequence[torch.Tensor]) -> torch.Tensor:
+    """Concatenate along dim 0. Device tensors are copied into one buffer with
+    device-to-device DMA (hipMemcpyAsync: contiguous same-dtype copy_), so no
+    ATen concat kernel runs on the engine's GPU paths."""
+    ts = list(ts)
+    if len(ts) == 1:
+        return ts[0]
+    t0 = ts[0]
+    if not t0.is_cuda:
+        return torch.cat(ts, 0)
+    out = torch.empty((sum(int(t.shape[0]) for t in ts),) + tuple(t0.shape[1:]), dtype=t0.dtype, device=t0.device)
+    a = 0
+    for t in ts:
+        b = a + int(t.shape[0])
+        if b > a:
+            out[a:b].copy_(t if t.is_contiguous() else t.contiguous())
+        a = b
+    return out
+
+
+def stack_rows(ts: Sequence[torch.Tensor]) -> torch.Tensor:
+    """torch.stack along a new dim 0, through cat_rows."""
+    return cat_rows([t.unsqueeze(0) for t in ts])
+
+
 def is_pinned(t: torch.Tensor) -> bool:
     return (not t.is_cuda) and gpu_available() and (t.is_pinned() or _C.is_pinned(t))
 

@@ -177,6 +177,47 @@ def column_values(col: Column) -> List[Any]:
     return list(col.values)
 
 
+_NATIVE_ROW_KINDS = {"f": (4, 8), "i": (1, 2, 4, 8), "u": (1, 2, 4, 8), "b": (1,)}
+
+
+def build_rows(names: Sequence[str], segments: Sequence[tuple]) -> list:
+    """Row objects from column payloads, segment after segment: `segments` =
+    [(nrows, [column payload per name])] with numpy arrays [rows, *cell],
+    tensors or value lists. Built natively in one list (runtime/packer.cpp
+    build_rows): scalars for rank-0 cells, nested lists for array cells
+    (reference convertBack: DataOps.scala:20-61)."""
+    import gc
+
+    from .._native import _C
+    from .types import Row
+    cls = Row.of_fields(names)
+    prepared = [(int(n), [_row_payload(c) for c in cols]) for n, cols in segments]
+    # millions of new container objects: the cyclic GC would rescan them
+    # every few hundred allocations (they cannot form cycles)
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        return _C.build_rows(cls, prepared)
+    finally:
+        if enabled:
+            gc.enable()
+
+
+def _row_payload(c: Any):
+    if isinstance(c, torch.Tensor):
+        c = c.detach().cpu()
+        c = c.numpy() if c.dtype in _NUMPY_OK else column_values(c)
+    if isinstance(c, np.ndarray):
+        if c.dtype.kind in _NATIVE_ROW_KINDS and c.dtype.itemsize in _NATIVE_ROW_KINDS[c.dtype.kind] and c.ndim >= 1:
+            return c
+        return c.tolist() if c.dtype.kind != "O" else list(c)
+    return c if isinstance(c, list) else list(c)
+
+
+_NUMPY_OK = (torch.float32, torch.float64, torch.int8, torch.int16, torch.int32, torch.int64, torch.uint8,
+             torch.bool)
+
+
 def column_cell(col: Column, i: int):
     if isinstance(col, torch.Tensor):
         v = col[i]

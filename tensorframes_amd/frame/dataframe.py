@@ -26,7 +26,7 @@ import torch
 
 from ..parallel import dist
 from ..utils import dtypes as D
-from .block import (Block, ObjectColumn, RaggedColumn, build_column, column_values, concat_blocks,
+from .block import (Block, ObjectColumn, RaggedColumn, build_column, build_rows, column_values, concat_blocks,
                     is_dense)
 from .column_info import ColumnInformation, DataFrameInfo, explain_schema
 from .types import (ArrayType, BinaryType, BooleanType, DataType, DoubleType, FloatType, IntegerType,
@@ -239,14 +239,9 @@ class DataFrame:
         return column_values(col)[a:b]
 
     def _rows_of(self, nrows: int, payload: Dict[str, Any]) -> List[Row]:
-        names = self._schema.names
-        if not names:
-            return [Row.from_fields([], []) for _ in range(nrows)]
-        cols = []
-        for n in names:
-            v = payload[n]
-            cols.append(column_values(torch.from_numpy(np.ascontiguousarray(v))) if isinstance(v, np.ndarray) else v)
-        return [Row.from_fields(names, vals) for vals in zip(*cols)]
+        """Row objects straight from the column buffers (native convertBack,
+        runtime/packer.cpp build_rows; reference: DataOps.scala:20-61)."""
+        return build_rows(self._schema.names, [(nrows, [payload[n] for n in self._schema.names])])
 
     def _local_columns(self) -> List[tuple]:
         out = []
@@ -259,7 +254,8 @@ class DataFrame:
         columns as arrays), and every rank builds the Row objects once."""
         parts = [x for chunk in dist.all_gather_object(self._local_columns()) for x in chunk]
         parts.sort(key=lambda x: x[0])
-        return [r for _, nrows, payload in parts for r in self._rows_of(nrows, payload)]
+        names = self._schema.names
+        return build_rows(names, [(nrows, [payload[n] for n in names]) for _, nrows, payload in parts])
 
     def count(self) -> int:
         n = sum(b.nrows for _, b in self._iter_blocks())

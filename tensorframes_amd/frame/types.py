@@ -225,22 +225,31 @@ class Row(tuple):
     ``Row(key='0', x=2.0)`` keeps the keyword order given.
     """
 
+    __fields__: Optional[List[str]] = None  # per-schema subclasses set it once (see of_fields)
+
     def __new__(cls, *args, **kwargs):
         if args and kwargs:
             raise ValueError("Row takes positional or keyword values, not both")
         if kwargs:
-            row = tuple.__new__(cls, list(kwargs.values()))
-            row.__fields__ = list(kwargs.keys())
-            return row
-        row = tuple.__new__(cls, args)
-        row.__fields__ = None
-        return row
+            return tuple.__new__(Row.of_fields(tuple(kwargs)), list(kwargs.values()))
+        return tuple.__new__(cls, args)
+
+    @staticmethod
+    def of_fields(names) -> type:
+        """The Row class of one field list: a Row subclass whose field names
+        live on the class, so its instances carry no per-row dict (the
+        native row builder, runtime/packer.cpp build_rows, fills them in
+        place)."""
+        names = tuple(names)
+        cls = _ROW_CLASSES.get(names)
+        if cls is None:
+            cls = type("Row", (Row,), {"__slots__": (), "__fields__": list(names), "__module__": Row.__module__})
+            _ROW_CLASSES[names] = cls
+        return cls
 
     @classmethod
     def from_fields(cls, names, values) -> "Row":
-        row = tuple.__new__(cls, list(values))
-        row.__fields__ = list(names)
-        return row
+        return tuple.__new__(Row.of_fields(names), list(values))
 
     def asDict(self) -> Dict[str, Any]:  # noqa: N802
         if self.__fields__ is None:
@@ -250,7 +259,7 @@ class Row(tuple):
     def __getattr__(self, item):
         if item.startswith("__"):
             raise AttributeError(item)
-        fields = self.__dict__.get("__fields__")
+        fields = self.__fields__
         if fields is None or item not in fields:
             raise AttributeError(item)
         return tuple.__getitem__(self, fields.index(item))
@@ -269,4 +278,9 @@ class Row(tuple):
         return "<Row(" + ", ".join(repr(v) for v in self) + ")>"
 
     def __reduce__(self):
-        return (Row.from_fields, (self.__fields__ or [], tuple(self)))
+        if self.__fields__ is None:
+            return (Row, tuple(self))
+        return (Row.from_fields, (self.__fields__, tuple(self)))
+
+
+_ROW_CLASSES: Dict[tuple, type] = {}

@@ -149,3 +149,111 @@ def test_unsorted_segment_many_segments_gpu(op, fn, inner):
     torch.testing.assert_close(got, want, rtol=1e-12, atol=1e-12)
     again = engine.run_program(prog, [torch.from_numpy(x), torch.from_numpy(ids)], dev)[0].cpu()
     assert torch.equal(got, again)  # deterministic
+
+
+def _float_keys_with_specials(n, dt, seed):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(-20, 20, n).astype(np.float64) / 4
+    k[rng.random(n) < 0.05] = np.nan
+    k[rng.random(n) < 0.05] = -0.0
+    k[rng.random(n) < 0.02] = np.inf
+    k[rng.random(n) < 0.02] = -np.inf
+    nan2 = np.frombuffer(np.uint64(0xfff8000000000001).tobytes(), np.float64)[0]  # another NaN payload
+    k[rng.random(n) < 0.02] = nan2
+    return torch.tensor(k).to(dt)
+
+
+def _check_special_groups(k, ids, uniq, ng):
+    kn = k.cpu().double().numpy()
+    u = uniq[0].cpu().double().numpy()
+    want = np.unique(np.where(kn == 0, 0.0, kn))  # numpy: NaNs equal, one group last
+    assert ng == len(want), (ng, want)
+    np.testing.assert_array_equal(u, want)
+    assert not np.signbit(u[u == 0]).any()  # the zero group is +0.0
+    idn = ids.cpu().numpy()
+    canon = np.where(np.isnan(kn), np.inf * 2, kn)  # compare NaN as one value
+    wantc = np.where(np.isnan(want), np.inf * 2, want)
+    assert np.array_equal(wantc[idn], np.where(canon == 0, 0.0, canon))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_group_ids_nan_and_signed_zero_keys_cpu(dt):
+    k = _float_keys_with_specials(5000, dt, 7)
+    ids, uniq, ng = G.group_ids([k])
+    _check_special_groups(k, ids, uniq, ng)
+
+
+def test_key_hash_routes_equal_float_keys_together():
+    from tensorframes_amd.core import _key_hash
+    nan2 = np.frombuffer(np.uint64(0xfff8000000000001).tobytes(), np.float64)[0]
+    a = np.array([np.nan, nan2, 0.0, -0.0])
+    h = _key_hash([a])
+    assert h[0] == h[1] and h[2] == h[3]
+
+
+def test_aggregate_nan_keys_form_one_group():
+    k = np.array([1.0, np.nan, -0.0, 0.0, np.nan, 1.0])
+    x = np.arange(6, dtype=np.float64)
+    df = tfs.from_columns({"k": k, "x": x}, num_partitions=2)
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, [None], name="x_input")
+        rows = tfs.aggregate(tf.reduce_sum(xi, [0], name="x"), df.groupBy("k")).collect()
+    got = {("nan" if np.isnan(r.k) else float(r.k)): float(r.x) for r in rows}
+    assert got == {0.0: 5.0, 1.0: 5.0, "nan": 5.0}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_factorize_nan_and_signed_zero_keys_gpu(dt):
+    dev = _gpu()
+    k = _float_keys_with_specials(200_001, dt, 8)
+    ids, uniq, ng = G.group_ids([k.to(dev)])
+    _check_special_groups(k, ids, uniq, ng)
+    ids_c, uniq_c, ng_c = G.group_ids([k])
+    assert ng == ng_c and torch.equal(ids.cpu(), ids_c)
+    assert torch.equal(uniq[0].cpu().isnan(), uniq_c[0].isnan())
+    dest = _C.key_dest([k.to(dev)], 8).cpu().numpy()
+    kn = k.double().numpy()
+    assert len(set(dest[np.isnan(kn)])) == 1 and len(set(dest[kn == 0])) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["dense", "narrow_sort", "wide", "single", "one_tile"])
+@pytest.mark.parametrize("dt", [torch.int32, torch.int64])
+def test_factorize_int_paths_gpu(kind, dt):
+    """The dense (direct-address), narrow radix-sort and full-width radix-sort
+    factorisations agree with the host oracle; sizes straddle the 4096-key
+    sort tile and the 2048-element scan tile."""
+    dev = _gpu()
+    rng = np.random.default_rng(9)
+    n = {"dense": 3_000_017, "narrow_sort": 1_000_003, "wide": 777_777, "single": 1, "one_tile": 4095}[kind]
+    if kind == "dense":
+        k = rng.integers(-50_000, 50_000, n)
+    elif kind == "narrow_sort":  # range >> rows: sorted on the bits of key - min
+        k = rng.integers(0, 1 << 30, n) * (1 if dt == torch.int64 else 1) - (1 << 29)
+    elif kind == "wide":
+        if dt == torch.int32:
+            k = rng.integers(-(1 << 31), (1 << 31) - 1, n)
+        else:
+            k = rng.integers(-(1 << 62), 1 << 62, n)
+    else:
+        k = rng.integers(-3, 1 << 20, n)
+    kt = torch.tensor(k).to(dt)
+    ids, uniq, ng = G.group_ids([kt.to(dev)])
+    want_u, want_inv = np.unique(kt.numpy(), return_inverse=True)
+    assert ng == len(want_u)
+    np.testing.assert_array_equal(uniq[0].cpu().numpy(), want_u)
+    np.testing.assert_array_equal(ids.cpu().numpy(), want_inv.reshape(-1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 3, 8, 256])
+def test_partition_rows_is_stable_gpu(world):
+    dev = _gpu()
+    n = 300_001
+    dest = torch.tensor(np.random.default_rng(10).integers(0, world, n)).to(dev)
+    perm, counts = _C.partition_rows(dest, world)
+    p = perm.cpu().numpy()
+    want = np.argsort(dest.cpu().numpy(), kind="stable")
+    np.testing.assert_array_equal(p, want)
+    np.testing.assert_array_equal(counts.cpu().numpy(), np.bincount(dest.cpu().numpy(), minlength=world))
