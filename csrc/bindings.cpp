@@ -382,6 +382,45 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                       ws.data_ptr(), wsb, s);
     return py::make_tuple(perm, counts);
   }, "rows ordered by destination rank (stable) + rows per destination (device)");
+  m.def("segment_csr", [](const at::Tensor& ids0, int64_t nseg) {
+    TFA_CHECK(ids0.is_cuda() && ids0.dim() == 1 && (ids0.scalar_type() == at::kLong || ids0.scalar_type() == at::kInt),
+              "segment_csr: device int ids");
+    c10::hip::HIPGuard guard(ids0.device().index());
+    at::Tensor ids = ids0.contiguous();
+    const int64_t n = ids.size(0);
+    hipStream_t s = c10::hip::getCurrentHIPStream(ids.device().index()).stream();
+    at::Tensor perm = at::empty({n}, ids.options().dtype(at::kLong));
+    at::Tensor off = at::empty({nseg + 1}, ids.options().dtype(at::kLong));
+    const size_t wsb = k::segment_csr_workspace_bytes(n, nseg);
+    at::Tensor ws = at::empty({static_cast<int64_t>(wsb)}, ids.options().dtype(at::kByte));
+    k::segment_csr(from_scalar_type(ids.scalar_type()), ids.data_ptr(), n, nseg, perm.data_ptr<int64_t>(),
+                   off.data_ptr<int64_t>(), ws.data_ptr(), wsb, s);
+    return py::make_tuple(perm, off);
+  }, "ids [n] in [0, nseg) -> (rows ordered by segment, stable; CSR offsets [nseg + 1]) on the device");
+  m.def("segment_rows", [](const at::Tensor& perm, const at::Tensor& offs, int64_t size) {
+    TFA_CHECK(perm.is_cuda() && offs.is_cuda() && perm.scalar_type() == at::kLong && offs.scalar_type() == at::kLong,
+              "segment_rows: device int64 tensors");
+    c10::hip::HIPGuard guard(perm.device().index());
+    const int64_t G = offs.size(0);
+    at::Tensor idx = at::empty({G * size}, perm.options());
+    k::segment_rows(perm.contiguous().data_ptr<int64_t>(), offs.contiguous().data_ptr<int64_t>(), G, size,
+                    idx.data_ptr<int64_t>(), c10::hip::getCurrentHIPStream(perm.device().index()).stream());
+    return idx;
+  }, "row ids of G equal-size segments: perm[offs[g] + j] for j < size -> [G * size]");
+  m.def("scatter_rows", [](at::Tensor dst, const at::Tensor& idx, const at::Tensor& src0) {
+    TFA_CHECK(dst.is_cuda() && idx.is_cuda() && src0.is_cuda() && idx.scalar_type() == at::kLong,
+              "scatter_rows: device tensors");
+    TFA_CHECK(dst.is_contiguous() && dst.dim() >= 1 && src0.scalar_type() == dst.scalar_type(),
+              "scatter_rows: contiguous dst of the source dtype");
+    c10::hip::HIPGuard guard(dst.device().index());
+    at::Tensor src = src0.contiguous();
+    TFA_CHECK(src.size(0) == idx.size(0), "scatter_rows: one index per source row");
+    const int64_t row = dst.size(0) ? dst.numel() / dst.size(0) : 0;
+    TFA_CHECK(src.numel() == idx.size(0) * row, "scatter_rows: source rows must match the destination row shape");
+    k::scatter_rows(row * dst.element_size(), src.data_ptr(), idx.contiguous().data_ptr<int64_t>(), dst.data_ptr(),
+                    idx.size(0), c10::hip::getCurrentHIPStream(dst.device().index()).stream());
+    return dst;
+  }, "dst[idx[j]] = src[j] along dim 0 (device scatter kernel), in place");
   m.def("gather_rows", [](const at::Tensor& x0, const at::Tensor& idx) {
     TFA_CHECK(x0.is_cuda() && idx.is_cuda() && idx.scalar_type() == at::kLong, "gather_rows: device tensors");
     c10::hip::HIPGuard guard(x0.device().index());

@@ -403,6 +403,30 @@ int64_t factorize_typed(const K* keys, int64_t n, int64_t* ids, K* uniq, void* w
   return (int64_t)count;
 }
 
+// idx[g * size + j] = perm[offs[g] + j]: the rows of G equal-size segments
+__global__ __launch_bounds__(kT) void segment_rows_kernel(const int64_t* __restrict__ perm,
+                                                          const int64_t* __restrict__ offs, int64_t G, int64_t size,
+                                                          int64_t* __restrict__ idx) {
+  const int64_t n = G * size;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t g = i / size;
+    idx[i] = perm[offs[g] + (i - g * size)];
+  }
+}
+
+// dst row idx[j] = src row j, rows of `words` W-sized words
+template <typename W>
+__global__ __launch_bounds__(kT) void scatter_rows_kernel(const W* __restrict__ src, const int64_t* __restrict__ idx,
+                                                          W* __restrict__ dst, int64_t nidx, int64_t words) {
+  const int64_t n = nidx * words;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t j = i / words, w = i - j * words;
+    dst[idx[j] * words + w] = src[i];
+  }
+}
+
 }  // namespace
 
 size_t factorize_workspace_bytes(DType dt, int64_t n) {
@@ -503,6 +527,27 @@ void partition_rows(const int64_t* dest, int64_t n, int64_t world, int64_t* perm
   // stable: rows keep their order within a destination
   radix::sort_pairs<uint32_t, int64_t>(key, nullptr, sorted, perm, n, bits_for((unsigned long long)world - 1), p, tmp, s);
   TFA_LAUNCH_CHECK("partition_rows");
+}
+
+void segment_rows(const int64_t* perm, const int64_t* offs, int64_t G, int64_t size, int64_t* idx, hipStream_t s) {
+  if (G * size == 0) return;
+  hipLaunchKernelGGL(segment_rows_kernel, dim3(ew_grid(G * size)), dim3(kT), 0, s, perm, offs, G, size, idx);
+  TFA_LAUNCH_CHECK("segment_rows");
+}
+
+void scatter_rows(int64_t row_bytes, const void* src, const int64_t* idx, void* dst, int64_t nidx, hipStream_t s) {
+  if (nidx * row_bytes == 0) return;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst);
+  if (row_bytes % 8 == 0 && al % 8 == 0)
+    hipLaunchKernelGGL((scatter_rows_kernel<uint64_t>), dim3(ew_grid(nidx * row_bytes / 8)), dim3(kT), 0, s,
+                       (const uint64_t*)src, idx, (uint64_t*)dst, nidx, row_bytes / 8);
+  else if (row_bytes % 4 == 0 && al % 4 == 0)
+    hipLaunchKernelGGL((scatter_rows_kernel<uint32_t>), dim3(ew_grid(nidx * row_bytes / 4)), dim3(kT), 0, s,
+                       (const uint32_t*)src, idx, (uint32_t*)dst, nidx, row_bytes / 4);
+  else
+    hipLaunchKernelGGL((scatter_rows_kernel<uint8_t>), dim3(ew_grid(nidx * row_bytes)), dim3(kT), 0, s,
+                       (const uint8_t*)src, idx, (uint8_t*)dst, nidx, row_bytes);
+  TFA_LAUNCH_CHECK("scatter_rows");
 }
 
 void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s) {

@@ -94,6 +94,10 @@ void segment_reduce_perm(RedOp op, DType dt, const void* x, const int64_t* perm,
                          int64_t nseg, int64_t inner, hipStream_t s);
 // rep[g] = some row of group g (ids in [0, nseg))
 void group_representatives(const int64_t* ids, int64_t n, int64_t* rep, hipStream_t s);
+// idx[g * size + j] = perm[offs[g] + j]: row ids of G segments of one size
+void segment_rows(const int64_t* perm, const int64_t* offs, int64_t G, int64_t size, int64_t* idx, hipStream_t s);
+// dst row idx[j] = src row j (rows of row_bytes bytes)
+void scatter_rows(int64_t row_bytes, const void* src, const int64_t* idx, void* dst, int64_t nidx, hipStream_t s);
 // rows ordered by destination (stable): perm [n]; counts [world] rows per destination
 size_t partition_workspace_bytes(int64_t n);
 void partition_rows(const int64_t* dest, int64_t n, int64_t world, int64_t* perm, int64_t* counts, void* workspace,

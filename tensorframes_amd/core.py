@@ -1335,26 +1335,83 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
         for n in names:
             results[n] = comb[n].cpu().numpy()
         return _unpack(results, spec, summary)
-    # generic: sequential fold per partition, then fold the partials
+    # generic pair graph: lifted over a batch of row pairs (graph/vectorize.py)
+    # it folds a whole block as a tree on the device, log2(rows) launches;
+    # graphs that cannot be lifted fold row by row
+    fetch_refs = [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in names]
+    feed_names = [n + "_1" for n in names] + [n + "_2" for n in names]
+    lifter = _RowVectorizer(spec.graph_bytes, fetch_refs, feed_names, [summary[n].tf_dtype for n in names] * 2)
+
+    def fold_block(cols: List[Any]) -> List[torch.Tensor]:
+        if config.map_rows_vectorize and all(is_dense(c) for c in cols):
+            dev = _fold_device(cols)
+            cells = [tuple(c.shape[1:]) for c in cols]
+            lifted = lifter._program(tuple(cells) * 2)
+            if lifted is not None:
+                metrics.add("reduce_rows_tree_folds")
+                return _tree_fold(lifted, [c.to(dev) for c in cols], dev)
+        return _fold_rows(prog, names, [_cells(c) for c in cols])
+
     def fold_task(blocks):
-        return {pid: [t.cpu() for t in _fold_rows(prog, names, [_cells(b.columns[n]) for n in names])]
-                for pid, b in sorted(blocks.items()) if b.nrows > 0}
+        return {pid: fold_block([b.columns[n] for n in names]) for pid, b in sorted(blocks.items()) if b.nrows > 0}
     per_part = faults.with_retries("reduce_rows", fold_task)(dframe.local_blocks())
     partials_rows = [per_part[pid] for pid in sorted(per_part)]
-    # this rank's partials folded pairwise, then the per-rank partials gathered
+    # this rank's partials folded as a tree too, then the per-rank partials gathered
     local: Dict[str, Optional[torch.Tensor]] = {n: None for n in names}
     if partials_rows:
-        acc = partials_rows[0]
-        for r in partials_rows[1:]:
-            acc = engine.run_program(prog, list(acc) + list(r), engine.small_work_device())
+        acc = partials_rows[0] if len(partials_rows) == 1 else _fold_partials(fold_block, partials_rows)
         local = dict(zip(names, acc))
     static = {n: None for n in names}  # generic pair graphs: shapes agreed at run time
     allp = _gather_rank_values(local, static, {n: summary[n].tf_dtype for n in names})
     _check(all(allp[n] for n in names), "Cannot reduce an empty DataFrame")
-    acc = [allp[n][0] for n in names]
-    for r in range(1, len(allp[names[0]])):
-        acc = engine.run_program(prog, acc + [allp[n][r] for n in names], engine.small_work_device())
+    rank_rows = [[allp[n][r] for n in names] for r in range(len(allp[names[0]]))]
+    acc = rank_rows[0] if len(rank_rows) == 1 else _fold_partials(fold_block, rank_rows)
     return _unpack({n: a.cpu().numpy() for n, a in zip(names, acc)}, spec, summary)
+
+
+def _fold_device(cols: List[torch.Tensor]) -> torch.device:
+    """Where a tree fold runs: the data's device, or the compute device for
+    host blocks big enough to pay for the copy."""
+    if cols[0].is_cuda:
+        return cols[0].device
+    if not engine.gpu_available() or config.device == "cpu":
+        return torch.device("cpu")
+    if config.device == "cuda":
+        return engine.compute_device()
+    nbytes = sum(c.numel() * c.element_size() for c in cols)
+    return engine.compute_device() if nbytes >= config.map_rows_gpu_min_elems * 4 else torch.device("cpu")
+
+
+def _fold_partials(fold_block, rows: List[List[torch.Tensor]]) -> List[torch.Tensor]:
+    """Folds per-partition (or per-rank) partial cells: stacked into blocks
+    of equal cell shapes when possible, then through the block fold."""
+    ncol = len(rows[0])
+    shapes = {tuple(tuple(r[j].shape) for j in range(ncol)) for r in rows}
+    if len(shapes) == 1:
+        dev = rows[0][0].device
+        return fold_block([engine.stack_rows([r[j].to(dev) for r in rows]) for j in range(ncol)])
+    return fold_block([RaggedColumn([r[j].cpu().numpy() for r in rows], D.as_dtype(rows[0][j].dtype).enum)
+                       for j in range(ncol)])
+
+
+def _tree_fold(lifted, cols: List[torch.Tensor], dev: torch.device) -> List[torch.Tensor]:
+    """Fold n rows of a lifted pair graph as a tree: the first half of the
+    rows is paired with the second half (one launch over n/2 pairs) until one
+    row is left; an odd row is folded into row 0 of the next level. The pair
+    order differs from a left fold, which the reduce_rows contract allows
+    (reference: the partition fold and RDD.reduce order are unspecified,
+    DebugRowOps.scala:930-969)."""
+    xs = [c.contiguous() for c in cols]
+    n = int(xs[0].shape[0])
+    while n > 1:
+        h = n // 2
+        out = engine.run_program(lifted, [x[:h] for x in xs] + [x[h:2 * h] for x in xs], dev)
+        if n % 2:
+            tail = engine.run_program(lifted, [o[:1] for o in out] + [x[2 * h:2 * h + 1] for x in xs], dev)
+            for o, t in zip(out, tail):
+                o[:1].copy_(t)
+        xs, n = out, h
+    return [x[0] for x in xs]
 
 
 def _fold_rows(prog, names, cells_per_col) -> List[torch.Tensor]:
@@ -1621,9 +1678,84 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
     lifter = _RowVectorizer(spec.graph_bytes, [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names],
                             in_names, [summary[n].tf_dtype for n in out_names])
 
+    def device_generic(blocks):
+        """Any associative reducer graph, numeric keys, dense columns, on the
+        GPU: keys and values stay in HBM. Rows are routed to their key's owner
+        (RCCL all-to-all), factorised (groupby.hip), ordered by group
+        (segment CSR); groups of equal size run as ONE launch of the graph
+        lifted over a group axis ([G, size, ...] -> [G, ...]), gathered and
+        scattered by our kernels. Unliftable graphs / unique sizes run group
+        by group from the same device CSR."""
+        from .ops import groupby as G
+        dev = engine.compute_device()
+        parts = [b for _, b in sorted(blocks.items()) if b.nrows]
+        kdt = [D.torch_dtype(tf_types[k]) for k in keys]
+        if parts:
+            K = [engine.cat_rows([b.columns[k].to(dev) for b in parts]) for k in keys]
+            V = [engine.cat_rows([b.columns[n].to(dev).contiguous() for b in parts]) for n in out_names]
+        else:
+            K = [torch.empty(0, dtype=t, device=dev) for t in kdt]
+            cells = {n: agg_static_in.get(n) for n in out_names}
+            V = [torch.empty((0,) + tuple(cells[n] or ()), dtype=D.torch_dtype(summary[n].tf_dtype), device=dev)
+                 for n in out_names]
+        if dist.is_distributed():
+            recv = G.route(K, V)
+            K, V = recv[:len(keys)], recv[len(keys):]
+        if K[0].shape[0] == 0:
+            return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, dist.world_size()))}
+        ids, uniq, ng = G.group_ids(K)
+        perm, offsets = _C.segment_csr(ids, ng)
+        off_h = offsets.cpu().numpy()
+        counts = np.diff(off_h)
+        by_size: Dict[int, List[int]] = {}
+        for g, c in enumerate(counts.tolist()):
+            by_size.setdefault(c, []).append(g)
+        out: Dict[str, Optional[torch.Tensor]] = {n: None for n in out_names}
+        batched = 0
+
+        def put(gidx: torch.Tensor, outs):
+            for n, o in zip(out_names, outs):
+                o = o.to(dev)
+                if out[n] is None:
+                    out[n] = torch.empty((ng,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev)
+                _C.scatter_rows(out[n], gidx, o)
+
+        for size, gl in sorted(by_size.items()):
+            gidx = torch.from_numpy(np.asarray(gl, dtype=np.int64)).to(dev)
+            idx = _C.segment_rows(perm, torch.from_numpy(off_h[gl]).to(dev), size)
+            ins = [_C.gather_rows(v, idx).reshape((len(gl), size) + tuple(v.shape[1:])) for v in V]
+            lifted = lifter.program_for(tuple((size,) + tuple(v.shape[1:]) for v in V)) if len(gl) >= 2 else None
+            if lifted is not None:
+                outs = engine.run_program(lifted, ins, dev)
+                if all(o.dim() >= 1 and o.shape[0] == len(gl) for o in outs):
+                    put(gidx, outs)
+                    batched += len(gl)
+                    continue
+            for j in range(len(gl)):
+                outs = engine.run_program(prog, [x[j] for x in ins], dev)
+                put(gidx[j:j + 1], [o.unsqueeze(0) for o in outs])
+        metrics.add("aggregate_batched_groups", batched)
+        metrics.add("aggregate_single_groups", ng - batched)
+        metrics.add("aggregate_device_generic")
+        out_cols: Dict[str, Any] = dict(zip(keys, uniq))
+        out_cols.update(out)
+        if not keep_on_device:
+            out_cols = {k: v.cpu() for k, v in out_cols.items()}
+        return {dist.rank(): Block(ng, out_cols)}
+
+    # static cell shapes of the input columns, for ranks without rows
+    agg_static_in = {}
+    for n in out_names:
+        cell = _col_info(df.schema[n]).shape.tail()
+        agg_static_in[n] = None if cell.has_unknown() else tuple(cell.dims)
+
     def compute(blocks):
         if uniform and all(is_dense(b.columns[n]) for b in blocks.values() for n in out_names):
             return combine(blocks)
+        # decided from the schema + device, so every rank takes the same (collective) path
+        if numeric_keys and engine.gpu_available() and config.device != "cpu" and \
+                all(is_dense(b.columns[n]) for b in blocks.values() for n in out_names):
+            return device_generic(blocks)
         # 1. shuffle: rows go to rank hash(key) % world (all-to-all)
         w = dist.world_size()
         send = [[] for _ in range(w)]

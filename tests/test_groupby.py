@@ -257,3 +257,63 @@ def test_partition_rows_is_stable_gpu(world):
     want = np.argsort(dest.cpu().numpy(), kind="stable")
     np.testing.assert_array_equal(p, want)
     np.testing.assert_array_equal(counts.cpu().numpy(), np.bincount(dest.cpu().numpy(), minlength=world))
+
+
+def _range_graph(width):
+    xi = tf.placeholder(tf.double, [None, width], name="x_input")
+    # not a monoid: per-key range (max - min) of every column
+    return tf.identity(tf.reduce_max(xi, [0]) - tf.reduce_min(xi, [0]), name="x")
+
+
+@pytest.mark.gpu
+def test_generic_aggregate_device_matches_numpy_gpu():
+    dev = _gpu()
+    rng = np.random.default_rng(11)
+    n = 200_003
+    k = rng.integers(-500, 1500, n)
+    k[:7] = 99_999  # one big group, and sizes that occur once
+    x = rng.standard_normal((n, 2))
+    df = tfs.from_columns({"k": torch.tensor(k).to(dev), "x": torch.tensor(x).to(dev)},
+                          num_partitions=3).cache_on_device(dev)
+    before = metrics.snapshot().get("aggregate_device_generic", 0)
+    with tf.Graph().as_default():
+        blk = tfs.aggregate(_range_graph(2), df.groupBy("k")).local_blocks()
+    assert metrics.snapshot().get("aggregate_device_generic", 0) - before == 1
+    (b,) = blk.values()
+    kk, xx = b.columns["k"].cpu().numpy(), b.columns["x"].cpu().numpy()
+    want_k, inv = np.unique(k, return_inverse=True)
+    assert np.array_equal(kk, want_k)
+    mx = np.full((len(want_k), 2), -np.inf)
+    mn = np.full((len(want_k), 2), np.inf)
+    np.maximum.at(mx, inv.reshape(-1), x)
+    np.minimum.at(mn, inv.reshape(-1), x)
+    np.testing.assert_array_equal(xx, mx - mn)
+
+
+@pytest.mark.gpu
+def test_generic_aggregate_10m_rows_100k_keys_gpu():
+    """a non-monoid aggregate over 10M device-cached rows /
+    100k keys in < 50 ms (round 2: host pandas/np.unique + per-group loop)."""
+    import time
+    dev = _gpu()
+    n, nk = 10_000_000, 100_000
+    g = torch.Generator(device=dev).manual_seed(12)
+    keys = torch.randint(0, nk, (n,), device=dev, generator=g, dtype=torch.int64)
+    x = torch.rand((n, 4), device=dev, generator=g, dtype=torch.float64)
+    df = tfs.from_columns({"k": keys, "x": x}, num_partitions=4).cache_on_device(dev)
+    with tf.Graph().as_default():
+        gr = _range_graph(4)
+        tfs.aggregate(gr, df.groupBy("k")).local_blocks()  # lifts + plans once per group size
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        blk = tfs.aggregate(gr, df.groupBy("k")).local_blocks()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    (b,) = blk.values()
+    assert b.nrows == nk
+    print(f"generic aggregate 10M rows / 100k keys: {dt * 1e3:.1f} ms")
+    kn = keys.cpu().numpy()
+    xn = x.cpu().numpy()
+    sel = np.nonzero(kn == 12345)[0]
+    np.testing.assert_array_equal(b.columns["x"][12345].cpu().numpy(), xn[sel].max(0) - xn[sel].min(0))
+    assert dt < 0.05, dt
