@@ -93,8 +93,13 @@ def rank_main(args):
     use_gpu = args.device == "cuda"
     dist.init(backend=None if use_gpu else "gloo")
     rank, world = dist.rank(), dist.world_size()
-    if world != args.gpus and rank == 0:
-        print(f"bench.py: --gpus {args.gpus} but the job has {world} ranks; reporting {world}", file=sys.stderr)
+    backend = dist.backend_name()
+    # the multi-GPU numbers are only meaningful on the job the driver asked
+    # for: N ranks over RCCL. A silent fallback (gloo, or fewer ranks) fails here.
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)")
+    if use_gpu and world > 1 and backend != "nccl":
+        raise SystemExit(f"bench.py: GPU job with backend {backend!r}; expected 'nccl' (RCCL over xGMI)")
     if use_gpu:
         assert torch.cuda.is_available(), "bench.py needs a GPU (or --device cpu)"
         dev = torch.device("cuda", dist.local_rank() % torch.cuda.device_count())
@@ -149,14 +154,15 @@ def rank_main(args):
         sync()
         dist.barrier()
         dt = time.perf_counter() - t0
+        own_dt = dt
         if dist.is_distributed():
             t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce_(t, "Max")
             dt = float(t.item())
-        return dt, res
+        return dt, own_dt, res
 
-    results = {}
-    dt, res = timed(step_host, args.steps, args.warmup)
+    results, own = {}, {}
+    dt, own["host"], res = timed(step_host, args.steps, args.warmup)
     # correctness spot check on a few rows of the first local partition
     pid = min(res)
     xin = blocks[pid].columns["x"][:64].double()
@@ -171,13 +177,26 @@ def rank_main(args):
 
         def step_dev():
             return tfs.map_blocks(y, base_dev, trim=True).local_blocks()
-        ddt, _ = timed(step_dev, args.steps, args.warmup)
+        ddt, own["device"], _ = timed(step_dev, args.steps, args.warmup)
         dev_rows_per_s = args.rows * args.steps / ddt
         results["device"] = ddt
         del base_dev
 
     ms = results["host"] / args.steps * 1e3
     value = args.rows * args.steps / results["host"]
+    # one diagnostic line per rank on stderr (the driver's 8-GPU run is
+    # diagnosable from its log): placement, backend, page-locked memory, own time
+    pool = _C.pinned_pool_stats() if use_gpu else {}
+    print(json.dumps({"bench_rank": rank, "local_rank": dist.local_rank(), "world_size": world,
+                      "backend": backend, "device": str(dev),
+                      "numa_cpus": (f"{min(numa_cpus)}-{max(numa_cpus)}" if numa_cpus else None),
+                      "numa_cpu_count": len(numa_cpus),
+                      "pinned_live_bytes": pool.get("live"), "pinned_peak_bytes": pool.get("peak"),
+                      "pinned_cap_bytes": pool.get("limit"),
+                      "own_ms_per_step": own["host"] / args.steps * 1e3,
+                      "own_device_ms_per_step": (own["device"] / args.steps * 1e3) if "device" in own else None,
+                      "rows": sum(b.nrows for b in blocks.values()), "partitions": sorted(blocks)}),
+          file=sys.stderr, flush=True)
     if rank == 0:
         out = {
             "metric": "rows/sec map_blocks MatMul on 10M-row DF at 1/2/4/8 MI355X",

@@ -421,6 +421,60 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                     idx.size(0), c10::hip::getCurrentHIPStream(dst.device().index()).stream());
     return dst;
   }, "dst[idx[j]] = src[j] along dim 0 (device scatter kernel), in place");
+  // one record per row holding every column (the keyed shuffle's single
+  // all-to-all payload): column c at byte offset offs[c] of R-byte records
+  m.def("pack_rows", [](const std::vector<at::Tensor>& cols, std::optional<at::Tensor> perm) {
+    TFA_CHECK(!cols.empty() && cols.size() <= static_cast<size_t>(k::kMaxPackCols), "pack_rows: 1..16 columns");
+    const int64_t n = perm ? perm->size(0) : cols[0].size(0);
+    k::PackCols pc;
+    pc.n = static_cast<int>(cols.size());
+    std::vector<at::Tensor> keep;
+    int64_t R = 0;
+    for (size_t c = 0; c < cols.size(); ++c) {
+      at::Tensor t = cols[c].contiguous();
+      TFA_CHECK(t.is_cuda() && t.dim() >= 1 && t.device() == cols[0].device(), "pack_rows: device columns");
+      TFA_CHECK(perm || t.size(0) == n, "pack_rows: columns disagree on rows");
+      const int64_t rb = t.size(0) ? t.numel() / t.size(0) * t.element_size() : 0;
+      pc.row_bytes[c] = rb;
+      pc.off[c] = R;
+      pc.ptr[c] = t.data_ptr();
+      R += (rb + 3) / 4 * 4;
+      keep.push_back(t);
+    }
+    c10::hip::HIPGuard guard(cols[0].device().index());
+    at::Tensor out = at::empty({n, R}, cols[0].options().dtype(at::kByte));
+    const int64_t* pp = nullptr;
+    at::Tensor pc_t;
+    if (perm) {
+      pc_t = perm->contiguous();
+      TFA_CHECK(pc_t.is_cuda() && pc_t.scalar_type() == at::kLong, "pack_rows: device int64 perm");
+      pp = pc_t.data_ptr<int64_t>();
+    }
+    k::pack_rows(pc, pp, n, R, out.data_ptr(), c10::hip::getCurrentHIPStream(cols[0].device().index()).stream());
+    std::vector<int64_t> offs(pc.off, pc.off + pc.n);
+    return py::make_tuple(out, offs);
+  }, py::arg("cols"), py::arg("perm") = py::none(),
+     "device columns -> (uint8 records [n, R] in perm order, byte offset of each column)");
+  m.def("unpack_rows", [](const at::Tensor& rec, const std::vector<at::Tensor>& outs) {
+    TFA_CHECK(rec.is_cuda() && rec.dim() == 2 && rec.scalar_type() == at::kByte, "unpack_rows: device uint8 records");
+    TFA_CHECK(!outs.empty() && outs.size() <= static_cast<size_t>(k::kMaxPackCols), "unpack_rows: 1..16 columns");
+    const int64_t n = rec.size(0);
+    k::PackCols pc;
+    pc.n = static_cast<int>(outs.size());
+    int64_t R = 0;
+    for (size_t c = 0; c < outs.size(); ++c) {
+      const at::Tensor& t = outs[c];
+      TFA_CHECK(t.is_cuda() && t.is_contiguous() && t.size(0) == n, "unpack_rows: contiguous device outputs of n rows");
+      const int64_t rb = n ? t.numel() / n * t.element_size() : 0;
+      pc.row_bytes[c] = rb;
+      pc.off[c] = R;
+      pc.ptr[c] = t.data_ptr();
+      R += (rb + 3) / 4 * 4;
+    }
+    TFA_CHECK(R == rec.size(1), "unpack_rows: record width ", rec.size(1), " does not match the columns (", R, ")");
+    c10::hip::HIPGuard guard(rec.device().index());
+    k::unpack_rows(pc, rec.contiguous().data_ptr(), n, R, c10::hip::getCurrentHIPStream(rec.device().index()).stream());
+  }, "records [n, R] -> the preallocated device columns (same layout as pack_rows)");
   m.def("gather_rows", [](const at::Tensor& x0, const at::Tensor& idx) {
     TFA_CHECK(x0.is_cuda() && idx.is_cuda() && idx.scalar_type() == at::kLong, "gather_rows: device tensors");
     c10::hip::HIPGuard guard(x0.device().index());
@@ -564,6 +618,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return attr.type == hipMemoryTypeHost;
   });
   m.def("pinned_pool_cached_bytes", &pinned_pool_cached_bytes);
+  m.def("pinned_pool_stats", [] {
+    auto v = pinned_pool_stats();
+    py::dict d;
+    d["limit"] = v[0];
+    d["cached"] = v[1];
+    d["live"] = v[2];
+    d["peak"] = v[3];
+    return d;
+  }, "page-locked pool: cap, cached free bytes, live bytes, peak live bytes");
   m.def("pin_host_tensor", &pin_host_tensor);
   m.def("unpin_host_tensor", &unpin_host_tensor);
 }

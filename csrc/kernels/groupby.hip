@@ -427,6 +427,37 @@ __global__ __launch_bounds__(kT) void scatter_rows_kernel(const W* __restrict__ 
   }
 }
 
+// Row packing for the keyed shuffle: the columns of a row, each in a
+// word-aligned slot of one R-byte record, so ONE all-to-all moves them all.
+template <typename W>
+__global__ __launch_bounds__(kT) void pack_rows_kernel(PackCols pc, const int64_t* __restrict__ perm, int64_t nrows,
+                                                       int64_t rwords, W* __restrict__ out) {
+  const int64_t n = nrows * rwords;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t j = i / rwords, w = i - j * rwords;
+    int c = 0;
+    while (c + 1 < pc.n && w >= pc.off[c + 1] / (int64_t)sizeof(W)) ++c;
+    const int64_t cw = w - pc.off[c] / (int64_t)sizeof(W), cwords = pc.row_bytes[c] / (int64_t)sizeof(W);
+    const int64_t src_row = perm ? perm[j] : j;
+    out[i] = cw < cwords ? static_cast<const W*>(pc.ptr[c])[src_row * cwords + cw] : W(0);
+  }
+}
+
+template <typename W>
+__global__ __launch_bounds__(kT) void unpack_rows_kernel(PackCols pc, const W* __restrict__ in, int64_t nrows,
+                                                         int64_t rwords) {
+  const int64_t n = nrows * rwords;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t j = i / rwords, w = i - j * rwords;
+    int c = 0;
+    while (c + 1 < pc.n && w >= pc.off[c + 1] / (int64_t)sizeof(W)) ++c;
+    const int64_t cw = w - pc.off[c] / (int64_t)sizeof(W), cwords = pc.row_bytes[c] / (int64_t)sizeof(W);
+    if (cw < cwords) static_cast<W*>(const_cast<void*>(pc.ptr[c]))[j * cwords + cw] = in[i];
+  }
+}
+
 }  // namespace
 
 size_t factorize_workspace_bytes(DType dt, int64_t n) {
@@ -548,6 +579,37 @@ void scatter_rows(int64_t row_bytes, const void* src, const int64_t* idx, void* 
     hipLaunchKernelGGL((scatter_rows_kernel<uint8_t>), dim3(ew_grid(nidx * row_bytes)), dim3(kT), 0, s,
                        (const uint8_t*)src, idx, (uint8_t*)dst, nidx, row_bytes);
   TFA_LAUNCH_CHECK("scatter_rows");
+}
+
+static bool pack_words4(const PackCols& pc) {
+  for (int c = 0; c < pc.n; ++c)
+    if (pc.row_bytes[c] % 4 || pc.off[c] % 4 || reinterpret_cast<uintptr_t>(pc.ptr[c]) % 4) return false;
+  return true;
+}
+
+void pack_rows(const PackCols& pc, const int64_t* perm, int64_t nrows, int64_t record_bytes, void* out,
+               hipStream_t s) {
+  TFA_CHECK(pc.n >= 1 && pc.n <= kMaxPackCols, "pack_rows: 1..", kMaxPackCols, " columns");
+  if (nrows == 0) return;
+  if (pack_words4(pc) && record_bytes % 4 == 0)
+    hipLaunchKernelGGL((pack_rows_kernel<uint32_t>), dim3(ew_grid(nrows * record_bytes / 4)), dim3(kT), 0, s, pc, perm,
+                       nrows, record_bytes / 4, (uint32_t*)out);
+  else
+    hipLaunchKernelGGL((pack_rows_kernel<uint8_t>), dim3(ew_grid(nrows * record_bytes)), dim3(kT), 0, s, pc, perm,
+                       nrows, record_bytes, (uint8_t*)out);
+  TFA_LAUNCH_CHECK("pack_rows");
+}
+
+void unpack_rows(const PackCols& pc, const void* in, int64_t nrows, int64_t record_bytes, hipStream_t s) {
+  TFA_CHECK(pc.n >= 1 && pc.n <= kMaxPackCols, "unpack_rows: 1..", kMaxPackCols, " columns");
+  if (nrows == 0) return;
+  if (pack_words4(pc) && record_bytes % 4 == 0)
+    hipLaunchKernelGGL((unpack_rows_kernel<uint32_t>), dim3(ew_grid(nrows * record_bytes / 4)), dim3(kT), 0, s, pc,
+                       (const uint32_t*)in, nrows, record_bytes / 4);
+  else
+    hipLaunchKernelGGL((unpack_rows_kernel<uint8_t>), dim3(ew_grid(nrows * record_bytes)), dim3(kT), 0, s, pc,
+                       (const uint8_t*)in, nrows, record_bytes);
+  TFA_LAUNCH_CHECK("unpack_rows");
 }
 
 void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s) {

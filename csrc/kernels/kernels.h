@@ -98,6 +98,20 @@ void group_representatives(const int64_t* ids, int64_t n, int64_t* rep, hipStrea
 void segment_rows(const int64_t* perm, const int64_t* offs, int64_t G, int64_t size, int64_t* idx, hipStream_t s);
 // dst row idx[j] = src row j (rows of row_bytes bytes)
 void scatter_rows(int64_t row_bytes, const void* src, const int64_t* idx, void* dst, int64_t nidx, hipStream_t s);
+// shuffle records: column c of a row occupies bytes [off[c], off[c] + row_bytes[c])
+// of an R-byte record (off ascending, word-aligned slots when possible)
+constexpr int kMaxPackCols = 16;
+struct PackCols {
+  int n = 0;
+  int64_t row_bytes[kMaxPackCols];
+  int64_t off[kMaxPackCols];
+  const void* ptr[kMaxPackCols];
+};
+// out[j] = record of source row perm[j] (perm null: row j)
+void pack_rows(const PackCols& pc, const int64_t* perm, int64_t nrows, int64_t record_bytes, void* out,
+               hipStream_t s);
+// column buffers pc.ptr[c] [nrows, row_bytes[c]] <- records
+void unpack_rows(const PackCols& pc, const void* in, int64_t nrows, int64_t record_bytes, hipStream_t s);
 // rows ordered by destination (stable): perm [n]; counts [world] rows per destination
 size_t partition_workspace_bytes(int64_t n);
 void partition_rows(const int64_t* dest, int64_t n, int64_t world, int64_t* perm, int64_t* counts, void* workspace,

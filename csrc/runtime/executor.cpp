@@ -12,6 +12,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <unistd.h>
 #include <cstdlib>
 #include <set>
 #include <sstream>
@@ -1404,6 +1405,9 @@ class PinnedPool {
         return p;
       }
     }
+    // page-locked memory cannot be swapped: beyond the cap, cached blocks
+    // are released before new ones are locked
+    if (live_.load() + cached_ + r > limit_) trim(limit_ > live_.load() + r ? limit_ - live_.load() - r : 0);
     void* p = nullptr;
     hipError_t e = hipHostMalloc(&p, r, hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -1411,6 +1415,12 @@ class PinnedPool {
       HIP_OK(hipHostMalloc(&p, r, hipHostMallocDefault));
     }
     return p;
+  }
+  void note_live(size_t r, bool add) {
+    const size_t now = add ? (live_ += r) : (live_ -= r);
+    size_t pk = peak_.load();
+    while (now > pk && !peak_.compare_exchange_weak(pk, now)) {
+    }
   }
   void release(void* p, size_t r) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -1433,15 +1443,29 @@ class PinnedPool {
     }
   }
   size_t cached() const { return cached_; }
+  size_t live() const { return live_.load(); }
+  size_t peak() const { return peak_.load(); }
+  size_t limit() const { return limit_; }
 
  private:
-  PinnedPool() {
-    limit_ = static_cast<size_t>(env_positive("TFA_PINNED_POOL_MB", 65536)) << 20;
+  PinnedPool() { limit_ = default_limit(); }
+  // TFA_PINNED_POOL_MB, else half of this process's share of host RAM (one
+  // rank per GPU: RAM / LOCAL_WORLD_SIZE), at most 64 GiB: eight ranks of a
+  // node must not lock more memory than the machine has
+  static size_t default_limit() {
+    if (const char* e = std::getenv("TFA_PINNED_POOL_MB"))
+      if (std::atoll(e) > 0) return static_cast<size_t>(std::atoll(e)) << 20;
+    const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
+    size_t ram = pages > 0 && psz > 0 ? static_cast<size_t>(pages) * static_cast<size_t>(psz) : (size_t(64) << 30);
+    int local = 1;
+    if (const char* lw = std::getenv("LOCAL_WORLD_SIZE")) local = std::max(1, std::atoi(lw));
+    return std::min(size_t(64) << 30, ram / static_cast<size_t>(local) / 2);
   }
   static constexpr size_t kGran = size_t(2) << 20;
   std::mutex mu_;
   std::multimap<size_t, void*> free_;
   size_t cached_ = 0;
+  std::atomic<size_t> live_{0}, peak_{0};
   size_t limit_;
 };
 }  // namespace
@@ -1452,12 +1476,21 @@ at::Tensor empty_pinned(const std::vector<int64_t>& sizes, at::ScalarType dt) {
   size_t bytes = static_cast<size_t>(std::max<int64_t>(n, 1)) * c10::elementSize(dt);
   size_t r = 0;
   void* p = PinnedPool::get().alloc(bytes, &r);
-  return at::from_blob(p, sizes, [r](void* q) { PinnedPool::get().release(q, r); },
+  PinnedPool::get().note_live(r, true);
+  return at::from_blob(p, sizes,
+                       [r](void* q) {
+                         PinnedPool::get().note_live(r, false);
+                         PinnedPool::get().release(q, r);
+                       },
                        at::TensorOptions().dtype(dt));
 }
 
 void trim_pinned_pool() { PinnedPool::get().trim(0); }
 size_t pinned_pool_cached_bytes() { return PinnedPool::get().cached(); }
+std::vector<size_t> pinned_pool_stats() {
+  auto& p = PinnedPool::get();
+  return {p.limit(), p.cached(), p.live(), p.peak()};
+}
 
 void pin_host_tensor(const at::Tensor& t) {
   TFA_CHECK(!t.is_cuda(), "pin_host_tensor needs a host tensor");

@@ -109,6 +109,8 @@ class Program {
 at::Tensor empty_pinned(const std::vector<int64_t>& sizes, at::ScalarType dt);
 void trim_pinned_pool();
 size_t pinned_pool_cached_bytes();
+// {limit, cached (free) bytes, live bytes, peak live bytes} of the pinned pool
+std::vector<size_t> pinned_pool_stats();
 // page-lock an existing host tensor's memory in place (hipHostRegister)
 void pin_host_tensor(const at::Tensor& t);
 void unpin_host_tensor(const at::Tensor& t);

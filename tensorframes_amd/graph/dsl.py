@@ -370,6 +370,14 @@ class Tensor:
         return self._dtype
 
     def get_shape(self) -> TensorShape:
+        nd = self.op.node_def
+        # placeholders and constants carry their shape: no graph inference
+        # (rebuilding a graph per iteration, e.g. K-Means, asks for these often)
+        if nd.op in ("Placeholder", "PlaceholderV2") and "shape" in nd.attr:
+            shp = nd.attr["shape"].value
+            return TensorShape(None if shp.unknown_rank else [None if d < 0 else d for d in shp.dims])
+        if nd.op == "Const" and "value" in nd.attr:
+            return TensorShape(list(nd.attr["value"].value.shape))
         info = self.graph._inferred()[self.op.name][self.value_index]
         return TensorShape(info["shape"])
 

@@ -9,9 +9,9 @@ via compareRows). String keys are dictionary-encoded on the host once.
 
 The cross-rank shuffle of per-key partials hashes the keys on the device
 (`_C.key_dest`: the same 64-bit hash on every rank), orders the rows by
-destination with one radix sort (`_C.partition_rows`), gathers every column
-in that order (`_C.gather_rows`) and exchanges them with one all-to-all per
-column (RCCL for device tensors). Reference counterpart: the UDAF shuffle
+destination with one radix sort (`_C.partition_rows`), packs every column of
+a row into one record in that order (`_C.pack_rows`) and exchanges the
+records in ONE all-to-all (RCCL for device tensors), unpacked on arrival. Reference counterpart: the UDAF shuffle
 (src/main/scala/org/tensorframes/impl/DebugRowOps.scala:573-576).
 """
 from __future__ import annotations
@@ -72,6 +72,20 @@ def route(keys: List[torch.Tensor], cols: List[torch.Tensor]) -> List[torch.Tens
     allc = list(keys) + list(cols)
     dev = allc[0].device
     n = allc[0].shape[0]
+    if dev.type == "cuda" and len(allc) <= 16:
+        # every column of a row packed into one record: the rows move in ONE
+        # all-to-all (plus the tiny count exchange), not one per column
+        dest = _C.key_dest([k.contiguous() for k in keys], w) if n else torch.empty(0, dtype=torch.int64, device=dev)
+        perm, counts = _C.partition_rows(dest, w)
+        send_rows = [int(c) for c in counts.cpu().tolist()]
+        recv_rows = dist.all_to_all_counts(send_rows)
+        rec, _ = _C.pack_rows([c.contiguous() for c in allc], perm)
+        got = dist.all_to_all_rows(rec, send_rows, recv_rows)
+        m = int(sum(recv_rows))
+        outs = [torch.empty((m,) + tuple(c.shape[1:]), dtype=c.dtype, device=dev) for c in allc]
+        if m:
+            _C.unpack_rows(got, outs)
+        return outs
     if dev.type == "cuda":
         dest = _C.key_dest([k.contiguous() for k in keys], w) if n else torch.empty(0, dtype=torch.int64, device=dev)
         perm, counts = _C.partition_rows(dest, w)

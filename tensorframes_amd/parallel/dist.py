@@ -52,6 +52,14 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", str(rank())))
 
 
+def backend_name() -> Optional[str]:
+    """The default process group's backend ("nccl" = RCCL, "gloo"), or None
+    without a process group."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    return str(dist.get_backend())
+
+
 def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, force: bool = False) -> bool:
     """Initialise the default process group from torchrun's env (idempotent).
 

@@ -317,3 +317,53 @@ def test_generic_aggregate_10m_rows_100k_keys_gpu():
     sel = np.nonzero(kn == 12345)[0]
     np.testing.assert_array_equal(b.columns["x"][12345].cpu().numpy(), xn[sel].max(0) - xn[sel].min(0))
     assert dt < 0.05, dt
+
+
+@pytest.mark.gpu
+def test_pack_unpack_records_roundtrip_gpu():
+    """The keyed shuffle's single-payload records: every column of a row in
+    one word-aligned record (pack_rows), restored by unpack_rows."""
+    dev = _gpu()
+    rng = np.random.default_rng(13)
+    n = 10_007
+    cols = [torch.tensor(rng.integers(-9, 9, n)).to(dev),
+            torch.tensor(rng.standard_normal((n, 4))).to(dev),
+            torch.tensor(rng.integers(0, 5, n), dtype=torch.int32).to(dev),
+            torch.tensor(rng.integers(0, 255, (n, 3)), dtype=torch.uint8).to(dev)]
+    perm = torch.tensor(rng.permutation(n)).to(dev)
+    rec, offs = _C.pack_rows(cols, perm)
+    assert rec.shape == (n, 8 + 32 + 4 + 4) and list(offs) == [0, 8, 40, 44]
+    outs = [torch.empty_like(c) for c in cols]
+    _C.unpack_rows(rec, outs)
+    for c, o in zip(cols, outs):
+        assert torch.equal(o, c[perm])
+    # all-float columns take the word path, a lone uint8 column the byte path
+    rec2, _ = _C.pack_rows([cols[3]])
+    back = torch.empty_like(cols[3])
+    _C.unpack_rows(rec2, [back])
+    assert rec2.shape == (n, 4) and torch.equal(back, cols[3])
+
+
+def test_pinned_pool_cap_is_bounded_by_host_ram():
+    st = _C.pinned_pool_stats()
+    import os
+    ram = os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGE_SIZE")
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    assert 0 < st["limit"] <= min(64 << 30, ram // local // 2) or os.environ.get("TFA_PINNED_POOL_MB")
+    assert st["live"] >= 0 and st["peak"] >= st["live"]
+
+
+def test_pinned_pool_cap_scales_with_local_ranks():
+    import os
+    import subprocess
+    import sys
+    code = "from tensorframes_amd._native import _C; print(_C.pinned_pool_stats()['limit'])"
+
+    def limit(local):
+        env = {k: v for k, v in os.environ.items() if k != "TFA_PINNED_POOL_MB"}
+        env["LOCAL_WORLD_SIZE"] = str(local)
+        return int(subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                                  check=True).stdout.strip())
+    ram = os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGE_SIZE")
+    assert limit(8) == min(64 << 30, ram // 8 // 2)
+    assert limit(1) == min(64 << 30, ram // 2)

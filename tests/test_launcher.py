@@ -24,7 +24,9 @@ def _run_bench(n, rows=4096, extra=()):
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout  # rank 0 only
-    return json.loads(lines[0])
+    out = json.loads(lines[0])
+    out["_rank_lines"] = [json.loads(ln) for ln in p.stderr.splitlines() if ln.startswith('{"bench_rank"')]
+    return out
 
 
 @pytest.mark.parametrize("n", [1, 2, 4, 8])
@@ -36,6 +38,14 @@ def test_bench_spawns_n_ranks(n):
     assert out["steps"] == 2 and out["warmup"] == 1
     assert out["value"] > 0 and out["max_abs_err"] < 1e-3
     assert out["scaling"] == "strong"
+    # one stderr diagnostic line per rank: rank, world, backend, own time, its partitions
+    ranks = sorted(out["_rank_lines"], key=lambda d: d["bench_rank"])
+    assert [d["bench_rank"] for d in ranks] == list(range(n))
+    assert all(d["world_size"] == n and d["own_ms_per_step"] > 0 for d in ranks)
+    assert all(d["backend"] == ("gloo" if n > 1 else None) for d in ranks)
+    assert sorted(p for d in ranks for p in d["partitions"]) == list(range(4 * n))
+    assert all(p % n == d["bench_rank"] for d in ranks for p in d["partitions"])
+    assert sum(d["rows"] for d in ranks) == 4096
 
 
 def test_launcher_propagates_failure(tmp_path):
