@@ -85,6 +85,10 @@ inline at::Tensor apply_epi_host(at::Tensor r, const std::vector<EpiStep>* epi) 
 // shared by the ops and the planner's fused steps
 void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, bool tb,
               const at::Tensor* bias, int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
+// sibling convs fused along OC (GPU): w0 = the members' filters concatenated
+// along OC, outs[k] = member k's output (NHWC, possibly a channel slice)
+void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,
+                         std::vector<at::Tensor>& outs);
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
                 int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
 

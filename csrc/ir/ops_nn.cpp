@@ -129,6 +129,47 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
   k::conv2d_nhwc(DType::F32, a, stream_of(c));
 }
 
+void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,
+                         std::vector<at::Tensor>& outs) {
+  TFA_CHECK(c.gpu, "Conv2D siblings: GPU plans only");
+  TFA_CHECK(!outs.empty() && outs.size() <= static_cast<size_t>(k::kMaxOutSegs), "Conv2D siblings: 1..",
+            k::kMaxOutSegs, " outputs");
+  Conv2DGeom g = conv_geom(c.node, x0.sizes().vec(), w0.sizes().vec());
+  require_gpu_dtype(x0, {at::kFloat}, "Conv2D");
+  at::Tensor x = materialize(c, x0), w = materialize(c, w0);
+  k::ConvArgs a;
+  a.N = g.N; a.H = g.H; a.W = g.W; a.C = g.C;
+  a.KH = g.KH; a.KW = g.KW; a.OC = g.OC; a.OH = g.OH; a.OW = g.OW;
+  a.sh = g.sh; a.sw = g.sw; a.dh = g.dh; a.dw = g.dw; a.pad_t = g.pt; a.pad_l = g.pl;
+  a.x = x.data_ptr(); a.w = w.data_ptr();
+  a.bias = bias ? bias->data_ptr() : nullptr;
+  a.act = act;
+  int64_t begin = 0;
+  a.seg.n = static_cast<int>(outs.size());
+  for (size_t k = 0; k < outs.size(); ++k) {
+    const at::Tensor& o = outs[k];
+    TFA_CHECK(o.dim() == 4 && o.size(0) == g.N && o.size(1) == g.OH && o.size(2) == g.OW,
+              "Conv2D siblings: output ", k, " has the wrong spatial shape");
+    TFA_CHECK(o.stride(3) == 1 && o.stride(1) == o.size(2) * o.stride(2) && o.stride(0) == o.size(1) * o.stride(1),
+              "Conv2D siblings: outputs must be NHWC-contiguous up to the channel stride");
+    a.seg.begin[k] = begin;
+    a.seg.ptr[k] = o.data_ptr();
+    a.seg.ldc[k] = o.stride(2);
+    begin += o.size(3);
+  }
+  a.seg.begin[outs.size()] = begin;
+  TFA_CHECK(begin == g.OC, "Conv2D siblings: outputs cover ", begin, " channels of ", g.OC);
+  a.y = outs[0].data_ptr();
+  a.ldc = outs[0].stride(2);
+  if (g.N * g.OH * g.OW == 0) return;
+  at::Tensor work;
+  if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
+    work = at::empty({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
+    a.workspace = work.data_ptr();
+  }
+  k::conv2d_nhwc(DType::F32, a, stream_of(c));
+}
+
 void register_nn_ops(OpRegistry& r) {
   // ---- BiasAdd
   OpDef bias;

@@ -87,6 +87,22 @@ __device__ __forceinline__ void sched_interleave() {
   }
 }
 
+// where output column `col` lives: its column base pointer and row stride
+// (one output, or one of the sibling-conv segments)
+__device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t col, float*& base, int64_t& ld) {
+  if (g.seg.n == 0) {
+    base = Cb + col;
+    ld = g.ldc;
+    return;
+  }
+  int s = 0;
+#pragma unroll
+  for (int q = 1; q < kMaxOutSegs; ++q)
+    if (q < g.seg.n && col >= g.seg.begin[q]) s = q;
+  base = static_cast<float*>(g.seg.ptr[s]) + (col - g.seg.begin[s]);
+  ld = g.seg.ldc[s];
+}
+
 template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
 __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
                                                          int64_t k_per_split) {
@@ -383,6 +399,9 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
     const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
     if (col >= N) return;
     const float bv = (!ws && bias) ? bias[col] : 0.f;
+    float* cbase;
+    int64_t cld;
+    out_col(g, Cb, col, cbase, cld);
     static_for<TM>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       const f32x16 v = acc[i][j];
@@ -393,7 +412,7 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
         if (ws)  // split-K partial slab [split][batch][M][N]
           ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = v[r];
         else
-          Cb[row * g.ldc + col] = act_fast(v[r] + bv, cheap_act);
+          cbase[row * cld] = act_fast(v[r] + bv, cheap_act);
       }
     });
   });
@@ -404,18 +423,20 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
       const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
       const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (col >= N || row >= M) continue;
-      float* p = Cb + row * g.ldc + col;
+      float* cbase;
+      int64_t cld;
+      out_col(g, Cb, col, cbase, cld);
+      float* p = cbase + row * cld;
       *p = epi_apply(g.epi, act_apply(*p, g.act), row, col, N, bz * M * N);
     }
   }
 }
 
 // split-K combine: fixed summation order over the splits (deterministic)
-__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ ws, float* __restrict__ C,
-                                                     const float* __restrict__ bias, int64_t M, int64_t N,
-                                                     int64_t ldc, int64_t strideC, int64_t batch,
-                                                     int splits, int act, EpiProg epi) {
-  const int64_t total = batch * M * N;
+__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ ws, GemmArgs g, int splits) {
+  const int64_t M = g.M, N = g.N;
+  const int64_t total = g.batch * M * N;
+  const float* bias = static_cast<const float*>(g.bias);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     float s = 0.f;
@@ -424,7 +445,10 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
     const int64_t row = (i / N) % M;
     const int64_t b = i / (M * N);
     if (bias) s += bias[col];
-    C[b * strideC + row * ldc + col] = epi_apply(epi, act_apply(s, act), row, col, N, b * M * N);
+    float* cbase;
+    int64_t cld;
+    out_col(g, static_cast<float*>(g.C) + b * g.strideC, col, cbase, cld);
+    cbase[row * cld] = epi_apply(g.epi, act_apply(s, g.act), row, col, N, b * M * N);
   }
 }
 
@@ -561,7 +585,7 @@ F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, co
   GemmArgs g = g0;
   g.workspace = nullptr;  // single-pass candidates only (a workspace would select the split-K epilogue)
   const TuneKey key{g.M, g.N, g.K, g.batch, al, g.tb, vec, cg.H, cg.W, cg.C, cg.KW, cg.OH, cg.OW,
-                    cg.sh, cg.sw, cg.dh, cg.dw, cg.pt, cg.pl, g.ldc == g.N};
+                    cg.sh, cg.sw, cg.dh, cg.dw, cg.pt, cg.pl, (g.ldc == g.N) + 2 * g.seg.n};
   {
     std::lock_guard<std::mutex> lk(tune_mu());
     auto it = tune_cache().find(key);
@@ -626,9 +650,8 @@ void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream
   launch_plan(p, g, al, vec, cg, s);
   if (p.splits > 1) {
     int64_t total = g.batch * g.M * g.N;
-    hipLaunchKernelGGL(splitk_reduce, dim3(ew_grid(total)), dim3(256), 0, s, static_cast<const float*>(g.workspace),
-                       static_cast<float*>(g.C), static_cast<const float*>(g.bias), g.M, g.N, g.ldc, g.strideC,
-                       g.batch, p.splits, g.act, g.epi);
+    hipLaunchKernelGGL(splitk_reduce, dim3(ew_grid(total)), dim3(256), 0, s, static_cast<const float*>(g.workspace), g,
+                       p.splits);
   }
 }
 
@@ -673,6 +696,7 @@ GemmArgs conv_as_gemm(const ConvArgs& a) {
   g.batch = 1;
   g.workspace = a.workspace;
   g.epi = a.epi;
+  g.seg = a.seg;
   return g;
 }
 
@@ -699,7 +723,7 @@ size_t gemm_workspace_bytes(DType dt, const GemmArgs& g) {
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a) {
   if (dt != DType::F32) return 0;
   const GemmArgs g = conv_as_gemm(a);
-  if (bf16_candidate(g)) return bf16_workspace_bytes(f32_precision(), g.N, g.K);
+  if (a.seg.n == 0 && bf16_candidate(g)) return bf16_workspace_bytes(f32_precision(), g.N, g.K);
   return f32_ws_bytes(g.M, g.N, g.K, 1);
 }
 
@@ -732,7 +756,8 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
   TFA_CHECK(a.N > 0 && a.OH > 0 && a.OW > 0 && a.OC > 0, "conv2d: empty output");
   TFA_CHECK(a.H < (1 << 30) && a.W < (1 << 30) && a.C < (1 << 30), "conv2d: dims too large");
   GemmArgs g = conv_as_gemm(a);
-  if (bf16_candidate(g) && bf16_gemm_eligible(g, true, a.C)) {
+  // the bf16 modes have no segmented epilogue: fused sibling convs stay exact f32
+  if (a.seg.n == 0 && bf16_candidate(g) && bf16_gemm_eligible(g, true, a.C)) {
     Im2colGeom cg;
     cg.H = (int)a.H; cg.W = (int)a.W; cg.C = (int)a.C; cg.KW = (int)a.KW;
     cg.OH = (int)a.OH; cg.OW = (int)a.OW;

@@ -154,6 +154,17 @@ struct EpiProg {
   EpiOp op[kMaxEpi];
 };
 
+// Output column segments (horizontally fused sibling convs): columns
+// [begin[s], begin[s+1]) of the product go to their own tensor ptr[s] with
+// row stride ldc[s] (column begin[s] lands at ptr[s][0]); n == 0: one output C.
+constexpr int kMaxOutSegs = 4;
+struct OutSegs {
+  int n = 0;
+  int64_t begin[kMaxOutSegs + 1];
+  void* ptr[kMaxOutSegs];
+  int64_t ldc[kMaxOutSegs];
+};
+
 // C[b] = op(A[b]) @ op(B[b]) (+ bias[N]) (relu); row-major, leading dims in elements.
 struct GemmArgs {
   int64_t M, N, K;
@@ -166,6 +177,7 @@ struct GemmArgs {
   int64_t batch;
   void* workspace = nullptr;  // split-K partials (gemm_workspace_bytes)
   EpiProg epi;                // absorbed elementwise chain (epi.n == 0: none)
+  OutSegs seg;                // split output (seg.n == 0: C / ldc)
 };
 // bytes of scratch the launch needs (0 = none); allocate before the launch
 size_t gemm_workspace_bytes(DType dt, const GemmArgs& g);
@@ -191,6 +203,7 @@ struct ConvArgs {
   void* workspace = nullptr;
   int64_t ldc = 0;  // output pixel stride in elements (0 = OC; > OC writes a channel slice)
   EpiProg epi;      // absorbed elementwise chain over the [N*OH*OW, OC] output
+  OutSegs seg;      // sibling convs fused along OC: per-sibling outputs (seg.n == 0: y / ldc)
 };
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a);
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s);

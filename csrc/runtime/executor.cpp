@@ -85,6 +85,15 @@ bool epi_chain_enabled() {
   return on;
 }
 
+// TFA_SIBLING_FUSION=0: sibling convs (same input, same geometry) stay separate GEMMs
+bool sibling_fusion_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TFA_SIBLING_FUSION");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // transposition flags of MatMul (transpose_a/b) and BatchMatMul (adj_x/y)
 bool gemm_ta(const Node& nd) {
   return nd.op == "MatMul" ? nd.attr_b("transpose_a", false) : nd.attr_b("adj_x", false);
@@ -151,6 +160,18 @@ struct Program::Step {
   int64_t alias_offset = 0;      // producer: first channel in the concat output
   const TensorInfo* alias_info = nullptr;  // producer: concat output info
   std::vector<char> preplaced;   // concat: per value input, already written in place
+  // horizontally fused sibling convs (GPU plans): Conv2Ds that read the same
+  // input with the same geometry run as ONE implicit GEMM over their
+  // concatenated filters (wider N: more blocks, less tile padding); every
+  // member writes its own output, or its concat slice
+  struct Sib {
+    int node;
+    int64_t oc;
+    int alias_slot;
+    int64_t alias_offset;
+    const TensorInfo* alias_info;
+  };
+  std::vector<Sib> sibs;
 };
 
 struct Program::Plan {
@@ -159,9 +180,11 @@ struct Program::Plan {
   int nslots = 0;
   std::vector<int> feed_slots;
   std::vector<std::pair<int, TensorRef>> const_slots;  // slot <- constant value of ref
+  std::map<int, at::Tensor> synth_consts;               // slot <- plan-made constant (fused sibling filters)
   std::vector<int> fetch_slots;
   std::map<int, std::map<int, at::Tensor>> dev_consts;  // device index -> slot -> tensor
   int fused = 0;
+  int fused_siblings = 0;  // convs folded into sibling-fused steps
   // fused elementwise regions (GPU plans): generated source + loaded kernel per device
   struct Fused {
     FusedRegion region;
@@ -698,6 +721,85 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     }
   }
 
+  // ---- horizontal fusion of sibling convs (GPU plans): CONV steps with the
+  // same input slot, the same geometry and activation, constant filters (and
+  // biases) and no epilogue chain become one step over the filters
+  // concatenated along OC (at most kMaxOutSegs members per step). The merged
+  // step runs where the first member ran: the others depend only on the same
+  // input and on constants.
+  if (gpu_plan && sibling_fusion_enabled()) {
+    std::map<int, TensorRef> const_ref;
+    for (auto& cs : p->const_slots) const_ref[cs.first] = cs.second;
+    auto const_val = [&](int slot) -> const at::Tensor* {
+      auto it = const_ref.find(slot);
+      if (it == const_ref.end()) return nullptr;
+      const auto& v = infos[it->second.node][it->second.index].value;
+      return v ? &*v : nullptr;
+    };
+    std::map<std::tuple<int, std::string, int, bool>, std::vector<size_t>> groups;
+    for (size_t i = 0; i < p->steps.size(); ++i) {
+      const Step& st = p->steps[i];
+      if (st.kind != Step::CONV || !st.epi.empty() || st.in_slots.size() != 2 || !st.sibs.empty()) continue;
+      if (!(st.out_info[0].shape == st.gemm_shape) || !st.out_info[0].shape.fully_known()) continue;
+      const Node& nd = g_->node(st.node);
+      if (nd.op != "Conv2D" || nd.attr_s("data_format", std::string("NHWC")) != "NHWC") continue;
+      const std::string pad = nd.attr_s("padding", std::string("VALID"));
+      if (pad != "SAME" && pad != "VALID") continue;
+      const at::Tensor* w = const_val(st.in_slots[1]);
+      if (!w || w->dim() != 4 || w->scalar_type() != at::kFloat) continue;
+      const at::Tensor* b = st.bias_slot >= 0 ? const_val(st.bias_slot) : nullptr;
+      if (st.bias_slot >= 0 && (!b || b->scalar_type() != at::kFloat)) continue;
+      std::string sig = pad;
+      for (int64_t v : nd.attr_ilist("strides", {1, 1, 1, 1})) sig += "," + std::to_string(v);
+      for (int64_t v : nd.attr_ilist("dilations", {1, 1, 1, 1})) sig += "," + std::to_string(v);
+      for (int d = 0; d < 3; ++d) sig += "," + std::to_string(w->size(d));
+      groups[std::make_tuple(st.in_slots[0], sig, st.act, st.bias_slot >= 0)].push_back(i);
+    }
+    std::map<size_t, Step> merged_at;
+    std::set<size_t> dropped;
+    for (auto& kv : groups) {
+      const auto& idx = kv.second;
+      for (size_t g0 = 0; g0 + 1 < idx.size(); g0 += k::kMaxOutSegs) {
+        const size_t g1 = std::min(idx.size(), g0 + k::kMaxOutSegs);
+        if (g1 - g0 < 2) break;
+        Step ms = p->steps[idx[g0]];
+        ms.out_slots.clear();
+        ms.out_info.clear();
+        ms.alias_slot = -1;
+        std::vector<at::Tensor> ws, bs;
+        for (size_t q = g0; q < g1; ++q) {
+          const Step& m = p->steps[idx[q]];
+          const at::Tensor* w = const_val(m.in_slots[1]);
+          ws.push_back(*w);
+          if (m.bias_slot >= 0) bs.push_back(*const_val(m.bias_slot));
+          ms.sibs.push_back({m.node, w->size(3), m.alias_slot, m.alias_offset, m.alias_info});
+          ms.out_slots.push_back(m.out_slots[0]);
+          ms.out_info.push_back(m.out_info[0]);
+          if (q > g0) dropped.insert(idx[q]);
+        }
+        const int wslot = p->nslots++;
+        p->synth_consts[wslot] = at::cat(ws, 3).contiguous();
+        ms.in_slots[1] = wslot;
+        if (!bs.empty()) {
+          const int bslot = p->nslots++;
+          p->synth_consts[bslot] = at::cat(bs, 0).contiguous();
+          ms.bias_slot = bslot;
+        }
+        merged_at[idx[g0]] = std::move(ms);
+        p->fused_siblings += static_cast<int>(g1 - g0);
+      }
+    }
+    if (!merged_at.empty()) {
+      std::vector<Step> steps;
+      for (size_t i = 0; i < p->steps.size(); ++i) {
+        if (dropped.count(i)) continue;
+        auto it = merged_at.find(i);
+        steps.push_back(it != merged_at.end() ? std::move(it->second) : std::move(p->steps[i]));
+      }
+      p->steps = std::move(steps);
+    }
+  }
+
   // liveness: release each slot after its last reading step (fetches/consts are kept)
   std::vector<int> last(p->nslots, -1);
   for (size_t i = 0; i < p->steps.size(); ++i) {
@@ -708,6 +810,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
   }
   std::set<int> keep(p->fetch_slots.begin(), p->fetch_slots.end());
   for (auto& cs : p->const_slots) keep.insert(cs.first);
+  for (auto& sc : p->synth_consts) keep.insert(sc.first);
   for (int s = 0; s < p->nslots; ++s)
     if (last[s] >= 0 && !keep.count(s)) p->steps[last[s]].release.push_back(s);
   return p;
@@ -818,6 +921,13 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
   std::vector<at::Tensor> slots(p.nslots);
   for (size_t i = 0; i < inputs.size(); ++i) slots[p.feed_slots[i]] = inputs[i].contiguous();
   for (auto& cs : p.const_slots) slots[cs.first] = device_const(p, cs.first, dev);
+  for (auto& sc : p.synth_consts) {
+    std::lock_guard<std::mutex> lk(const_mu_);
+    auto& m = p.dev_consts[dev.is_cuda() ? dev.index() : -1];
+    auto it = m.find(sc.first);
+    if (it == m.end()) it = m.emplace(sc.first, dev.is_cuda() ? sc.second.to(dev) : sc.second).first;
+    slots[sc.first] = it->second;
+  }
   for (auto& st : p.steps) {
     const Node& nd = g_->node(st.node);
     ExecCtx c{nd, {}, {}, &st.out_info, &st.in_info, gpu, stream};
@@ -871,6 +981,25 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           c.out[0] = out;
         } else if (st.kind == Step::OP) {
           reg.find(nd.op)->compute(c);
+        } else if (!st.sibs.empty()) {
+          TFA_CHECK(gpu, "internal: sibling-fused conv in a host plan");
+          std::vector<at::Tensor> outs;
+          for (size_t k = 0; k < st.sibs.size(); ++k) {
+            const Step::Sib& sb = st.sibs[k];
+            if (sb.alias_slot >= 0) {
+              at::Tensor& whole = slots[sb.alias_slot];
+              if (!whole.defined())
+                whole = at::empty(dims_or_throw(sb.alias_info->shape, "concat output"),
+                                  at::TensorOptions().dtype(at::kFloat).device(dev));
+              outs.push_back(whole.narrow(whole.dim() - 1, sb.alias_offset, sb.oc));
+            } else {
+              outs.push_back(c.alloc_out(static_cast<int>(k)));
+            }
+          }
+          at::Tensor bias;
+          if (st.bias_slot >= 0) bias = slots[st.bias_slot];
+          run_conv2d_siblings(c, c.in[0], c.in[1], st.bias_slot >= 0 ? &bias : nullptr, st.act, outs);
+          for (size_t k = 0; k < outs.size(); ++k) c.out[k] = outs[k];
         } else if (gpu && st.alias_slot >= 0) {
           at::Tensor& whole = slots[st.alias_slot];
           if (!whole.defined())
@@ -1345,7 +1474,9 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
   auto p = as_gpu ? build_plan(inputs, true) : plan_for(inputs);
   std::ostringstream os;
   os << "plan: " << p->steps.size() << " steps, " << p->const_slots.size() << " constants, "
-     << p->fused << " fused epilogues, " << p->fused_regions.size() << " fused regions\n";
+     << p->fused << " fused epilogues, " << p->fused_regions.size() << " fused regions";
+  if (p->fused_siblings) os << ", " << p->fused_siblings << " sibling convs fused";
+  os << "\n";
   for (auto& st : p->steps) {
     const Node& nd = g_->node(st.node);
     if (st.kind == Step::FUSED) {
@@ -1371,6 +1502,15 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
       os << "]";
     }
     if (st.alias_slot >= 0) os << " ->concat-slice@" << st.alias_offset;
+    if (!st.sibs.empty()) {
+      os << " siblings[";
+      for (size_t k = 0; k < st.sibs.size(); ++k) {
+        const auto& sb = st.sibs[k];
+        os << (k ? "," : "") << g_->node(sb.node).name << ":" << sb.oc;
+        if (sb.alias_slot >= 0) os << "->concat-slice@" << sb.alias_offset;
+      }
+      os << "]";
+    }
     if (!st.preplaced.empty()) {
       int n = 0;
       for (char c : st.preplaced) n += c;

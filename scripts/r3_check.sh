@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round-3 GPU check: named steps, each under its own time limit; stops at the
+# first step that faults, aborts or times out (scripts/gpu_check.sh runner).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() {
+  local name=$1; shift
+  local secs=$1; shift
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 4 "gpurun_out/$name.log"
+  if grep -qiE "memory access fault|illegal address|hipErrorIllegal|HSA_STATUS_ERROR|core dumped" "gpurun_out/$name.log"; then
+    echo "GPU fault in $name: stopping"; exit 99
+  fi
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-tests}; do
+  case $s in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    newtests) run newtests 600 python -u -m pytest tests/test_groupby.py tests/test_generic_reduce.py tests/test_packer.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    sib) run sib 600 python -u -m pytest tests/test_sibling_fusion.py -x -q --timeout 120 --timeout-method thread ;;
+    kmeans) run kmeans 300 python scripts/kmeans_profile.py --iters 50 ;;
+    kmeans_cprof) run kmeans_cprof 300 python scripts/kmeans_profile.py --iters 20 --cprofile ;;
+    refperf) run refperf 600 python bench/configs.py refperf ;;
+    cfg_add) run cfg_add 600 python bench/configs.py add ;;
+    cfg_plumbing) run cfg_plumbing 300 python bench/configs.py plumbing ;;
+    cfg_reduce) run cfg_reduce 900 python bench/configs.py reduce ;;
+    bench) run bench 900 python bench.py --steps 5 --warmup 2 ;;
+    rehearse2) TFA_DIST_BACKEND=gloo run rehearse2 600 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 scripts/multirank_rehearsal.py ;;
+    incep_sweep2) for b in 2048 4096 8192; do run incep_b$b 600 python bench/configs.py inception --source device --rows 16384 --batch $b --steps 2 --warmup 1; done ;;
+    incep_host_sweep2) for c in 1024 2048; do run incep_host_c$c 900 python bench/configs.py inception --rows 65536 --batch 4096 --chunk-images $c --steps 1 --warmup 1; done ;;
+    incep_sweep) for b in 256 512 1024 2048; do run incep_b$b 600 python bench/configs.py inception --source device --rows 8192 --batch $b --steps 2 --warmup 1; done ;;
+    incep_host_sweep) for c in 256 1024; do run incep_host_c$c 900 python bench/configs.py inception --rows 65536 --batch 2048 --chunk-images $c --steps 1 --warmup 1; done ;;
+    incep) run incep 900 python bench/configs.py inception --source device --rows ${INC_ROWS:-8192} --batch ${INC_BATCH:-512} --steps 1 --warmup 1 ;;
+  esac
+done
+echo "all steps done"
