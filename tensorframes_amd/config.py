@@ -22,6 +22,10 @@ def _env(name, default, cast):
 class Config:
     # "auto" (GPU when present), "cpu", "cuda"
     device: str = dataclasses.field(default_factory=lambda: _env("TFA_DEVICE", "auto", str))
+    # where DataFrame.collect() delivers rows across ranks: "all" (every rank,
+    # the SPMD-safe default) or a rank number (the Spark driver's view; the
+    # other ranks get [])
+    collect_to: str = dataclasses.field(default_factory=lambda: _env("TFA_COLLECT_TO", "all", str))
     # target bytes of one input column per pipelined chunk (host->device->host)
     chunk_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_CHUNK_BYTES", 128 << 20, int))
     # a pipelined job is cut into at least this many chunks (when chunks stay >= 4 MB)

@@ -1498,33 +1498,27 @@ def _factorize(arrays: List[np.ndarray]):
     return inv.astype(np.int64), list(reversed(uniq_cols))
 
 
-def _shuffle_blocks(send: List[List[Block]], names: List[str], tf_types: Dict[str, Optional[int]]) -> List[Block]:
+def _shuffle_blocks(send: List[List[Block]], names: List[str], tf_types: Dict[str, Optional[int]],
+                    schema: StructType) -> List[Block]:
     """The groupBy shuffle: send[r] = blocks for rank r; returns the blocks
     this rank received. Dense columns (same dtype and cell shape on every
-    rank) travel as tensors in one all_to_all per column, device-resident
-    ones over RCCL; other columns (strings, ragged cells) as pickled values."""
+    rank: read from the schema, parallel/frame_comm.column_kinds) travel as
+    tensors in one all_to_all per column, over RCCL when the compute device is
+    a GPU; other columns (strings, ragged cells) as pickled values."""
+    from .parallel import frame_comm
     w = dist.world_size()
     if not dist.is_distributed():
         return list(send[0])
     per = [concat_blocks(s, names) if s else None for s in send]
     recv_rows = dist.all_to_all_counts([0 if p is None else p.nrows for p in per])
-
-    def meta(n):
-        cols = [p.columns[n] for p in per if p is not None and p.nrows]
-        if not cols:
-            return None
-        if all(is_dense(c) for c in cols) and len({(c.dtype, tuple(c.shape[1:])) for c in cols}) == 1:
-            return ("dense", str(cols[0].dtype).split(".")[-1], tuple(cols[0].shape[1:]), all(c.is_cuda for c in cols))
-        return ("obj",)
-
-    metas = dist.all_gather_object([meta(n) for n in names])
+    kinds = frame_comm.column_kinds([p for p in per if p is not None], names, schema)
+    # one decision for every rank (the group an all_to_all runs on must agree)
+    dev = engine.compute_device() if engine.compute_device().type == "cuda" and dist.gpu_collectives() \
+        else torch.device("cpu")
     cols: Dict[str, Any] = {}
     for j, n in enumerate(names):
-        ms = [m[j] for m in metas if m[j] is not None]
-        dense = all(m[0] == "dense" for m in ms) and len({m[1:3] for m in ms}) == 1
-        if dense:
-            dtype, cell = getattr(torch, ms[0][1]), ms[0][2]
-            dev = engine.compute_device() if all(m[3] for m in ms) and dist.gpu_collectives() else torch.device("cpu")
+        if kinds[n] is not None:
+            dtype, cell = kinds[n]
             chunks = [p.columns[n].to(dev) if p is not None and p.nrows else
                       torch.empty((0,) + cell, dtype=dtype, device=dev) for p in per]
             cols[n] = dist.all_to_all_tensors(chunks, recv_rows)
@@ -1660,7 +1654,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 idx = np.nonzero(dest == r)[0]
                 if len(idx):
                     send[r].append(part.take(idx))
-        mine = _shuffle_blocks(send, all_cols, tf_types)
+        mine = _shuffle_blocks(send, all_cols, tf_types, StructType([df.schema[c] for c in all_cols]))
         if not mine:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, w))}
         full = concat_blocks(mine, all_cols)
@@ -1771,7 +1765,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 idx = np.nonzero(dest == r)[0]
                 if len(idx):
                     send[r].append(host.take(idx))
-        mine = _shuffle_blocks(send, all_cols, tf_types)
+        mine = _shuffle_blocks(send, all_cols, tf_types, StructType([df.schema[c] for c in all_cols]))
         if not mine:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, w))}
         full = concat_blocks(mine, all_cols)

@@ -243,23 +243,34 @@ class DataFrame:
         runtime/packer.cpp build_rows; reference: DataOps.scala:20-61)."""
         return build_rows(self._schema.names, [(nrows, [payload[n] for n in self._schema.names])])
 
-    def _local_columns(self) -> List[tuple]:
-        out = []
-        for pid, b in self._iter_blocks():  # evaluated once, partition by partition
-            out.append((pid, b.nrows, {n: self._column_payload(b.columns[n]) for n in self._schema.names}))
-        return out
+    def collect(self, to: Optional[int] = None) -> List[Row]:
+        """All rows, in partition order, as Row objects built natively from the
+        column buffers (runtime/packer.cpp build_rows).
 
-    def collect(self) -> List[Row]:
-        """All rows, in partition order. Ranks exchange column payloads (dense
-        columns as arrays), and every rank builds the Row objects once."""
-        parts = [x for chunk in dist.all_gather_object(self._local_columns()) for x in chunk]
-        parts.sort(key=lambda x: x[0])
+        Across ranks the rows go to every rank (SPMD programs branch on the
+        result, so every rank must see it) or, with `to=<rank>` (or
+        `Config.collect_to`), only to that rank, the Spark driver's view
+        (reference: ExperimentalOperations.scala:92); the others get [].
+        Dense columns move as tensors (one padded gather per column), only
+        ragged / string columns are pickled (parallel/frame_comm.py)."""
+        from ..config import config
+        from ..parallel import frame_comm
         names = self._schema.names
-        return build_rows(names, [(nrows, [payload[n] for n in names]) for _, nrows, payload in parts])
+        if to is None and config.collect_to != "all":
+            to = int(config.collect_to) if str(config.collect_to).isdigit() else 0
+        local = list(self._iter_blocks())  # evaluated once, partition by partition
+        if not dist.is_distributed():
+            return build_rows(names, [(b.nrows, [self._column_payload(b.columns[n]) for n in names])
+                                      for _, b in local if b.nrows])
+        parts = frame_comm.gather_blocks(local, names, self._schema, self._nparts, root=to)
+        if parts is None:
+            return []
+        return build_rows(names, [(nrows, cols) for _, nrows, cols in parts])
 
     def count(self) -> int:
-        n = sum(b.nrows for _, b in self._iter_blocks())
-        return sum(dist.all_gather_object(n))
+        """Rows over all ranks: one int64 all-reduce."""
+        n = torch.tensor([sum(b.nrows for _, b in self._iter_blocks())], dtype=torch.int64)
+        return int(dist.all_reduce_host_(n, "Sum").item())
 
     def first(self) -> Optional[Row]:
         rows = self.take(1)
@@ -270,40 +281,13 @@ class DataFrame:
     def take(self, n: int) -> List[Row]:
         """The first n rows in partition order. Partitions are evaluated in
         order and evaluation stops once n rows are in hand (later partitions
-        are never computed); across ranks, each partition's owner sends only
-        the rows still needed."""
+        are never computed); across ranks, each partition's owner broadcasts
+        only the rows still needed, dense columns as tensors."""
         if n <= 0:
             return []
-        out: List[Row] = []
-        local = iter(self._iter_blocks())
-        buffered: Dict[int, Block] = {}
-
-        def local_block(p: int) -> Optional[Block]:
-            while p not in buffered:
-                try:
-                    pid, b = next(local)
-                except StopIteration:
-                    return None
-                buffered[pid] = b
-            return buffered.pop(p)
-
-        w = dist.world_size()
-        for p in range(self._nparts):
-            need = n - len(out)
-            owner = p % w if dist.is_distributed() else 0
-            payload = None
-            if owner == dist.rank():
-                b = local_block(p)
-                if b is not None and b.nrows:
-                    k = min(need, b.nrows)
-                    payload = (k, {c: self._column_payload(b.columns[c], 0, k) for c in self._schema.names})
-            if dist.is_distributed():
-                payload = dist.broadcast_object(payload, src=owner)
-            if payload is not None:
-                out.extend(self._rows_of(*payload))
-            if len(out) >= n:
-                break
-        return out[:n]
+        from ..parallel import frame_comm
+        got = frame_comm.take_rows(self._iter_blocks(), self._schema.names, self._schema, self._nparts, n)
+        return build_rows(self._schema.names, got)[:n]
 
     def show(self, n: int = 20):
         rows = self.take(n)
@@ -317,15 +301,16 @@ class DataFrame:
         return pd.DataFrame([list(r) for r in rows], columns=self.columns)
 
     def to_numpy(self, column: str) -> np.ndarray:
-        """All rows of a dense column as one array (gathered on every rank)."""
-        local = []
+        """All rows of a column as one array, on every rank (dense columns are
+        gathered as tensors)."""
+        from ..parallel import frame_comm
         blocks = self._blocks()
-        for pid in sorted(blocks):
-            c = blocks[pid].columns[column]
-            local.append((pid, c.detach().cpu().numpy() if is_dense(c) else np.asarray(column_values(c), dtype=object)))
-        parts = [x for chunk in dist.all_gather_object(local) for x in chunk]
-        parts.sort(key=lambda x: x[0])
-        arrs = [a for _, a in parts if len(a)]
+        local = [(pid, blocks[pid]) for pid in sorted(blocks)]
+        if not dist.is_distributed():
+            parts = [(pid, b.nrows, [self._column_payload(b.columns[column])]) for pid, b in local if b.nrows]
+        else:
+            parts = frame_comm.gather_blocks(local, [column], self._schema, self._nparts)
+        arrs = [c[0] if isinstance(c[0], np.ndarray) else np.asarray(c[0], dtype=object) for _, _, c in parts]
         return np.concatenate(arrs, 0) if arrs else np.zeros((0,))
 
     # -- transformations
@@ -355,15 +340,15 @@ class DataFrame:
         return df
 
     def repartition(self, n: int) -> "DataFrame":
+        """n even partitions in row order. Each rank receives only the rows of
+        the partitions it owns: dense columns in one all-to-all per column
+        (RCCL for device-resident frames), other columns pickled."""
+        from ..parallel import frame_comm
         names = self.columns
+        nin = self._nparts
 
         def fn(bs):
-            allb = []
-            for chunk in dist.all_gather_object([(p, b.to(torch.device("cpu"))) for p, b in sorted(bs.items())]):
-                allb.extend(chunk)
-            allb.sort(key=lambda x: x[0])
-            full = concat_blocks([b for _, b in allb], names)
-            return {p: full.slice(*_bounds(full.nrows, n, p)) for p in dist.local_partitions(n)}
+            return frame_comm.repartition_blocks(bs, names, self._schema, nin, n)
         return DataFrame(self._schema, _Derived(self, fn, streamable=False), n)
 
     def coalesce(self, n: int) -> "DataFrame":
@@ -432,14 +417,27 @@ class GroupedData:
         return core.aggregate(fetches, self, **kw)
 
     def count(self) -> DataFrame:
-        rows = self.df.select(self.keys).collect()
-        counts: Dict[tuple, int] = {}
-        for r in rows:
-            counts[tuple(r)] = counts.get(tuple(r), 0) + 1
-        keys = sorted(counts, key=_sort_key)
-        data = [Row.from_fields(self.keys + ["count"], list(k) + [counts[k]]) for k in keys]
-        fields = [self.df.schema[k] for k in self.keys] + [StructField("count", LongType(), False)]
-        return create_dataframe(data, StructType(fields))
+        """Rows per key: the keys plus a column of ones go through `aggregate`
+        with a Sum graph (device factorisation + segmented sum, keyed
+        all-to-all across ranks); no rows are collected."""
+        from .. import core
+        from ..graph import dsl as tf
+        keys = list(self.keys)
+
+        def fn(bs):
+            out = {}
+            for p, b in bs.items():
+                kc = b.columns[keys[0]]
+                dev = kc.device if isinstance(kc, torch.Tensor) else torch.device("cpu")
+                cols = {k: b.columns[k] for k in keys}
+                cols["count"] = torch.ones(b.nrows, dtype=torch.int64, device=dev)
+                out[p] = Block(b.nrows, cols)
+            return out
+        fields = [self.df.schema[k] for k in keys] + [tensor_field("count", D.DT_INT64, [])]
+        ones = DataFrame(StructType(fields), _Derived(self.df, fn), self.df._nparts)
+        with tf.Graph().as_default():
+            ci = tf.placeholder(tf.int64, [None], name="count_input")
+            return core.aggregate(tf.reduce_sum(ci, [0], name="count"), ones.groupBy(*keys))
 
 
 def _sort_key(k):

@@ -277,7 +277,8 @@ def broadcast_object(obj: Any, src: int = 0) -> Any:
         return obj
     _ensure_groups()
     box = [obj]
-    dist.broadcast_object_list(box, src=src, group=_state["cpu_group"])
+    with _traced("broadcast_object"):
+        dist.broadcast_object_list(box, src=src, group=_state["cpu_group"])
     return box[0]
 
 
@@ -300,6 +301,63 @@ def all_to_all_objects(per_dest: List[Any]) -> List[Any]:
         out.append(pickle.loads(raw[off:off + n]))  # payloads written by our own ranks
         off += n
     return out
+
+
+def gather_object(obj: Any, root: int = 0) -> Optional[List[Any]]:
+    """Every rank's object on `root` (rank order); None elsewhere."""
+    if not is_distributed():
+        return [obj]
+    _ensure_groups()
+    out = [None] * world_size() if rank() == root else None
+    with _traced("gather_object"):
+        dist.gather_object(obj, out, dst=root, group=_state["cpu_group"])
+    return out
+
+
+def gather_rows(x: torch.Tensor, rows_per_rank: List[int], root: Optional[int] = None) -> Optional[List[torch.Tensor]]:
+    """Variable-length row blocks of every rank (x: this rank's [rows, ...]
+    host tensor, rows_per_rank known everywhere): each rank's block, in rank
+    order, on every rank (root None) or only on `root` (None elsewhere).
+    One padded all_gather / gather of the tensor itself: no pickling."""
+    if not is_distributed():
+        return [x]
+    _ensure_groups()
+    x = x.contiguous()
+    mx = max(int(r) for r in rows_per_rank) if rows_per_rank else 0
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype)
+    if x.shape[0]:
+        pad[:x.shape[0]].copy_(x)
+    group = _state["cpu_group"]
+    with _traced("gather_rows", _nbytes(pad)):
+        if root is None:
+            parts = [torch.empty_like(pad) for _ in range(world_size())]
+            dist.all_gather(parts, pad, group=group)
+        else:
+            parts = [torch.empty_like(pad) for _ in range(world_size())] if rank() == root else None
+            dist.gather(pad, parts, dst=root, group=group)
+    if parts is None:
+        return None
+    return [p[:int(r)] for p, r in zip(parts, rows_per_rank)]
+
+
+def broadcast_tensor(t: Optional[torch.Tensor], shape: tuple, dtype: torch.dtype, src: int) -> torch.Tensor:
+    """`src`'s host tensor of a known shape/dtype on every rank (no pickling)."""
+    if not is_distributed():
+        return t
+    _ensure_groups()
+    buf = t.contiguous() if rank() == src else torch.empty(shape, dtype=dtype)
+    with _traced("broadcast", _nbytes(buf)):
+        dist.broadcast(buf, src=src, group=_state["cpu_group"])
+    return buf
+
+
+def all_reduce_host_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
+    """In-place all-reduce of a small host tensor over the gloo group."""
+    if not is_distributed():
+        return t
+    _ensure_groups()
+    dist.all_reduce(t, op=_OPS[op], group=_state["cpu_group"])
+    return t
 
 
 def all_to_all_counts(send_counts: List[int]) -> List[int]:

@@ -1,0 +1,99 @@
+"""Rank-scalable frame actions (parallel/frame_comm.py), rehearsed with gloo
+at world size 2/4/8 on the CPU: collect to every rank or to one rank, count,
+take, repartition (each rank receives only the partitions it owns), groupBy
+count. Dense columns must move as tensors: no pickling collective runs for a
+frame whose schema pins its columns (reference:
+ExperimentalOperations.scala:92, PythonInterface.scala:165-169)."""
+import json
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = 1000
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _pickles(m):
+    return sum(m.get(f"collective_{k}", 0) for k in ("all_gather_object", "all_to_all_objects", "gather_object",
+                                                      "broadcast_object"))
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TFA_DEVICE="cpu", OMP_NUM_THREADS="1")
+    sys.path.insert(0, REPO)
+    import numpy as np
+
+    import tensorframes_amd as tfs
+    from tensorframes_amd.parallel import dist
+    from tensorframes_amd.utils.logging import metrics
+
+    assert dist.init(backend="gloo")
+    res = {}
+    x = np.arange(N, dtype=np.float64)
+    v = np.arange(3 * N, dtype=np.float32).reshape(N, 3)
+    k = (np.arange(N) % 7).astype(np.int64)
+    df = tfs.analyze(tfs.from_columns({"x": x, "v": v, "k": k}, num_partitions=5)).cache()
+    df.local_blocks()
+    metrics.reset()
+    rows = df.collect()
+    res["collect_ok"] = len(rows) == N and all(r.x == i and r.v == v[i].tolist() and r.k == k[i]
+                                               for i, r in enumerate(rows))
+    res["collect_pickles"] = _pickles(metrics.snapshot())
+    metrics.reset()
+    r0 = df.collect(to=0)
+    res["collect_to0_len"] = len(r0)
+    res["collect_to0_ok"] = (rank != 0) or [r.x for r in r0] == x.tolist()
+    res["count"] = df.count()
+    t = df.take(7)
+    res["take"] = [r.x for r in t]
+    res["take_v"] = t[6].v
+    res["pickles_dense"] = _pickles(metrics.snapshot())
+    metrics.reset()
+    rep = df.repartition(3)
+    blocks = rep.local_blocks()
+    res["rep_parts"] = sorted(blocks)
+    res["rep_x"] = {str(q): blocks[q].columns["x"].tolist() for q in blocks}
+    res["rep_pickles"] = _pickles(metrics.snapshot())
+    res["rep_count"] = rep.count()
+    cnt = df.groupBy("k").count().collect()
+    res["group_count"] = sorted((int(r.k), int(r["count"])) for r in cnt)
+    # a string column still works (pickled values)
+    s = tfs.create_dataframe([tfs.Row(name=f"n{i}", x=float(i)) for i in range(11)], num_partitions=4)
+    res["strings"] = [r.name for r in s.collect()]
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_frame_actions_scale_with_ranks(world, tmp_path):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    out = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+    for r, res in enumerate(out):
+        assert res["collect_ok"], r
+        assert res["collect_pickles"] == 0  # dense columns moved as tensors
+        assert res["collect_to0_len"] == (N if r == 0 else 0) and res["collect_to0_ok"]
+        assert res["count"] == N
+        assert res["take"] == [float(i) for i in range(7)] and res["take_v"] == [18.0, 19.0, 20.0]
+        assert res["pickles_dense"] == 0
+        # repartition: each rank holds only the new partitions it owns, with their rows
+        assert res["rep_parts"] == [q for q in range(3) if q % world == r]
+        for q, xs in res["rep_x"].items():
+            q = int(q)
+            assert xs == [float(i) for i in range((q * N) // 3, ((q + 1) * N) // 3)]
+        assert res["rep_pickles"] == 0
+        assert res["rep_count"] == N
+        assert res["group_count"] == [[j, len(range(j, N, 7))] for j in range(7)]
+        assert res["strings"] == [f"n{i}" for i in range(11)]
