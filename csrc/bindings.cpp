@@ -9,6 +9,7 @@
 
 #include "ir/graph.h"
 #include "kernels/kernels.h"
+#include "runtime/device_pool.h"
 #include "runtime/executor.h"
 #include "runtime/jit.h"
 
@@ -618,6 +619,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return attr.type == hipMemoryTypeHost;
   });
   m.def("pinned_pool_cached_bytes", &pinned_pool_cached_bytes);
+  m.def("device_pool_stats", [] {
+    DevPoolStats v = dev_pool_stats();
+    py::dict d;
+    d["allocs"] = v.allocs;
+    d["frees"] = v.frees;
+    d["fallbacks"] = v.fallbacks;
+    d["device_mallocs"] = v.device_mallocs;
+    d["live"] = v.live_bytes;
+    d["peak"] = v.peak_bytes;
+    d["cached"] = v.cached_bytes;
+    return d;
+  }, "engine-owned device pool: allocations, frees, c10 fallbacks, hipMallocs, live / peak / cached bytes");
+  m.def("trim_device_pool", &dev_pool_trim);
   m.def("pinned_pool_stats", [] {
     auto v = pinned_pool_stats();
     py::dict d;

@@ -1,6 +1,10 @@
 // Graph import, edge resolution, closure and static inference / constant folding.
 #include "graph.h"
 
+#include <c10/hip/HIPFunctions.h>
+
+#include "../runtime/device_pool.h"
+
 #include <algorithm>
 #include <set>
 
@@ -236,8 +240,14 @@ at::Tensor ExecCtx::alloc_out(int i) {
   auto dims = dims_or_throw(oi.shape, "output");
   at::TensorOptions opt = at::TensorOptions().dtype(to_scalar_type(oi.dtype));
   if (!in.empty() && in[0].defined()) opt = opt.device(in[0].device());
-  else if (gpu) opt = opt.device(at::kCUDA);
-  return at::empty(dims, opt);
+  else if (gpu) opt = opt.device(at::Device(at::kCUDA, c10::hip::current_device()));
+  return alloc(dims, opt);
+}
+
+at::Tensor ExecCtx::alloc(at::IntArrayRef sizes, const at::TensorOptions& opts) const {
+  if (gpu && opts.device().is_cuda())
+    return dev_empty(sizes, opts.dtype().toScalarType(), opts.device(), static_cast<hipStream_t>(stream));
+  return at::empty(sizes, opts);
 }
 
 // ------------------------------------------------------------------ Graph

@@ -140,6 +140,9 @@ struct ExecCtx {
   DType out_dtype(int i = 0) const { return out_info->at(i).dtype; }
   std::vector<int64_t> host_ivalue(int i) const;  // plan-time value of input i
   at::Tensor alloc_out(int i = 0);                  // allocate output i per out_info
+  // scratch / intermediate tensor: on a GPU step from the engine's
+  // stream-ordered device pool (runtime/device_pool.h), else at::empty
+  at::Tensor alloc(at::IntArrayRef sizes, const at::TensorOptions& opts) const;
 };
 
 // Imported graph.

@@ -239,7 +239,7 @@ at::Tensor gpu_reduce(ExecCtx& c, k::RedOp op, const at::Tensor& x0, const std::
   if (out.numel() == 0) return out;
   size_t ws = k::reduce_workspace_bytes(dt, outer, r, inner);
   at::Tensor work;
-  if (ws) work = at::empty({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
+  if (ws) work = c.alloc({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
   k::reduce(op, dt, x.data_ptr(), out.data_ptr(), outer, r, inner, ws ? work.data_ptr() : nullptr,
             stream_of(c));
   return out;
@@ -433,7 +433,7 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
   }
   at::Tensor work;
   if (size_t ws = k::gemm_workspace_bytes(dt_of(a), g)) {
-    work = at::empty({static_cast<int64_t>(ws)}, a.options().dtype(at::kByte));
+    work = c.alloc({static_cast<int64_t>(ws)}, a.options().dtype(at::kByte));
     g.workspace = work.data_ptr();
   }
   k::gemm(dt_of(a), g, stream_of(c));
@@ -628,7 +628,7 @@ void register_math_ops(OpRegistry& r) {
       if (!c.out[0].numel()) return;
       size_t ws = k::unsorted_segment_workspace_bytes(op, dt_of(xc), nrows, inner, nseg);
       at::Tensor work;
-      if (ws) work = at::empty({static_cast<int64_t>(ws)}, xc.options().dtype(at::kByte));
+      if (ws) work = c.alloc({static_cast<int64_t>(ws)}, xc.options().dtype(at::kByte));
       k::unsorted_segment_reduce(op, dt_of(xc), dt_of(ic), xc.data_ptr(), ic.data_ptr(),
                                  c.out[0].data_ptr(), nrows, inner, nseg,
                                  ws ? work.data_ptr() : nullptr, stream_of(c));

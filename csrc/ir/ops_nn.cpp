@@ -123,7 +123,7 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
   a.ldc = out.stride(2);
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
-    work = at::empty({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
+    work = c.alloc({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
     a.workspace = work.data_ptr();
   }
   k::conv2d_nhwc(DType::F32, a, stream_of(c));
@@ -164,7 +164,7 @@ void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0,
   if (g.N * g.OH * g.OW == 0) return;
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
-    work = at::empty({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
+    work = c.alloc({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
     a.workspace = work.data_ptr();
   }
   k::conv2d_nhwc(DType::F32, a, stream_of(c));

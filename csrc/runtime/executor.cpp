@@ -1,5 +1,6 @@
 // Planner + executor (see executor.h).
 #include "executor.h"
+#include "device_pool.h"
 
 
 #include <ATen/hip/HIPContext.h>
@@ -989,8 +990,8 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
             if (sb.alias_slot >= 0) {
               at::Tensor& whole = slots[sb.alias_slot];
               if (!whole.defined())
-                whole = at::empty(dims_or_throw(sb.alias_info->shape, "concat output"),
-                                  at::TensorOptions().dtype(at::kFloat).device(dev));
+                whole = dev_empty(dims_or_throw(sb.alias_info->shape, "concat output"), at::kFloat, dev,
+                                  static_cast<hipStream_t>(stream));
               outs.push_back(whole.narrow(whole.dim() - 1, sb.alias_offset, sb.oc));
             } else {
               outs.push_back(c.alloc_out(static_cast<int>(k)));
@@ -1003,8 +1004,8 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
         } else if (gpu && st.alias_slot >= 0) {
           at::Tensor& whole = slots[st.alias_slot];
           if (!whole.defined())
-            whole = at::empty(dims_or_throw(st.alias_info->shape, "concat output"),
-                              at::TensorOptions().dtype(at::kFloat).device(dev));
+            whole = dev_empty(dims_or_throw(st.alias_info->shape, "concat output"), at::kFloat, dev,
+                              static_cast<hipStream_t>(stream));
           at::Tensor out = whole.narrow(whole.dim() - 1, st.alias_offset, st.out_info[0].shape.dims.back());
           at::Tensor bias;
           if (st.bias_slot >= 0) bias = slots[st.bias_slot];
@@ -1167,7 +1168,8 @@ std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor
   c.graph->replay(cur);
   std::vector<at::Tensor> outs;
   outs.reserve(c.static_out.size());
-  for (auto& o : c.static_out) outs.push_back(o.clone());
+  // replay outputs are copied out of the graph's static buffers by DMA
+  for (auto& o : c.static_out) outs.push_back(dev_clone(o.contiguous(), cur));
   stats_.graph_replays++;
   return outs;
 }
@@ -1263,7 +1265,7 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
     for (size_t i = 0; i < nin; ++i) {
       auto sz = seg_inputs[0][i].sizes().vec();
       sz[0] = chunk_rows;
-      ring[d].push_back(at::empty(sz, seg_inputs[0][i].options().device(dev).pinned_memory(false)));
+      ring[d].push_back(dev_empty(sz, seg_inputs[0][i].scalar_type(), dev, compute.stream()));
     }
   std::vector<hipEvent_t> ev_h2d(depth), ev_comp(depth), ev_d2h(depth);
   for (int d = 0; d < depth; ++d) {
@@ -1329,7 +1331,7 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
       char* dp = static_cast<char*>(dst.data_ptr()) + ch.start * row_bytes;
       if (ch.rows * row_bytes)
         HIP_OK(hipMemcpyAsync(dp, o.data_ptr(), ch.rows * row_bytes, hipMemcpyDeviceToHost, d2h.stream()));
-      c10::hip::HIPCachingAllocator::recordStream(o.storage().data_ptr(), d2h);
+      dev_record_stream(o, d2h.stream());
       d2h_bytes += ch.rows * row_bytes;
     }
     stamp(ci, 5, d2h.stream());
@@ -1394,7 +1396,7 @@ std::vector<at::Tensor> Program::run_chunked_reduce(const std::vector<std::vecto
     for (size_t i = 0; i < nin; ++i) {
       auto sz = seg_inputs[0][i].sizes().vec();
       sz[0] = chunk_rows;
-      ring[d].push_back(at::empty(sz, seg_inputs[0][i].options().device(dev).pinned_memory(false)));
+      ring[d].push_back(dev_empty(sz, seg_inputs[0][i].scalar_type(), dev, compute.stream()));
     }
   std::vector<hipEvent_t> ev_h2d(depth), ev_comp(depth);
   for (int d = 0; d < depth; ++d) {
@@ -1431,7 +1433,7 @@ std::vector<at::Tensor> Program::run_chunked_reduce(const std::vector<std::vecto
       for (auto& o : outs) {
         auto sz = o.sizes().vec();
         sz.insert(sz.begin(), static_cast<int64_t>(chunks.size()));
-        acc.push_back(at::empty(sz, o.options().device(dev)));
+        acc.push_back(dev_empty(sz, o.scalar_type(), dev, compute.stream()));
       }
     }
     for (size_t j = 0; j < outs.size(); ++j) {

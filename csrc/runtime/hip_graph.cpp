@@ -6,6 +6,7 @@
 #include <atomic>
 
 #include "../common.h"
+#include "device_pool.h"
 
 namespace tfa {
 namespace {
@@ -27,8 +28,10 @@ void HipGraph::begin(hipStream_t stream, int device) {
   c10::hip::HIPCachingAllocator::get()->beginAllocateToPool(
       static_cast<c10::DeviceIndex>(device), pool_, [stream](hipStream_t s) { return s == stream; });
   pool_open_ = pool_owned_ = true;
+  dev_capture_begin(stream);
   hipError_t e = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal);
   if (e != hipSuccess) {
+    dev_capture_end(stream);
     c10::hip::HIPCachingAllocator::get()->endAllocateToPool(static_cast<c10::DeviceIndex>(device), pool_);
     pool_open_ = false;
     TFA_CHECK(false, "hipStreamBeginCapture failed: ", hipGetErrorString(e));
@@ -37,6 +40,7 @@ void HipGraph::begin(hipStream_t stream, int device) {
 
 void HipGraph::end() {
   hipError_t e = hipStreamEndCapture(stream_, &graph_);
+  dev_capture_end(stream_);
   c10::hip::HIPCachingAllocator::get()->endAllocateToPool(static_cast<c10::DeviceIndex>(device_), pool_);
   pool_open_ = false;
   TFA_CHECK(e == hipSuccess && graph_ != nullptr, "hipStreamEndCapture failed: ", hipGetErrorString(e));
@@ -52,6 +56,7 @@ void HipGraph::abort() {
     if (g) (void)hipGraphDestroy(g);
   }
   (void)hipGetLastError();  // clear the capture error
+  if (stream_) dev_capture_end(stream_);
   if (pool_open_) {
     c10::hip::HIPCachingAllocator::get()->endAllocateToPool(static_cast<c10::DeviceIndex>(device_), pool_);
     pool_open_ = false;

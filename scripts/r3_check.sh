@@ -23,6 +23,7 @@ for s in ${STEPS:-tests}; do
   case $s in
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_groupby.py tests/test_generic_reduce.py tests/test_packer.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    ab) for i in 1 2; do run ab_old_$i 300 python ab_old/scripts/gemm_bench.py --json gpurun_out/ab_old_$i.json; run ab_new_$i 300 python scripts/gemm_bench.py --json gpurun_out/ab_new_$i.json; done ;;
     sib) run sib 600 python -u -m pytest tests/test_sibling_fusion.py -x -q --timeout 120 --timeout-method thread ;;
     kmeans) run kmeans 300 python scripts/kmeans_profile.py --iters 50 ;;
     kmeans_cprof) run kmeans_cprof 300 python scripts/kmeans_profile.py --iters 20 --cprofile ;;
