@@ -24,6 +24,13 @@ for s in ${STEPS:-tests}; do
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_groupby.py tests/test_generic_reduce.py tests/test_packer.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
     ab) for i in 1 2; do run ab_old_$i 300 python ab_old/scripts/gemm_bench.py --json gpurun_out/ab_old_$i.json; run ab_new_$i 300 python scripts/gemm_bench.py --json gpurun_out/ab_new_$i.json; done ;;
+    incep1m) run incep1m 900 python bench/configs.py inception --rows 1000000 --steps 1 --warmup 1 ;;
+    incep1m_u8) run incep1m_u8 900 python bench/configs.py inception --rows 1000000 --steps 1 --warmup 1 --input-dtype uint8 ;;
+    incep_dev) run incep_dev 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
+    prof_kmeans) export TMPDIR=/tmp; run prof_kmeans 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_kmeans" -o run -- python scripts/kmeans_profile.py --iters 20 ;;
+    prof_reduce) export TMPDIR=/tmp; run prof_reduce 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_reduce" -o run -- python bench/configs.py reduce --steps 2 --warmup 1 ;;
+    prof_bench) export TMPDIR=/tmp; run prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_bench" -o run -- python bench.py --steps 3 --warmup 1 ;;
+    prof_incep) export TMPDIR=/tmp; run prof_incep 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_incep" -o run -- python bench/configs.py inception --source device --rows 8192 --steps 1 --warmup 1 ;;
     sib) run sib 600 python -u -m pytest tests/test_sibling_fusion.py -x -q --timeout 120 --timeout-method thread ;;
     kmeans) run kmeans 300 python scripts/kmeans_profile.py --iters 50 ;;
     kmeans_cprof) run kmeans_cprof 300 python scripts/kmeans_profile.py --iters 20 --cprofile ;;

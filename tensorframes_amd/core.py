@@ -842,7 +842,7 @@ class _RowVectorizer:
                 return done
             if len(rows) < 2:
                 continue
-            ins = [torch.stack([cv[i] for i in rows], 0) for cv in cell_views]
+            ins = [engine.stack_rows([cv[i] for i in rows]) for cv in cell_views]
             idx, n = rows, len(rows)
             outs = engine.run_program(prog, ins, dev)
             if any(o.dim() == 0 or o.shape[0] != n for o in outs):
@@ -939,7 +939,7 @@ def _stack_cells(vals: List[torch.Tensor], tf_dtype: int, shape: Optional[Shape]
         return _empty_output(shape.prepend(UNKNOWN) if shape is not None else None, tf_dtype)
     shapes = {tuple(v.shape) for v in vals}
     if len(shapes) == 1:
-        return torch.stack(vals, 0)
+        return engine.stack_rows(vals)
     return RaggedColumn([v.cpu().numpy() for v in vals], tf_dtype)
 
 
@@ -1145,7 +1145,7 @@ def _to_host_batched(vals: Dict[str, torch.Tensor]) -> Dict[str, np.ndarray]:
         if len(names) == 1:
             out[names[0]] = vals[names[0]].cpu().numpy()
             continue
-        flat = torch.cat([vals[n].reshape(-1) for n in names]).cpu().numpy()
+        flat = engine.cat_rows([vals[n].reshape(-1) for n in names]).cpu().numpy()
         off = 0
         for n in names:
             k = vals[n].numel()
@@ -1815,7 +1815,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         metrics.add("aggregate_batched_groups", batched)
         metrics.add("aggregate_single_groups", ngroups - batched)
         for n in out_names:
-            out_cols[n] = torch.stack(per[n], 0)
+            out_cols[n] = engine.stack_rows(per[n])
         return {dist.rank(): Block(len(uniq), out_cols)}
 
     out_fields = [df.schema[k] for k in keys]

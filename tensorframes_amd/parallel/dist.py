@@ -382,7 +382,8 @@ def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torc
     received rows, concatenated in source-rank order. Device tensors move in
     ONE RCCL all_to_all over xGMI (the groupBy shuffle: SURVEY D4, reference
     DebugRowOps.scala:576), host tensors over gloo."""
-    x = torch.cat(chunks, 0).contiguous()
+    from ..engine import cat_rows
+    x = cat_rows(chunks).contiguous()
     if not is_distributed():
         return x
     _ensure_groups()
