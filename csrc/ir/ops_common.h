@@ -88,7 +88,7 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
 // sibling convs fused along OC (GPU): w0 = the members' filters concatenated
 // along OC, outs[k] = member k's output (NHWC, possibly a channel slice)
 void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,
-                         std::vector<at::Tensor>& outs);
+                         std::vector<at::Tensor>& outs, const std::vector<int>& acts);
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
                 int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
 

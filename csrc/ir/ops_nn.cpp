@@ -130,7 +130,7 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
 }
 
 void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,
-                         std::vector<at::Tensor>& outs) {
+                         std::vector<at::Tensor>& outs, const std::vector<int>& acts) {
   TFA_CHECK(c.gpu, "Conv2D siblings: GPU plans only");
   TFA_CHECK(!outs.empty() && outs.size() <= static_cast<size_t>(k::kMaxOutSegs), "Conv2D siblings: 1..",
             k::kMaxOutSegs, " outputs");
@@ -155,6 +155,7 @@ void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0,
     a.seg.begin[k] = begin;
     a.seg.ptr[k] = o.data_ptr();
     a.seg.ldc[k] = o.stride(2);
+    a.seg.act[k] = k < acts.size() ? acts[k] : act;
     begin += o.size(3);
   }
   a.seg.begin[outs.size()] = begin;

@@ -89,10 +89,12 @@ __device__ __forceinline__ void sched_interleave() {
 
 // where output column `col` lives: its column base pointer and row stride
 // (one output, or one of the sibling-conv segments)
-__device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t col, float*& base, int64_t& ld) {
+__device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t col, float*& base, int64_t& ld,
+                                        int& act) {
   if (g.seg.n == 0) {
     base = Cb + col;
     ld = g.ldc;
+    act = g.act;
     return;
   }
   int s = 0;
@@ -101,6 +103,7 @@ __device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t co
     if (q < g.seg.n && col >= g.seg.begin[q]) s = q;
   base = static_cast<float*>(g.seg.ptr[s]) + (col - g.seg.begin[s]);
   ld = g.seg.ldc[s];
+  act = g.seg.act[s];
 }
 
 template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
@@ -392,7 +395,6 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
   // applied afterwards by a runtime loop over the elements this thread just
   // wrote (re-read from its own stores: small code, no dynamic acc index).
   const bool heavy = !ws && !(g.act <= ACT_RELU6 && g.epi.n == 0);
-  const int cheap_act = heavy ? ACT_NONE : g.act;
   float* Cb = static_cast<float*>(g.C) + bz * g.strideC;
   static_for<TN>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
@@ -401,7 +403,9 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
     const float bv = (!ws && bias) ? bias[col] : 0.f;
     float* cbase;
     int64_t cld;
-    out_col(g, Cb, col, cbase, cld);
+    int cact;
+    out_col(g, Cb, col, cbase, cld, cact);
+    if (heavy) cact = ACT_NONE;
     static_for<TM>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       const f32x16 v = acc[i][j];
@@ -412,7 +416,7 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
         if (ws)  // split-K partial slab [split][batch][M][N]
           ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = v[r];
         else
-          cbase[row * cld] = act_fast(v[r] + bv, cheap_act);
+          cbase[row * cld] = act_fast(v[r] + bv, cact);
       }
     });
   });
@@ -425,9 +429,10 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
       if (col >= N || row >= M) continue;
       float* cbase;
       int64_t cld;
-      out_col(g, Cb, col, cbase, cld);
+      int cact;
+      out_col(g, Cb, col, cbase, cld, cact);
       float* p = cbase + row * cld;
-      *p = epi_apply(g.epi, act_apply(*p, g.act), row, col, N, bz * M * N);
+      *p = epi_apply(g.epi, act_apply(*p, cact), row, col, N, bz * M * N);
     }
   }
 }
@@ -447,8 +452,9 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
     if (bias) s += bias[col];
     float* cbase;
     int64_t cld;
-    out_col(g, static_cast<float*>(g.C) + b * g.strideC, col, cbase, cld);
-    cbase[row * cld] = epi_apply(g.epi, act_apply(s, g.act), row, col, N, b * M * N);
+    int cact;
+    out_col(g, static_cast<float*>(g.C) + b * g.strideC, col, cbase, cld, cact);
+    cbase[row * cld] = epi_apply(g.epi, act_apply(s, cact), row, col, N, b * M * N);
   }
 }
 

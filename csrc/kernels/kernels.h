@@ -163,6 +163,7 @@ struct OutSegs {
   int64_t begin[kMaxOutSegs + 1];
   void* ptr[kMaxOutSegs];
   int64_t ldc[kMaxOutSegs];
+  int act[kMaxOutSegs];  // per-segment activation (used in place of GemmArgs::act)
 };
 
 // C[b] = op(A[b]) @ op(B[b]) (+ bias[N]) (relu); row-major, leading dims in elements.

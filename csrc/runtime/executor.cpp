@@ -171,6 +171,7 @@ struct Program::Step {
     int alias_slot;
     int64_t alias_offset;
     const TensorInfo* alias_info;
+    int act;  // this member's epilogue activation (members may differ)
   };
   std::vector<Sib> sibs;
 };
@@ -737,7 +738,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
       const auto& v = infos[it->second.node][it->second.index].value;
       return v ? &*v : nullptr;
     };
-    std::map<std::tuple<int, std::string, int, bool>, std::vector<size_t>> groups;
+    std::map<std::pair<int, std::string>, std::vector<size_t>> groups;
     for (size_t i = 0; i < p->steps.size(); ++i) {
       const Step& st = p->steps[i];
       if (st.kind != Step::CONV || !st.epi.empty() || st.in_slots.size() != 2 || !st.sibs.empty()) continue;
@@ -754,7 +755,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
       for (int64_t v : nd.attr_ilist("strides", {1, 1, 1, 1})) sig += "," + std::to_string(v);
       for (int64_t v : nd.attr_ilist("dilations", {1, 1, 1, 1})) sig += "," + std::to_string(v);
       for (int d = 0; d < 3; ++d) sig += "," + std::to_string(w->size(d));
-      groups[std::make_tuple(st.in_slots[0], sig, st.act, st.bias_slot >= 0)].push_back(i);
+      groups[{st.in_slots[0], sig}].push_back(i);
     }
     std::map<size_t, Step> merged_at;
     std::set<size_t> dropped;
@@ -767,13 +768,19 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
         ms.out_slots.clear();
         ms.out_info.clear();
         ms.alias_slot = -1;
+        ms.act = 0;
         std::vector<at::Tensor> ws, bs;
+        bool any_bias = false;
+        for (size_t q = g0; q < g1; ++q) any_bias = any_bias || p->steps[idx[q]].bias_slot >= 0;
         for (size_t q = g0; q < g1; ++q) {
           const Step& m = p->steps[idx[q]];
           const at::Tensor* w = const_val(m.in_slots[1]);
           ws.push_back(*w);
-          if (m.bias_slot >= 0) bs.push_back(*const_val(m.bias_slot));
-          ms.sibs.push_back({m.node, w->size(3), m.alias_slot, m.alias_offset, m.alias_info});
+          // members without a bias add zeros (e.g. the pool branch's conv, whose
+          // bias follows the moved AvgPool: graph/rewrite.py)
+          if (any_bias) bs.push_back(m.bias_slot >= 0 ? *const_val(m.bias_slot) : at::zeros({w->size(3)}, w->options()));
+          ms.sibs.push_back({m.node, w->size(3), m.alias_slot, m.alias_offset, m.alias_info, m.act});
+          ms.act = std::max(ms.act, m.act);  // > RELU6 selects the general epilogue
           ms.out_slots.push_back(m.out_slots[0]);
           ms.out_info.push_back(m.out_info[0]);
           if (q > g0) dropped.insert(idx[q]);
@@ -781,7 +788,8 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
         const int wslot = p->nslots++;
         p->synth_consts[wslot] = at::cat(ws, 3).contiguous();
         ms.in_slots[1] = wslot;
-        if (!bs.empty()) {
+        ms.bias_slot = -1;
+        if (any_bias) {
           const int bslot = p->nslots++;
           p->synth_consts[bslot] = at::cat(bs, 0).contiguous();
           ms.bias_slot = bslot;
@@ -999,7 +1007,9 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           }
           at::Tensor bias;
           if (st.bias_slot >= 0) bias = slots[st.bias_slot];
-          run_conv2d_siblings(c, c.in[0], c.in[1], st.bias_slot >= 0 ? &bias : nullptr, st.act, outs);
+          std::vector<int> acts;
+          for (const auto& sb : st.sibs) acts.push_back(sb.act);
+          run_conv2d_siblings(c, c.in[0], c.in[1], st.bias_slot >= 0 ? &bias : nullptr, st.act, outs, acts);
           for (size_t k = 0; k < outs.size(); ++k) c.out[k] = outs[k];
         } else if (gpu && st.alias_slot >= 0) {
           at::Tensor& whole = slots[st.alias_slot];
@@ -1509,6 +1519,7 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
       for (size_t k = 0; k < st.sibs.size(); ++k) {
         const auto& sb = st.sibs[k];
         os << (k ? "," : "") << g_->node(sb.node).name << ":" << sb.oc;
+        if (sb.act) os << "+" << act_name(sb.act);
         if (sb.alias_slot >= 0) os << "->concat-slice@" << sb.alias_offset;
       }
       os << "]";

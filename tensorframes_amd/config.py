@@ -26,6 +26,8 @@ class Config:
     # the SPMD-safe default) or a rank number (the Spark driver's view; the
     # other ranks get [])
     collect_to: str = dataclasses.field(default_factory=lambda: _env("TFA_COLLECT_TO", "all", str))
+    # value-preserving algebraic GraphDef rewrites before planning (graph/rewrite.py)
+    graph_rewrites: bool = dataclasses.field(default_factory=lambda: _env("TFA_GRAPH_REWRITES", True, bool))
     # target bytes of one input column per pipelined chunk (host->device->host)
     chunk_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_CHUNK_BYTES", 128 << 20, int))
     # a pipelined job is cut into at least this many chunks (when chunks stay >= 4 MB)

@@ -81,13 +81,35 @@ def program(graph_bytes: bytes, fetches: Sequence[str], feeds: Sequence[str]):
         if p is not None:
             _prog_cache.move_to_end(k)
             return p
-    g = native_graph(graph_bytes)
+    g = native_graph(_planned_bytes(graph_bytes))
     p = _C.Program(g, list(fetches), list(feeds))
     with _lock:
         _prog_cache[k] = p
         while len(_prog_cache) > _MAX_CACHE:
             _prog_cache.popitem(last=False)
     return p
+
+
+_rewritten: "OrderedDict[str, bytes]" = OrderedDict()
+
+
+def _planned_bytes(graph_bytes: bytes) -> bytes:
+    """The GraphDef the executor plans: the user's, after the algebraic
+    rewrites of graph/rewrite.py (value-preserving for every fetch;
+    `Config.graph_rewrites` = False plans the graph as given)."""
+    if not config.graph_rewrites:
+        return graph_bytes
+    k = _key(graph_bytes)
+    with _lock:
+        if k in _rewritten:
+            return _rewritten[k] or graph_bytes
+    from .graph import rewrite
+    out = rewrite.optimize(graph_bytes)
+    with _lock:
+        _rewritten[k] = out
+        while len(_rewritten) > _MAX_CACHE:
+            _rewritten.popitem(last=False)
+    return out or graph_bytes
 
 
 def clear_program_cache():

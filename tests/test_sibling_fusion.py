@@ -82,3 +82,51 @@ def test_sibling_convs_split_k_reducer():
     dev = _gpu()
     g = _graph(np.random.default_rng(3), [32, 32, 48], cin=512, hw=4, extra_branch=False)
     _check(g, torch.rand(1, 4, 4, 512), dev, 3)
+
+
+def _pool_branch_graph(rng, cin=16, hw=12):
+    """An Inception mixed block: three 1x1 heads on x plus AvgPool -> 1x1 conv."""
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, hw, hw, cin], name="x")
+
+        def conv(inp, oc, name):
+            w = tf.constant((rng.standard_normal((1, 1, int(inp.get_shape()[3]), oc)) * 0.2).astype(np.float32))
+            b = tf.constant(rng.uniform(-1, 1, oc).astype(np.float32))
+            return tf.nn.relu(tf.nn.bias_add(tf.nn.conv2d(inp, w, [1, 1, 1, 1], "SAME"), b), name=name)
+        heads = [conv(x, 24, "h0"), conv(x, 8, "h1"), conv(x, 12, "h2")]
+        pooled = tf.nn.avg_pool(x, [1, 3, 3, 1], [1, 1, 1, 1], "SAME")
+        tf.concat(heads + [conv(pooled, 16, "pool_proj")], 3, name="y")
+    return g
+
+
+def test_avgpool_then_pointwise_conv_is_reordered_and_value_preserving():
+    import tensorframes_amd as tfs
+    from tensorframes_amd.graph import rewrite
+    g = _pool_branch_graph(np.random.default_rng(4))
+    out = rewrite.optimize(g.serialize())
+    assert out is not None
+    xin = torch.rand(2, 12, 12, 16)
+    engine.clear_program_cache()
+    prog = engine.program(g.serialize(), ["y"], ["x"])
+    plan = prog.describe([xin], True)
+    # the pool branch's conv now reads x and joins the 1x1 siblings; the pool runs on its 16 channels
+    assert "4 sibling convs fused" in plan, plan
+    got = engine.run_program(prog, [xin], torch.device("cpu"))[0].double()
+    tfs.set_config(graph_rewrites=False)
+    try:
+        engine.clear_program_cache()
+        ref = engine.program(g.serialize(), ["y"], ["x"])
+        assert "3 sibling convs fused" in ref.describe([xin], True)  # the pool branch stays apart
+        want = engine.run_program(ref, [xin], torch.device("cpu"))[0].double()
+    finally:
+        tfs.set_config(graph_rewrites=True)
+        engine.clear_program_cache()
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_pool_branch_fused_siblings_match_host():
+    dev = _gpu()
+    g = _pool_branch_graph(np.random.default_rng(5))
+    _check(g, torch.rand(3, 12, 12, 16), dev, 4)
