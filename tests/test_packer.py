@@ -101,11 +101,13 @@ def test_collect_rows_throughput():
     """The reference's ConvertBackPerformanceSuite case (10M Int cells ->
     Rows; 2M here to keep the suite fast, bench/configs.py refperf times 10M).
     Round 2 built Rows in Python at 0.36M rows/s; pinned at >= 20x that."""
+    import gc
     n = 2_000_000
     df = tfs.from_columns({"x": np.arange(n, dtype=np.int32)}, num_partitions=2).cache()
     df.local_blocks()
     best = 1e9
-    for _ in range(3):
+    for _ in range(6):  # best of several: the suite may share the CPUs with other workers
+        gc.collect()
         t0 = time.perf_counter()
         rows = df.collect()
         best = min(best, time.perf_counter() - t0)
