@@ -507,6 +507,21 @@ def _normalize_rows(data: Sequence[Any], names: Optional[List[str]]):
     return [(r,) for r in rows], names
 
 
+def _validate_all_rows(rows: List[tuple], st: StructType) -> None:
+    """Width and null checks over ALL rows. In a multi-rank job every rank
+    holds the same local `rows` but packs only its own partitions; checking
+    the whole list first makes a bad row fail on every rank before any rank
+    enters a collective (instead of one rank raising while the rest block)."""
+    ncols = len(st.fields)
+    bad = next((r for r in rows if len(r) != ncols), None)
+    if bad is not None:
+        raise ValueError(f"row {bad} has {len(bad)} values, schema has {ncols} columns")
+    for i, f in enumerate(st.fields):
+        if any(r[i] is None for r in rows):
+            raise ValueError(f"column '{f.name}' contains null values; tensorframes_amd requires "
+                             f"non-null columns (the reference silently accepted them)")
+
+
 def create_dataframe(data, schema=None, num_partitions: Optional[int] = None) -> DataFrame:
     """Build a DataFrame from local data (rows, dicts, tuples, scalars, or a
     dict of column arrays). `schema`: a StructType, a list of column names, or None."""
@@ -541,6 +556,8 @@ def create_dataframe(data, schema=None, num_partitions: Optional[int] = None) ->
     ncols = len(names)
     blocks = {}
     n = len(rows)
+    if dist.world_size() > 1:
+        _validate_all_rows(rows, st)  # every rank raises, not only the owner of the bad row
     from .._native import _C
     for p in dist.local_partitions(nparts):
         a, b = _bounds(n, nparts, p)

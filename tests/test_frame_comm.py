@@ -72,6 +72,14 @@ def _worker(rank, world, port, outdir):
     # a string column still works (pickled values)
     s = tfs.create_dataframe([tfs.Row(name=f"n{i}", x=float(i)) for i in range(11)], num_partitions=4)
     res["strings"] = [r.name for r in s.collect()]
+    # a malformed row in the LAST partition (owned by the last rank) fails on every rank
+    for bad in ([(float(i), 1.0) for i in range(19)] + [(1.0,)], [(float(i), 1.0) for i in range(19)] + [(1.0, None)]):
+        try:
+            tfs.create_dataframe(bad, ["a", "b"], num_partitions=world)
+            res.setdefault("bad_rows", []).append("accepted")
+        except ValueError as e:
+            res.setdefault("bad_rows", []).append("width" if "schema has" in str(e) else "null")
+    dist.barrier()
     with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
         json.dump(res, f)
     dist.shutdown()
@@ -97,3 +105,4 @@ def test_frame_actions_scale_with_ranks(world, tmp_path):
         assert res["rep_count"] == N
         assert res["group_count"] == [[j, len(range(j, N, 7))] for j in range(7)]
         assert res["strings"] == [f"n{i}" for i in range(11)]
+        assert res["bad_rows"] == ["width", "null"], r  # raised on every rank, not only the owner
