@@ -18,6 +18,7 @@ using namespace tfa;
 
 namespace tfa {
 void register_packer(py::module& m);  // runtime/packer.cpp
+void register_pyencode(py::module& m);  // proto/pyencode.cpp
 }
 
 namespace {
@@ -490,6 +491,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return out;
   }, "out[j] = x[idx[j]] along dim 0 (device gather kernel)");
   register_packer(m);
+  register_pyencode(m);
   m.def("jit_compile", [](const std::string& src) { return jit::compile_only(src); },
         "compile a generated kernel with hiprtc for gfx950 (no device needed); returns the code-object size");
   m.def("jit_stats", []() {

@@ -236,6 +236,18 @@ class Graph:
             cache = self._enc_view if view else self._enc_full
             other = self._enc_full if view else self._enc_view
             i = len(cache)  # (no range(): this module defines the tf.range op)
+            enc = _native_encoder()
+            if enc is not None and i < len(self._nodes):
+                # one C++ pass (csrc/proto/pyencode.cpp); None marks a node it
+                # does not cover, encoded below by graph/proto.py
+                for n, e in zip(self._nodes[i:], enc(self._nodes[i:], 1024 if view else -1)):
+                    if e is None:
+                        vn = self._view_node(n) if view else n
+                        e = P._ld(1, P.serialize_node(vn))
+                        cache.append(list(e.parts) if isinstance(e, P._Rope) else [e])
+                    else:
+                        cache.append([e])
+                return cache[:len(self._nodes)]
             for n in self._nodes[i:]:
                 vn = self._view_node(n)
                 if vn is n and i < len(other):  # same node in both views: encode once
@@ -269,6 +281,21 @@ class Graph:
 
     def __exit__(self, *a):
         return self._ctx.__exit__(*a)
+
+
+_ENCODER: List[Any] = []
+
+
+def _native_encoder():
+    """`_C.encode_nodes` when the extension is built (the DSL itself stays
+    importable without it: graph/proto.py is the reference encoder)."""
+    if not _ENCODER:
+        try:
+            from .._native import _C
+            _ENCODER.append(getattr(_C, "encode_nodes", None))
+        except Exception:  # noqa: BLE001
+            _ENCODER.append(None)
+    return _ENCODER[0]
 
 
 _tls = threading.local()
@@ -529,29 +556,40 @@ def _graph_of(values) -> Graph:
 def _op(op_type: str, inputs: List[Tuple[str, Any]], attrs: Dict[str, P.AttrValue],
         name: Optional[str], n_out: int = 1, out_dtypes: Optional[List[DType]] = None,
         dtype_hint: Optional[DType] = None, list_inputs: Sequence[str] = ()) -> Operation:
-    """Create an op: open its name scope, lift python values to `<op>/<arg>` Consts."""
+    """Create an op: open its name scope, lift python values to `<op>/<arg>` Consts.
+
+    Hot for graphs rebuilt per iteration (K-Means): no default-graph context
+    switch, and the op's name scope is only entered when a value is lifted."""
     g = _graph_of([v for _, v in inputs])
-    with g.as_default():
-        op_name = g.unique_name(name or op_type)
-        names: List[str] = []
-        g_scope = g._scope
-        g._scope = op_name.split("/")
-        try:
-            for arg, v in inputs:
-                vals = v if arg in list_inputs else [v]
-                for j, item in enumerate(vals):
-                    if isinstance(item, Tensor):
-                        t = item
-                    else:
-                        nm = arg if arg not in list_inputs else (f"{arg}_{j}" if j else arg)
-                        t = _const_node(g, item, dtype_hint if dtype_hint is not None and
-                                        not isinstance(item, np.ndarray) else None,
-                                        g.unique_name(nm))
-                    names.append(t.op.name if t.value_index == 0 else t.name)
-        finally:
+    op_name = g.unique_name(name or op_type)
+    names: List[str] = []
+    g_scope = None
+    try:
+        for arg, v in inputs:
+            if arg in list_inputs:
+                vals = v
+            elif isinstance(v, Tensor):
+                names.append(v.op.node_def.name if v.value_index == 0 else v.name)
+                continue
+            else:
+                vals = (v,)
+            for j, item in enumerate(vals):
+                if isinstance(item, Tensor):
+                    t = item
+                else:
+                    if g_scope is None:
+                        g_scope = g._scope
+                        g._scope = op_name.split("/")
+                    nm = arg if arg not in list_inputs else (f"{arg}_{j}" if j else arg)
+                    t = _const_node(g, item, dtype_hint if dtype_hint is not None and
+                                    not isinstance(item, np.ndarray) else None,
+                                    g.unique_name(nm))
+                names.append(t.op.node_def.name if t.value_index == 0 else t.name)
+    finally:
+        if g_scope is not None:
             g._scope = g_scope
-        node = P.NodeDef(op_name, op_type, names, attrs)
-        return g._add(node, n_out, out_dtypes or [])
+    node = P.NodeDef(op_name, op_type, names, attrs)
+    return g._add(node, n_out, out_dtypes or [])
 
 
 def _first_dtype(*vals) -> Optional[DType]:
@@ -749,9 +787,76 @@ is_inf = _mk_unary("IsInf")
 is_finite = _mk_unary("IsFinite")
 
 
+_SAME_RANK_OPS = frozenset((
+    "Identity", "Neg", "Abs", "Square", "Sqrt", "Rsqrt", "Exp", "Log", "Log1p", "Expm1", "Reciprocal", "Inv",
+    "Floor", "Ceil", "Round", "Sign", "Sin", "Cos", "Tan", "Tanh", "Sigmoid", "Erf", "IsNan", "IsInf", "IsFinite",
+    "LogicalNot", "Cast", "Relu", "Relu6", "Elu", "Selu", "Softplus", "Softsign", "Softmax", "LogSoftmax", "Tile",
+    "BiasAdd", "ZerosLike", "OnesLike", "StopGradient", "CheckNumerics"))
+_BROADCAST_OPS = frozenset((
+    "Add", "AddV2", "Sub", "Mul", "RealDiv", "Div", "DivNoNan", "Maximum", "Minimum", "Pow", "SquaredDifference",
+    "FloorDiv", "FloorMod", "Mod", "Less", "LessEqual", "Greater", "GreaterEqual", "Equal", "NotEqual",
+    "LogicalAnd", "LogicalOr", "Atan2", "Select", "SelectV2"))
+_REDUCE_OPS = frozenset(("Sum", "Min", "Max", "Prod", "Mean", "All", "Any"))
+
+
+def _const_value(t: Tensor) -> Optional[np.ndarray]:
+    nd = t.op.node_def
+    if nd.op == "Const" and "value" in nd.attr:
+        return nd.attr["value"].value.to_numpy()
+    return None
+
+
+def _static_rank(t: Tensor, depth: int = 0) -> Optional[int]:
+    """Rank of `t` from the local op structure, without whole-graph shape
+    inference (None when a rule does not apply). Reductions over all axes need
+    only the rank, and graphs rebuilt per iteration (K-Means) would otherwise
+    re-serialise and re-infer the whole graph for every `reduce_sum(x)`."""
+    r = getattr(t, "_rank", False)
+    if r is not False:
+        return r
+    nd = t.op.node_def
+    r = None
+    if nd.op in ("Placeholder", "PlaceholderV2", "Const"):
+        s = t.get_shape()
+        r = s.ndims
+    elif depth < 64 and t.value_index == 0:
+        ins = t.op.inputs
+        if nd.op in _SAME_RANK_OPS and ins:
+            r = _static_rank(ins[0], depth + 1)
+        elif nd.op in _BROADCAST_OPS and ins:
+            rs = [_static_rank(i, depth + 1) for i in ins]
+            r = None if any(x is None for x in rs) else max(rs)
+        elif nd.op == "MatMul":
+            r = 2
+        elif nd.op in ("Shape",):
+            r = 1
+        elif nd.op in ("Size", "Rank"):
+            r = 0
+        elif nd.op == "ExpandDims" and ins:
+            r0 = _static_rank(ins[0], depth + 1)
+            r = None if r0 is None else r0 + 1
+        elif nd.op in ("ArgMin", "ArgMax") and ins:
+            r0 = _static_rank(ins[0], depth + 1)
+            r = None if r0 is None or r0 == 0 else r0 - 1
+        elif nd.op == "Reshape" and len(ins) == 2:
+            sv = _const_value(ins[1])
+            r = None if sv is None else int(sv.size)
+        elif nd.op in _REDUCE_OPS and len(ins) == 2:
+            r0 = _static_rank(ins[0], depth + 1)
+            ax = _const_value(ins[1])
+            kd = nd.attr.get("keep_dims")
+            if r0 is not None and ax is not None and kd is not None:
+                axes = {int(a) % r0 for a in ax.reshape(-1)} if r0 else set()
+                r = r0 if kd.value else r0 - len(axes)
+    t._rank = r
+    return r
+
+
 def _axis_input(input_tensor: Tensor, axis) -> Any:
     if axis is None:
-        rk = input_tensor.get_shape().ndims
+        rk = _static_rank(input_tensor)
+        if rk is None:
+            rk = input_tensor.get_shape().ndims
         if rk is not None:
             return constant(np.arange(rk, dtype=np.int32), dtype=int32)
         r = rank(input_tensor)

@@ -243,3 +243,30 @@ def test_analyze_graph_summary():
     assert str(s["y"].shape) == "[?,2]"
     from tensorframes_amd.utils import dtypes as D
     assert s["y"].tf_dtype == D.DT_DOUBLE
+
+
+def test_static_rank_matches_inference_and_skips_it():
+    """reduce_*(x) over all axes takes x's rank from the local op structure
+    (graph/dsl.py _static_rank), not from whole-graph shape inference."""
+    import numpy as np
+    from tensorframes_amd.graph import dsl
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.double, [None, 4], name="x")
+        c = tf.constant(np.ones((3, 4)))
+        m = tf.matmul(x, c, transpose_b=True)
+        e = tf.expand_dims(tf.reduce_sum(tf.square(c), 1), 0)
+        d = tf.tile(e, tf.stack([tf.shape(x)[0], 1])) + 2.0 * m
+        a = tf.argmin(d, 1)
+        r = tf.reduce_min(d, 1, keep_dims=True)
+        s = tf.reshape(d, [-1])
+        cands = [x, c, m, e, d, a, r, s, tf.cast(a, tf.float32), tf.reduce_sum(d, [0, 1])]
+        ranks = [dsl._static_rank(t) for t in cands]
+        calls = []
+        orig = g._inferred
+        g._inferred = lambda: calls.append(1) or orig()
+        tot = tf.reduce_sum(tf.reduce_min(d, 1), name="tot")
+        assert not calls
+        g._inferred = orig
+    assert ranks == [t.get_shape().ndims for t in cands] == [2, 2, 2, 2, 2, 1, 2, 1, 1, 0]
+    assert tot.get_shape().ndims == 0

@@ -113,3 +113,68 @@ def test_attr_kinds_roundtrip():
     assert m.attr["shape"].value.dims == [-1, 3]
     assert m.attr["ul"].value["i"] == [1, 2, -1]
     assert m.attr["tl"].value["type"] == [D.DT_FLOAT, D.DT_INT32]
+
+
+def _py_enc(n, view):
+    from tensorframes_amd.graph.dsl import Graph
+    vn = Graph._view_node(n) if view else n
+    e = P._ld(1, P.serialize_node(vn))
+    return b"".join(e.parts) if isinstance(e, P._Rope) else e
+
+
+def _zoo_nodes():
+    """Nodes covering every attr kind, typed-val dtype and view rule."""
+    T = P.TensorProto.from_numpy
+    nodes = []
+    for i, (arr, dt) in enumerate([
+            (np.float32(1.5), None), (np.float64(-2.25), None), (np.int32(-7), None), (np.int64(-(1 << 40)), None),
+            (np.bool_(True), None), (np.float16(3.0), None), (np.uint8(200), None), (np.int16(-300), None),
+            (np.int8(-5), None), (np.zeros((0, 3), np.float32), None), (np.arange(6, dtype=np.int32).reshape(2, 3), None),
+            (np.ones((40, 40), np.float64), None),
+            (np.array([b"ab", b"c"], dtype=object), D.DT_STRING)]):
+        tp = T(arr, dt)
+        nodes.append(P.NodeDef(f"c{i}", "Const", [], {"dtype": P.AttrValue.type(tp.dtype), "value": P.AttrValue.tensor(tp)}))
+    bf = P.TensorProto(D.DT_BFLOAT16, [1], b"\x80\x3f")  # one bf16 element: tensor_content, not a typed val
+    nodes.append(P.NodeDef("bf", "Const", [], {"dtype": P.AttrValue.type(D.DT_BFLOAT16), "value": P.AttrValue.tensor(bf)}))
+    nodes.append(P.NodeDef("p", "Placeholder", [], {"dtype": P.AttrValue.type(D.DT_FLOAT),
+                                                    "shape": P.AttrValue.shape([None, 3, 0])}))
+    nodes.append(P.NodeDef("q", "Placeholder", [], {"dtype": P.AttrValue.type(D.DT_FLOAT), "shape": P.AttrValue.shape(None)},
+                           device="/device:GPU:0"))
+    nodes.append(P.NodeDef("conv", "Conv2D", ["p", "c1:0", "^q"], {
+        "T": P.AttrValue.type(D.DT_FLOAT), "strides": P.AttrValue.ilist([1, 2, 2, 1]), "padding": P.AttrValue.s("SAME"),
+        "data_format": P.AttrValue.s(b"NHWC"), "use_cudnn_on_gpu": P.AttrValue.b(False), "axis": P.AttrValue.i(-1),
+        "alpha": P.AttrValue.f(0.1), "names": P.AttrValue.slist(["a", "b"]), "Ts": P.AttrValue.tlist([D.DT_FLOAT, D.DT_INT32]),
+        "_output_shapes": P.AttrValue.shapelist([[None, 4], None, []]), "empty": P.AttrValue.ilist([]),
+        "fl": P.AttrValue("list", {"f": [0.5, -1.0], "b": [True, False]}),
+        "tl": P.AttrValue("list", {"tensor": [T(np.arange(3, dtype=np.int64))]}),
+        "ph": P.AttrValue("placeholder", "x"), "fn": P.AttrValue("func", "my_fn")}))
+    return nodes
+
+
+@pytest.mark.parametrize("view", [False, True])
+def test_native_node_encoder_is_byte_identical(view):
+    """csrc/proto/pyencode.cpp must write exactly what graph/proto.py writes."""
+    nodes = _zoo_nodes()
+    enc = _C.encode_nodes(nodes, 1024 if view else -1)
+    assert len(enc) == len(nodes)
+    for n, e in zip(nodes, enc):
+        assert e is not None, n.name
+        assert e == _py_enc(n, view), n.name
+
+
+def test_native_encoder_falls_back_and_dsl_graphs_match():
+    # a value the native encoder does not take (numpy int in an int attr) -> None, Python encodes it
+    odd = P.NodeDef("odd", "Foo", [], {"n": P.AttrValue("i", np.int64(3))})
+    assert _C.encode_nodes([odd], -1) == [None]
+    from tensorframes_amd import tf
+    from tensorframes_amd.models import kmeans
+    g = tf.Graph()
+    with g.as_default():
+        pts = tf.placeholder(tf.double, [None, 5], name="features")
+        d = kmeans.tf_compute_distances(pts, np.random.default_rng(0).standard_normal((3, 5)))
+        tf.reduce_sum(tf.reduce_min(d, 1), name="total")
+        tf.constant(np.ones((64, 64), np.float32), name="big")
+    g._nodes.append(odd)
+    ref = b"".join(_py_enc(n, False) for n in g._nodes)
+    assert g.serialize().startswith(ref)
+    assert g._shape_view() == b"".join(_py_enc(n, True) for n in g._nodes)
