@@ -135,6 +135,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   py::class_<Graph, std::shared_ptr<Graph>>(m, "Graph")
       .def(py::init([](py::bytes b) { return Graph::from_bytes(std::string(b)); }))
+      .def("structure_key", [](const Graph& g) { return g.structure_key(); },
+           "hash of the graph without its parameter constants' payloads (Graph::structure_key)")
+      .def("parameter_consts",
+           [](const Graph& g) {
+             std::vector<std::string> v;
+             const auto& p = g.parameter_consts();
+             for (size_t i = 0; i < p.size(); ++i)
+               if (p[i]) v.push_back(g.node(static_cast<int>(i)).name);
+             return v;
+           })
       .def("node_names",
            [](const Graph& g) {
              std::vector<std::string> v;
@@ -210,6 +220,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("feed_names", &Program::feed_names)
       .def("row_separable",
            [](const Program& p, py::dict hints) { return p.row_separable(infos_from_py(hints)); })
+      .def("adopt", &Program::adopt, py::arg("old"), py::call_guard<py::gil_scoped_release>(),
+           "take over the plans of a structurally equal program (see executor.h)")
       .def("monoids",
            [](const Program& p) {
              py::list l;
@@ -231,10 +243,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["runs"] = s.runs;
         d["kernels"] = s.kernels;
         d["plans_built"] = s.plans_built;
+        d["plans_adopted"] = s.plans_adopted;
         d["h2d_bytes"] = s.h2d_bytes;
         d["d2h_bytes"] = s.d2h_bytes;
         d["chunks"] = s.chunks;
         d["wall_ms"] = s.wall_ms;
+        d["plan_ms"] = s.plan_ms;
+        d["exec_ms"] = s.exec_ms;
         d["h2d_ms"] = s.h2d_ms;        // device time of the host->device copies (hipEvents)
         d["compute_ms"] = s.compute_ms;
         d["d2h_ms"] = s.d2h_ms;

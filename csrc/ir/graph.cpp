@@ -1,6 +1,12 @@
 // Graph import, edge resolution, closure and static inference / constant folding.
 #include "graph.h"
 
+#include <chrono>
+#include <cstring>
+#include <string_view>
+#include <cstdio>
+#include <cstdlib>
+
 #include <c10/hip/HIPFunctions.h>
 
 #include "../runtime/device_pool.h"
@@ -331,6 +337,139 @@ std::vector<int> Graph::closure(const std::vector<TensorRef>& fetches) const {
   return order;
 }
 
+namespace {
+struct KeyHash {
+  uint64_t h = 1469598103934665603ull;
+  void mix(uint64_t x) { h ^= x + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2); }
+  void str(const std::string& s) {
+    mix(std::hash<std::string_view>{}(s));
+    mix(s.size());
+  }
+  void bytes(const void* p, size_t n) {
+    mix(std::hash<std::string_view>{}(std::string_view(static_cast<const char*>(p), n)));
+    mix(n);
+  }
+  void shape(const Shape& s) {
+    mix(s.unknown_rank ? 1 : 0);
+    mix(s.dims.size());
+    for (auto d : s.dims) mix(static_cast<uint64_t>(d));
+  }
+  void tensor(const HostTensor& t, bool payload) {
+    mix(static_cast<uint64_t>(t.dtype));
+    shape(t.shape);
+    if (!payload) return;
+    bytes(t.bytes.data(), t.bytes.size());
+    mix(t.strings.size());
+    for (auto& x : t.strings) str(x);
+  }
+};
+}  // namespace
+
+const std::vector<char>& Graph::parameter_consts() const {
+  (void)structure_key();
+  return params_;
+}
+
+uint64_t Graph::structure_key() const {
+  std::lock_guard<std::mutex> lk(key_mu_);
+  if (key_) return *key_;
+  std::vector<char> param(nodes_.size(), 0);
+  bool any = false;
+  for (size_t i = 0; i < nodes_.size(); ++i) {
+    if (nodes_[i].op != "Const") continue;
+    const AttrValue* v = nodes_[i].def->find_attr("value");
+    if (v && v->kind == AttrValue::TENSOR && v->tensor && dtype_is_float(v->tensor->dtype) &&
+        !v->tensor->shape.unknown_rank && v->tensor->num_elements() >= 2) {
+      param[i] = 1;
+      any = true;
+    }
+  }
+  if (any) {
+    // taint: a folded value computed from a parameter must itself be a
+    // floating tensor of >= 2 elements (never an integer shape/axis/multiple
+    // or a scalar the planner bakes into a kernel)
+    bool safe = true;
+    try {
+      std::vector<TensorRef> all;
+      all.reserve(nodes_.size());
+      for (size_t i = 0; i < nodes_.size(); ++i) all.push_back({static_cast<int>(i), 0});
+      std::vector<int> order = closure(all);
+      Infos inf = infer(order, {}, false);
+      std::vector<char> taint(nodes_.size(), 0);
+      for (int n : order) {
+        bool t = param[n] != 0;
+        for (auto& r : nodes_[n].inputs) t = t || taint[r.node];
+        taint[n] = t;
+        if (!t || param[n]) continue;
+        for (auto& o : inf[n])
+          if (o.value && !(dtype_is_float(o.dtype) && o.value->numel() >= 2)) safe = false;
+      }
+    } catch (const std::exception&) {
+      safe = false;
+    }
+    if (!safe) std::fill(param.begin(), param.end(), 0);
+  }
+  KeyHash k;
+  for (size_t i = 0; i < nodes_.size(); ++i) {
+    const NodeDef& d = *nodes_[i].def;
+    k.str(d.name);
+    k.str(d.op);
+    k.mix(d.inputs.size());
+    for (auto& in : d.inputs) k.str(in);
+    k.str(d.device);
+    k.mix(d.attr.size());
+    for (auto& [name, a] : d.attr) {
+      k.str(name);
+      k.mix(static_cast<uint64_t>(a.kind));
+      switch (a.kind) {
+        case AttrValue::S:
+        case AttrValue::PLACEHOLDER:
+        case AttrValue::FUNC: k.str(a.s); break;
+        case AttrValue::I: k.mix(static_cast<uint64_t>(a.i)); break;
+        case AttrValue::F: {
+          uint32_t b;
+          std::memcpy(&b, &a.f, 4);
+          k.mix(b);
+          break;
+        }
+        case AttrValue::B: k.mix(a.b ? 1 : 0); break;
+        case AttrValue::TYPE: k.mix(static_cast<uint64_t>(a.type)); break;
+        case AttrValue::SHAPE: k.shape(a.shape); break;
+        case AttrValue::TENSOR:
+          if (a.tensor) k.tensor(*a.tensor, !(param[i] && name == "value"));
+          break;
+        case AttrValue::LIST:
+          if (a.list) {
+            const AttrList& l = *a.list;
+            k.mix(l.s.size());
+            for (auto& x : l.s) k.str(x);
+            k.mix(l.i.size());
+            for (auto x : l.i) k.mix(static_cast<uint64_t>(x));
+            k.mix(l.f.size());
+            for (auto x : l.f) {
+              uint32_t b;
+              std::memcpy(&b, &x, 4);
+              k.mix(b);
+            }
+            k.mix(l.b.size());
+            for (bool x : l.b) k.mix(x ? 1 : 0);
+            k.mix(l.type.size());
+            for (auto x : l.type) k.mix(static_cast<uint64_t>(x));
+            k.mix(l.shape.size());
+            for (auto& x : l.shape) k.shape(x);
+            k.mix(l.tensor.size());
+            for (auto& x : l.tensor) k.tensor(x, true);
+          }
+          break;
+        default: break;
+      }
+    }
+  }
+  params_ = std::move(param);
+  key_ = k.h;
+  return k.h;
+}
+
 std::vector<int> Graph::placeholders() const {
   std::vector<int> v;
   for (size_t i = 0; i < nodes_.size(); ++i)
@@ -344,22 +483,55 @@ std::vector<int> Graph::placeholders() const {
 // block row count, K-Means) is cheaper to compute on the device each run than
 // to build with ATen on the host at every analysis/plan and upload.
 static constexpr int64_t kFoldLimit = int64_t(1) << 16;
+// values that depend on the feeds' shapes (Shape -> StridedSlice -> Pack ->
+// Tile/Fill multiples) fold only while small: shape arithmetic is a few
+// elements, while a row-sized Tile/Fill folded on the host would be rebuilt
+// and uploaded for every plan (every partition size, every rebuilt graph)
+// instead of being written by one device kernel
+static constexpr int64_t kDynFoldLimit = 1024;
 
 Graph::Infos Graph::infer(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds,
                           bool concrete) const {
   const OpRegistry& reg = OpRegistry::get();
   Infos infos(nodes_.size());
+  // dyn[n]: n depends on a placeholder or a stateful op (its info may change
+  // with the feeds); every other node's info is memoised per graph
+  std::vector<char> dyn(nodes_.size(), 0);
+  const int ci = 0;  // (no op's inference of a placeholder-free node depends on `concrete`)
+  {
+    std::lock_guard<std::mutex> lk(static_mu_);
+    if (static_known_[ci].size() != nodes_.size()) {
+      static_known_[ci].assign(nodes_.size(), 0);
+      static_infos_[ci].assign(nodes_.size(), {});
+    }
+  }
   for (int ni : order) {
     const Node& n = nodes_[ni];
     auto fit = feeds.find(ni);
     if (fit != feeds.end()) {
       infos[ni] = {fit->second};
       infos[ni][0].row = fit->second.row;
+      dyn[ni] = 1;
       continue;
     }
     const OpDef* od = reg.find(n.op);
     TFA_CHECK(od, "Op type not registered '", n.op, "' (node '", n.name,
               "'): tensorframes_amd has no kernel for it");
+    bool d = od->stateful || n.op == "Placeholder" || n.op == "PlaceholderV2";
+    for (auto& r : n.inputs) d = d || dyn[r.node];
+    dyn[ni] = d;
+    if (!d) {
+      std::lock_guard<std::mutex> lk(static_mu_);
+      if (static_known_[ci][ni]) {
+        infos[ni] = static_infos_[ci][ni];
+        continue;
+      }
+    }
+    static const bool node_timing = [] {
+      const char* e = std::getenv("TFA_PLAN_TIMING");
+      return e && std::string(e) == "2";
+    }();
+    const auto tn0 = std::chrono::steady_clock::now();
     InferCtx ctx{n, {}, std::vector<TensorInfo>(n.num_outputs), concrete};
     for (auto& r : n.inputs) {
       TFA_CHECK(r.index < static_cast<int>(infos[r.node].size()), "node '", n.name,
@@ -379,7 +551,7 @@ Graph::Infos Graph::infer(const std::vector<int>& order, const std::map<int, Ten
     for (auto* t : ctx.in)
       if (!t->value) foldable = false;
     for (auto& o : ctx.out)
-      if (o.value || !o.shape.fully_known() || o.shape.num_elements() > kFoldLimit ||
+      if (o.value || !o.shape.fully_known() || o.shape.num_elements() > (d ? kDynFoldLimit : kFoldLimit) ||
           o.dtype == DType::STRING)
         foldable = false;
     if (foldable && !ctx.in.empty() && od->compute) {
@@ -391,6 +563,16 @@ Graph::Infos Graph::infer(const std::vector<int>& order, const std::map<int, Ten
     }
     for (auto& o : ctx.out)
       if (o.value) o.row = RowClass::CONST;
+    if (node_timing) {
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tn0).count();
+      std::fprintf(stderr, "[tfa infer] %8.1fus %s %s%s\n", us, n.op.c_str(), n.name.c_str(),
+                   ctx.out.size() && ctx.out[0].value ? " (folded)" : "");
+    }
+    if (!d) {
+      std::lock_guard<std::mutex> lk(static_mu_);
+      static_infos_[ci][ni] = ctx.out;
+      static_known_[ci][ni] = 1;
+    }
     infos[ni] = std::move(ctx.out);
   }
   return infos;

@@ -10,6 +10,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <string>
 #include <unordered_map>
@@ -171,10 +172,30 @@ class Graph {
   Infos infer(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds,
               bool concrete) const;
 
+  // Hash of the graph's structure: every node, input and attribute, except
+  // the payloads of PARAMETER constants (floating-point Consts of >= 2
+  // elements whose value reaches no plan-time decision: no folded integer or
+  // scalar depends on them). Two graphs with equal keys have the same
+  // inference results and plans up to those payloads (reference workload:
+  // kmeans_demo.py:68-168 rebuilds its graphs with new centres every step).
+  uint64_t structure_key() const;
+  // node -> is a parameter constant (as used by structure_key)
+  const std::vector<char>& parameter_consts() const;
+
  private:
   GraphDef def_;
   std::vector<Node> nodes_;
   std::unordered_map<std::string, int> by_name_;
+  // infos of nodes that depend on no placeholder (constants and what folds
+  // from them): the same in every inference of this graph, so analysis, the
+  // row-separability check and planning fold each constant subgraph once
+  // instead of once per call
+  mutable std::mutex static_mu_;
+  mutable std::vector<std::vector<TensorInfo>> static_infos_[1];
+  mutable std::vector<char> static_known_[1];
+  mutable std::mutex key_mu_;
+  mutable std::optional<uint64_t> key_;
+  mutable std::vector<char> params_;
 };
 
 // dtype <-> ATen

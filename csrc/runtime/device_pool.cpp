@@ -156,6 +156,8 @@ void release(Block* b) {
 
 }  // namespace
 
+bool dev_stream_capturing(hipStream_t s) { return capturing(s); }
+
 void dev_capture_begin(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_cap_mu);
   cap_streams().push_back(s);

@@ -34,6 +34,7 @@ void dev_pool_trim();  // hipFree every cached block (after a device sync)
 // capturing stream go to the capture's private (framework) pool
 void dev_capture_begin(hipStream_t s);
 void dev_capture_end(hipStream_t s);
+bool dev_stream_capturing(hipStream_t s);  // inside the engine's own capture on `s`
 bool dev_pool_enabled();  // TFA_DEVICE_POOL=0: every allocation goes to c10
 
 }  // namespace tfa

@@ -185,6 +185,17 @@ struct Program::Plan {
   std::map<int, at::Tensor> synth_consts;               // slot <- plan-made constant (fused sibling filters)
   std::vector<int> fetch_slots;
   std::map<int, std::map<int, at::Tensor>> dev_consts;  // device index -> slot -> tensor
+  std::map<int, TensorInfo> feed_infos;                  // what the plan was inferred with
+  // one device arena per device (upload_consts): the slots it holds, for an
+  // in-place refresh after adopt()
+  struct Arena {
+    at::Tensor dev;
+    std::vector<std::tuple<int, TensorRef, size_t, size_t>> items;  // slot, ref, offset, bytes
+  };
+  std::map<int, Arena> arenas;
+  std::set<int> stale;                  // devices whose constants predate adopt()
+  bool cap_reset = false;               // the capture reads constants that were replaced
+  std::map<int, void*> last_stream;     // device -> stream of the last run
   int fused = 0;
   int fused_siblings = 0;  // convs folded into sibling-fused steps
   // fused elementwise regions (GPU plans): generated source + loaded kernel per device
@@ -344,7 +355,9 @@ std::shared_ptr<Program::Plan> Program::plan_for(const std::vector<at::Tensor>& 
   std::lock_guard<std::mutex> lk(mu_);
   auto it = plans_.find(key);
   if (it != plans_.end()) return it->second;
+  const auto tp = std::chrono::steady_clock::now();
   auto p = build_plan(inputs, false);
+  stats_.plan_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
   if (plans_.size() >= kMaxPlans) plans_.erase(plans_.begin());  // bounded (e.g. many image sizes)
   plans_[key] = p;
   stats_.plans_built++;
@@ -376,8 +389,23 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     }
     feeds[feed_nodes_[i]] = ti;
   }
+  // TFA_PLAN_TIMING=1: host time of each planning phase on stderr
+  static const bool plan_timing = [] {
+    const char* e = std::getenv("TFA_PLAN_TIMING");
+    return e && *e && std::string(e) != "0";
+  }();
+  auto tp0 = std::chrono::steady_clock::now();
+  std::vector<std::pair<const char*, double>> phases;
+  auto phase = [&](const char* name) {
+    if (!plan_timing) return;
+    auto t = std::chrono::steady_clock::now();
+    phases.push_back({name, std::chrono::duration<double, std::micro>(t - tp0).count()});
+    tp0 = t;
+  };
+  p->feed_infos = feeds;
   p->infos = g_->infer(order_, feeds, true);
   const Graph::Infos& infos = p->infos;
+  phase("infer");
 
   // slots
   std::map<TensorRef, int> slot_of;
@@ -624,6 +652,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     place(st);
   }
   TFA_CHECK(deferred.empty(), "internal: a fused step was never placed");
+  phase("steps+epilogue_chains");
   // ---- elementwise-region fusion (GPU plans): regions replace their member steps
   if (gpu_plan && fusion_enabled()) {
     FusionInput fi;
@@ -723,6 +752,7 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     }
   }
 
+  phase("elementwise_regions");
   // ---- horizontal fusion of sibling convs (GPU plans): CONV steps with the
   // same input slot, the same geometry and activation, constant filters (and
   // biases) and no epilogue chain become one step over the filters
@@ -822,17 +852,23 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
   for (auto& sc : p->synth_consts) keep.insert(sc.first);
   for (int s = 0; s < p->nslots; ++s)
     if (last[s] >= 0 && !keep.count(s)) p->steps[last[s]].release.push_back(s);
+  phase("siblings+liveness");
+  if (plan_timing) {
+    std::string line = "[tfa plan]";
+    for (auto& ph : phases) line += str_cat(" ", ph.first, "=", static_cast<int>(ph.second), "us");
+    std::fprintf(stderr, "%s steps=%zu\n", line.c_str(), p->steps.size());
+  }
   return p;
 }
 
-at::Tensor Program::device_const(Plan& p, int slot, const at::Device& dev) {
+at::Tensor Program::device_const(Plan& p, int slot, const at::Device& dev, void* stream) {
   int di = dev.is_cuda() ? dev.index() : -1;
   std::lock_guard<std::mutex> lk(const_mu_);
   auto& m = p.dev_consts[di];
   auto it = m.find(slot);
   if (it != m.end()) return it->second;
   if (dev.is_cuda() && m.empty()) {
-    upload_consts(p, m, dev);
+    upload_consts(p, m, dev, stream);
     it = m.find(slot);
     if (it != m.end()) return it->second;
   }
@@ -862,8 +898,11 @@ at::Tensor Program::device_const(Plan& p, int slot, const at::Device& dev) {
 // host->device copy: they are packed (256-byte aligned) into a pinned staging
 // buffer and the device arena is sliced into typed views. A program built per
 // iteration (K-Means rebuilds its graph with new centres) then pays one
-// transfer instead of one synchronous copy per constant.
-void Program::upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Device& dev) {
+// transfer instead of one synchronous copy per constant, and the copy is
+// asynchronous on the run's own stream (the host does not wait for the GPU to
+// drain before every new program's first run); runs on other streams wait
+// for its event (wait_consts).
+void Program::upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Device& dev, void* stream) {
   const int di = dev.index();
   struct Item {
     int slot;
@@ -897,17 +936,171 @@ void Program::upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Dev
                               at::TensorOptions().dtype(at::kByte).pinned_memory(true));
   auto* hp = static_cast<uint8_t*>(host.data_ptr());
   for (auto& it : items) std::memcpy(hp + it.off, it.v.data_ptr(), it.v.nbytes());
-  at::Tensor arena = host.to(dev, /*non_blocking=*/false);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  at::Tensor arena;
+  {
+    // copy_ on `s` records the staging block's use there (the pinned caching
+    // host allocator keeps it until the copy has run)
+    c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromExternal(s, static_cast<c10::DeviceIndex>(di)));
+    arena = at::empty({static_cast<int64_t>(total)}, at::TensorOptions().dtype(at::kByte).device(dev));
+    arena.copy_(host, /*non_blocking=*/true);
+  }
+  void*& ev = const_events_[{di, stream}];
+  if (!ev) {
+    hipEvent_t e;
+    TFA_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+    ev = e;
+  }
+  (void)hipEventRecord(static_cast<hipEvent_t>(ev), s);
+  Plan::Arena ar;
+  ar.dev = arena;
   for (auto& it : items) {
     at::Tensor t = arena.narrow(0, static_cast<int64_t>(it.off), static_cast<int64_t>(it.v.nbytes()))
                        .view(it.v.scalar_type())
                        .view(it.v.sizes());
     m[it.slot] = t;
     if (it.graph_const) graph_consts_[it.gkey] = t;
+    TensorRef r{};
+    for (auto& cs : p.const_slots)
+      if (cs.first == it.slot) r = cs.second;
+    ar.items.emplace_back(it.slot, r, it.off, it.v.nbytes());
+  }
+  p.arenas[di] = std::move(ar);
+}
+
+// caller holds const_mu_. Rewrites a plan's device constants with the values
+// of its (adopted) graph: the arena is repacked in pinned memory and copied
+// over itself asynchronously on `stream`, so every pointer into it (captured
+// HIP graphs included) stays valid. A plan whose constants on this device do
+// not all live in its own arena (some came from another plan's upload) drops
+// them, and its capture, and uploads afresh.
+void Program::refresh_consts(Plan& p, int di, void* stream) {
+  p.stale.erase(di);
+  auto& m = p.dev_consts[di];
+  if (m.empty()) return;
+  auto drop = [&]() {
+    m.clear();
+    p.arenas.erase(di);
+    p.cap_reset = true;  // its capture read the old arena: run() discards it
+  };
+  if (di < 0) {  // host plan: the slots are clones, rebuilt from the new values
+    m.clear();
+    return;
+  }
+  auto ait = p.arenas.find(di);
+  if (ait == p.arenas.end()) return drop();
+  Plan::Arena& ar = ait->second;
+  std::set<int> in_arena;
+  for (auto& it : ar.items) in_arena.insert(std::get<0>(it));
+  for (auto& kv : m)
+    if (!in_arena.count(kv.first) && kv.second.numel() > 0) return drop();
+  at::Tensor host = at::empty({ar.dev.numel()}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  auto* hp = static_cast<uint8_t*>(host.data_ptr());
+  for (auto& it : ar.items) {
+    const TensorRef& r = std::get<1>(it);
+    const auto& v = p.infos[r.node][r.index].value;
+    if (!v) return drop();
+    at::Tensor c = v->contiguous();
+    if (static_cast<size_t>(c.nbytes()) != std::get<3>(it)) return drop();
+    std::memcpy(hp + std::get<2>(it), c.data_ptr(), c.nbytes());
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto ls = p.last_stream.find(di);
+  // the previous runs may still read the arena: same stream = ordered, else wait
+  if (ls != p.last_stream.end() && ls->second && ls->second != stream)
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(ls->second));
+  {
+    c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromExternal(s, static_cast<c10::DeviceIndex>(di)));
+    ar.dev.copy_(host, /*non_blocking=*/true);
+  }
+  void*& ev = const_events_[{di, stream}];
+  if (!ev) {
+    hipEvent_t e;
+    TFA_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+    ev = e;
+  }
+  (void)hipEventRecord(static_cast<hipEvent_t>(ev), s);
+}
+
+bool Program::adopt(Program& old) {
+  if (&old == this) return false;
+  if (g_->structure_key() != old.g_->structure_key() || g_->nodes().size() != old.g_->nodes().size())
+    return false;
+  if (fetch_names_ != old.fetch_names_ || feed_names_ != old.feed_names_ || order_ != old.order_) return false;
+  if (!host_op_error_.empty() || !old.host_op_error_.empty()) return false;
+  std::scoped_lock lk(mu_, old.mu_, const_mu_, old.const_mu_);
+  if (!plans_.empty()) return false;
+  for (auto& kv : old.plans_)
+    if (!kv.second->synth_consts.empty()) return false;  // plan-made constants derive from the weights
+  // new values of every constant slot (the same nodes: equal structure);
+  // shapes and dtypes must match (the parameter rule guarantees it)
+  std::vector<std::pair<std::shared_ptr<Plan>, Graph::Infos>> fresh;
+  for (auto& kv : old.plans_) {
+    Plan& p = *kv.second;
+    Graph::Infos ni = g_->infer(order_, p.feed_infos, true);
+    for (auto& cs : p.const_slots) {
+      const TensorRef& r = cs.second;
+      const TensorInfo& a = p.infos[r.node][r.index];
+      const TensorInfo& b = ni[r.node][r.index];
+      if (a.dtype != b.dtype || a.shape.dims != b.shape.dims || !b.value || !a.value ||
+          a.value->sizes() != b.value->sizes())
+        return false;
+    }
+    fresh.emplace_back(kv.second, std::move(ni));
+  }
+  for (auto& [pp, ni] : fresh) {
+    Plan& p = *pp;
+    for (auto& cs : p.const_slots) {  // in place: steps hold pointers into p.infos
+      const TensorRef& r = cs.second;
+      p.infos[r.node][r.index].value = ni[r.node][r.index].value;
+    }
+    for (auto& kv : p.dev_consts)
+      if (!kv.second.empty()) p.stale.insert(kv.first);
+  }
+  plans_ = std::move(old.plans_);
+  old.plans_.clear();
+  old.graph_consts_.clear();  // its arenas belong to the moved plans now
+  for (auto& kv : old.const_events_) {
+    void*& ev = const_events_[kv.first];
+    if (ev) (void)hipEventDestroy(static_cast<hipEvent_t>(ev));
+    ev = kv.second;
+  }
+  old.const_events_.clear();
+  stats_.plans_adopted += static_cast<int64_t>(plans_.size());
+  return true;
+}
+
+// a run on `stream` reads constants uploaded on other streams: order it after
+// those copies (completed uploads are forgotten, so steady state costs a map
+// lookup). Inside the engine's own capture the capture stream already waits
+// for the eager warm-up runs that uploaded everything.
+void Program::wait_consts(const at::Device& dev, void* stream) {
+  std::lock_guard<std::mutex> lk(const_mu_);
+  if (const_events_.empty()) return;
+  const int di = dev.index();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (auto it = const_events_.begin(); it != const_events_.end();) {
+    hipEvent_t e = static_cast<hipEvent_t>(it->second);
+    if (it->first.first != di) {
+      ++it;
+      continue;
+    }
+    if (hipEventQuery(e) == hipSuccess) {
+      (void)hipEventDestroy(e);
+      it = const_events_.erase(it);
+      continue;
+    }
+    if (it->first.second != stream && !dev_stream_capturing(s)) (void)hipStreamWaitEvent(s, e, 0);
+    ++it;
   }
 }
 
+Program::~Program() {
+  for (auto& kv : const_events_) (void)hipEventDestroy(static_cast<hipEvent_t>(kv.second));
+}
+
 std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream) {
+  const auto t_exec = std::chrono::steady_clock::now();
   // operands of a step's absorbed epilogue chain (contiguous, on the step's device)
   auto epi_steps = [](const Step& st, const std::vector<at::Tensor>& slots) {
     std::vector<EpiStep> ep;
@@ -929,7 +1122,17 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
     TFA_CHECK(t.device() == dev, "all inputs must live on the same device");
   std::vector<at::Tensor> slots(p.nslots);
   for (size_t i = 0; i < inputs.size(); ++i) slots[p.feed_slots[i]] = inputs[i].contiguous();
-  for (auto& cs : p.const_slots) slots[cs.first] = device_const(p, cs.first, dev);
+  if (!p.stale.empty()) {
+    std::lock_guard<std::mutex> lk(const_mu_);
+    const int di = gpu ? dev.index() : -1;
+    if (p.stale.count(di)) refresh_consts(p, di, stream);
+  }
+  for (auto& cs : p.const_slots) slots[cs.first] = device_const(p, cs.first, dev, stream);
+  if (gpu) {
+    wait_consts(dev, stream);
+    std::lock_guard<std::mutex> lk(const_mu_);
+    p.last_stream[dev.index()] = stream;
+  }
   for (auto& sc : p.synth_consts) {
     std::lock_guard<std::mutex> lk(const_mu_);
     auto& m = p.dev_consts[dev.is_cuda() ? dev.index() : -1];
@@ -1075,6 +1278,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
   }
   std::vector<at::Tensor> outs;
   for (int s : p.fetch_slots) outs.push_back(slots[s]);
+  stats_.exec_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_exec).count();
   return outs;
 }
 
@@ -1193,11 +1397,26 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
   if (gpu) {
     guard.emplace(inputs[0].device().index());
     stream = c10::hip::getCurrentHIPStream(inputs[0].device().index()).stream();
+    if (!p->stale.empty()) {  // before a replay, which reads the arena without execute()
+      std::lock_guard<std::mutex> lk(const_mu_);
+      if (p->stale.count(inputs[0].device().index())) refresh_consts(*p, inputs[0].device().index(), stream);
+    }
     if (hip_graphs_enabled()) {
       int64_t bytes = 0;
       for (auto& t : inputs) bytes += t.numel() * t.element_size();
       auto& c = p->cap;
       std::lock_guard<std::mutex> lk(c.mu);
+      if (p->cap_reset) {
+        p->cap_reset = false;
+        if (c.graph) {
+          if (c.stream) (void)hipStreamSynchronize(c.stream);
+          c.graph.reset();
+          c.static_in.clear();
+          c.static_out.clear();
+        }
+        c.gpu_runs = 0;
+        c.eager_ns = c.eager_n = c.replay_ns = c.replay_n = 0;
+      }
       const bool same_dev = c.device < 0 || c.device == inputs[0].device().index();
       const bool big_enough = hip_graphs_mode() == 2 || p->steps.size() >= kGraphMinSteps;
       if (!c.failed && !c.declined && same_dev && big_enough && bytes <= hip_graph_max_bytes() && graphable(*p)) {

@@ -32,10 +32,13 @@ struct ExecStats {
   int64_t runs = 0;
   int64_t kernels = 0;
   int64_t plans_built = 0;
+  int64_t plans_adopted = 0;  // plans taken over from a structurally equal program
   int64_t h2d_bytes = 0;
   int64_t d2h_bytes = 0;
   int64_t chunks = 0;
   double h2d_ms = 0, compute_ms = 0, d2h_ms = 0, wall_ms = 0;
+  double plan_ms = 0;     // host time building plans (inference, fusion, kernel choice)
+  double exec_ms = 0;     // host time issuing a plan's steps (launch overhead on a GPU)
   int64_t graphs_captured = 0, graph_replays = 0, graph_failures = 0, graphs_declined = 0;
 };
 
@@ -43,6 +46,7 @@ class Program {
  public:
   Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetches,
           const std::vector<std::string>& feeds);
+  ~Program();
 
   const std::vector<std::string>& fetch_names() const { return fetch_names_; }
   const std::vector<std::string>& feed_names() const { return feed_names_; }
@@ -53,6 +57,16 @@ class Program {
   bool row_separable(const std::map<std::string, TensorInfo>& feed_infos) const;
   // Per-fetch monoid reduction `fetch = Op(placeholder, axis 0)` (empty if not all are).
   std::vector<MonoidInfo> monoids() const;
+
+  // Plan reuse across rebuilt graphs of the same structure (Graph::structure_key):
+  // take over `old`'s plans (step lists, fused kernels, HIP-graph captures and
+  // device constant arenas) for this program's graph, whose parameter
+  // constants may hold different values. Each arena is refreshed in place with
+  // this graph's values by one asynchronous host->device copy before its next
+  // run, so captured graphs stay valid. `old` keeps its own graph and plans
+  // afresh if it runs again (a lazy frame built on it still sees its own
+  // constants). False (nothing moved) when the structures differ.
+  bool adopt(Program& old);
 
   // Run on concrete inputs (all on one device: CPU or a GPU). Returns the fetches.
   std::vector<at::Tensor> run(const std::vector<at::Tensor>& inputs);
@@ -87,8 +101,10 @@ class Program {
   std::shared_ptr<Plan> plan_for(const std::vector<at::Tensor>& inputs);
   std::shared_ptr<Plan> build_plan(const std::vector<at::Tensor>& inputs, bool force_gpu);
   std::vector<at::Tensor> execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream);
-  at::Tensor device_const(Plan& p, int slot, const at::Device& dev);
-  void upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Device& dev);
+  at::Tensor device_const(Plan& p, int slot, const at::Device& dev, void* stream);
+  void upload_consts(Plan& p, std::map<int, at::Tensor>& m, const at::Device& dev, void* stream);
+  void wait_consts(const at::Device& dev, void* stream);
+  void refresh_consts(Plan& p, int di, void* stream);
   bool graphable(const Plan& p) const;
   std::vector<at::Tensor> run_graph(Plan& p, const std::vector<at::Tensor>& inputs);
 
@@ -102,6 +118,9 @@ class Program {
   std::map<std::string, std::shared_ptr<Plan>> plans_;
   std::mutex const_mu_;
   std::map<std::tuple<int, int, int>, at::Tensor> graph_consts_;  // (node, output, device) -> tensor
+  // constants go up with an asynchronous copy on the stream of the run that
+  // needs them first; a run on another stream waits for that copy's event
+  std::map<std::pair<int, void*>, void*> const_events_;  // (device, upload stream) -> hipEvent_t
   ExecStats stats_;
 };
 

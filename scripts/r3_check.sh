@@ -22,7 +22,7 @@ run() {
 for s in ${STEPS:-tests}; do
   case $s in
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
-    newtests) run newtests 600 python -u -m pytest tests/test_groupby.py tests/test_generic_reduce.py tests/test_packer.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    newtests) run newtests 600 python -u -m pytest tests/test_plan_reuse.py tests/test_gpu_engine.py tests/test_models.py tests/test_gpu_models.py tests/test_fusion.py -x -q --timeout 120 --timeout-method thread ;;
     ab) for i in 1 2; do run ab_old_$i 300 python ab_old/scripts/gemm_bench.py --json gpurun_out/ab_old_$i.json; run ab_new_$i 300 python scripts/gemm_bench.py --json gpurun_out/ab_new_$i.json; done ;;
     incep1m) run incep1m 900 python bench/configs.py inception --rows 1000000 --steps 1 --warmup 1 ;;
     incep1m_u8) run incep1m_u8 900 python bench/configs.py inception --rows 1000000 --steps 1 --warmup 1 --input-dtype uint8 ;;
@@ -32,6 +32,8 @@ for s in ${STEPS:-tests}; do
     prof_bench) export TMPDIR=/tmp; run prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_bench" -o run -- python bench.py --steps 3 --warmup 1 ;;
     prof_incep) export TMPDIR=/tmp; run prof_incep 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_incep" -o run -- python bench/configs.py inception --source device --rows 8192 --steps 1 --warmup 1 ;;
     sib) run sib 600 python -u -m pytest tests/test_sibling_fusion.py -x -q --timeout 120 --timeout-method thread ;;
+    kparts) run kparts 300 python scripts/kmeans_parts.py gpurun_out/kparts_cprofile.txt ;;
+    kparts_plan) TFA_PLAN_TIMING=1 run kparts_plan 300 python scripts/kmeans_parts.py ;;
     kmeans) run kmeans 300 python scripts/kmeans_profile.py --iters 50 ;;
     kmeans_cprof) run kmeans_cprof 300 python scripts/kmeans_profile.py --iters 20 --cprofile ;;
     refperf) run refperf 600 python bench/configs.py refperf ;;

@@ -28,6 +28,9 @@ class Config:
     collect_to: str = dataclasses.field(default_factory=lambda: _env("TFA_COLLECT_TO", "all", str))
     # value-preserving algebraic GraphDef rewrites before planning (graph/rewrite.py)
     graph_rewrites: bool = dataclasses.field(default_factory=lambda: _env("TFA_GRAPH_REWRITES", True, bool))
+    # a program for a graph that differs from an earlier one only in the values
+    # of its parameter constants takes over that program's plans (engine.program)
+    plan_reuse: bool = dataclasses.field(default_factory=lambda: _env("TFA_PLAN_REUSE", True, bool))
     # target bytes of one input column per pipelined chunk (host->device->host)
     chunk_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_CHUNK_BYTES", 128 << 20, int))
     # a pipelined job is cut into at least this many chunks (when chunks stay >= 4 MB)

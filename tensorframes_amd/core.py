@@ -12,6 +12,7 @@ as RCCL collectives.
 from __future__ import annotations
 
 import functools
+from collections import OrderedDict
 import os
 import time
 import zlib
@@ -186,12 +187,32 @@ class NodeSummary:
         return sql_type_for_tf(self.tf_dtype)
 
 
+_STRUCT_MEMO: "OrderedDict[tuple, Any]" = OrderedDict()
+
+
+def _structural(what: tuple, graph_bytes: bytes, fn):
+    """Static-analysis results (dtypes, shapes, row separability) memoised by
+    the graph's structure key: a graph rebuilt with new parameter constants
+    (K-Means centres) has the same analysis (Graph::structure_key)."""
+    if not config.plan_reuse:
+        return fn()
+    k = (engine.structure_key(graph_bytes),) + what
+    v = _STRUCT_MEMO.get(k)
+    if v is None:
+        v = fn()
+        _STRUCT_MEMO[k] = v
+        while len(_STRUCT_MEMO) > 256:
+            _STRUCT_MEMO.popitem(last=False)
+    return v
+
+
 def analyze_graph(spec: GraphSpec) -> Dict[str, NodeSummary]:
     """Inputs = every zero-input Placeholder of the graph, outputs = the fetches;
     a shape hint overrides the inferred shape (reference: TensorFlowOps.scala:101-141)."""
     g = engine.native_graph(spec.graph_bytes)
     inputs = list(g.placeholders())
-    infos = _C.analyze_fetches(g, spec.fetch_refs, inputs, {})
+    infos = _structural(("analyze", tuple(spec.fetch_refs)), spec.graph_bytes,
+                        lambda: _C.analyze_fetches(g, spec.fetch_refs, inputs, {}))
     out: Dict[str, NodeSummary] = {}
     for ph in inputs:
         i = infos[ph]
@@ -303,7 +324,9 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
     fetch_refs = [ref_of[o.name] for o in outputs]
     prog = engine.program(spec.graph_bytes, fetch_refs, feed_names)
     hints = {n: (summary[n].tf_dtype, list(_col_info(fields[c]).shape.dims)) for n, c in zip(feed_names, feed_cols)}
-    separable = bool(feed_names) and prog.row_separable(hints)
+    separable = bool(feed_names) and _structural(
+        ("separable", tuple(fetch_refs), tuple(feed_names), repr(sorted(hints.items()))), spec.graph_bytes,
+        lambda: prog.row_separable(hints))
     out_meta = [(o.name, o.tf_dtype, o.shape) for o in outputs]
 
     def compute(blocks: Dict[int, Block]) -> Dict[int, Block]:

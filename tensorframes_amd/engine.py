@@ -74,7 +74,22 @@ def native_graph(graph_bytes: bytes):
     return g
 
 
+_struct_cache: "OrderedDict[tuple, object]" = OrderedDict()
+
+
+def structure_key(graph_bytes: bytes) -> int:
+    """Graph::structure_key of the graph: equal for graphs that differ only
+    in the payloads of parameter constants (e.g. K-Means centres)."""
+    return native_graph(graph_bytes).structure_key()
+
+
 def program(graph_bytes: bytes, fetches: Sequence[str], feeds: Sequence[str]):
+    """The cached program for (graph, fetches, feeds). A new graph with the
+    structure of an earlier one (only parameter constants changed: an
+    iterative workload rebuilding its graph every step, reference
+    kmeans_demo.py:101-168) takes over that program's plans, fused kernels,
+    HIP-graph captures and constant arenas instead of planning again
+    (executor.h Program::adopt); the earlier program stays usable."""
     k = (_key(graph_bytes), tuple(fetches), tuple(feeds))
     with _lock:
         p = _prog_cache.get(k)
@@ -83,6 +98,17 @@ def program(graph_bytes: bytes, fetches: Sequence[str], feeds: Sequence[str]):
             return p
     g = native_graph(_planned_bytes(graph_bytes))
     p = _C.Program(g, list(fetches), list(feeds))
+    if config.plan_reuse:
+        sk = (g.structure_key(), tuple(fetches), tuple(feeds))
+        with _lock:
+            old = _struct_cache.get(sk)
+        if old is not None and p.adopt(old):
+            metrics.add("programs_adopted")
+        with _lock:
+            _struct_cache[sk] = p
+            _struct_cache.move_to_end(sk)
+            while len(_struct_cache) > _MAX_CACHE:
+                _struct_cache.popitem(last=False)
     with _lock:
         _prog_cache[k] = p
         while len(_prog_cache) > _MAX_CACHE:
@@ -115,6 +141,7 @@ def _planned_bytes(graph_bytes: bytes) -> bytes:
 def clear_program_cache():
     with _lock:
         _prog_cache.clear()
+        _struct_cache.clear()
 
 
 # ------------------------------------------------------------------ devices

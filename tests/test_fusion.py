@@ -47,8 +47,12 @@ def test_distance_chain_fetched_is_an_elementwise_region():
     gb, _ = _kmeans_graph()
     prog = engine.program(gb, ["d"], ["features"])
     plan = prog.describe([torch.zeros(1000, 100, dtype=torch.float64)], True)
-    # (the constant t1 = tile(center_squares) is folded on the host at this size)
-    assert "FUSED d [ExpandDims Tile Add Sub Identity]" in plan, plan
+    # t1 = tile(center_squares, [rows, 1]) depends on the fed shape: it is not
+    # folded into a row-sized host constant (graph.cpp kDynFoldLimit) but read
+    # inside the region
+    assert "FUSED d [Tile ExpandDims Tile Add Sub Identity]" in plan, plan
+    small = prog.describe([torch.zeros(40, 100, dtype=torch.float64)], True)
+    assert "FUSED d [ExpandDims Tile Add Sub Identity]" in small, small  # 40x10: folded
 
 
 def test_generated_sources_compile_for_gfx950():

@@ -194,3 +194,30 @@ def test_reduce_blocks_streams_large_host_partitions():
     finally:
         tfs.set_config(chunk_bytes=old)
     np.testing.assert_allclose(s, x.astype(np.float64).sum(0), rtol=1e-4, atol=1e-2)
+
+
+def test_const_upload_is_async_and_ordered_across_streams():
+    """A new program's constants go up asynchronously on the stream of its
+    first run; a run on another stream waits for that copy (executor.cpp
+    upload_consts / wait_consts)."""
+    rng = np.random.default_rng(0)
+    w = rng.standard_normal((256, 256)).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, 256], name="x")
+        tf.matmul(x, tf.constant(w), name="y")
+    prog = engine.program(g.serialize(), ["y"], ["x"])
+    dev = torch.device("cuda", 0)
+    xin = torch.randn(4096, 256, device=dev)
+    big = torch.randn(4096, 4096, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(8):  # keep the side stream busy so its upload lands late
+            big = torch.mm(big, big) * 1e-3
+        y1 = engine.run_program(prog, [xin], dev)[0]
+    y2 = engine.run_program(prog, [xin], dev)[0]  # default stream: ordered after side's upload
+    torch.cuda.synchronize()
+    ref = (xin.double() @ torch.from_numpy(w).double().to(dev)).float()
+    assert torch.allclose(y1, ref, atol=1e-3, rtol=1e-4)
+    assert torch.allclose(y2, ref, atol=1e-3, rtol=1e-4)
