@@ -157,12 +157,15 @@ class Graph:
         return full
 
     # -- nodes
-    def _add(self, node: P.NodeDef, n_out: int, out_dtypes: List[DType]) -> "Operation":
+    def _add(self, node: P.NodeDef, n_out: int, out_dtypes: List[DType],
+             inputs: Optional[List["Tensor"]] = None) -> "Operation":
         with self._lock:
             if node.name in self._ops:
                 raise ValueError(f"Duplicate node name in graph: '{node.name}'")
             self._nodes.append(node)
             op = Operation(self, node, n_out, out_dtypes)
+            if inputs is not None:
+                op._inputs = inputs
             self._ops[node.name] = op
             return op
 
@@ -344,8 +347,9 @@ class Operation:
     def __init__(self, graph: Graph, node: P.NodeDef, n_out: int, out_dtypes: List[DType]):
         self.graph = graph
         self.node_def = node
-        self.outputs = [Tensor(self, i, out_dtypes[i] if i < len(out_dtypes) else None)
-                        for i in _builtins.range(n_out)]
+        self._inputs: Optional[List["Tensor"]] = None  # data inputs, when known at creation
+        nd = len(out_dtypes)
+        self.outputs = [Tensor(self, i, out_dtypes[i] if i < nd else None) for i in _builtins.range(n_out)]
 
     @property
     def name(self) -> str:
@@ -357,6 +361,8 @@ class Operation:
 
     @property
     def inputs(self) -> List["Tensor"]:
+        if self._inputs is not None:
+            return list(self._inputs)
         out = []
         for i in self.node_def.input:
             if not i.startswith("^"):
@@ -563,6 +569,7 @@ def _op(op_type: str, inputs: List[Tuple[str, Any]], attrs: Dict[str, P.AttrValu
     g = _graph_of([v for _, v in inputs])
     op_name = g.unique_name(name or op_type)
     names: List[str] = []
+    tensors: List[Tensor] = []
     g_scope = None
     try:
         for arg, v in inputs:
@@ -570,6 +577,7 @@ def _op(op_type: str, inputs: List[Tuple[str, Any]], attrs: Dict[str, P.AttrValu
                 vals = v
             elif isinstance(v, Tensor):
                 names.append(v.op.node_def.name if v.value_index == 0 else v.name)
+                tensors.append(v)
                 continue
             else:
                 vals = (v,)
@@ -585,11 +593,12 @@ def _op(op_type: str, inputs: List[Tuple[str, Any]], attrs: Dict[str, P.AttrValu
                                     not isinstance(item, np.ndarray) else None,
                                     g.unique_name(nm))
                 names.append(t.op.node_def.name if t.value_index == 0 else t.name)
+                tensors.append(t)
     finally:
         if g_scope is not None:
             g._scope = g_scope
     node = P.NodeDef(op_name, op_type, names, attrs)
-    return g._add(node, n_out, out_dtypes or [])
+    return g._add(node, n_out, out_dtypes or [], tensors)
 
 
 def _first_dtype(*vals) -> Optional[DType]:

@@ -11,11 +11,14 @@ text formatter used by the golden tests.
 from __future__ import annotations
 
 import struct
+import sys
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
 from ..utils import dtypes as D
+
+_LITTLE = sys.byteorder == "little"
 
 _DT_ENUM_NAMES = {
     0: "DT_INVALID", 1: "DT_FLOAT", 2: "DT_DOUBLE", 3: "DT_INT32", 4: "DT_UINT8", 5: "DT_INT16",
@@ -53,6 +56,8 @@ class TensorProto:
             vals = [v if isinstance(v, bytes) else str(v).encode() for v in np.asarray(arr).reshape(-1)]
             return TensorProto(dtype, list(np.shape(arr)), strings=vals)
         a = np.asarray(arr, dtype=D.numpy_dtype(dtype), order="C")
+        if a.dtype.byteorder in ("<", "|") or (a.dtype.byteorder == "=" and _LITTLE):
+            return TensorProto(dtype, list(a.shape), a.tobytes())  # already little-endian: one copy
         return TensorProto(dtype, list(a.shape), a.astype(a.dtype.newbyteorder("<")).tobytes())
 
     def to_numpy(self) -> np.ndarray:
@@ -89,11 +94,17 @@ class AttrValue:
 
     @staticmethod
     def b(v) -> "AttrValue":
-        return AttrValue("b", bool(v))
+        return _B_ATTRS[bool(v)]
 
     @staticmethod
     def type(v) -> "AttrValue":
-        return AttrValue("type", D.as_dtype(v).enum)
+        # shared immutable instances: graphs rebuilt per iteration create
+        # thousands of these (attr values are never mutated in place)
+        e = v.enum if isinstance(v, D.DType) else D.as_dtype(v).enum
+        a = _TYPE_ATTRS.get(e)
+        if a is None:
+            a = _TYPE_ATTRS[e] = AttrValue("type", e)
+        return a
 
     @staticmethod
     def shape(dims: Optional[List[int]]) -> "AttrValue":
@@ -128,6 +139,10 @@ class AttrValue:
 
     def __repr__(self):
         return f"AttrValue({self.kind}={self.value!r})"
+
+
+_TYPE_ATTRS: Dict[int, AttrValue] = {}
+_B_ATTRS = {False: AttrValue("b", False), True: AttrValue("b", True)}
 
 
 class NodeDef:
