@@ -1,0 +1,126 @@
+"""Per-layer f32 conv throughput of Inception-v3 (the BASELINE config-5 model)
+on device-resident tensors: every Conv2D+BiasAdd+Relu of the network, timed
+on its own through the engine (autotuned tile), with its share of the total.
+Shows which layers hold the network below the f32 MFMA peak.
+
+    python scripts/conv_layers.py [--batch 2048] [--image 224] [--json out.json] [--vendor]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tensorframes_amd import engine, tf  # noqa: E402
+from tensorframes_amd.models import cnn  # noqa: E402
+
+F32_PEAK_TF = 157.3
+
+
+def inception_convs(image):
+    """(H, W, C, KH, KW, OC, stride, padding) of every conv, in network order."""
+    seen = []
+    orig = cnn._Builder.conv
+
+    def rec(self, x, out_c, kh, kw, stride=1, padding="SAME", name=None, relu=True, scale_out=True):
+        _, h, w, c = x.get_shape().as_list()
+        oc = self.ch(out_c) if scale_out else out_c
+        seen.append((h, w, c, kh, kw, oc, stride, padding, name))
+        return orig(self, x, out_c, kh, kw, stride, padding, name, relu, scale_out)
+
+    cnn._Builder.conv = rec
+    try:
+        cnn.inception_v3(image_size=image)
+    finally:
+        cnn._Builder.conv = orig
+    return seen
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--vendor", action="store_true", help="also time MIOpen (F.conv2d, channels_last, exact f32)")
+    a = ap.parse_args()
+    torch.backends.cudnn.allow_tf32 = False
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(0)
+    layers = inception_convs(a.image)
+    uniq = {}
+    for l in layers:
+        uniq.setdefault(l[:8], []).append(l[8])
+    res, tot_ms, tot_fl = [], 0.0, 0.0
+    for (h, w, c, kh, kw, oc, s, pad), names in uniq.items():
+        g = tf.Graph()
+        with g.as_default():
+            x = tf.placeholder(tf.float32, [None, h, w, c], name="x")
+            f = tf.constant((rng.standard_normal((kh, kw, c, oc)) * 0.05).astype(np.float32))
+            y = tf.nn.conv2d(x, f, [1, s, s, 1], pad)
+            tf.nn.relu(tf.nn.bias_add(y, tf.constant(np.zeros(oc, np.float32))), name="y")
+        prog = engine.program(g.serialize(), ["y"], ["x"])
+        xin = torch.randn((a.batch, h, w, c), device=dev)
+        engine.run_program(prog, [xin], dev)
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(a.iters):
+            engine.run_program(prog, [xin], dev)
+        ev[1].record()
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / a.iters
+        oh = (h - kh) // s + 1 if pad == "VALID" else (h + s - 1) // s
+        ow = (w - kw) // s + 1 if pad == "VALID" else (w + s - 1) // s
+        fl = 2.0 * a.batch * oh * ow * oc * kh * kw * c
+        n = len(names)
+        tot_ms += ms * n
+        tot_fl += fl * n
+        r = {"layer": names[0], "count": n, "H": h, "W": w, "C": c, "KH": kh, "KW": kw, "OC": oc, "stride": s,
+             "pad": pad, "M": a.batch * oh * ow, "K": kh * kw * c, "ms": ms, "tflops": fl / ms / 1e9}
+        if a.vendor:
+            import torch.nn.functional as F
+            xn = xin.permute(0, 3, 1, 2)
+            wt = torch.randn((oc, c, kh, kw), device=dev).contiguous(memory_format=torch.channels_last)
+            bt = torch.zeros((oc,), device=dev)
+            padding = "same" if pad == "SAME" and s == 1 else 0
+            if pad == "SAME" and s != 1:
+                ph, pw = max((oh - 1) * s + kh - h, 0), max((ow - 1) * s + kw - w, 0)
+                xn = F.pad(xn, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2)).contiguous(
+                    memory_format=torch.channels_last)
+            fn = lambda: torch.relu(F.conv2d(xn, wt, bt, stride=s, padding=padding))  # noqa: E731
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            ev[0].record()
+            for _ in range(a.iters):
+                fn()
+            ev[1].record()
+            torch.cuda.synchronize()
+            vms = ev[0].elapsed_time(ev[1]) / a.iters
+            r.update(vendor_ms=vms, vendor_tflops=fl / vms / 1e9)
+            del xn, wt, bt
+        print(json.dumps(r), flush=True)
+        res.append(r)
+        del xin
+    for r in res:
+        r["share"] = r["ms"] * r["count"] / tot_ms
+    summ = {"batch": a.batch, "image": a.image, "conv_ms_total": tot_ms, "conv_tflops": tot_fl / tot_ms / 1e9,
+            "fraction_of_f32_peak": tot_fl / tot_ms / 1e9 / F32_PEAK_TF,
+            "images_per_s_conv_only": a.batch / tot_ms * 1e3}
+    print(json.dumps(summ), flush=True)
+    for r in sorted(res, key=lambda r: -r["share"])[:15]:
+        print(f"{r['share'] * 100:5.1f}%  {r['tflops']:6.1f} TF  {r['layer']:>14s} x{r['count']}  "
+              f"{r['H']}x{r['W']}x{r['C']} k{r['KH']}x{r['KW']} s{r['stride']} -> {r['OC']}  M={r['M']} K={r['K']}",
+              flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"summary": summ, "layers": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -28,7 +28,7 @@ df = tfs.analyze(tfs.from_columns({"features": pts}, num_partitions=4)).cache_on
 c0 = np.random.default_rng(2).standard_normal((10, 100))
 agg = a.variant == "in_graph"
 kmeans.kmeans(df, c0, num_iters=1, tf_aggregate=agg)  # warm: plans, JIT, tile tuning
-torch.cuda.synchronize()
+torch.cuda.synchronize() if torch.cuda.is_available() else None
 prof = None
 if a.cprofile:
     import cProfile
@@ -38,7 +38,7 @@ t0 = time.perf_counter()
 c = c0
 for _ in range(a.iters):
     c, _d = (kmeans.run_one_step2 if agg else kmeans.run_one_step)(df, c)
-torch.cuda.synchronize()
+torch.cuda.synchronize() if torch.cuda.is_available() else None
 dt = (time.perf_counter() - t0) / a.iters
 if prof is not None:
     import pstats
