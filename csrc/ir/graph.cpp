@@ -1,4 +1,5 @@
 // Graph import, edge resolution, closure and static inference / constant folding.
+#include <unordered_map>
 #include "graph.h"
 
 #include <chrono>
@@ -370,45 +371,22 @@ const std::vector<char>& Graph::parameter_consts() const {
   return params_;
 }
 
-uint64_t Graph::structure_key() const {
-  std::lock_guard<std::mutex> lk(key_mu_);
-  if (key_) return *key_;
-  std::vector<char> param(nodes_.size(), 0);
-  bool any = false;
-  for (size_t i = 0; i < nodes_.size(); ++i) {
-    if (nodes_[i].op != "Const") continue;
-    const AttrValue* v = nodes_[i].def->find_attr("value");
-    if (v && v->kind == AttrValue::TENSOR && v->tensor && dtype_is_float(v->tensor->dtype) &&
-        !v->tensor->shape.unknown_rank && v->tensor->num_elements() >= 2) {
-      param[i] = 1;
-      any = true;
-    }
-  }
-  if (any) {
-    // taint: a folded value computed from a parameter must itself be a
-    // floating tensor of >= 2 elements (never an integer shape/axis/multiple
-    // or a scalar the planner bakes into a kernel)
-    bool safe = true;
-    try {
-      std::vector<TensorRef> all;
-      all.reserve(nodes_.size());
-      for (size_t i = 0; i < nodes_.size(); ++i) all.push_back({static_cast<int>(i), 0});
-      std::vector<int> order = closure(all);
-      Infos inf = infer(order, {}, false);
-      std::vector<char> taint(nodes_.size(), 0);
-      for (int n : order) {
-        bool t = param[n] != 0;
-        for (auto& r : nodes_[n].inputs) t = t || taint[r.node];
-        taint[n] = t;
-        if (!t || param[n]) continue;
-        for (auto& o : inf[n])
-          if (o.value && !(dtype_is_float(o.dtype) && o.value->numel() >= 2)) safe = false;
-      }
-    } catch (const std::exception&) {
-      safe = false;
-    }
-    if (!safe) std::fill(param.begin(), param.end(), 0);
-  }
+namespace {
+// structure hash -> whether its candidate parameter constants are safe to
+// treat as parameters (the taint walk below needs a whole-graph inference;
+// a graph rebuilt every iteration with new parameter values has the same
+// structure hash, so the walk runs once per structure, not per rebuild)
+std::mutex& safe_mu() {
+  static std::mutex m;
+  return m;
+}
+std::unordered_map<uint64_t, bool>& safe_cache() {
+  static std::unordered_map<uint64_t, bool> c;
+  return c;
+}
+}  // namespace
+
+uint64_t Graph::hash_nodes(const std::vector<char>& param) const {
   KeyHash k;
   for (size_t i = 0; i < nodes_.size(); ++i) {
     const NodeDef& d = *nodes_[i].def;
@@ -465,9 +443,70 @@ uint64_t Graph::structure_key() const {
       }
     }
   }
-  params_ = std::move(param);
-  key_ = k.h;
   return k.h;
+}
+
+uint64_t Graph::structure_key() const {
+  std::lock_guard<std::mutex> lk(key_mu_);
+  if (key_) return *key_;
+  std::vector<char> param(nodes_.size(), 0);
+  bool any = false;
+  for (size_t i = 0; i < nodes_.size(); ++i) {
+    if (nodes_[i].op != "Const") continue;
+    const AttrValue* v = nodes_[i].def->find_attr("value");
+    if (v && v->kind == AttrValue::TENSOR && v->tensor && dtype_is_float(v->tensor->dtype) &&
+        !v->tensor->shape.unknown_rank && v->tensor->num_elements() >= 2) {
+      param[i] = 1;
+      any = true;
+    }
+  }
+  uint64_t h = hash_nodes(param);
+  if (any) {
+    bool safe;
+    bool known = false;
+    {
+      std::lock_guard<std::mutex> g(safe_mu());
+      auto it = safe_cache().find(h);
+      if (it != safe_cache().end()) {
+        safe = it->second;
+        known = true;
+      }
+    }
+    if (!known) {
+      // taint: a folded value computed from a parameter must itself be a
+      // floating tensor of >= 2 elements (never an integer shape/axis/multiple
+      // or a scalar the planner bakes into a kernel)
+      safe = true;
+      try {
+        std::vector<TensorRef> all;
+        all.reserve(nodes_.size());
+        for (size_t i = 0; i < nodes_.size(); ++i) all.push_back({static_cast<int>(i), 0});
+        std::vector<int> order = closure(all);
+        Infos inf = infer(order, {}, false);
+        std::vector<char> taint(nodes_.size(), 0);
+        for (int n : order) {
+          bool t = param[n] != 0;
+          for (auto& r : nodes_[n].inputs) t = t || taint[r.node];
+          taint[n] = t;
+          if (!t || param[n]) continue;
+          for (auto& o : inf[n])
+            if (o.value && !(dtype_is_float(o.dtype) && o.value->numel() >= 2)) safe = false;
+        }
+      } catch (const std::exception&) {
+        safe = false;
+      }
+      std::lock_guard<std::mutex> g(safe_mu());
+      if (safe_cache().size() > 4096) safe_cache().clear();
+      safe_cache()[h] = safe;
+    }
+    if (!safe) {
+      std::fill(param.begin(), param.end(), 0);
+      h = hash_nodes(param);
+    }
+  }
+  params_ = std::move(param);
+  key_ = h;
+  return h;
 }
 
 std::vector<int> Graph::placeholders() const {

@@ -179,6 +179,8 @@ class Graph {
   // inference results and plans up to those payloads (reference workload:
   // kmeans_demo.py:68-168 rebuilds its graphs with new centres every step).
   uint64_t structure_key() const;
+  // hash of every node, parameter constants (param[i]) without their payloads
+  uint64_t hash_nodes(const std::vector<char>& param) const;
   // node -> is a parameter constant (as used by structure_key)
   const std::vector<char>& parameter_consts() const;
 

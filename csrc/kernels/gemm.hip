@@ -106,15 +106,20 @@ __device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t co
   act = g.seg.act[s];
 }
 
+// NT = 64 * WM * WN threads: 4-wave blocks (one wave per SIMD per block) or
+// 8-wave blocks (two waves per SIMD sharing one LDS tile: a 256x128 / 256x192
+// block tile at a 64x64 / 64x96 wave tile, half the global traffic per FLOP of
+// a 4-wave 256x64 and half the accumulator registers of a 4-wave 256x128)
 template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
-__global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
-                                                         int64_t k_per_split) {
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 8 ? 2 : (BM * BN > 128 * 192 ? 1 : 2)))
+void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_per_split) {
+  constexpr int NT = 64 * WM * WN;
   constexpr int LDA = BM + 4, LDB = BN + 4;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves, >= one 32x32 tile each");
+  static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves, >= one 32x32 tile each");
   constexpr int KQ = BK / 4;  // float4 pieces along k
   constexpr int APIECES = BM * BK / 4, BPIECES = BN * BK / 4;  // float4 pieces per tile
-  constexpr int AP = (APIECES + 255) / 256, BP = (BPIECES + 255) / 256;
+  constexpr int AP = (APIECES + NT - 1) / NT, BP = (BPIECES + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
 
@@ -139,7 +144,7 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
   if (AL == A_CONV) {
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
-      const int64_t m = m0 + (tid + 256 * p) / KQ;
+      const int64_t m = m0 + (tid + NT * p) / KQ;
       cbase[p] = -1;
       cih[p] = ciw[p] = 0;
       if (m < M) {
@@ -188,8 +193,8 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
     constexpr bool CHECK = decltype(chk)::value;
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
-      const int idx = tid + 256 * p;
-      if (APIECES % 256 != 0 && idx >= APIECES) break;
+      const int idx = tid + NT * p;
+      if (APIECES % NT != 0 && idx >= APIECES) break;
       if (AL == A_MCONTIG) {
         const int kr = idx / (BM / 4), mq = idx % (BM / 4);
         const int64_t gk = k0 + kr, gm = m0 + 4 * mq;
@@ -257,8 +262,8 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
     }
 #pragma unroll
     for (int p = 0; p < BP; ++p) {
-      const int idx = tid + 256 * p;
-      if (BPIECES % 256 != 0 && idx >= BPIECES) break;
+      const int idx = tid + NT * p;
+      if (BPIECES % NT != 0 && idx >= BPIECES) break;
       if (!TB) {  // B [K][N]
         const int kr = idx / (BN / 4), nq = idx % (BN / 4);
         const int64_t gk = k0 + kr, gn = n0 + 4 * nq;
@@ -284,8 +289,8 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
   auto store = [&](int st) {
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
-      const int idx = tid + 256 * p;
-      if (APIECES % 256 != 0 && idx >= APIECES) break;
+      const int idx = tid + NT * p;
+      if (APIECES % NT != 0 && idx >= APIECES) break;
       if (AL == A_MCONTIG) {
         const int kr = idx / (BM / 4), mq = idx % (BM / 4);
         *reinterpret_cast<float4*>(&As[st][kr][4 * mq]) = ra[p];
@@ -299,8 +304,8 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 192 ? 1 : 2)) void gemm_f32_t
     }
 #pragma unroll
     for (int p = 0; p < BP; ++p) {
-      const int idx = tid + 256 * p;
-      if (BPIECES % 256 != 0 && idx >= BPIECES) break;
+      const int idx = tid + NT * p;
+      if (BPIECES % NT != 0 && idx >= BPIECES) break;
       if (!TB) {
         const int kr = idx / (BN / 4), nq = idx % (BN / 4);
         *reinterpret_cast<float4*>(&Bs[st][kr][4 * nq]) = rb[p];
@@ -471,10 +476,15 @@ struct F32Plan {
 // loses on grids of a few hundred blocks
 // {BM, BN}; the N-widths 96/160/192 fit Inception-style channel counts without
 // padding a 128-wide tile (a 128 tile on N=96 computes 25% zeros)
-constexpr int kNumTiles = 13;
+// 13-15 are 8-wave blocks (512 threads). Measured (scripts/tile_ab.sh,
+// profiles/r3_tiles/): the 8-wave 256x128 wins 4096^3 (137.5 TF vs 133.6 for
+// 128x128) and ties the headline 2.5Mx512x512; 256x96 (8x1) and 128x128 (2x4)
+// win some Inception convs. 256x192 and a BK=32 256x128 never won.
+constexpr int kNumTiles = 16;
 constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
                                       {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128},
-                                      {256, 64}, {256, 32}, {256, 96}};
+                                      {256, 64}, {256, 32}, {256, 96}, {256, 128}, {256, 96},
+                                      {128, 128}};
 
 int64_t tile_blocks(int c, int64_t M, int64_t N, int64_t batch) {
   return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
@@ -527,9 +537,10 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
   TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");
   dim3 grid((unsigned)(tm * tn), (unsigned)g.batch, (unsigned)p.splits);
-#define TFA_LAUNCH_TILE(BM_, BN_, WM_, WN_)                                                                  \
-  hipLaunchKernelGGL((gemm_f32_tile<BM_, BN_, WM_, WN_, AL, TB, VEC, kBK>), grid, dim3(256), 0, s, g, (int)tm, \
-                     (int)tn, cg, p.k_per_split)
+#define TFA_LAUNCH_TILE_BK(BM_, BN_, WM_, WN_, BK_)                                                         \
+  hipLaunchKernelGGL((gemm_f32_tile<BM_, BN_, WM_, WN_, AL, TB, VEC, BK_>), grid, dim3(64 * WM_ * WN_), 0, s, g, \
+                     (int)tm, (int)tn, cg, p.k_per_split)
+#define TFA_LAUNCH_TILE(BM_, BN_, WM_, WN_) TFA_LAUNCH_TILE_BK(BM_, BN_, WM_, WN_, kBK)
   switch (p.cfg) {
     case 0: TFA_LAUNCH_TILE(128, 128, 2, 2); break;
     case 1: TFA_LAUNCH_TILE(128, 64, 2, 2); break;
@@ -545,9 +556,14 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     // runs 2 x TN MFMAs per k-step instead of 1 x TN (128x32 / 128x64 / 128x96)
     case 10: TFA_LAUNCH_TILE(256, 64, 4, 1); break;
     case 11: TFA_LAUNCH_TILE(256, 32, 4, 1); break;
-    default: TFA_LAUNCH_TILE(256, 96, 4, 1); break;
+    case 12: TFA_LAUNCH_TILE(256, 96, 4, 1); break;
+    // 8-wave blocks: two waves per SIMD share the block's LDS tile
+    case 13: TFA_LAUNCH_TILE(256, 128, 4, 2); break;
+    case 14: TFA_LAUNCH_TILE(256, 96, 8, 1); break;
+    default: TFA_LAUNCH_TILE(128, 128, 2, 4); break;
   }
 #undef TFA_LAUNCH_TILE
+#undef TFA_LAUNCH_TILE_BK
 }
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }

@@ -474,6 +474,10 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
             dev = _rows_device(cell_views + host_views)
             per_out: List[Any] = [None for _ in outputs]
             whole = vec.run_whole_block(b, feed_cols, per_out) if vec is not None and not host else False
+            if not whole and vec is not None and not host:
+                cols = vec.run_groups_columns(b, cell_views, dev, [dt for _, dt, _ in out_meta])
+                if cols is not None:
+                    per_out, whole = cols, True
             if not whole:
                 per_out = [[None] * b.nrows for _ in outputs]
                 # rows are enqueued back to back; device outputs stay on the GPU until
@@ -501,7 +505,7 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
             host_rows = not any(len(cv) and cv.is_cuda for cv in cell_views)
             cols_out = {}
             for (name, dt, shp), vals in zip(out_meta, per_out):
-                col = vals if isinstance(vals, torch.Tensor) else _stack_cells(vals, dt, shp)
+                col = vals if isinstance(vals, (torch.Tensor, RaggedColumn)) else _stack_cells(vals, dt, shp)
                 if host_rows and isinstance(col, torch.Tensor) and col.is_cuda:
                     col = col.cpu()
                 cols_out[name] = col
@@ -849,6 +853,68 @@ class _RowVectorizer:
             per_out[j] = o
         metrics.add("map_rows_vectorized_rows", b.nrows)
         return True
+
+    def run_groups_columns(self, b: Block, cell_views, dev, out_dtypes: List[int]) -> Optional[List[Any]]:
+        """Ragged blocks, whole-column form: rows grouped by cell shapes with
+        numpy (no per-row tensors), each group stacked by one np.stack and run
+        as one lifted block, and every output assembled with one index copy per
+        group (dense when all groups give the same cell shape, else a
+        RaggedColumn of row views). None when a group cannot be lifted or has
+        one row; the caller then takes the per-row-capable path."""
+        n = b.nrows
+        if n < 2 or any(cv._dense is not None and cv._dense.is_cuda for cv in cell_views):
+            return None
+        arrs = []  # per view: a per-row sequence of numpy cells
+        keys = []
+        for cv in cell_views:
+            if cv._ragged is not None:
+                cells = [np.asarray(c) for c in cv._ragged]
+                arrs.append(cells)
+                keys.append([c.shape for c in cells])
+            else:
+                d = cv._dense.numpy()
+                arrs.append(d)
+                keys.append(None)
+        shape_of = list(zip(*[k if k is not None else [tuple(arrs[j].shape[1:])] * n
+                              for j, k in enumerate(keys)]))
+        groups: Dict[tuple, List[int]] = {}
+        for i, s in enumerate(shape_of):
+            groups.setdefault(s, []).append(i)
+        if any(len(r) < 2 for r in groups.values()):
+            return None
+        results = []
+        for shapes, rows in groups.items():
+            prog = self._program(shapes)
+            if prog is None:
+                return None
+            idx = np.asarray(rows, dtype=np.int64)
+            ins = []
+            for a in arrs:
+                if isinstance(a, np.ndarray):
+                    ins.append(torch.from_numpy(np.ascontiguousarray(a[idx])))
+                else:
+                    ins.append(torch.from_numpy(np.stack([a[i] for i in rows])))
+            outs = engine.run_program(prog, ins, dev)
+            if any(o.dim() == 0 or o.shape[0] != len(rows) for o in outs):
+                return None
+            results.append((idx, outs))
+        cols: List[Any] = []
+        for j in range(len(results[0][1])):
+            cell_shapes = {tuple(o[j].shape[1:]) for _, o in results}
+            first = results[0][1][j]
+            if len(cell_shapes) == 1:
+                out = torch.empty((n,) + tuple(first.shape[1:]), dtype=first.dtype, device=first.device)
+                for idx, o in results:
+                    out[torch.from_numpy(idx).to(out.device)] = o[j]
+                cols.append(out)
+            else:
+                cells: List[Any] = [None] * n
+                for idx, o in results:
+                    for i, r in zip(idx.tolist(), o[j].cpu().numpy()):
+                        cells[i] = r
+                cols.append(RaggedColumn(cells, out_dtypes[j]))
+        metrics.add("map_rows_vectorized_rows", n)
+        return cols
 
     def run_groups(self, b: Block, feed_cols: List[str], cell_views, dev, per_out) -> list:
         """Ragged blocks: rows grouped by cell shapes, each group of >= 2 rows
