@@ -128,6 +128,12 @@ at::Tensor host_key_from_image(const at::Tensor& img, at::ScalarType st) {
 
 }  // namespace
 
+namespace tfa {
+namespace k {
+void set_conv_smallc(int on);  // kernels/conv_smallc.hip
+}  // namespace k
+}  // namespace tfa
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "tensorframes_amd native runtime (GraphDef executor + HIP/CDNA4 kernels)";
 
@@ -522,6 +528,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("get_debug_sync", &get_debug_sync);
   m.def("f32_precision", [] { return k::f32_precision(); });
   m.def("set_gemm_tile", [](int cfg) { k::set_gemm_tile(cfg); });
+  m.def("set_conv_smallc", [](bool on) { k::set_conv_smallc(on ? 1 : 0); },
+        "route tiny-reduction convs (KH*KW*C <= 32) to the direct kernel (default on)");
   m.def("gemm_tile_count", [] { return k::gemm_tile_count(); });
   m.def("roundtrip_graphdef",
         [](py::bytes b) { return py::bytes(serialize_graphdef(parse_graphdef(std::string(b)))); });

@@ -1,0 +1,194 @@
+// Direct f32 Conv2D for tiny reductions (KH*KW*C <= 32: the RGB stem of every
+// CNN, e.g. Inception-v3 Conv2d_1a 3x3x3 -> 32 and VGG-16 conv1_1 3x3x3 -> 64)
+// on v_mfma_f32_32x32x2f32, NHWC input, HWIO filter.
+//
+// The implicit-GEMM core (gemm.hip) stages A/B tiles through LDS in k tiles of
+// 16; with K = 27 that is two k tiles per block, each paying a barrier, a
+// scalar im2col loader with per-element index arithmetic and a full prologue
+// and epilogue for 27 MACs per output. Here:
+//  * the whole filter lives in registers for the kernel's life: lane l holds
+//    W[k = 2s + (l >> 5)][n = 32j + (l & 31)] for every k-step s and column
+//    tile j (the B operand layout of 32x32x2), loaded once per wave;
+//  * the per-lane tap table (k -> filter row/col offset and channel) is in
+//    registers too, so an A element is one bounds test and one global load
+//    from the output pixel's window origin (no LDS, no barriers);
+//  * each wave walks 32-pixel groups grid-stride, two groups in flight, and
+//    writes bias + activation straight from the accumulators.
+// The k order of every output (k-steps of 2, ascending) is the implicit-GEMM
+// core's, so the results are bitwise identical to it (tests/test_gpu_conv_smallc.py).
+#include <atomic>
+#include <cstdlib>
+
+#include "gemm_internal.h"
+#include "hip_common.h"
+
+namespace tfa {
+namespace k {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct SmallConv {
+  int64_t M;  // N * OH * OW output pixels
+  int H, W, C, KW, OH, OW, sh, sw, dh, dw, pt, pl, K, OC;
+  int64_t ldc;
+  const float* x;
+  const float* w;
+  const float* bias;
+  float* y;
+  int act;
+  FastDivU32 fOW, fOH;
+};
+
+template <int KS, int TN>
+__global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5, col = lane & 31;
+  // tap table and filter registers (constant-indexed: fully unrolled)
+  int toff[KS], tdy[KS], tdx[KS];
+  float b[KS][TN];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    if (k < p.K) {
+      const int c = k % p.C, t = k / p.C;
+      tdy[s] = (t / p.KW) * p.dh;
+      tdx[s] = (t % p.KW) * p.dw;
+      toff[s] = (tdy[s] * p.W + tdx[s]) * p.C + c;
+    } else {
+      tdy[s] = 1 << 29;  // never in bounds: the padded k reads 0
+      tdx[s] = 0;
+      toff[s] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = 32 * j + col;
+      b[s][j] = (k < p.K && n < p.OC) ? p.w[(int64_t)k * p.OC + n] : 0.f;
+    }
+  }
+  float bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = 32 * j + col;
+    bv[j] = (p.bias && n < p.OC) ? p.bias[n] : 0.f;
+  }
+
+  const int64_t groups = (p.M + 31) / 32;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // two 32-pixel groups per pass: 2*KS independent loads in flight per lane
+  for (int64_t g0 = 2 * wave0; g0 < groups; g0 += 2 * nwaves) {
+    float a[2][KS];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t m = (g0 + q) * 32 + col;  // A row of this lane = output pixel
+      const bool live = (g0 + q) < groups && m < p.M;
+      const uint32_t mm = live ? (uint32_t)m : 0u;  // M < 2^32 (conv_smallc_eligible)
+      const uint32_t t = fdiv(mm, p.fOW);
+      const int ow = (int)(mm - t * (uint32_t)p.OW);
+      const uint32_t n = fdiv(t, p.fOH);
+      const int oh = (int)(t - n * (uint32_t)p.OH);
+      const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
+      const float* org = p.x + (int64_t)n * p.H * p.W * p.C + ((int64_t)ih0 * p.W + iw0) * p.C;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int ih = ih0 + tdy[s], iw = iw0 + tdx[s];
+        const bool inb = live && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const float v = *(inb ? org + toff[s] : p.x);  // padding taps read a safe address
+        a[q][s] = inb ? v : 0.f;
+      }
+    }
+    f32x16 acc[2][TN];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[q][j][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[q][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][s], b[s][j], acc[q][j], 0, 0, 0);
+    // C/D layout: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (g0 + q >= groups) break;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = 32 * j + col;
+        if (n >= p.OC) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = (g0 + q) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (m < p.M) p.y[m * p.ldc + n] = act_fast(acc[q][j][r] + bv[j], p.act);
+        }
+      }
+    }
+  }
+}
+
+template <int KS>
+void launch_ks(const SmallConv& p, int tn, hipStream_t s) {
+  const int64_t groups = (p.M + 31) / 32;
+  const int64_t waves = (groups + 1) / 2;
+  // enough waves to fill 256 CUs x 8 waves a few times over; grid-stride beyond
+  const int64_t blocks = std::min<int64_t>((waves + 3) / 4, 256 * 16);
+  if (tn == 1)
+    hipLaunchKernelGGL((conv_smallc_kernel<KS, 1>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_smallc_kernel<KS, 2>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+}
+
+// TFA_CONV_SMALLC=0 (or set_conv_smallc(0)) sends these convs to the
+// implicit-GEMM core instead (A/B and the bitwise-equality test)
+std::atomic<int>& smallc_state() {
+  static std::atomic<int> v([] {
+    const char* e = std::getenv("TFA_CONV_SMALLC");
+    return (e && std::atoi(e) == 0) ? 0 : 1;
+  }());
+  return v;
+}
+bool smallc_enabled() { return smallc_state().load() != 0; }
+
+}  // namespace
+
+void set_conv_smallc(int on) { smallc_state().store(on ? 1 : 0); }
+
+bool conv_smallc_eligible(const ConvArgs& a) {
+  const int64_t K = a.KH * a.KW * a.C;
+  return smallc_enabled() && K <= 32 && a.OC <= 64 && a.seg.n == 0 && a.epi.n == 0 &&
+         (a.act == ACT_NONE || a.act == ACT_RELU || a.act == ACT_RELU6) && a.H * a.W * a.C < (int64_t(1) << 30) &&
+         a.N * a.OH * a.OW < (int64_t(1) << 32);
+}
+
+void conv_smallc_launch(const ConvArgs& a, hipStream_t s) {
+  SmallConv p;
+  p.M = a.N * a.OH * a.OW;
+  p.H = (int)a.H; p.W = (int)a.W; p.C = (int)a.C; p.KW = (int)a.KW;
+  p.OH = (int)a.OH; p.OW = (int)a.OW;
+  p.sh = (int)a.sh; p.sw = (int)a.sw; p.dh = (int)a.dh; p.dw = (int)a.dw;
+  p.pt = (int)a.pad_t; p.pl = (int)a.pad_l;
+  p.K = (int)(a.KH * a.KW * a.C);
+  p.OC = (int)a.OC;
+  p.ldc = a.ldc > 0 ? a.ldc : a.OC;
+  p.x = static_cast<const float*>(a.x);
+  p.w = static_cast<const float*>(a.w);
+  p.bias = static_cast<const float*>(a.bias);
+  p.y = static_cast<float*>(a.y);
+  p.act = a.act;
+  p.fOW = make_fastdiv((uint32_t)a.OW);
+  p.fOH = make_fastdiv((uint32_t)a.OH);
+  const int tn = a.OC <= 32 ? 1 : 2;
+  const int ks = (p.K + 1) / 2;
+  if (ks <= 4) launch_ks<4>(p, tn, s);
+  else if (ks <= 8) launch_ks<8>(p, tn, s);
+  else if (ks <= 14) launch_ks<14>(p, tn, s);
+  else launch_ks<16>(p, tn, s);
+  TFA_LAUNCH_CHECK("conv2d small-C");
+}
+
+}  // namespace k
+}  // namespace tfa

@@ -46,6 +46,8 @@ enum ALoad { A_KCONTIG = 0, A_MCONTIG = 1, A_CONV = 2 };
 
 struct ConvGeom {
   int H, W, C, KW, OH, OW, sh, sw, dh, dw, pt, pl;
+  FastDivU32 fOW, fOH;  // row -> (n, oh, ow) without an integer divide (M < 2^32)
+  bool fast = false;
 };
 
 constexpr int kBK = 16;          // k depth of one LDS stage
@@ -148,10 +150,18 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
       cbase[p] = -1;
       cih[p] = ciw[p] = 0;
       if (m < M) {
-        const int64_t ow = m % cg.OW;
-        const int64_t t = m / cg.OW;
-        const int64_t oh = t % cg.OH;
-        const int64_t n = t / cg.OH;
+        int64_t ow, oh, n;
+        if (cg.fast) {  // the 64-bit divide sequence is ~100 VALU ops per piece
+          const uint32_t m32 = (uint32_t)m, t = fdiv(m32, cg.fOW), q = fdiv(t, cg.fOH);
+          ow = m32 - t * (uint32_t)cg.OW;
+          oh = t - q * (uint32_t)cg.OH;
+          n = q;
+        } else {
+          ow = m % cg.OW;
+          const int64_t t = m / cg.OW;
+          oh = t % cg.OH;
+          n = t / cg.OH;
+        }
         cbase[p] = n * (int64_t)cg.H * cg.W * cg.C;
         cih[p] = (int)(oh * cg.sh - cg.pt);
         ciw[p] = (int)(ow * cg.sw - cg.pl);
@@ -163,9 +173,9 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
   // k -> (kh, kw, c) split is computed once and advanced by BK per tile (no divides in the loop)
   int kc = 0, kkw = 0, kkh = 0;
   if (AL == A_CONV && VEC) {
-    const int64_t k = kbeg + 4 * (tid % KQ);
-    kc = (int)(k % cg.C);
-    const int t = (int)(k / cg.C);
+    const int k = (int)(kbeg + 4 * (tid % KQ));  // K < 2^31: 32-bit divides
+    kc = k % cg.C;
+    const int t = k / cg.C;
     kkw = t % cg.KW;
     kkh = t / cg.KW;
   }
@@ -175,9 +185,9 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
   if (AL == A_CONV && !VEC) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int64_t k = kbeg + 4 * (tid % KQ) + j;
-      sc[j] = (int)(k % cg.C);
-      const int t = (int)(k / cg.C);
+      const int k = (int)(kbeg + 4 * (tid % KQ) + j);
+      sc[j] = k % cg.C;
+      const int t = k / cg.C;
       skw[j] = t % cg.KW;
       skh[j] = t / cg.KW;
     }
@@ -220,7 +230,8 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
           const bool inb = cbase[p] >= 0 && (!CHECK || gk < kend) && ih >= 0 && ih < cg.H && iw >= 0 &&
                            iw < cg.W;
           // padding taps load a safe address and are zeroed by a select (branch-free)
-          const float* src = inb ? A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + kc : A;
+          // in-image offset in 32 bits (H*W*C < 2^30, conv2d_nhwc): no 64-bit multiplies per piece
+          const float* src = inb ? A + cbase[p] + ((ih * cg.W + iw) * cg.C + kc) : A;
           const float4 val = *reinterpret_cast<const float4*>(src);
           ra[p] = make_float4(inb ? val.x : 0.f, inb ? val.y : 0.f, inb ? val.z : 0.f, inb ? val.w : 0.f);
         } else {
@@ -229,7 +240,7 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
           for (int j = 0; j < 4; ++j) {
             const int ih = cih[p] + skh[j] * cg.dh, iw = ciw[p] + skw[j] * cg.dw;
             const bool inb = cbase[p] >= 0 && gk + j < kend && ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W;
-            const float* src = inb ? A + cbase[p] + ((int64_t)ih * cg.W + iw) * cg.C + sc[j] : A;
+            const float* src = inb ? A + cbase[p] + ((ih * cg.W + iw) * cg.C + sc[j]) : A;
             const float val = *src;
             sv[j] = inb ? val : 0.f;
           }
@@ -777,6 +788,7 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
   TFA_CHECK(dt == DType::F32, "conv2d: f32 only");
   TFA_CHECK(a.N > 0 && a.OH > 0 && a.OW > 0 && a.OC > 0, "conv2d: empty output");
   TFA_CHECK(a.H < (1 << 30) && a.W < (1 << 30) && a.C < (1 << 30), "conv2d: dims too large");
+  TFA_CHECK(a.H * a.W * a.C < (int64_t(1) << 31), "conv2d: one input image must hold < 2^31 elements");
   GemmArgs g = conv_as_gemm(a);
   // the bf16 modes have no segmented epilogue: fused sibling convs stay exact f32
   if (a.seg.n == 0 && bf16_candidate(g) && bf16_gemm_eligible(g, true, a.C)) {
@@ -788,6 +800,10 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     bf16_gemm_launch(f32_precision(), g, !conv_is_pointwise(a), cg, s);
     return;
   }
+  if (!conv_is_pointwise(a) && conv_smallc_eligible(a)) {  // RGB stems: filter in registers, no LDS
+    conv_smallc_launch(a, s);
+    return;
+  }
   if (conv_is_pointwise(a)) {  // 1x1/s1: x is already the [N*H*W, C] A matrix
     bool vec = al16(a.x) && al16(a.w) && a.C % 4 == 0 && a.OC % 4 == 0;
     run_f32(g, A_KCONTIG, vec, ConvGeom{}, s);
@@ -797,6 +813,9 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     cg.OH = (int)a.OH; cg.OW = (int)a.OW;
     cg.sh = (int)a.sh; cg.sw = (int)a.sw; cg.dh = (int)a.dh; cg.dw = (int)a.dw;
     cg.pt = (int)a.pad_t; cg.pl = (int)a.pad_l;
+    cg.fast = g.M < (int64_t(1) << 32);
+    cg.fOW = make_fastdiv((uint32_t)a.OW);
+    cg.fOH = make_fastdiv((uint32_t)a.OH);
     bool vec = a.C % 4 == 0 && al16(a.x) && al16(a.w) && a.OC % 4 == 0;
     run_f32(g, A_CONV, vec, cg, s);
   }

@@ -17,5 +17,9 @@ struct Im2colGeom {
 size_t bf16_workspace_bytes(int mode, int64_t N, int64_t K);
 bool bf16_gemm_eligible(const GemmArgs& g, bool conv, int64_t conv_c);
 void bf16_gemm_launch(int mode, const GemmArgs& g, bool conv, const Im2colGeom& cg, hipStream_t s);
+// direct small-reduction conv (conv_smallc.hip): KH*KW*C <= 32, OC <= 64,
+// no fused siblings / epilogue chain; bitwise equal to the implicit-GEMM core
+bool conv_smallc_eligible(const ConvArgs& a);
+void conv_smallc_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace k
 }  // namespace tfa

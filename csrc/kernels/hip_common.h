@@ -24,6 +24,27 @@ inline int ew_grid(int64_t work_items, int block = 256, int max_blocks = 256 * 8
   return static_cast<int>(b);
 }
 
+// Division by a launch-constant divisor without the integer-divide sequence
+// (a 64-bit `%`/`/` is ~100 VALU instructions on CDNA; an implicit-GEMM conv
+// decomposes every output-row index into (n, oh, ow)). Round-up magic number:
+// n / d == (umulhi(n, m) + n) >> s for every 32-bit n, d in [1, 2^31)
+// (checked exhaustively on edge cases in tests/test_fastdiv.py).
+struct FastDivU32 {
+  uint32_t d = 1, m = 1, s = 0;
+};
+inline FastDivU32 make_fastdiv(uint32_t d) {
+  FastDivU32 f;
+  f.d = d;
+  f.s = 0;
+  while ((uint64_t(1) << f.s) < d) ++f.s;
+  f.m = static_cast<uint32_t>(((uint64_t(1) << 32) * ((uint64_t(1) << f.s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDivU32& f) {
+  const uint32_t hi = __umulhi(n, f.m);
+  return static_cast<uint32_t>((static_cast<uint64_t>(hi) + n) >> f.s);
+}
+
 // the cheap epilogue activations (none / relu / relu6): kernels branch once
 // on `act` between an epilogue built from this and one built from act_apply,
 // so the transcendental forms do not bloat the common hot epilogue
