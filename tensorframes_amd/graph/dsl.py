@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import builtins as _builtins
 import contextlib
+import struct
 import threading
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
 
@@ -349,7 +350,10 @@ class Operation:
         self.node_def = node
         self._inputs: Optional[List["Tensor"]] = None  # data inputs, when known at creation
         nd = len(out_dtypes)
-        self.outputs = [Tensor(self, i, out_dtypes[i] if i < nd else None) for i in _builtins.range(n_out)]
+        if n_out == 1:
+            self.outputs = [Tensor(self, 0, out_dtypes[0] if nd else None)]
+        else:
+            self.outputs = [Tensor(self, i, out_dtypes[i] if i < nd else None) for i in _builtins.range(n_out)]
 
     @property
     def name(self) -> str:
@@ -507,7 +511,32 @@ class Tensor:
 
 
 # ------------------------------------------------------------------ core builders
+# value attrs of small constants, shared between graphs (TensorProto / AttrValue
+# are never mutated once built): graphs rebuilt per iteration lift the same
+# axes, multiples and scalars every time (K-Means: ~24 of its 53 nodes)
+_CONST_ATTRS: Dict[tuple, Tuple["P.AttrValue", "P.AttrValue", DType]] = {}
+
+
+def _small_const_key(value, dtype) -> Optional[tuple]:
+    tv = type(value)
+    de = None if dtype is None else as_dtype(dtype).enum
+    if tv is int or tv is bool:
+        return (tv, value, de)
+    if tv is float:
+        return (tv, struct.pack("<d", value), de)  # keeps -0.0 and NaN payloads apart
+    if tv is np.ndarray and value.size <= 16 and value.dtype.kind in "iufb":
+        return (tv, value.dtype.str, value.shape, value.tobytes(), de)
+    if isinstance(value, np.generic) and value.dtype.kind in "iufb":
+        return (np.ndarray, value.dtype.str, (), value.tobytes(), de)
+    return None
+
+
 def _const_node(graph: Graph, value, dtype: Optional[DType], name: str, shape=None) -> Tensor:
+    key = _small_const_key(value, dtype) if shape is None else None
+    ent = _CONST_ATTRS.get(key) if key is not None else None
+    if ent is not None:
+        node = P.NodeDef._make(name, "Const", [], {"dtype": ent[0], "value": ent[1]})
+        return graph._add(node, 1, [ent[2]]).outputs[0]
     arr, dt = _to_numpy(value, dtype)
     if shape is not None:
         shape = [int(s) for s in shape]
@@ -516,7 +545,12 @@ def _const_node(graph: Graph, value, dtype: Optional[DType], name: str, shape=No
         else:
             arr = arr.reshape(shape)
     tp = P.TensorProto.from_numpy(arr, dt.enum)
-    node = P.NodeDef(name, "Const", [], {"dtype": P.AttrValue.type(dt), "value": P.AttrValue.tensor(tp)})
+    ta, va = P.AttrValue.type(dt), P.AttrValue.tensor(tp)
+    if key is not None:
+        if len(_CONST_ATTRS) > 4096:
+            _CONST_ATTRS.clear()
+        _CONST_ATTRS[key] = (ta, va, dt)
+    node = P.NodeDef._make(name, "Const", [], {"dtype": ta, "value": va})
     return graph._add(node, 1, [dt]).outputs[0]
 
 
@@ -597,7 +631,7 @@ def _op(op_type: str, inputs: List[Tuple[str, Any]], attrs: Dict[str, P.AttrValu
     finally:
         if g_scope is not None:
             g._scope = g_scope
-    node = P.NodeDef(op_name, op_type, names, attrs)
+    node = P.NodeDef._make(op_name, op_type, names, dict(attrs))
     return g._add(node, n_out, out_dtypes or [], tensors)
 
 

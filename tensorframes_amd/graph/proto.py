@@ -154,6 +154,13 @@ class NodeDef:
         self.attr = dict(attr or {})
         self.device = device
 
+    @classmethod
+    def _make(cls, name: str, op: str, input: List[str], attr: Dict[str, AttrValue]) -> "NodeDef":  # noqa: A002
+        """Internal constructor: takes ownership of `input` / `attr` (no copies)."""
+        n = cls.__new__(cls)
+        n.name, n.op, n.input, n.attr, n.device = name, op, input, attr, ""
+        return n
+
     def __repr__(self):
         return f"NodeDef({self.name!r}, {self.op!r}, inputs={self.input})"
 
