@@ -632,22 +632,34 @@ F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, co
     (void)hipEventDestroy(e0);
     return heur;
   }
-  // two rounds over the candidates, each timed over 3 launches after a warm-up;
-  // a candidate's time is its better round (short kernels are noisy)
+  // Three rounds over the candidates (interleaved, so clock drift hits every
+  // tile alike); a candidate's time is its best round, each round >= ~1 ms of
+  // launches (a 3-launch round of a 0.3 ms conv was noisy enough to keep a
+  // tile 3-5 % off the best; profiles/r3_tiles/)
+  int reps = 3;
+  {
+    launch_plan(heur, g, al, vec, cg, s);  // warm
+    (void)hipEventRecord(e0, s);
+    for (int r = 0; r < 3; ++r) launch_plan(heur, g, al, vec, cg, s);
+    (void)hipEventRecord(e1, s);
+    float ms = 0.f;
+    if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f)
+      reps = std::max(3, std::min(16, (int)std::ceil(1.0f / (ms / 3))));
+  }
   float cand_ms[kNumTiles];
   for (int c = 0; c < kNumTiles; ++c) cand_ms[c] = 1e30f;
-  for (int round = 0; round < 2; ++round) {
+  for (int round = 0; round < 3; ++round) {
     for (int c = 0; c < kNumTiles; ++c) {
       const F32Plan q = plan_for(c, g.M, g.N, g.K, g.batch);
       if (q.splits != 1) continue;
       if (c != heur.cfg && kTiles[c][1] >= 2 * g.N && kTiles[c][1] > 32) continue;  // mostly-padding tile
       if (round == 0) launch_plan(q, g, al, vec, cg, s);  // warm
       (void)hipEventRecord(e0, s);
-      for (int r = 0; r < 3; ++r) launch_plan(q, g, al, vec, cg, s);
+      for (int r = 0; r < reps; ++r) launch_plan(q, g, al, vec, cg, s);
       (void)hipEventRecord(e1, s);
       float ms = 0.f;
       if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
-      cand_ms[c] = std::min(cand_ms[c], ms);
+      cand_ms[c] = std::min(cand_ms[c], ms / reps);
     }
   }
   int best = heur.cfg;
@@ -658,7 +670,7 @@ F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, co
     std::fprintf(stderr, "[gemm tune] M=%lld N=%lld K=%lld al=%d conv=%dx%dx%d heur=%d best=%d |",
                  (long long)g.M, (long long)g.N, (long long)g.K, al, cg.H, cg.W, cg.C, heur.cfg, best);
     for (int c = 0; c < kNumTiles; ++c)
-      if (cand_ms[c] < 1e29f) std::fprintf(stderr, " %d:%.4f", c, cand_ms[c] / 3);
+      if (cand_ms[c] < 1e29f) std::fprintf(stderr, " %d:%.4f", c, cand_ms[c]);
     std::fprintf(stderr, "\n");
   }
   (void)hipEventDestroy(e0);
