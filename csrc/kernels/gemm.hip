@@ -114,7 +114,7 @@ __device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t co
 // a 4-wave 256x64 and half the accumulator registers of a 4-wave 256x128)
 template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 8 ? 2 : (BM * BN > 128 * 192 ? 1 : 2)))
-void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_per_split) {
+void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_per_split, int vepi) {
   constexpr int NT = 64 * WM * WN;
   constexpr int LDA = BM + 4, LDB = BN + 4;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -122,8 +122,13 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
   constexpr int KQ = BK / 4;  // float4 pieces along k
   constexpr int APIECES = BM * BK / 4, BPIECES = BN * BK / 4;  // float4 pieces per tile
   constexpr int AP = (APIECES + NT - 1) / NT, BP = (BPIECES + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
+  // one LDS buffer: the two A/B stages of the main loop, then (vector
+  // epilogue) one 32x36 staging tile per wave
+  constexpr int kStage = 32 * 36;
+  constexpr int kMain = 2 * BK * (LDA + LDB), kEpi = (NT / 64) * kStage;
+  __shared__ __attribute__((aligned(16))) float smem[kMain > kEpi ? kMain : kEpi];
+  float(&As)[2][BK][LDA] = *reinterpret_cast<float(*)[2][BK][LDA]>(smem);
+  float(&Bs)[2][BK][LDB] = *reinterpret_cast<float(*)[2][BK][LDB]>(smem + 2 * BK * LDA);
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -412,6 +417,45 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
   // wrote (re-read from its own stores: small code, no dynamic acc index).
   const bool heavy = !ws && !(g.act <= ACT_RELU6 && g.epi.n == 0);
   float* Cb = static_cast<float*>(g.C) + bz * g.strideC;
+  if (vepi) {
+    // Vector epilogue (single pass, cheap activation, 16-byte aligned rows):
+    // each 32x32 accumulator tile goes through a wave-private LDS tile and
+    // leaves as float4 rows, 4 global_store_dwordx4 per lane instead of 16
+    // scalar stores (the scalar stores cost up to 15 % of a conv layer;
+    // profiles/r3_epilogue/). LDS is free: the main loop ended on a barrier,
+    // and each wave only touches its own staging tile (in-order LDS per wave).
+    float* st = smem + wave * kStage;
+    static_for<TN>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      static_for<TM>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        const f32x16 v = acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 36 + (lane & 31)] = v[r];
+        const int64_t col = n0 + wn * (BN / WN) + j * 32 + 4 * (lane & 7);
+        if (col < N) {
+          float* cbase;
+          int64_t cld;
+          int cact;
+          out_col(g, Cb, col, cbase, cld, cact);
+          float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (bias) bv = make_float4(bias[col], bias[col + 1], bias[col + 2], bias[col + 3]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rr = 8 * q + (lane >> 3);
+            const int64_t row = m0 + wm * (BM / WM) + i * 32 + rr;
+            float4 o = *reinterpret_cast<const float4*>(&st[rr * 36 + 4 * (lane & 7)]);
+            o.x = act_fast(o.x + bv.x, cact);
+            o.y = act_fast(o.y + bv.y, cact);
+            o.z = act_fast(o.z + bv.z, cact);
+            o.w = act_fast(o.w + bv.w, cact);
+            if (row < M) *reinterpret_cast<float4*>(cbase + row * cld) = o;
+          }
+        }
+      });
+    });
+    return;
+  }
   static_for<TN>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     const int64_t col = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
@@ -542,15 +586,37 @@ F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
   return plan_for(cfg, M, N, K, batch);
 }
 
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// the vector epilogue applies: single pass, bias + none/ReLU/ReLU6 only, and
+// every output row segment of 4 columns is 16-byte aligned in one output
+int vector_epilogue(const GemmArgs& g) {
+  static const bool off = [] {
+    const char* e = std::getenv("TFA_GEMM_VEC_EPILOGUE");
+    return e && std::atoi(e) == 0;
+  }();
+  if (off || g.workspace || g.act > ACT_RELU6 || g.epi.n != 0 || g.N % 4 != 0) return 0;
+  if (g.seg.n == 0) {
+    if (!al16(g.C) || g.ldc % 4 != 0 || (g.batch > 1 && g.strideC % 4 != 0)) return 0;
+  } else {
+    for (int q = 0; q < g.seg.n; ++q)
+      if (g.seg.begin[q] % 4 != 0 || g.seg.ldc[q] % 4 != 0 || !al16(g.seg.ptr[q]) || g.seg.act[q] > ACT_RELU6)
+        return 0;
+    if (g.seg.begin[g.seg.n] % 4 != 0) return 0;
+  }
+  return 1;
+}
+
 template <int AL, bool TB, bool VEC>
 void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s) {
+  const int vepi = p.splits == 1 ? vector_epilogue(g) : 0;
   const int64_t tm = (g.M + p.bm - 1) / p.bm, tn = (g.N + p.bn - 1) / p.bn;
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
   TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");
   dim3 grid((unsigned)(tm * tn), (unsigned)g.batch, (unsigned)p.splits);
 #define TFA_LAUNCH_TILE_BK(BM_, BN_, WM_, WN_, BK_)                                                         \
   hipLaunchKernelGGL((gemm_f32_tile<BM_, BN_, WM_, WN_, AL, TB, VEC, BK_>), grid, dim3(64 * WM_ * WN_), 0, s, g, \
-                     (int)tm, (int)tn, cg, p.k_per_split)
+                     (int)tm, (int)tn, cg, p.k_per_split, vepi)
 #define TFA_LAUNCH_TILE(BM_, BN_, WM_, WN_) TFA_LAUNCH_TILE_BK(BM_, BN_, WM_, WN_, kBK)
   switch (p.cfg) {
     case 0: TFA_LAUNCH_TILE(128, 128, 2, 2); break;
@@ -576,8 +642,6 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
 #undef TFA_LAUNCH_TILE
 #undef TFA_LAUNCH_TILE_BK
 }
-
-bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 void launch_plan(const F32Plan& p, const GemmArgs& g, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
 #define TFA_VEC(AL_, TB_) \
