@@ -91,6 +91,10 @@ void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0,
                          std::vector<at::Tensor>& outs, const std::vector<int>& acts);
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
                 int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
+// MaxPool/AvgPool with a fused bias + activation, into `out` (GPU; `out` may
+// be a channel slice of a concat output)
+void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Tensor* bias, int act,
+                    const at::Tensor& out);
 
 // host (ATen) form of a fused epilogue activation (k::Act codes); same
 // formulas as the standalone ops

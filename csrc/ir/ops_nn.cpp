@@ -87,6 +87,34 @@ void rows_batch(InferCtx& c) {
 
 }  // namespace
 
+// planner-fused pool step (GPU): Pool -> BiasAdd -> Relu/Relu6 in one pass,
+// written into `out`, possibly a channel slice of a concat output
+void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Tensor* bias, int act,
+                    const at::Tensor& out) {
+  at::Tensor x = materialize(c, x0);
+  require_gpu_dtype(x, {at::kFloat}, c.node.op.c_str());
+  PoolGeom g = pool_geom(c.node, x.sizes().vec());
+  TFA_CHECK(out.dim() == 4 && out.size(0) == g.N && out.size(1) == g.OH && out.size(2) == g.OW &&
+                out.size(3) == g.C && out.stride(3) == 1 && out.stride(1) == out.stride(2) * g.OW &&
+                out.stride(0) == out.stride(1) * g.OH,
+            "internal: fused pool output layout");
+  if (!out.numel()) return;
+  k::PoolArgs a;
+  a.N = g.N; a.H = g.H; a.W = g.W; a.C = g.C; a.OH = g.OH; a.OW = g.OW;
+  a.KH = g.KH; a.KW = g.KW; a.sh = g.sh; a.sw = g.sw; a.pad_t = g.pt; a.pad_l = g.pl;
+  a.is_max = is_max;
+  a.x = x.data_ptr();
+  a.y = out.data_ptr();
+  if (bias) {
+    TFA_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == g.C,
+              "internal: fused pool bias");
+    a.bias = bias->data_ptr();
+  }
+  a.act = act;
+  a.ldc = out.stride(2) == g.C ? 0 : out.stride(2);
+  k::pool2d_nhwc(DType::F32, a, stream_of(c));
+}
+
 // shared with the planner's fused conv epilogue
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
                 int act, at::Tensor& out, const std::vector<EpiStep>* epi) {

@@ -295,6 +295,7 @@ __global__ __launch_bounds__(256) void pool2d_kernel(PoolArgs a, I n_items) {
   for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
     const I cv = i % CV;
     I t = i / CV;
+    const I pix = t;
     const I ow = t % OW;
     t /= OW;
     const I oh = t % OH;
@@ -319,14 +320,23 @@ __global__ __launch_bounds__(256) void pool2d_kernel(PoolArgs a, I n_items) {
     float* of = reinterpret_cast<float*>(&o);
 #pragma unroll
     for (int j = 0; j < V; ++j) of[j] = MAX ? acc[j] : (cnt > 0 ? acc[j] / (float)cnt : 0.f);
-    *reinterpret_cast<vec_t*>(y + (int64_t)i * V) = o;
+    if (a.bias) {
+      const float* b = static_cast<const float*>(a.bias) + (int64_t)cv * V;
+#pragma unroll
+      for (int j = 0; j < V; ++j) of[j] = act_fast(of[j] + b[j], a.act);
+    } else if (a.act) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) of[j] = act_fast(of[j], a.act);
+    }
+    float* dst = a.ldc ? y + (int64_t)pix * a.ldc + (int64_t)cv * V : y + (int64_t)i * V;
+    *reinterpret_cast<vec_t*>(dst) = o;
   }
 }
 
 template <bool MAX>
 void pool2d_launch(const PoolArgs& a, hipStream_t s) {
   const bool v4 = a.C % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
-                  (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
+                  (reinterpret_cast<uintptr_t>(a.y) & 15) == 0 && a.ldc % 4 == 0;
   const int V = v4 ? 4 : 1;
   const int64_t items = a.N * a.OH * a.OW * (a.C / V);
   const bool small = a.N * a.H * a.W * a.C < (int64_t(1) << 31) && a.N * a.OH * a.OW * a.C < (int64_t(1) << 31);

@@ -212,6 +212,11 @@ struct PoolArgs {
   int64_t N, H, W, C, OH, OW, KH, KW, sh, sw, pad_t, pad_l;
   bool is_max;
   const void* x; void* y;
+  // fused epilogue (planner: Pool -> BiasAdd -> Relu/Relu6) and output pixel
+  // stride (> C: the pool writes its channel slice of a concat output)
+  const void* bias = nullptr;  // [C] f32 or null
+  int act = 0;                 // Act code (none / relu / relu6)
+  int64_t ldc = 0;             // 0 = C
 };
 void pool2d_nhwc(DType dt, const PoolArgs& a, hipStream_t s);
 // image resize, NHWC. mode: 0 legacy (src = dst*scale), 1 align_corners, 2 half_pixel_centers

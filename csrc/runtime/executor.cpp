@@ -95,6 +95,16 @@ bool sibling_fusion_enabled() {
   return on;
 }
 
+// TFA_POOL_FUSION=0: pools keep their own BiasAdd/Relu steps and write
+// their own outputs (no fused epilogue, no concat slice)
+bool pool_fusion_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TFA_POOL_FUSION");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // transposition flags of MatMul (transpose_a/b) and BatchMatMul (adj_x/y)
 bool gemm_ta(const Node& nd) {
   return nd.op == "MatMul" ? nd.attr_b("transpose_a", false) : nd.attr_b("adj_x", false);
@@ -645,6 +655,49 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
       st.gemm_shape = infos[n][0].shape;
       if (cur != n) p->fused++;
     }
+    // ---- fusion (GPU): MaxPool/AvgPool -> BiasAdd [C] -> (Relu | Relu6) in
+    // the pool kernel (Inception's reordered pool branch: 1x1 conv, pool,
+    // bias, relu), so the pooled tensor is written once
+    const bool pool = gpu_plan && pool_fusion_enabled() && (nd.op == "AvgPool" || nd.op == "MaxPool") &&
+                      infos[n][0].dtype == DType::F32 && infos[n][0].shape.fully_known() &&
+                      infos[n][0].shape.rank() == 4 && nd.attr_s("data_format", std::string("NHWC")) == "NHWC";
+    if (pool) {
+      const int64_t ch = infos[n][0].shape.dims.back();
+      auto only = [&](int node) -> int {
+        TensorRef r{node, 0};
+        if (fetched.count(r) || uses[r] != 1 || !consumer.count(node)) return -1;
+        return consumer[node];
+      };
+      int cur = n;
+      int c1 = only(cur);
+      if (c1 >= 0) {
+        const Node& cn = g_->node(c1);
+        if (cn.op == "BiasAdd" && cn.inputs[0] == TensorRef{cur, 0} &&
+            cn.attr_s("data_format", std::string("NHWC")) != "NCHW") {
+          const TensorRef& br = cn.inputs[1];
+          const TensorInfo& bi = infos[br.node][br.index];
+          if (bi.shape.rank() == 1 && bi.shape.dims[0] == ch && bi.dtype == DType::F32 &&
+              infos[c1][0].shape == infos[n][0].shape) {
+            st.bias_ref = br;
+            absorbed.insert(c1);
+            cur = c1;
+          }
+        }
+      }
+      int c2 = only(cur);
+      if (c2 >= 0) {
+        const Node& cn = g_->node(c2);
+        const int act = epilogue_act(cn.op);
+        if ((act == k::ACT_RELU || act == k::ACT_RELU6) && cn.inputs[0] == TensorRef{cur, 0}) {
+          st.act = act;
+          absorbed.insert(c2);
+          cur = c2;
+        }
+      }
+      st.out_node = cur;
+      st.gemm_shape = infos[n][0].shape;
+      if (cur != n) p->fused++;
+    }
     if (st.out_node != n) {
       deferred.emplace(st.out_node, std::move(st));
       continue;
@@ -736,7 +789,10 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
           Step& ps = p->steps[it->second];
           const TensorRef out_ref{ps.out_node, 0};
           const bool single_use = uses[out_ref] == 1 && !fetched.count(out_ref);
-          if ((ps.kind == Step::CONV || ps.kind == Step::GEMM) && single_use && ps.alias_slot < 0 &&
+          const bool pool_step = ps.kind == Step::OP && gpu_plan && pool_fusion_enabled() &&
+                                 (g_->node(ps.node).op == "AvgPool" || g_->node(ps.node).op == "MaxPool") &&
+                                 ps.gemm_shape.rank() == 4;
+          if ((ps.kind == Step::CONV || ps.kind == Step::GEMM || pool_step) && single_use && ps.alias_slot < 0 &&
               ps.out_info[0].dtype == DType::F32 && ps.out_info[0].shape == ps.gemm_shape) {
             ps.alias_slot = cs.out_slots[0];
             ps.alias_offset = off;
@@ -1190,6 +1246,22 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
             if (!st.preplaced[v] && len > 0) gpu_copy(c.in[v], out.narrow(ax, off, len), stream_of(c));
             off += len;
           }
+          c.out[0] = out;
+        } else if (st.kind == Step::OP && gpu && (st.bias_slot >= 0 || st.act || st.alias_slot >= 0) &&
+                   (nd.op == "AvgPool" || nd.op == "MaxPool")) {
+          at::Tensor out;
+          if (st.alias_slot >= 0) {
+            at::Tensor& whole = slots[st.alias_slot];
+            if (!whole.defined())
+              whole = dev_empty(dims_or_throw(st.alias_info->shape, "concat output"), at::kFloat, dev,
+                                static_cast<hipStream_t>(stream));
+            out = whole.narrow(whole.dim() - 1, st.alias_offset, st.out_info[0].shape.dims.back());
+          } else {
+            out = c.alloc_out(0);
+          }
+          at::Tensor bias;
+          if (st.bias_slot >= 0) bias = slots[st.bias_slot].contiguous();
+          run_pool_fused(c, nd.op == "MaxPool", c.in[0], st.bias_slot >= 0 ? &bias : nullptr, st.act, out);
           c.out[0] = out;
         } else if (st.kind == Step::OP) {
           reg.find(nd.op)->compute(c);

@@ -143,8 +143,9 @@ def test_pipeline_stage_device_timers():
 
 def test_concat_write_into_slice_matches_cpu():
     """Inception-style block: conv branches (+bias+relu) concatenated on the
-    channel axis write straight into the concat output; a pooled branch and
-    a reused branch are copied. Result must equal the CPU executor."""
+    channel axis write straight into the concat output, and so does the
+    pooled branch (planner-fused pool); a reused branch is copied. Result
+    must equal the CPU executor."""
     import numpy as np
     from tensorframes_amd import engine, tf
     r = np.random.default_rng(9)
@@ -167,7 +168,7 @@ def test_concat_write_into_slice_matches_cpu():
     x_ = torch.randn((3, 9, 9, 16))
     dev = torch.device("cuda", 0)
     plan = prog.describe([x_.to(dev)])
-    assert plan.count("->concat-slice@") == 2 and "(2 inputs written in place)" in plan
+    assert plan.count("->concat-slice@") == 3 and "(3 inputs written in place)" in plan
     gpu = engine.run_program(prog, [x_.to(dev)], dev)
     cpu = engine.run_program(prog, [x_], torch.device("cpu"))
     for a_, b_ in zip(gpu, cpu):
