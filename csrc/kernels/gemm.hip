@@ -534,7 +534,8 @@ struct F32Plan {
 // 13-15 are 8-wave blocks (512 threads). Measured (scripts/tile_ab.sh,
 // profiles/r3_tiles/): the 8-wave 256x128 wins 4096^3 (137.5 TF vs 133.6 for
 // 128x128) and ties the headline 2.5Mx512x512; 256x96 (8x1) and 128x128 (2x4)
-// win some Inception convs. 256x192 and a BK=32 256x128 never won.
+// win some Inception convs. 256x192, a BK=32 256x128 and BK=32 128x64 /
+// 128x32 (one whole C=32 filter tap per k tile) never won.
 constexpr int kNumTiles = 16;
 constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
                                       {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128},

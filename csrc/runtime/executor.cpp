@@ -798,6 +798,24 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
             ps.alias_offset = off;
             ps.alias_info = &cs.out_info[0];
             cs.preplaced[v] = 1;
+          } else if (ps.kind == Step::OP && g_->node(ps.node).op == "ConcatV2" && single_use &&
+                     ps.alias_slot < 0 && !ps.preplaced.empty() &&
+                     std::all_of(ps.preplaced.begin(), ps.preplaced.end(), [](char c) { return c != 0; }) &&
+                     ps.out_info[0].dtype == DType::F32 && ps.out_info[0].shape.rank() == oi.shape.rank()) {
+            // a nested concat whose inputs were all written in place: its
+            // producers write straight into the outer concat (offset by this
+            // slice), and the inner concat's output is that slice (no copy)
+            const int inner = ps.out_slots[0];
+            for (auto& q : p->steps)
+              if (q.alias_slot == inner) {
+                q.alias_slot = cs.out_slots[0];
+                q.alias_offset += off;
+                q.alias_info = &cs.out_info[0];
+              }
+            ps.alias_slot = cs.out_slots[0];
+            ps.alias_offset = off;
+            ps.alias_info = &cs.out_info[0];
+            cs.preplaced[v] = 1;
           }
         }
         off += len;
@@ -1237,6 +1255,14 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
                       w.size() * sizeof(int64_t), static_cast<hipStream_t>(stream));
         } else if (st.kind == Step::OP && gpu && !st.preplaced.empty()) {
           // concat whose producers wrote in place: copy only the other inputs
+          // (a nested concat's output is itself a slice of the outer concat)
+          if (st.alias_slot >= 0) {
+            at::Tensor& whole = slots[st.alias_slot];
+            if (!whole.defined())
+              whole = dev_empty(dims_or_throw(st.alias_info->shape, "concat output"), at::kFloat, dev,
+                                static_cast<hipStream_t>(stream));
+            slots[st.out_slots[0]] = whole.narrow(whole.dim() - 1, st.alias_offset, st.out_info[0].shape.dims.back());
+          }
           at::Tensor& out = slots[st.out_slots[0]];
           TFA_CHECK(out.defined(), "internal: concat output not allocated by its producers");
           int64_t off = 0;

@@ -89,3 +89,27 @@ def test_pool_branch_written_into_concat_slice():
     want_m = pool_ref(x64, 3, 1, "SAME", True)
     np.testing.assert_allclose(got, np.concatenate([want_a, want_p, want_m], 3), rtol=1e-5, atol=1e-5)
     assert "(3 inputs written in place)" in desc, desc
+
+
+def test_nested_concat_written_in_place():
+    """Inception-v3 Mixed_7b/7c: concat([b0, concat([b1a, b1b]), concat([b2a, b2b]), pool]);
+    the inner concats' producers write straight into the outer concat."""
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, (2, 5, 5, 8)).astype(np.float32)
+    ws = [rng.uniform(-0.3, 0.3, (1, 1, 8, oc)).astype(np.float32) for oc in (12, 8, 4, 16, 20)]
+    g = tf.Graph()
+    with g.as_default():
+        xi = tf.placeholder(tf.float32, [None, 5, 5, 8], name="x")
+        cv = [tf.nn.relu(tf.nn.conv2d(xi, tf.constant(w), [1, 1, 1, 1], "SAME")) for w in ws]
+        y1 = tf.nn.conv2d(cv[1], tf.constant(rng.uniform(-0.3, 0.3, (1, 3, 8, 8)).astype(np.float32)),
+                          [1, 1, 1, 1], "SAME")
+        inner1 = tf.concat([tf.nn.relu(y1), cv[2]], 3)
+        inner2 = tf.concat([cv[3], cv[4]], 3)
+        tf.concat([cv[0], inner1, inner2], 3, name="y")
+    prog = engine.program(g.serialize(), ["y"], ["x"])
+    desc = prog.describe([torch.from_numpy(x)], as_gpu=True)
+    got = engine.run_program(prog, [torch.from_numpy(x)], DEV)[0].cpu().numpy()
+    want = engine.run_program(prog, [torch.from_numpy(x)], torch.device("cpu"))[0].numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
+    assert desc.count("OP   ConcatV2") == 3
+    assert "(3 inputs written in place)" in desc, desc
