@@ -131,6 +131,7 @@ at::Tensor host_key_from_image(const at::Tensor& img, at::ScalarType st) {
 namespace tfa {
 namespace k {
 void set_conv_smallc(int on);  // kernels/conv_smallc.hip
+void set_conv_direct(int on);  // kernels/conv_direct.hip
 }  // namespace k
 }  // namespace tfa
 
@@ -530,6 +531,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemm_tile", [](int cfg) { k::set_gemm_tile(cfg); });
   m.def("set_conv_smallc", [](bool on) { k::set_conv_smallc(on ? 1 : 0); },
         "route tiny-reduction convs (KH*KW*C <= 32) to the direct kernel (default on)");
+  m.def("set_conv_direct", [](bool on) { k::set_conv_direct(on ? 1 : 0); },
+        "route narrow wide-image convs (C in {32, 64}, OC <= 64) to the direct LDS-filter kernel (default on)");
   m.def("gemm_tile_count", [] { return k::gemm_tile_count(); });
   m.def("roundtrip_graphdef",
         [](py::bytes b) { return py::bytes(serialize_graphdef(parse_graphdef(std::string(b)))); });

@@ -881,6 +881,10 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     conv_smallc_launch(a, s);
     return;
   }
+  if (!conv_is_pointwise(a) && conv_direct_eligible(a)) {  // narrow 3x3 stems: filter in LDS, A to registers
+    conv_direct_launch(a, s);
+    return;
+  }
   if (conv_is_pointwise(a)) {  // 1x1/s1: x is already the [N*H*W, C] A matrix
     bool vec = al16(a.x) && al16(a.w) && a.C % 4 == 0 && a.OC % 4 == 0;
     run_f32(g, A_KCONTIG, vec, ConvGeom{}, s);
