@@ -286,20 +286,32 @@ __global__ __launch_bounds__(256) void gemm_int(GemmArgs g) {
 // loads/stores when C % 4 == 0). Index math is 32-bit when the tensors fit
 // (64-bit div/mod costs ~40 VALU ops on CDNA).
 template <bool MAX, int V, typename I>
-__global__ __launch_bounds__(256) void pool2d_kernel(PoolArgs a, I n_items) {
+__global__ __launch_bounds__(256) void pool2d_kernel(PoolArgs a, I n_items, FastDivU32 fCV, FastDivU32 fOW,
+                                                     FastDivU32 fOH) {
   using vec_t = typename std::conditional<V == 4, float4, float>::type;
   const float* x = static_cast<const float*>(a.x);
   float* y = static_cast<float*>(a.y);
   const I CV = (I)(a.C / V), OW = (I)a.OW, OH = (I)a.OH, H = (I)a.H, W = (I)a.W;
   const I stride = (I)gridDim.x * blockDim.x;
   for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
-    const I cv = i % CV;
-    I t = i / CV;
-    const I pix = t;
-    const I ow = t % OW;
-    t /= OW;
-    const I oh = t % OH;
-    const I nn = t / OH;
+    I cv, t, pix, ow, oh, nn;
+    if constexpr (sizeof(I) == 4) {  // 32-bit items: magic-number divides (6 divides per item otherwise)
+      t = fdiv(i, fCV);
+      cv = i - t * CV;
+      pix = t;
+      const I t2 = fdiv(t, fOW);
+      ow = t - t2 * OW;
+      nn = fdiv(t2, fOH);
+      oh = t2 - nn * OH;
+    } else {
+      cv = i % CV;
+      t = i / CV;
+      pix = t;
+      ow = t % OW;
+      t /= OW;
+      oh = t % OH;
+      nn = t / OH;
+    }
     const int h0 = (int)(oh * (I)a.sh) - (int)a.pad_t, w0 = (int)(ow * (I)a.sw) - (int)a.pad_l;
     const int hb = h0 < 0 ? 0 : h0, he = min(h0 + (int)a.KH, (int)H);
     const int wb = w0 < 0 ? 0 : w0, we = min(w0 + (int)a.KW, (int)W);
@@ -341,10 +353,16 @@ void pool2d_launch(const PoolArgs& a, hipStream_t s) {
   const int64_t items = a.N * a.OH * a.OW * (a.C / V);
   const bool small = a.N * a.H * a.W * a.C < (int64_t(1) << 31) && a.N * a.OH * a.OW * a.C < (int64_t(1) << 31);
   const dim3 grid(ew_grid(items)), block(256);
-  if (v4 && small) hipLaunchKernelGGL((pool2d_kernel<MAX, 4, uint32_t>), grid, block, 0, s, a, (uint32_t)items);
-  else if (v4) hipLaunchKernelGGL((pool2d_kernel<MAX, 4, int64_t>), grid, block, 0, s, a, items);
-  else if (small) hipLaunchKernelGGL((pool2d_kernel<MAX, 1, uint32_t>), grid, block, 0, s, a, (uint32_t)items);
-  else hipLaunchKernelGGL((pool2d_kernel<MAX, 1, int64_t>), grid, block, 0, s, a, items);
+  const FastDivU32 fCV = make_fastdiv((uint32_t)(a.C / V)), fOW = make_fastdiv((uint32_t)a.OW),
+                   fOH = make_fastdiv((uint32_t)a.OH);
+  if (v4 && small)
+    hipLaunchKernelGGL((pool2d_kernel<MAX, 4, uint32_t>), grid, block, 0, s, a, (uint32_t)items, fCV, fOW, fOH);
+  else if (v4)
+    hipLaunchKernelGGL((pool2d_kernel<MAX, 4, int64_t>), grid, block, 0, s, a, items, fCV, fOW, fOH);
+  else if (small)
+    hipLaunchKernelGGL((pool2d_kernel<MAX, 1, uint32_t>), grid, block, 0, s, a, (uint32_t)items, fCV, fOW, fOH);
+  else
+    hipLaunchKernelGGL((pool2d_kernel<MAX, 1, int64_t>), grid, block, 0, s, a, items, fCV, fOW, fOH);
 }
 
 }  // namespace
