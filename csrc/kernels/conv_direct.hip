@@ -1,7 +1,7 @@
-// Direct f32 Conv2D for narrow convs on wide images: C in {32, 64} input
-// channels, OC <= 64 output channels, any KHxKW / stride / dilation (the
-// Inception-v3 stem Conv2d_2a 3x3x32 -> 32 and Conv2d_2b 3x3x32 -> 64 on
-// 111x111 / 109x109 images), on v_mfma_f32_32x32x2f32.
+// Direct f32 Conv2D for narrow stem convs: C in {32, 64} input channels,
+// OC <= 96 output channels, any KHxKW (>= 2 taps) / stride / dilation on wide
+// images (the Inception-v3 stem: Conv2d_2a 3x3x32 -> 32 and Conv2d_2b
+// 3x3x32 -> 64 on 111x111 / 109x109 images), on v_mfma_f32_32x32x2f32.
 //
 // The implicit-GEMM core (gemm.hip) streams A through LDS k tile by k tile
 // (16 k = half a 32-channel filter tap per tile, one barrier each) and holds
@@ -172,15 +172,17 @@ void set_conv_direct(int on) { direct_state().store(on ? 1 : 0); }
 
 bool conv_direct_eligible(const ConvArgs& a) {
   if (!direct_state().load()) return false;
-  if (!(a.C == 32 || a.C == 64) || a.OC > 64 || a.OC % 4 != 0 || a.seg.n != 0 || a.epi.n != 0) return false;
+  if (!(a.C == 32 || a.C == 64) || a.OC > 96 || a.OC % 4 != 0 || a.seg.n != 0 || a.epi.n != 0) return false;
   if (!(a.act == ACT_NONE || a.act == ACT_RELU || a.act == ACT_RELU6)) return false;
   const int64_t ldc = a.ldc > 0 ? a.ldc : a.OC;
   if (ldc % 4 != 0 || (reinterpret_cast<uintptr_t>(a.y) & 15) || (reinterpret_cast<uintptr_t>(a.x) & 15)) return false;
   if (a.N * a.OH * a.OW >= (int64_t(1) << 32) || a.H * a.W * a.C >= (int64_t(1) << 31)) return false;
   // wide images only: the direct kernel pays off where the GEMM core streams
-  // many k tiles per 64-byte A segment (the 3x3 stem layers)
-  if (a.OH * a.OW < 4096 || a.KH * a.KW < 2) return false;
-  const int tn = a.OC <= 32 ? 1 : 2;
+  // many k tiles per 64-byte A segment (the 3x3 stem layers); a 1x1 stem
+  // (Conv2d_3b 64 -> 80) is HBM-bound and runs the same on either kernel
+  // (profiles/r3_conv_direct/), so pointwise convs stay on the GEMM core
+  if (a.KH * a.KW < 2 || a.OH * a.OW < 4096) return false;
+  const int tn = (int)((a.OC + 31) / 32);
   return direct_lds_bytes(a.KH * a.KW * a.C, tn) <= 120 * 1024;
 }
 
@@ -201,7 +203,7 @@ void conv_direct_launch(const ConvArgs& a, hipStream_t s) {
   p.fOW = make_fastdiv((uint32_t)a.OW);
   p.fOH = make_fastdiv((uint32_t)a.OH);
   p.fKW = make_fastdiv((uint32_t)a.KW);
-  const int tn = a.OC <= 32 ? 1 : 2;
+  const int tn = (int)((a.OC + 31) / 32);
   const size_t lds = direct_lds_bytes(a.KH * a.KW * a.C, tn);
   const int64_t groups = (p.M + 31) / 32;
   const int per_cu = lds <= 80 * 1024 ? 2 : 1;
@@ -212,10 +214,15 @@ void conv_direct_launch(const ConvArgs& a, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
     hipLaunchKernelGGL((conv_direct_kernel<C8_, TN_>), dim3((unsigned)blocks), dim3(64 * kWaves), lds, s, p); \
   } while (0)
-  if (a.C == 32 && tn == 1) TFA_DIRECT(4, 1);
-  else if (a.C == 32) TFA_DIRECT(4, 2);
-  else if (tn == 1) TFA_DIRECT(8, 1);
-  else TFA_DIRECT(8, 2);
+  if (a.C == 32) {
+    if (tn == 1) TFA_DIRECT(4, 1);
+    else if (tn == 2) TFA_DIRECT(4, 2);
+    else TFA_DIRECT(4, 3);
+  } else {
+    if (tn == 1) TFA_DIRECT(8, 1);
+    else if (tn == 2) TFA_DIRECT(8, 2);
+    else TFA_DIRECT(8, 3);
+  }
 #undef TFA_DIRECT
   TFA_LAUNCH_CHECK("conv2d direct");
 }

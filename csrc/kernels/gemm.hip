@@ -881,7 +881,7 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     conv_smallc_launch(a, s);
     return;
   }
-  if (!conv_is_pointwise(a) && conv_direct_eligible(a)) {  // narrow 3x3 stems: filter in LDS, A to registers
+  if (conv_direct_eligible(a)) {  // narrow stem convs: filter in LDS, A to registers
     conv_direct_launch(a, s);
     return;
   }

@@ -21,7 +21,7 @@ void bf16_gemm_launch(int mode, const GemmArgs& g, bool conv, const Im2colGeom& 
 // no fused siblings / epilogue chain; bitwise equal to the implicit-GEMM core
 bool conv_smallc_eligible(const ConvArgs& a);
 void conv_smallc_launch(const ConvArgs& a, hipStream_t s);
-// direct conv for C in {32, 64}, OC <= 64 on wide images (conv_direct.hip):
+// direct conv for C in {32, 64}, OC <= 96 stem layers (conv_direct.hip):
 // filter in LDS, A straight to registers; chosen by shape only
 bool conv_direct_eligible(const ConvArgs& a);
 void conv_direct_launch(const ConvArgs& a, hipStream_t s);

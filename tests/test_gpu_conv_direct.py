@@ -55,3 +55,28 @@ def test_direct_conv_matches_fp64_and_gemm_core(case):
     want = conv_ref(x.astype(np.float64), f.astype(np.float64), b, s, pad, dil, relu)
     np.testing.assert_allclose(d1, want, rtol=1e-5, atol=2e-5)
     np.testing.assert_allclose(d1, core, rtol=1e-5, atol=2e-5)
+
+
+def test_direct_three_column_tiles():
+    """OC = 80: three 32-column tiles, the last one partial (1x2 filter, C = 64)."""
+    rng = np.random.default_rng(11)
+    n, h, w, c, oc = 8, 70, 70, 64, 80
+    x = rng.uniform(-1, 1, (n, h, w, c)).astype(np.float32)
+    f = (rng.uniform(-1, 1, (1, 2, c, oc)) / 11).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, oc).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        xi = tf.placeholder(tf.float32, [None, h, w, c], name="x")
+        tf.nn.relu(tf.nn.bias_add(tf.nn.conv2d(xi, tf.constant(f), [1, 1, 1, 1], "VALID"), tf.constant(b)), name="y")
+    prog = engine.program(g.serialize(), ["y"], ["x"])
+    xt = torch.from_numpy(x)
+    try:
+        _C.set_conv_direct(True)
+        d = engine.run_program(prog, [xt], DEV)[0].cpu().numpy()
+        _C.set_conv_direct(False)
+        core = engine.run_program(prog, [xt], DEV)[0].cpu().numpy()
+    finally:
+        _C.set_conv_direct(True)
+    want = conv_ref(x.astype(np.float64), f.astype(np.float64), b, 1, "VALID", 1, True)
+    np.testing.assert_allclose(d, want, rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(d, core, rtol=1e-5, atol=2e-5)
