@@ -89,7 +89,7 @@ py::dict infer_all(const std::string& bytes) {
 // -0.0 -> +0.0, negative values' magnitude bits flipped
 template <typename F, typename S>
 at::Tensor key_image_typed(const at::Tensor& keys, at::ScalarType st) {
-  at::Tensor out = at::empty({keys.size(0)}, keys.options().dtype(st));
+  at::Tensor out = pool_empty({keys.size(0)}, keys.options().dtype(st));
   const F* in = keys.data_ptr<F>();
   S* o = out.data_ptr<S>();
   const S flip = std::numeric_limits<S>::max();
@@ -106,7 +106,7 @@ at::Tensor key_image_typed(const at::Tensor& keys, at::ScalarType st) {
 
 template <typename F, typename S>
 at::Tensor key_from_image_typed(const at::Tensor& img, at::ScalarType st) {
-  at::Tensor out = at::empty({img.size(0)}, img.options().dtype(st));
+  at::Tensor out = pool_empty({img.size(0)}, img.options().dtype(st));
   const S* in = img.data_ptr<S>();
   F* o = out.data_ptr<F>();
   const S flip = std::numeric_limits<S>::max();
@@ -354,13 +354,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
     c10::hip::HIPGuard guard(keys.device().index());
     auto opts = keys.options();
-    if (n == 0) return py::make_tuple(at::empty({0}, opts.dtype(at::kLong)), at::empty({0}, opts));
+    if (n == 0) return py::make_tuple(pool_empty({0}, opts.dtype(at::kLong)), pool_empty({0}, opts));
     hipStream_t s = c10::hip::getCurrentHIPStream(keys.device().index()).stream();
     const DType dt = from_scalar_type(keys.scalar_type());
     const size_t wsb = k::factorize_workspace_bytes(dt, n);
-    at::Tensor ws = at::empty({static_cast<int64_t>(wsb)}, opts.dtype(at::kByte));
-    at::Tensor ids = at::empty({n}, opts.dtype(at::kLong));
-    at::Tensor uniq = at::empty({n}, opts);
+    at::Tensor ws = pool_empty({static_cast<int64_t>(wsb)}, opts.dtype(at::kByte));
+    at::Tensor ids = pool_empty({n}, opts.dtype(at::kLong));
+    at::Tensor uniq = pool_empty({n}, opts);
     int64_t nseg = 0;
     {
       py::gil_scoped_release nogil;
@@ -373,21 +373,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     c10::hip::HIPGuard guard(keys[0].device().index());
     const int64_t n = keys[0].size(0);
     hipStream_t s = c10::hip::getCurrentHIPStream(keys[0].device().index()).stream();
-    at::Tensor h = at::empty({n}, keys[0].options().dtype(at::kLong));
+    at::Tensor h = pool_empty({n}, keys[0].options().dtype(at::kLong));
     for (size_t i = 0; i < keys.size(); ++i) {
       at::Tensor kc = keys[i].contiguous();
       TFA_CHECK(kc.dim() == 1 && kc.size(0) == n, "key_dest: key columns must be 1-D of equal length");
       k::key_hash(from_scalar_type(kc.scalar_type()), kc.data_ptr(), n,
                   reinterpret_cast<uint64_t*>(h.data_ptr<int64_t>()), i > 0, s);
     }
-    at::Tensor dest = at::empty({n}, h.options());
+    at::Tensor dest = pool_empty({n}, h.options());
     k::hash_mod(reinterpret_cast<const uint64_t*>(h.data_ptr<int64_t>()), n, world, dest.data_ptr<int64_t>(), s);
     return dest;
   }, "destination rank of every row: hash(keys) % world (same on every rank)");
   m.def("group_representatives", [](const at::Tensor& ids, int64_t nseg) {
     TFA_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.dim() == 1, "group_representatives: device int64 ids");
     c10::hip::HIPGuard guard(ids.device().index());
-    at::Tensor rep = at::empty({nseg}, ids.options());
+    at::Tensor rep = pool_empty({nseg}, ids.options());
     k::group_representatives(ids.contiguous().data_ptr<int64_t>(), ids.size(0), rep.data_ptr<int64_t>(),
                              c10::hip::getCurrentHIPStream(ids.device().index()).stream());
     return rep;
@@ -399,9 +399,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     const int64_t n = dest.size(0);
     hipStream_t s = c10::hip::getCurrentHIPStream(dest.device().index()).stream();
     const size_t wsb = k::partition_workspace_bytes(n);
-    at::Tensor ws = at::empty({static_cast<int64_t>(wsb)}, dest.options().dtype(at::kByte));
-    at::Tensor perm = at::empty({n}, dest.options());
-    at::Tensor counts = at::empty({world}, dest.options());
+    at::Tensor ws = pool_empty({static_cast<int64_t>(wsb)}, dest.options().dtype(at::kByte));
+    at::Tensor perm = pool_empty({n}, dest.options());
+    at::Tensor counts = pool_empty({world}, dest.options());
     k::partition_rows(dest.data_ptr<int64_t>(), n, world, perm.data_ptr<int64_t>(), counts.data_ptr<int64_t>(),
                       ws.data_ptr(), wsb, s);
     return py::make_tuple(perm, counts);
@@ -413,10 +413,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     at::Tensor ids = ids0.contiguous();
     const int64_t n = ids.size(0);
     hipStream_t s = c10::hip::getCurrentHIPStream(ids.device().index()).stream();
-    at::Tensor perm = at::empty({n}, ids.options().dtype(at::kLong));
-    at::Tensor off = at::empty({nseg + 1}, ids.options().dtype(at::kLong));
+    at::Tensor perm = pool_empty({n}, ids.options().dtype(at::kLong));
+    at::Tensor off = pool_empty({nseg + 1}, ids.options().dtype(at::kLong));
     const size_t wsb = k::segment_csr_workspace_bytes(n, nseg);
-    at::Tensor ws = at::empty({static_cast<int64_t>(wsb)}, ids.options().dtype(at::kByte));
+    at::Tensor ws = pool_empty({static_cast<int64_t>(wsb)}, ids.options().dtype(at::kByte));
     k::segment_csr(from_scalar_type(ids.scalar_type()), ids.data_ptr(), n, nseg, perm.data_ptr<int64_t>(),
                    off.data_ptr<int64_t>(), ws.data_ptr(), wsb, s);
     return py::make_tuple(perm, off);
@@ -426,7 +426,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
               "segment_rows: device int64 tensors");
     c10::hip::HIPGuard guard(perm.device().index());
     const int64_t G = offs.size(0);
-    at::Tensor idx = at::empty({G * size}, perm.options());
+    at::Tensor idx = pool_empty({G * size}, perm.options());
     k::segment_rows(perm.contiguous().data_ptr<int64_t>(), offs.contiguous().data_ptr<int64_t>(), G, size,
                     idx.data_ptr<int64_t>(), c10::hip::getCurrentHIPStream(perm.device().index()).stream());
     return idx;
@@ -466,7 +466,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       keep.push_back(t);
     }
     c10::hip::HIPGuard guard(cols[0].device().index());
-    at::Tensor out = at::empty({n, R}, cols[0].options().dtype(at::kByte));
+    at::Tensor out = pool_empty({n, R}, cols[0].options().dtype(at::kByte));
     const int64_t* pp = nullptr;
     at::Tensor pc_t;
     if (perm) {
@@ -505,7 +505,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     at::Tensor x = x0.contiguous();
     auto sizes = x.sizes().vec();
     sizes[0] = idx.size(0);
-    at::Tensor out = at::empty(sizes, x.options());
+    at::Tensor out = pool_empty(sizes, x.options());
     const int64_t inner = x.size(0) ? x.numel() / x.size(0) : 0;
     if (out.numel())
       k::gather(x.element_size(), DType::I64, x.data_ptr(), idx.contiguous().data_ptr(), out.data_ptr(), 1, x.size(0),
@@ -586,14 +586,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       TFA_CHECK(out.is_cuda() && out.is_contiguous() && out.sizes().vec() == osz && out.scalar_type() == xc.scalar_type(),
                 "unsorted_segment_reduce: out must be a contiguous device tensor of the result shape and dtype");
     } else {
-      out = at::empty(osz, xc.options());
+      out = pool_empty(osz, xc.options());
     }
     if (!out.numel()) return out;
     const int64_t inner = out.numel() / nseg;
     const DType dt = from_scalar_type(xc.scalar_type());
     size_t ws = k::unsorted_segment_workspace_bytes(rop, dt, nrows, inner, nseg);
     at::Tensor work;
-    if (ws) work = at::empty({static_cast<int64_t>(ws)}, xc.options().dtype(at::kByte));
+    if (ws) work = pool_empty({static_cast<int64_t>(ws)}, xc.options().dtype(at::kByte));
     k::unsorted_segment_reduce(rop, dt, from_scalar_type(ic.scalar_type()), xc.data_ptr(), ic.data_ptr(),
                                out.data_ptr(), nrows, inner, nseg, ws ? work.data_ptr() : nullptr,
                                c10::hip::getCurrentHIPStream(x.device().index()).stream());
@@ -626,7 +626,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
     c10::hip::HIPGuard guard(x.device().index());
     at::Tensor xc = x.contiguous();
-    at::Tensor out = at::empty(osz, xc.options());
+    at::Tensor out = pool_empty(osz, xc.options());
     int64_t inner = nseg ? out.numel() / nseg : 0;
     if (out.numel())
       k::segment_reduce_csr(rop, from_scalar_type(xc.scalar_type()), xc.data_ptr(),
@@ -660,6 +660,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return d;
   }, "engine-owned device pool: allocations, frees, c10 fallbacks, hipMallocs, live / peak / cached bytes");
   m.def("trim_device_pool", &dev_pool_trim);
+  m.def("device_empty", [](const std::vector<int64_t>& sizes, at::ScalarType dt, int device) {
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+    return pool_empty(sizes, at::TensorOptions().dtype(dt).device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
+  }, py::arg("sizes"), py::arg("dtype"), py::arg("device"),
+        "uninitialised device tensor from the engine pool, ordered on the device's current stream");
+  m.def("record_stream", [](const at::Tensor& t, uint64_t stream) {
+    TFA_CHECK(t.is_cuda(), "record_stream: device tensor expected");
+    dev_record_stream(t, reinterpret_cast<hipStream_t>(stream));
+  }, py::arg("tensor"), py::arg("stream"),
+        "the tensor is also used on `stream` (a hipStream_t handle): its memory (engine pool or c10) is not "
+        "reused before that stream's work queued so far has finished");
   m.def("pinned_pool_stats", [] {
     auto v = pinned_pool_stats();
     py::dict d;

@@ -48,7 +48,7 @@ void gpu_copy(const at::Tensor& src, const at::Tensor& dst, hipStream_t s) {
 at::Tensor materialize(const ExecCtx& c, const at::Tensor& view) {
   if (!c.gpu) return view.contiguous();
   if (view.is_contiguous()) return view;
-  at::Tensor out = at::empty(view.sizes(), view.options());
+  at::Tensor out = pool_empty(view.sizes(), view.options());
   gpu_copy(view, out, stream_of(c));
   return out;
 }
@@ -175,7 +175,7 @@ static at::Tensor strided_view_copy(const ExecCtx& c, const at::Tensor& x, const
   }
   int64_t total = 1;
   for (auto v : vd) total *= v;
-  at::Tensor out = at::empty(vd, xc.options());
+  at::Tensor out = pool_empty(vd, xc.options());
   if (total > 0) {
     if (!c.gpu) {
       // negative strides are not expressible as an ATen view: gather via index math
@@ -558,7 +558,7 @@ void register_array_ops(OpRegistry& r) {
       es.push_back(m[i]); es.push_back(x.size(i));
     }
     at::Tensor v = x.contiguous().reshape(vs).expand(es);
-    at::Tensor out = at::empty(es, x.options());
+    at::Tensor out = pool_empty(es, x.options());
     gpu_copy(v, out, stream_of(c));
     c.out[0] = out.reshape(c.out_shape().dims);
   };

@@ -12,6 +12,7 @@
 #include <algorithm>
 
 #include "../kernels/kernels.h"
+#include "../runtime/device_pool.h"
 #include "graph.h"
 
 namespace tfa {

@@ -182,14 +182,14 @@ OpDef make_space_to_batch() {
     for (int64_t i = 0; i < M; ++i) perm.push_back(1 + 2 * i);  // P_i / b_i
     for (int64_t i = 2 * M + 1; i < static_cast<int64_t>(vsz.size()); ++i) perm.push_back(i);
     if (!c.gpu) {
-      at::Tensor p = at::zeros(psz, x.options());
+      at::Tensor p = pool_zeros(psz, x.options());
       at::Tensor inner = p;
       for (int64_t i = 0; i < M; ++i) inner = inner.narrow(i + 1, g.pads[i].first, x.size(i + 1));
       inner.copy_(x);
       c.out[0] = p.view(vsz).permute(perm).contiguous().reshape(c.out_shape().dims);
       return;
     }
-    at::Tensor p = at::empty(psz, x.options());
+    at::Tensor p = pool_empty(psz, x.options());
     k::fill(dt_of(p), p.data_ptr(), p.numel(), 0.0, stream_of(c));
     at::Tensor inner = p;
     for (int64_t i = 0; i < M; ++i) inner = inner.narrow(i + 1, g.pads[i].first, x.size(i + 1));
@@ -261,7 +261,7 @@ OpDef make_batch_to_space() {
       c.out[0] = crop(moved.contiguous().view(full)).contiguous();
       return;
     }
-    at::Tensor tmp = at::empty(full, x.options());
+    at::Tensor tmp = pool_empty(full, x.options());
     if (tmp.numel()) gpu_copy(moved, tmp.view(moved.sizes()), stream_of(c));
     c.out[0] = c.alloc_out(0);
     if (c.out[0].numel()) gpu_copy(crop(tmp), c.out[0], stream_of(c));
@@ -356,7 +356,7 @@ OpDef make_conv2d_backprop_input() {
     if (!c.out[0].numel()) return;
     // zero buffer [N, H + ekh - 1, W + ekw - 1, OC] with dy scattered at stride (sh, sw)
     const int64_t PH = g.H + ekh - 1, PW = g.W + ekw - 1;
-    at::Tensor buf = at::empty({g.N, PH, PW, g.OC}, dy.options());
+    at::Tensor buf = pool_empty({g.N, PH, PW, g.OC}, dy.options());
     k::fill(DType::F32, buf.data_ptr(), buf.numel(), 0.0, s);
     const int64_t top = ekh - 1 - g.pt, left = ekw - 1 - g.pl;
     if (dy.numel()) {
@@ -366,7 +366,7 @@ OpDef make_conv2d_backprop_input() {
     }
     // W'[kh][kw][oc][ic] = W[KH-1-kh][KW-1-kw][ic][oc] (negative source strides)
     at::Tensor wc = materialize(c, w);
-    at::Tensor wf = at::empty({g.KH, g.KW, g.OC, g.IC}, wc.options());
+    at::Tensor wf = pool_empty({g.KH, g.KW, g.OC, g.IC}, wc.options());
     {
       const int64_t dims[4] = {g.KH, g.KW, g.OC, g.IC};
       const int64_t sst[4] = {-g.KW * g.IC * g.OC, -g.IC * g.OC, 1, g.OC};
@@ -382,7 +382,7 @@ OpDef make_conv2d_backprop_input() {
     a.bias = nullptr; a.act = 0;
     at::Tensor work;
     if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
-      work = at::empty({static_cast<int64_t>(ws)}, buf.options().dtype(at::kByte));
+      work = pool_empty({static_cast<int64_t>(ws)}, buf.options().dtype(at::kByte));
       a.workspace = work.data_ptr();
     }
     k::conv2d_nhwc(DType::F32, a, s);
@@ -405,18 +405,18 @@ OpDef make_l2loss() {
     at::Tensor xc = materialize(c, x);
     const DType dt = dt_of(xc);
     c.out[0] = c.alloc_out(0);
-    at::Tensor sq = at::empty_like(xc);
-    at::Tensor half = at::empty({}, xc.options());
+    at::Tensor sq = pool_empty_like(xc);
+    at::Tensor half = pool_empty({}, xc.options());
     k::fill(dt, half.data_ptr(), 1, 0.5, stream_of(c));
     if (xc.numel() == 0) {
       k::fill(dt, c.out[0].data_ptr(), 1, 0.0, stream_of(c));
       return;
     }
     k::unary(k::UnOp::SQUARE, dt, xc.data_ptr(), sq.data_ptr(), xc.numel(), stream_of(c));
-    at::Tensor s = at::empty({}, xc.options());
+    at::Tensor s = pool_empty({}, xc.options());
     size_t ws = k::reduce_workspace_bytes(dt, 1, xc.numel(), 1);
     at::Tensor work;
-    if (ws) work = at::empty({static_cast<int64_t>(ws)}, xc.options().dtype(at::kByte));
+    if (ws) work = pool_empty({static_cast<int64_t>(ws)}, xc.options().dtype(at::kByte));
     k::reduce(k::RedOp::SUM, dt, sq.data_ptr(), s.data_ptr(), 1, xc.numel(), 1, ws ? work.data_ptr() : nullptr,
               stream_of(c));
     k::binary(k::BinOp::MUL, dt, s.data_ptr(), half.data_ptr(), c.out[0].data_ptr(), 1, 1, 1, nullptr,
@@ -434,17 +434,17 @@ void xent_gpu(ExecCtx& c, const at::Tensor& feat, const at::Tensor& labels_dense
   c.out[0] = c.alloc_out(0);
   c.out[1] = c.alloc_out(1);
   if (B == 0) return;
-  at::Tensor lsm = at::empty_like(feat);
+  at::Tensor lsm = pool_empty_like(feat);
   k::softmax(dt, true, feat.data_ptr(), lsm.data_ptr(), B, C, s);
-  at::Tensor prod = at::empty_like(feat);
+  at::Tensor prod = pool_empty_like(feat);
   k::binary(k::BinOp::MUL, dt, labels_dense.data_ptr(), lsm.data_ptr(), prod.data_ptr(), B * C, 0, 1, nullptr, s);
-  at::Tensor neg = at::empty({B}, feat.options());
+  at::Tensor neg = pool_empty({B}, feat.options());
   size_t ws = k::reduce_workspace_bytes(dt, B, C, 1);
   at::Tensor work;
-  if (ws) work = at::empty({static_cast<int64_t>(ws)}, feat.options().dtype(at::kByte));
+  if (ws) work = pool_empty({static_cast<int64_t>(ws)}, feat.options().dtype(at::kByte));
   k::reduce(k::RedOp::SUM, dt, prod.data_ptr(), neg.data_ptr(), B, C, 1, ws ? work.data_ptr() : nullptr, s);
   k::unary(k::UnOp::NEG, dt, neg.data_ptr(), c.out[0].data_ptr(), B, s);
-  at::Tensor sm = at::empty_like(feat);
+  at::Tensor sm = pool_empty_like(feat);
   k::softmax(dt, false, feat.data_ptr(), sm.data_ptr(), B, C, s);
   k::binary(k::BinOp::SUB, dt, sm.data_ptr(), labels_dense.data_ptr(), c.out[1].data_ptr(), B * C, 0, 1, nullptr, s);
 }
@@ -497,7 +497,7 @@ OpDef make_xent(bool sparse) {
     at::Tensor dense;
     if (sparse) {
       at::Tensor lc = materialize(c, l);
-      dense = at::empty_like(fc);
+      dense = pool_empty_like(fc);
       if (fc.numel())
         k::one_hot(dt_of(fc), dt_of(lc), lc.data_ptr(), dense.data_ptr(), fc.size(0), fc.size(1), 1.0, 0.0,
                    stream_of(c));

@@ -114,6 +114,9 @@ void drain_pending(State& S) {
 // caller holds the lock: hipFree every cached block of `device` (after the
 // device's queued work), to make room
 void trim_device(State& S, int device) {
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != device) (void)hipSetDevice(device);
   (void)hipDeviceSynchronize();
   for (auto it = S.free.begin(); it != S.free.end(); ++it) {
     if (it->first.first != device) continue;
@@ -124,6 +127,21 @@ void trim_device(State& S, int device) {
     }
     it->second.clear();
   }
+  if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+}
+
+// best fit: the smallest cached block of at least `want` bytes, if it wastes
+// at most half of `want` (a neighbouring size class serves a request instead
+// of a fresh hipMalloc: chunk tails and ragged batches vary in size)
+Block* take_best_fit(State& S, int device, hipStream_t stream, size_t want) {
+  auto fit = S.free.find({device, stream});
+  if (fit == S.free.end()) return nullptr;
+  auto it = fit->second.lower_bound(want);
+  if (it == fit->second.end() || it->first > want + want / 2) return nullptr;
+  Block* b = it->second;
+  fit->second.erase(it);
+  S.cached -= b->size;
+  return b;
 }
 
 void release(Block* b) {
@@ -188,29 +206,28 @@ at::Tensor dev_empty(at::IntArrayRef sizes, at::ScalarType dt, const at::Device&
     if (dev.is_cuda()) g_fallbacks++;
     return at::empty(sizes, opts);
   }
+  dev_pool_install_oom_hook();  // once; the framework allocator is initialised by now
   int64_t n = 1;
   for (int64_t s : sizes) n *= s;
   const size_t want = size_class(static_cast<size_t>(std::max<int64_t>(n, 1)) * c10::elementSize(dt));
   State& S = st();
   Block* b = nullptr;
   {
-    std::lock_guard<std::mutex> lk(S.mu);
+    std::unique_lock<std::mutex> lk(S.mu);
     if (!S.pending.empty()) drain_pending(S);
-    auto fit = S.free.find({dev.index(), stream});
-    if (fit != S.free.end()) {
-      auto it = fit->second.find(want);
-      if (it != fit->second.end()) {
-        b = it->second;
-        fit->second.erase(it);
-        S.cached -= b->size;
-      }
-    }
+    b = take_best_fit(S, dev.index(), stream, want);
     if (!b) {
       void* p = nullptr;
       hipError_t e = hipMalloc(&p, want);
       if (e != hipSuccess) {
+        // out of memory: give back our own cache, then the framework
+        // allocator's (outside our lock: c10's OOM observer takes it), and
+        // retry once
         (void)hipGetLastError();
         trim_device(S, dev.index());
+        lk.unlock();
+        c10::hip::HIPCachingAllocator::emptyCache();
+        lk.lock();
         e = hipMalloc(&p, want);
       }
       if (e != hipSuccess || !p) {
@@ -259,6 +276,40 @@ at::Tensor dev_clone(const at::Tensor& t, hipStream_t stream) {
   if (nb) TFA_CHECK(hipMemcpyAsync(o.data_ptr(), t.data_ptr(), nb, hipMemcpyDeviceToDevice, stream) == hipSuccess,
                     "dev_clone: hipMemcpyAsync failed");
   return o;
+}
+
+at::Tensor pool_empty(at::IntArrayRef sizes, const at::TensorOptions& opts) {
+  if (!opts.device().is_cuda()) return at::empty(sizes, opts);
+  const int d = opts.device().has_index() ? opts.device().index() : c10::hip::current_device();
+  at::Device dev(at::kCUDA, static_cast<c10::DeviceIndex>(d));
+  return dev_empty(sizes, opts.dtype().toScalarType(), dev, c10::hip::getCurrentHIPStream(d).stream());
+}
+
+at::Tensor pool_empty_like(const at::Tensor& t) { return pool_empty(t.sizes(), t.options()); }
+
+at::Tensor pool_zeros(at::IntArrayRef sizes, const at::TensorOptions& opts) {
+  at::Tensor t = pool_empty(sizes, opts);
+  if (t.is_cuda()) {
+    const size_t nb = t.numel() * t.element_size();
+    if (nb) TFA_CHECK(hipMemsetAsync(t.data_ptr(), 0, nb, c10::hip::getCurrentHIPStream(t.device().index()).stream()) ==
+                          hipSuccess, "pool_zeros: hipMemsetAsync failed");
+    return t;
+  }
+  return t.zero_();
+}
+
+void dev_pool_install_oom_hook() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    // c10 calls observers before it raises OutOfMemoryError: hand our cached
+    // blocks back so the caller's retry (or the next allocation) finds room
+    c10::hip::HIPCachingAllocator::attachOutOfMemoryObserver(
+        [](int64_t device, size_t, size_t, size_t) {
+          State& S = st();
+          std::lock_guard<std::mutex> lk(S.mu);
+          trim_device(S, static_cast<int>(device));
+        });
+  });
 }
 
 DevPoolStats dev_pool_stats() {

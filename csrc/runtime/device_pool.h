@@ -23,6 +23,12 @@ at::Tensor dev_empty_like(const at::Tensor& t, hipStream_t stream);
 void dev_record_stream(const at::Tensor& t, hipStream_t s);
 // D2D copy of a contiguous tensor into fresh pool memory (hipMemcpyAsync)
 at::Tensor dev_clone(const at::Tensor& t, hipStream_t stream);
+// at::empty for op temporaries: device tensors come from the pool, ordered
+// on the device's CURRENT HIP stream (where the calling op launches); host
+// tensors from at::empty
+at::Tensor pool_empty(at::IntArrayRef sizes, const at::TensorOptions& opts);
+at::Tensor pool_empty_like(const at::Tensor& t);
+at::Tensor pool_zeros(at::IntArrayRef sizes, const at::TensorOptions& opts);
 
 struct DevPoolStats {
   int64_t allocs = 0, frees = 0, fallbacks = 0, device_mallocs = 0;
@@ -30,6 +36,9 @@ struct DevPoolStats {
 };
 DevPoolStats dev_pool_stats();
 void dev_pool_trim();  // hipFree every cached block (after a device sync)
+// hooks the framework allocator's out-of-memory path: when c10 runs out of
+// device memory it first gets the pool's cached blocks back (idempotent)
+void dev_pool_install_oom_hook();
 // the engine's HIP-graph capture on `s` starts / ends: allocations on a
 // capturing stream go to the capture's private (framework) pool
 void dev_capture_begin(hipStream_t s);

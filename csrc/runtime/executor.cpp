@@ -1104,8 +1104,14 @@ bool Program::adopt(Program& old) {
   if (!host_op_error_.empty() || !old.host_op_error_.empty()) return false;
   std::scoped_lock lk(mu_, old.mu_, const_mu_, old.const_mu_);
   if (!plans_.empty()) return false;
-  for (auto& kv : old.plans_)
+  for (auto& kv : old.plans_) {
     if (!kv.second->synth_consts.empty()) return false;  // plan-made constants derive from the weights
+    // a run of the old program still holds this plan (in flight, or about to
+    // execute on another thread): its constants must not change under it.
+    // Under old.mu_ no new reference can be handed out, so a count of one
+    // means the map's is the only one.
+    if (kv.second.use_count() != 1) return false;
+  }
   // new values of every constant slot (the same nodes: equal structure);
   // shapes and dtypes must match (the parameter rule guarantees it)
   std::vector<std::pair<std::shared_ptr<Plan>, Graph::Infos>> fresh;
@@ -1548,6 +1554,17 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
   return outs;
 }
 
+// The pipeline rings come from pool blocks cached for the compute stream:
+// compute-stream work queued before this call (an earlier partition's last
+// chunk) may still read them. The copy stream's first writes wait for it.
+static void order_copy_after_compute(hipStream_t copy, hipStream_t compute) {
+  hipEvent_t e;
+  HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(e, compute));
+  HIP_OK(hipStreamWaitEvent(copy, e, 0));
+  HIP_OK(hipEventDestroy(e));
+}
+
 void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
                           const std::vector<std::vector<at::Tensor>>& seg_outputs,
                           int64_t chunk_rows, int device, int depth) {
@@ -1594,6 +1611,7 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
       sz[0] = chunk_rows;
       ring[d].push_back(dev_empty(sz, seg_inputs[0][i].scalar_type(), dev, compute.stream()));
     }
+  order_copy_after_compute(h2d.stream(), compute.stream());
   std::vector<hipEvent_t> ev_h2d(depth), ev_comp(depth), ev_d2h(depth);
   for (int d = 0; d < depth; ++d) {
     HIP_OK(hipEventCreateWithFlags(&ev_h2d[d], hipEventDisableTiming));
@@ -1725,6 +1743,7 @@ std::vector<at::Tensor> Program::run_chunked_reduce(const std::vector<std::vecto
       sz[0] = chunk_rows;
       ring[d].push_back(dev_empty(sz, seg_inputs[0][i].scalar_type(), dev, compute.stream()));
     }
+  order_copy_after_compute(h2d.stream(), compute.stream());
   std::vector<hipEvent_t> ev_h2d(depth), ev_comp(depth);
   for (int d = 0; d < depth; ++d) {
     HIP_OK(hipEventCreateWithFlags(&ev_h2d[d], hipEventDisableTiming));

@@ -712,7 +712,10 @@ class _BatchCut:
                         feeds = [f.pin_memory().to(dev, non_blocking=True) if f.device.type == "cpu" else f
                                  for f in feeds]
                         c = engine.run_program(self.pre, feeds, dev)[0]
-                    c.record_stream(main)
+                    # c is engine-pool memory (side stream): the batched
+                    # part reads it on main, so it must not be recycled by the
+                    # next batch's per-row runs before main got there
+                    engine.record_stream(c, main)
                 else:
                     c = engine.run_program(self.pre, feeds, dev)[0]
                 cut.append(c)
@@ -903,7 +906,7 @@ class _RowVectorizer:
             cell_shapes = {tuple(o[j].shape[1:]) for _, o in results}
             first = results[0][1][j]
             if len(cell_shapes) == 1:
-                out = torch.empty((n,) + tuple(first.shape[1:]), dtype=first.dtype, device=first.device)
+                out = engine.device_empty((n,) + tuple(first.shape[1:]), first.dtype, first.device)
                 for idx, o in results:
                     out[torch.from_numpy(idx).to(out.device)] = o[j]
                 cols.append(out)
@@ -1158,7 +1161,7 @@ def _combine_monoids(partials: Dict[str, List[torch.Tensor]], ops: Dict[str, str
         sizes = [int(np.prod(shapes[n])) if shapes[n] else 1 for n in names]
         # one buffer per (op, dtype): the partials by device DMA, the has-data
         # flag (and a data-less rank's identities) by one small host copy
-        buf = torch.empty(sum(sizes) + 1, dtype=tdt, device=dev)
+        buf = engine.device_empty(sum(sizes) + 1, tdt, dev)
         off = 0
         for n, k in zip(names, sizes):
             v = local[n]
@@ -1200,7 +1203,7 @@ def _gather_rank_values(local: Dict[str, Optional[torch.Tensor]], static: Dict[s
     out = {}
     for n in names:
         tdt = D.torch_dtype(dtypes[n])
-        v = local[n].to(dev) if local[n] is not None else torch.zeros(shapes[n], dtype=tdt, device=dev)
+        v = local[n].to(dev) if local[n] is not None else engine.device_zeros(shapes[n], tdt, dev)
         allv = dist.all_gather_tensor(v.to(tdt).contiguous())
         out[n] = [allv[r] for r in range(allv.shape[0]) if int(flags[r])]
     return out
@@ -1245,7 +1248,7 @@ def _to_host_batched(vals: Dict[str, torch.Tensor]) -> Dict[str, np.ndarray]:
 
 def _identity(op: str, shape, dtype, dev) -> torch.Tensor:
     if op == "Sum":
-        return torch.zeros(shape, dtype=dtype, device=dev)
+        return engine.device_zeros(shape, dtype, dev)
     if op == "Prod":
         return torch.ones(shape, dtype=dtype, device=dev)
     info = torch.finfo(dtype) if dtype.is_floating_point else torch.iinfo(dtype)
@@ -1609,7 +1612,7 @@ def _shuffle_blocks(send: List[List[Block]], names: List[str], tf_types: Dict[st
         if kinds[n] is not None:
             dtype, cell = kinds[n]
             chunks = [p.columns[n].to(dev) if p is not None and p.nrows else
-                      torch.empty((0,) + cell, dtype=dtype, device=dev) for p in per]
+                      engine.device_empty((0,) + cell, dtype, dev) for p in per]
             cols[n] = dist.all_to_all_tensors(chunks, recv_rows)
         else:
             got = dist.all_to_all_objects([column_values(p.columns[n]) if p is not None and p.nrows else []
@@ -1654,7 +1657,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             dev.type == "cuda"
         parts = [b for _, b in sorted(blocks.items()) if b.nrows]
         kdt = [D.torch_dtype(tf_types[k]) for k in keys]
-        K: List[torch.Tensor] = [torch.empty(0, dtype=t, device=dev) for t in kdt]
+        K: List[torch.Tensor] = [engine.device_empty(0, t, dev) for t in kdt]
         V: Dict[str, Optional[torch.Tensor]] = {n: None for n in out_names}
         if parts:
             # this rank's keys are factorised ONCE over all its partitions
@@ -1668,7 +1671,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 if len(parts) == 1:
                     V[n] = _C.unsorted_segment_reduce(monoid[n], vals[0], ids, ng)
                     continue
-                stacked = torch.empty((len(parts), ng) + tuple(vals[0].shape[1:]), dtype=vals[0].dtype, device=dev)
+                stacked = engine.device_empty((len(parts), ng) + tuple(vals[0].shape[1:]), vals[0].dtype, dev)
                 for p, v in enumerate(vals):
                     _C.unsorted_segment_reduce(monoid[n], v, ids[int(bounds[p]):int(bounds[p + 1])], ng,
                                                out=stacked[p])
@@ -1689,7 +1692,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 {n: tuple(V[n].shape[1:]) for n in out_names}
             for n in out_names:
                 if V[n] is None:
-                    V[n] = torch.empty((0,) + tuple(cells[n]), dtype=D.torch_dtype(summary[n].tf_dtype), device=dev)
+                    V[n] = engine.device_empty((0,) + tuple(cells[n]), D.torch_dtype(summary[n].tf_dtype), dev)
             recv = G.route(K, [V[n] for n in out_names])
             K, V = recv[:len(keys)], dict(zip(out_names, recv[len(keys):]))
         if K[0].shape[0] == 0:
@@ -1777,9 +1780,9 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             K = [engine.cat_rows([b.columns[k].to(dev) for b in parts]) for k in keys]
             V = [engine.cat_rows([b.columns[n].to(dev).contiguous() for b in parts]) for n in out_names]
         else:
-            K = [torch.empty(0, dtype=t, device=dev) for t in kdt]
+            K = [engine.device_empty(0, t, dev) for t in kdt]
             cells = {n: agg_static_in.get(n) for n in out_names}
-            V = [torch.empty((0,) + tuple(cells[n] or ()), dtype=D.torch_dtype(summary[n].tf_dtype), device=dev)
+            V = [engine.device_empty((0,) + tuple(cells[n] or ()), D.torch_dtype(summary[n].tf_dtype), dev)
                  for n in out_names]
         if dist.is_distributed():
             recv = G.route(K, V)
@@ -1800,7 +1803,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             for n, o in zip(out_names, outs):
                 o = o.to(dev)
                 if out[n] is None:
-                    out[n] = torch.empty((ng,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev)
+                    out[n] = engine.device_empty((ng,) + tuple(o.shape[1:]), o.dtype, dev)
                 _C.scatter_rows(out[n], gidx, o)
 
         for size, gl in sorted(by_size.items()):

@@ -180,17 +180,43 @@ def empty_host(shape, dtype: torch.dtype, pinned: bool) -> torch.Tensor:
     return torch.empty(tuple(shape), dtype=dtype)
 
 
+def device_empty(shape, dtype: torch.dtype, device) -> torch.Tensor:
+    """Uninitialised tensor; on a GPU it comes from the engine's own
+    stream-ordered pool (csrc/runtime/device_pool.cpp), ordered on the
+    device's current stream, instead of the framework allocator."""
+    device = torch.device(device)
+    if isinstance(shape, int):
+        shape = (shape,)
+    if device.type != "cuda":
+        return torch.empty(tuple(shape), dtype=dtype, device=device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _C.device_empty([int(d) for d in shape], dtype, idx)
+
+
+def device_zeros(shape, dtype: torch.dtype, device) -> torch.Tensor:
+    return device_empty(shape, dtype, device).zero_()
+
+
+def record_stream(t: torch.Tensor, stream) -> None:
+    """`t` is also used on `stream`: its memory is not reused before the work
+    queued there so far has finished. Works for engine-pool tensors (for
+    which torch's Tensor.record_stream is a no-op: c10 did not allocate them)
+    and for framework tensors alike."""
+    if t.is_cuda:
+        _C.record_stream(t, int(stream.cuda_stream))
+
+
 def cat_rows(ts: Sequence[torch.Tensor]) -> torch.Tensor:
-    """Concatenate along dim 0. Device tensors are copied into one buffer with
-    device-to-device DMA (hipMemcpyAsync: contiguous same-dtype copy_), so no
-    ATen concat kernel runs on the engine's GPU paths."""
+    """Concatenate along dim 0. Device tensors are copied into one pool
+    buffer with device-to-device DMA (hipMemcpyAsync: contiguous same-dtype
+    copy_), so no ATen concat kernel runs on the engine's GPU paths."""
     ts = list(ts)
     if len(ts) == 1:
         return ts[0]
     t0 = ts[0]
     if not t0.is_cuda:
         return torch.cat(ts, 0)
-    out = torch.empty((sum(int(t.shape[0]) for t in ts),) + tuple(t0.shape[1:]), dtype=t0.dtype, device=t0.device)
+    out = device_empty((sum(int(t.shape[0]) for t in ts),) + tuple(t0.shape[1:]), t0.dtype, t0.device)
     a = 0
     for t in ts:
         b = a + int(t.shape[0])

@@ -257,6 +257,13 @@ def collective_device_ms() -> float:
     return metrics.snapshot().get("collective_device_ms", 0.0)
 
 
+def _empty(shape, dtype, device) -> torch.Tensor:
+    """Collective output buffers: the engine pool on a GPU (the collective
+    runs on the current stream, which orders the pool block)."""
+    from ..engine import device_empty
+    return device_empty(shape, dtype, device)
+
+
 def _nbytes(t: torch.Tensor) -> int:
     return t.numel() * t.element_size()
 
@@ -390,7 +397,7 @@ def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torc
     if x.is_cuda and not gpu_collectives():
         return all_to_all_tensors([c.cpu() for c in chunks], recv_rows).to(x.device)
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
-    out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    out = _empty((sum(recv_rows),) + tuple(x.shape[1:]), x.dtype, x.device)
     with _traced("all_to_all", _nbytes(x), x.device):
         dist.all_to_all_single(out, x, [int(r) for r in recv_rows], [int(c.shape[0]) for c in chunks],
                                group=group)
@@ -408,7 +415,7 @@ def all_to_all_rows(x: torch.Tensor, send_rows: List[int], recv_rows: List[int])
     if x.is_cuda and not gpu_collectives():
         return all_to_all_rows(x.cpu(), send_rows, recv_rows).to(x.device)
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
-    out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    out = _empty((sum(recv_rows),) + tuple(x.shape[1:]), x.dtype, x.device)
     with _traced("all_to_all", _nbytes(x), x.device):
         dist.all_to_all_single(out, x, [int(r) for r in recv_rows], [int(c) for c in send_rows], group=group)
     return out
@@ -440,7 +447,7 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     if t.is_cuda and not gpu_collectives():
         return all_gather_tensor(t.cpu()).to(t.device)
     if t.is_cuda:
-        out = torch.empty((world_size(),) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        out = _empty((world_size(),) + tuple(t.shape), t.dtype, t.device)
         with _traced("all_gather", _nbytes(t), t.device):
             dist.all_gather_into_tensor(out, t, group=_state["device_group"])
         return out

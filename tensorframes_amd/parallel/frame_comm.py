@@ -205,6 +205,33 @@ def take_rows(it, names: Sequence[str], schema, nparts: int, n: int) -> List[Tup
     return out
 
 
+def _agreed_devices(local: Dict[int, Any], names: Sequence[str]) -> Dict[str, torch.device]:
+    """Where each dense column's all-to-all runs, the SAME on every rank: the
+    GPU (RCCL) only when every rank that holds rows of it holds them on the
+    device. A rank with no local rows (more ranks than partitions, or empty
+    partitions) follows the others instead of deciding from nothing, so the
+    ranks never issue mismatched collectives (RCCL on some, gloo on others).
+    One small Min all-reduce for all columns."""
+    from .. import engine
+    if not names:
+        return {}
+    gpu_ok = dist.is_distributed() and dist.gpu_collectives() and engine.gpu_available()
+    flags = []
+    for n in names:
+        srcs = [local[p].columns[n] for p in local if local[p].nrows]
+        # 1 = "device is fine with me"; a rank without rows abstains (1), and
+        # an all-abstaining column (no rows anywhere) stays on the host (has)
+        flags.append([int(all(c.is_cuda for c in srcs)), -int(bool(srcs))])
+    t = torch.tensor(flags, dtype=torch.int64).reshape(-1)
+    dist.all_reduce_host_(t, "Min")
+    t = t.reshape(len(names), 2)
+    out = {}
+    for i, n in enumerate(names):
+        on_gpu = gpu_ok and bool(t[i, 0]) and int(t[i, 1]) < 0
+        out[n] = engine.compute_device() if on_gpu else torch.device("cpu")
+    return out
+
+
 def repartition_blocks(local: Dict[int, Any], names: Sequence[str], schema, nparts_in: int,
                        nparts_out: int) -> Dict[int, Any]:
     """Rows re-sliced into nparts_out even partitions (in row order); each
@@ -249,12 +276,11 @@ def repartition_blocks(local: Dict[int, Any], names: Sequence[str], schema, npar
     kinds = column_kinds(list(local.values()), names, schema)
     mine = [q for q in range(nparts_out) if q % w == me]
     cols_out: Dict[int, Dict[str, Any]] = {q: {} for q in mine}
+    devs = _agreed_devices(local, [n for n in names if kinds[n] is not None])
     for n in names:
         kind = kinds[n]
         if kind is not None:
-            srcs = [local[p].columns[n] for p in local if local[p].nrows]
-            dev = srcs[0].device if srcs and all(c.is_cuda for c in srcs) and dist.is_distributed() \
-                and dist.gpu_collectives() else torch.device("cpu")
+            dev = devs[n]
             parts = [local[p].columns[n][st:st + ln].to(dev) for r in range(w) for (_, p, st, ln) in send[r]]
             buf = engine.cat_rows(parts) if parts else torch.empty((0,) + kind[1], dtype=kind[0], device=dev)
             got = dist.all_to_all_rows(buf, send_rows, recv_rows) if dist.is_distributed() else buf

@@ -106,3 +106,48 @@ def test_frame_actions_scale_with_ranks(world, tmp_path):
         assert res["group_count"] == [[j, len(range(j, N, 7))] for j in range(7)]
         assert res["strings"] == [f"n{i}" for i in range(11)]
         assert res["bad_rows"] == ["width", "null"], r  # raised on every rank, not only the owner
+
+
+class _FakeCol:
+    def __init__(self, cuda):
+        self.is_cuda = cuda
+
+
+class _FakeBlock:
+    def __init__(self, nrows, cuda):
+        self.nrows = nrows
+        self.columns = {"x": _FakeCol(cuda), "y": _FakeCol(True)}
+
+
+def _device_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TFA_DEVICE="cpu", OMP_NUM_THREADS="1")
+    sys.path.insert(0, REPO)
+    import torch
+
+    from tensorframes_amd import engine
+    from tensorframes_amd.parallel import dist, frame_comm
+
+    assert dist.init(backend="gloo")
+    # pretend RCCL is available; rank 1 owns no partitions at all, rank 2
+    # holds column x on the host
+    dist.gpu_collectives = lambda: True
+    engine.gpu_available = lambda: True
+    engine.compute_device = lambda: torch.device("meta")
+    local = {} if rank == 1 else {rank: _FakeBlock(5, cuda=(rank != 2))}
+    got = frame_comm._agreed_devices(local, ["x", "y"])
+    with open(os.path.join(outdir, f"d{rank}.json"), "w") as f:
+        json.dump({k: str(v) for k, v in got.items()}, f)
+    dist.shutdown()
+
+
+def test_repartition_device_agreed_by_every_rank(tmp_path):
+    """a rank with no local rows must not pick gloo while the
+    others pick RCCL (mismatched collectives hang). Every rank gets the same
+    answer: y (device everywhere it exists) on the GPU, x (host on rank 2)
+    on the host."""
+    world = 3
+    mp.spawn(_device_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    out = [json.load(open(tmp_path / f"d{r}.json")) for r in range(world)]
+    for res in out:
+        assert res == {"x": "cpu", "y": "meta"}
