@@ -7,6 +7,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPGuard.h>
 
+#include "comm/comm.h"
 #include "ir/graph.h"
 #include "kernels/kernels.h"
 #include "runtime/device_pool.h"
@@ -660,6 +661,58 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return d;
   }, "engine-owned device pool: allocations, frees, c10 fallbacks, hipMallocs, live / peak / cached bytes");
   m.def("trim_device_pool", &dev_pool_trim);
+  // ---- engine-owned communicators (csrc/comm/comm.h)
+  {
+    using comm::Comm;
+    using GR = py::call_guard<py::gil_scoped_release>;
+    py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm",
+        "engine communicator: all_reduce / all_gather / all_to_all_v / broadcast on the current stream")
+        .def_property_readonly("rank", &Comm::rank)
+        .def_property_readonly("size", &Comm::size)
+        .def_property_readonly("kind", &Comm::kind)
+        .def_property_readonly("calls", &Comm::calls)
+        .def("all_reduce", [](Comm& c, at::Tensor t, const std::string& op) {
+          c.all_reduce(t, comm::parse_op(op));
+          return t;
+        }, py::arg("tensor"), py::arg("op") = "Sum", GR())
+        .def("all_gather", &Comm::all_gather, GR())
+        .def("all_to_all_v", &Comm::all_to_all_v, py::arg("x"), py::arg("send_rows"), py::arg("recv_rows"), GR())
+        .def("broadcast", [](Comm& c, at::Tensor t, int root) {
+          c.broadcast(t, root);
+          return t;
+        }, py::arg("tensor"), py::arg("root") = 0, GR())
+        .def("barrier", &Comm::barrier, GR());
+    py::class_<comm::FakeWorld, std::shared_ptr<comm::FakeWorld>>(m, "FakeWorld",
+        "N in-process ranks over host memory (CPU test double of the communicator)")
+        .def(py::init<int>())
+        .def_property_readonly("size", &comm::FakeWorld::size)
+        .def("comm", [](std::shared_ptr<comm::FakeWorld> w, int r) {
+          return std::shared_ptr<Comm>(std::make_shared<comm::FakeComm>(w, r));
+        });
+    py::class_<comm::RcclComm, Comm, std::shared_ptr<comm::RcclComm>>(m, "RcclComm",
+        "an RCCL communicator of the engine's own (ncclCommInitRank)")
+        .def(py::init([](py::bytes uid, int rank, int size, int device) {
+          std::string u = uid;
+          py::gil_scoped_release nogil;
+          return std::make_shared<comm::RcclComm>(u, rank, size, device);
+        }), py::arg("unique_id"), py::arg("rank"), py::arg("size"), py::arg("device"))
+        .def("abort", &comm::RcclComm::abort)
+        .def("async_error", &comm::RcclComm::async_error);
+    m.def("rccl_unique_id", [] { return py::bytes(comm::rccl_unique_id()); });
+    py::class_<comm::OneShotComm, std::shared_ptr<comm::OneShotComm>>(m, "OneShotComm",
+        "single-hop all-reduce of payloads <= 64 KB through IPC-mapped peer buffers")
+        .def(py::init<int, int, int>(), py::arg("rank"), py::arg("size"), py::arg("device"))
+        .def("ipc_handle", [](comm::OneShotComm& o) { return py::bytes(o.ipc_handle()); })
+        .def("open", &comm::OneShotComm::open)
+        .def_property_readonly("ready", &comm::OneShotComm::ready)
+        .def_property_readonly("calls", &comm::OneShotComm::calls)
+        .def_static("max_bytes", &comm::OneShotComm::max_bytes)
+        .def("all_reduce", [](comm::OneShotComm& o, at::Tensor t, const std::string& op) {
+          o.all_reduce(t, comm::parse_op(op));
+          return t;
+        }, py::arg("tensor"), py::arg("op") = "Sum", GR())
+        .def("check", &comm::OneShotComm::check, GR());
+  }
   m.def("device_empty", [](const std::vector<int64_t>& sizes, at::ScalarType dt, int device) {
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
     return pool_empty(sizes, at::TensorOptions().dtype(dt).device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));

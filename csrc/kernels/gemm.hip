@@ -44,6 +44,9 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 
 enum ALoad { A_KCONTIG = 0, A_MCONTIG = 1, A_CONV = 2 };
 
+// 16 zero bytes in global memory: the source of a conv padding tap
+__device__ __attribute__((aligned(16))) float kZeroPage[4] = {0.f, 0.f, 0.f, 0.f};
+
 struct ConvGeom {
   int H, W, C, KW, OH, OW, sh, sw, dh, dw, pt, pl;
   FastDivU32 fOW, fOH;  // row -> (n, oh, ow) without an integer divide (M < 2^32)
@@ -114,17 +117,29 @@ __device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t co
 // a 4-wave 256x64 and half the accumulator registers of a 4-wave 256x128)
 template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 8 ? 2 : (BM * BN > 128 * 192 ? 1 : 2)))
-void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_per_split, int vepi) {
+void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_per_split, int flags) {
   constexpr int NT = 64 * WM * WN;
-  constexpr int LDA = BM + 4, LDB = BN + 4;
+  // k-major LDS images. One written with scalar stores (a k-contiguous
+  // operand, 4 k rows x 8 m per half-wave store) gets a pitch of 2 mod 32
+  // banks: kq = 0..3 land on banks 8*kq + m, all 32 distinct (a pitch of 4 mod
+  // 32 put kq 0/2 and 1/3 on one bank: 2-way conflicts, ~15 % of the LDS
+  // cycles, profiles/r4_pmc/). Float4-stored images keep a 16-byte pitch.
+  constexpr int LDA = AL == A_MCONTIG ? BM + 4 : BM + 2;
+  constexpr int LDB = TB ? BN + 2 : BN + 4;
+  const int vepi = flags & 1;
+  // flags bit 1: static priority for the second half of an 8-wave block (the
+  // younger waves lose every issue arbitration to their SIMD partner)
+  if (NT == 512 && (flags & 2) && (threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves, >= one 32x32 tile each");
   constexpr int KQ = BK / 4;  // float4 pieces along k
   constexpr int APIECES = BM * BK / 4, BPIECES = BN * BK / 4;  // float4 pieces per tile
   constexpr int AP = (APIECES + NT - 1) / NT, BP = (BPIECES + NT - 1) / NT;
   // one LDS buffer: the two A/B stages of the main loop, then (vector
-  // epilogue) one 32x36 staging tile per wave
-  constexpr int kStage = 32 * 36;
+  // epilogue) one 32x32 staging tile per wave (pitch 32: the half-wave row
+  // stores and the float4 row reads are both conflict-free; 36 put 2 of 16
+  // lanes of a ds_read_b128 group on one bank)
+  constexpr int kStage = 32 * 32;
   constexpr int kMain = 2 * BK * (LDA + LDB), kEpi = (NT / 64) * kStage;
   __shared__ __attribute__((aligned(16))) float smem[kMain > kEpi ? kMain : kEpi];
   float(&As)[2][BK][LDA] = *reinterpret_cast<float(*)[2][BK][LDA]>(smem);
@@ -234,20 +249,20 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
           const int ih = cih[p] + kkh * cg.dh, iw = ciw[p] + kkw * cg.dw;
           const bool inb = cbase[p] >= 0 && (!CHECK || gk < kend) && ih >= 0 && ih < cg.H && iw >= 0 &&
                            iw < cg.W;
-          // padding taps load a safe address and are zeroed by a select (branch-free)
+          // padding taps read a zero page instead of being zeroed by selects
+          // on the loaded value (no VALU on the data, which also keeps the
+          // compiler from waiting for the load before the LDS store);
           // in-image offset in 32 bits (H*W*C < 2^30, conv2d_nhwc): no 64-bit multiplies per piece
-          const float* src = inb ? A + cbase[p] + ((ih * cg.W + iw) * cg.C + kc) : A;
-          const float4 val = *reinterpret_cast<const float4*>(src);
-          ra[p] = make_float4(inb ? val.x : 0.f, inb ? val.y : 0.f, inb ? val.z : 0.f, inb ? val.w : 0.f);
+          const float* src = inb ? A + cbase[p] + ((ih * cg.W + iw) * cg.C + kc) : kZeroPage;
+          ra[p] = *reinterpret_cast<const float4*>(src);
         } else {
           float sv[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int ih = cih[p] + skh[j] * cg.dh, iw = ciw[p] + skw[j] * cg.dw;
             const bool inb = cbase[p] >= 0 && gk + j < kend && ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W;
-            const float* src = inb ? A + cbase[p] + ((ih * cg.W + iw) * cg.C + sc[j]) : A;
-            const float val = *src;
-            sv[j] = inb ? val : 0.f;
+            const float* src = inb ? A + cbase[p] + ((ih * cg.W + iw) * cg.C + sc[j]) : kZeroPage;
+            sv[j] = *src;
           }
           ra[p] = make_float4(sv[0], sv[1], sv[2], sv[3]);
         }
@@ -431,7 +446,7 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
         constexpr int i = decltype(ic)::value;
         const f32x16 v = acc[i][j];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 36 + (lane & 31)] = v[r];
+        for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = v[r];
         const int64_t col = n0 + wn * (BN / WN) + j * 32 + 4 * (lane & 7);
         if (col < N) {
           float* cbase;
@@ -444,7 +459,7 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
           for (int q = 0; q < 4; ++q) {
             const int rr = 8 * q + (lane >> 3);
             const int64_t row = m0 + wm * (BM / WM) + i * 32 + rr;
-            float4 o = *reinterpret_cast<const float4*>(&st[rr * 36 + 4 * (lane & 7)]);
+            float4 o = *reinterpret_cast<const float4*>(&st[rr * 32 + 4 * (lane & 7)]);
             o.x = act_fast(o.x + bv.x, cact);
             o.y = act_fast(o.y + bv.y, cact);
             o.z = act_fast(o.z + bv.z, cact);
@@ -608,9 +623,18 @@ int vector_epilogue(const GemmArgs& g) {
   return 1;
 }
 
+// TFA_GEMM_PRIO=1: static s_setprio(1) for waves 4-7 of the 8-wave tiles
+int prio_flag() {
+  static const int v = [] {
+    const char* e = std::getenv("TFA_GEMM_PRIO");
+    return e && std::atoi(e) ? 2 : 0;
+  }();
+  return v;
+}
+
 template <int AL, bool TB, bool VEC>
 void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s) {
-  const int vepi = p.splits == 1 ? vector_epilogue(g) : 0;
+  const int vepi = (p.splits == 1 ? vector_epilogue(g) : 0) | prio_flag();
   const int64_t tm = (g.M + p.bm - 1) / p.bm, tn = (g.N + p.bn - 1) / p.bn;
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
   TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");

@@ -66,6 +66,18 @@ void softmax(DType dt, bool log, const void* x, void* y, int64_t rows, int64_t c
 void topk(DType dt, const void* x, void* vals, int32_t* idx, int64_t rows, int64_t cols, int k,
           hipStream_t s);
 // segmented reductions: rows of x [n, inner] with segment ids (sorted or not) into [nseg, inner]
+// ---- one-shot all-reduce over IPC-mapped peer buffers (oneshot.hip)
+constexpr int kOneShotMaxRanks = 8;
+constexpr size_t kOneShotSlotBytes = 64 << 10;                     // largest payload
+constexpr size_t kOneShotFlagOffset = 2 * kOneShotSlotBytes;       // 2 slots x 8 ranks u32
+constexpr size_t kOneShotErrOffset = kOneShotFlagOffset + 2 * 8 * 4;  // timeout word
+constexpr size_t kOneShotBufBytes = kOneShotErrOffset + 256;
+struct OneShotPeers {
+  void* buf[kOneShotMaxRanks];  // every rank's buffer, mapped into this process ([rank] = own)
+};
+void oneshot_all_reduce(RedOp op, DType dt, const void* in, void* out, int64_t n, int rank, int world,
+                        const OneShotPeers& p, uint32_t epoch, hipStream_t s);
+
 size_t unsorted_segment_workspace_bytes(RedOp op, DType dt, int64_t n, int64_t inner, int64_t nseg);
 void unsorted_segment_reduce(RedOp op, DType dt, DType idt, const void* x, const void* ids,
                              void* y, int64_t n, int64_t inner, int64_t nseg, void* workspace,

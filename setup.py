@@ -79,7 +79,7 @@ class BuildWithHip(BuildExtension):
 
 
 cpp_sources = ["csrc/bindings.cpp"]
-for sub in ("proto", "ir", "runtime"):
+for sub in ("proto", "ir", "runtime", "comm"):
     cpp_sources += sorted(os.path.relpath(p, HERE) for p in glob.glob(os.path.join(HERE, "csrc", sub, "*.cpp")))
 
 torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
@@ -90,7 +90,7 @@ ext = CppExtension(
     include_dirs=[os.path.join(HERE, "csrc"), os.path.join(ROCM, "include")],
     define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
     library_dirs=[os.path.join(ROCM, "lib"), torch_lib],
-    libraries=["amdhip64", "hiprtc", "c10_hip", "torch_hip", "rocprofiler-sdk-roctx"],
+    libraries=["amdhip64", "hiprtc", "c10_hip", "torch_hip", "rocprofiler-sdk-roctx", "rccl"],
     extra_compile_args=["-O3", "-std=c++17", "-g0", "-Wno-unused-function", "-Wno-sign-compare"],
     extra_link_args=[f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"],
 )

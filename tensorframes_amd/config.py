@@ -67,6 +67,12 @@ class Config:
     # run the cross-rank collectives even in a 1-rank job (an RCCL/gloo group of
     # world size 1): exercises the collective path on a single GPU
     force_collectives: bool = dataclasses.field(default_factory=lambda: _env("TFA_FORCE_COLLECTIVES", False, bool))
+    # device collectives: "engine" (the engine's own communicator,
+    # parallel/comm.py: one-shot IPC all-reduce for <= 64 KB, an RCCL
+    # communicator of its own for the rest) or "torch" (torch.distributed)
+    collective_backend: str = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_BACKEND", "engine", str))
+    # the single-hop IPC all-reduce for small payloads (kernels/oneshot.hip)
+    oneshot_allreduce: bool = dataclasses.field(default_factory=lambda: _env("TFA_ONESHOT_ALLREDUCE", True, bool))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 

@@ -1182,6 +1182,10 @@ def _combine_monoids(partials: Dict[str, List[torch.Tensor]], ops: Dict[str, str
     host = [f.to("cpu", non_blocking=True) if f.is_cuda else f for _, f in flags]
     if dev.type == "cuda":
         torch.cuda.current_stream(dev).synchronize()
+        from .parallel import comm as _comm
+        ec = _comm.get()
+        if ec is not None:
+            ec.check()  # a one-shot flag wait that timed out raises here
     for (op, _), h in zip(flags, host):
         _check(bool(_FLAG_ANY[op](h[0].item())), "Cannot reduce an empty DataFrame")
     return out

@@ -35,7 +35,7 @@ import torch
 from ..parallel import dist
 from ..utils import dtypes as D
 from ..utils.shape import Shape
-from .block import Block, ObjectColumn, RaggedColumn, column_values, is_dense
+from .block import Block, ObjectColumn, RaggedColumn, StringColumn, column_values, is_dense
 from .column_info import SHAPE_KEY, TYPE_KEY, ColumnInformation
 from .types import BinaryType, StringType, StructField, StructType
 
@@ -73,6 +73,17 @@ def _fixed_dims(t) -> Tuple[List[int], Any]:
     return dims, t
 
 
+def _string_column(arr) -> StringColumn:
+    """An Arrow string array as offsets + bytes (zero-copy views of its buffers
+    where the layout allows)."""
+    _, obuf, dbuf = arr.buffers()
+    odt = np.int64 if _pa().types.is_large_string(arr.type) else np.int32
+    offs = np.frombuffer(obuf, dtype=odt)[arr.offset:arr.offset + len(arr) + 1].astype(np.int64)
+    data = np.frombuffer(dbuf, dtype=np.uint8) if dbuf is not None else np.zeros(0, np.uint8)
+    lo, hi = (int(offs[0]), int(offs[-1])) if len(offs) else (0, 0)
+    return StringColumn(torch.from_numpy(offs - lo), torch.from_numpy(data[lo:hi].copy()))
+
+
 def _column_from_arrow(name: str, arr) -> Tuple[Any, StructField]:
     pa = _pa()
     if isinstance(arr, pa.ChunkedArray):
@@ -80,7 +91,8 @@ def _column_from_arrow(name: str, arr) -> Tuple[Any, StructField]:
     _no_nulls(arr, name)
     t = arr.type
     if pa.types.is_string(t) or pa.types.is_large_string(t):
-        return ObjectColumn(arr.to_pylist()), StructField(name, StringType(), False)
+        # Arrow layout kept: offsets + bytes, no Python str per row
+        return _string_column(arr), StructField(name, StringType(), False)
     if pa.types.is_binary(t) or pa.types.is_large_binary(t):
         return ObjectColumn([bytearray(v) for v in arr.to_pylist()]), StructField(name, BinaryType(), False)
     if str(t) in _NUMERIC:
@@ -179,6 +191,12 @@ def _arrow_column(col, field: StructField):
         return _arrow_from_dense(col)
     if isinstance(col, RaggedColumn):
         return pa.array([np.asarray(c).tolist() for c in col.cells])
+    if isinstance(col, StringColumn) and not isinstance(field.dataType, BinaryType) and not col.binary:
+        offs = col.offsets.cpu().numpy()
+        data = pa.py_buffer(col.data.cpu().numpy())
+        if len(offs) and int(offs[-1]) < (1 << 31):
+            return pa.StringArray.from_buffers(len(col), pa.py_buffer(offs.astype(np.int32)), data)
+        return pa.LargeStringArray.from_buffers(len(col), pa.py_buffer(offs.astype(np.int64)), data)
     vals = column_values(col)
     if isinstance(field.dataType, BinaryType):
         return pa.array([bytes(v) for v in vals], type=pa.binary())

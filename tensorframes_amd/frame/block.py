@@ -59,7 +59,99 @@ class ObjectColumn:
         return ObjectColumn(self.values[a:b])
 
 
-Column = Any  # torch.Tensor | RaggedColumn | ObjectColumn
+class StringColumn(ObjectColumn):
+    """UTF-8 string (or binary) column in Arrow layout: int64 offsets [n+1]
+    and one byte buffer, host or device tensors — no Python object per row.
+    groupBy keys of this type are grouped on the device
+    (ops/groupby.string_key_words); `values` decodes to Python str (or
+    bytes) only when rows are materialised (collect)."""
+
+    __slots__ = ("offsets", "data", "binary", "_values")
+
+    def __init__(self, offsets: torch.Tensor, data: torch.Tensor, binary: bool = False):
+        self.offsets = offsets
+        self.data = data
+        self.binary = binary
+        self._values = None
+
+    @staticmethod
+    def from_values(values, binary: bool = False) -> "StringColumn":
+        enc = [v if isinstance(v, (bytes, bytearray)) else str(v).encode("utf-8") for v in values]
+        lens = np.fromiter((len(b) for b in enc), dtype=np.int64, count=len(enc))
+        offs = np.zeros(len(enc) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        data = np.frombuffer(b"".join(enc), dtype=np.uint8).copy()
+        return StringColumn(torch.from_numpy(offs), torch.from_numpy(data), binary)
+
+    @staticmethod
+    def from_numpy(arr: np.ndarray) -> "StringColumn":
+        """A numpy 'U' / 'S' array (fixed width) -> Arrow layout, vectorised."""
+        binary = arr.dtype.kind == "S"
+        b = arr if binary else np.char.encode(arr, "utf-8")
+        b = np.ascontiguousarray(b)
+        w = b.dtype.itemsize
+        lens = np.char.str_len(b).astype(np.int64) if len(b) else np.zeros(0, np.int64)
+        offs = np.zeros(len(b) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        if w == 0 or len(b) == 0:
+            return StringColumn(torch.from_numpy(offs), torch.zeros(0, dtype=torch.uint8), binary)
+        raw = b.view(np.uint8).reshape(len(b), w)
+        mask = np.arange(w)[None, :] < lens[:, None]
+        return StringColumn(torch.from_numpy(offs), torch.from_numpy(np.ascontiguousarray(raw[mask])), binary)
+
+    def __len__(self):
+        return int(self.offsets.shape[0]) - 1
+
+    @property
+    def values(self):
+        if self._values is None:
+            offs = self.offsets.cpu().numpy()
+            raw = self.data.cpu().numpy().tobytes()
+            base = int(offs[0]) if len(offs) else 0
+            if self.binary:
+                self._values = [raw[a - base:b - base] for a, b in zip(offs[:-1].tolist(), offs[1:].tolist())]
+            else:
+                self._values = [raw[a - base:b - base].decode("utf-8") for a, b in
+                                zip(offs[:-1].tolist(), offs[1:].tolist())]
+        return self._values
+
+    @property
+    def device(self):
+        return self.data.device
+
+    @property
+    def is_cuda(self):
+        return self.data.is_cuda
+
+    def to(self, device) -> "StringColumn":
+        device = torch.device(device)
+        if self.data.device == device:
+            return self
+        return StringColumn(self.offsets.to(device), self.data.to(device), self.binary)
+
+    def lengths(self) -> torch.Tensor:
+        return self.offsets[1:] - self.offsets[:-1]
+
+    def take(self, idx) -> "StringColumn":
+        idx = np.asarray(idx, dtype=np.int64)
+        offs = self.offsets.cpu().numpy()
+        data = self.data.cpu().numpy()
+        starts = offs[idx]
+        lens = offs[idx + 1] - starts
+        new = np.zeros(len(idx) + 1, dtype=np.int64)
+        np.cumsum(lens, out=new[1:])
+        pos = np.repeat(starts - new[:-1], lens) + np.arange(new[-1], dtype=np.int64)
+        return StringColumn(torch.from_numpy(new), torch.from_numpy(data[pos]), self.binary)
+
+    def slice(self, a, b) -> "StringColumn":
+        offs = self.offsets[a:b + 1]
+        if offs.numel() == 0:
+            return StringColumn(torch.zeros(1, dtype=torch.int64), self.data[:0], self.binary)
+        lo, hi = int(offs[0]), int(offs[-1])
+        return StringColumn(offs - lo, self.data[lo:hi], self.binary)
+
+
+Column = Any  # torch.Tensor | RaggedColumn | ObjectColumn | StringColumn
 
 
 @dataclass
@@ -80,7 +172,7 @@ class Block:
         return Block(len(idx), {n: col_take(c, idx) for n, c in self.columns.items()})
 
     def to(self, device) -> "Block":
-        return Block(self.nrows, {n: (c.to(device) if isinstance(c, torch.Tensor) else c)
+        return Block(self.nrows, {n: (c.to(device) if isinstance(c, (torch.Tensor, StringColumn)) else c)
                                   for n, c in self.columns.items()})
 
 
@@ -122,6 +214,17 @@ def concat_columns(cols: List[Column]) -> Column:
                 dt = c.tf_dtype
                 cells.extend(c.cells)
         return RaggedColumn(cells, dt)
+    if cols and all(isinstance(c, StringColumn) for c in cols):
+        if len(cols) == 1:
+            return cols[0]
+        offs, datas, base = [torch.zeros(1, dtype=torch.int64)], [], 0
+        for c in cols:
+            o = c.offsets.cpu()
+            offs.append(o[1:] - o[0] + base)
+            base += int(o[-1] - o[0])
+            datas.append(c.data.cpu())
+        return StringColumn(torch.cat(offs), torch.cat(datas) if datas else torch.zeros(0, dtype=torch.uint8),
+                            cols[0].binary)
     vals = []
     for c in cols:
         vals.extend(column_values(c))

@@ -26,7 +26,7 @@ import torch
 
 from ..parallel import dist
 from ..utils import dtypes as D
-from .block import (Block, ObjectColumn, RaggedColumn, build_column, build_rows, column_values, concat_blocks,
+from .block import (Block, ObjectColumn, RaggedColumn, StringColumn, build_column, build_rows, column_values, concat_blocks,
                     is_dense)
 from .column_info import ColumnInformation, DataFrameInfo, explain_schema
 from .types import (ArrayType, BinaryType, BooleanType, DataType, DoubleType, FloatType, IntegerType,
@@ -629,8 +629,11 @@ def from_columns(columns: Dict[str, Any], num_partitions: Optional[int] = None,
             t = v
         else:
             a = np.asarray(v)
-            t = torch.from_numpy(np.asarray(a, order="C")) if a.dtype.kind not in ("U", "S", "O") else list(v)
-        ln = t.shape[0] if isinstance(t, torch.Tensor) else len(t)
+            if a.dtype.kind in ("U", "S") and a.ndim == 1:
+                t = a  # fixed-width strings: Arrow-layout StringColumn per partition, vectorised
+            else:
+                t = torch.from_numpy(np.asarray(a, order="C")) if a.dtype.kind not in ("U", "S", "O") else list(v)
+        ln = t.shape[0] if isinstance(t, (torch.Tensor, np.ndarray)) else len(t)
         if n is None:
             n = ln
         elif ln != n:
@@ -649,6 +652,8 @@ def from_columns(columns: Dict[str, Any], num_partitions: Optional[int] = None,
                     from ..engine import pin
                     s = pin(s)
                 bc[k] = s
+            elif isinstance(t, np.ndarray):
+                bc[k] = StringColumn.from_numpy(t[a:b])
             else:
                 bc[k] = ObjectColumn(t[a:b])
         blocks[p] = Block(b - a, bc)

@@ -173,6 +173,8 @@ def _ensure_groups():
 
 
 def shutdown():
+    from . import comm
+    comm.reset()
     if dist.is_initialized() and _state["initialized_here"]:
         dist.destroy_process_group()
     _state.update(device_group=None, cpu_group=None, initialized_here=False)
@@ -394,6 +396,10 @@ def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torc
     if not is_distributed():
         return x
     _ensure_groups()
+    if x.is_cuda:
+        ec = _engine_comm()
+        if ec is not None and ec.rccl is not None:
+            return ec.all_to_all_rows(x, [int(c.shape[0]) for c in chunks], recv_rows)
     if x.is_cuda and not gpu_collectives():
         return all_to_all_tensors([c.cpu() for c in chunks], recv_rows).to(x.device)
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
@@ -412,6 +418,10 @@ def all_to_all_rows(x: torch.Tensor, send_rows: List[int], recv_rows: List[int])
         return x
     _ensure_groups()
     x = x.contiguous()
+    if x.is_cuda:
+        ec = _engine_comm()
+        if ec is not None and ec.rccl is not None:
+            return ec.all_to_all_rows(x, send_rows, recv_rows)
     if x.is_cuda and not gpu_collectives():
         return all_to_all_rows(x.cpu(), send_rows, recv_rows).to(x.device)
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
@@ -426,10 +436,22 @@ _OPS = {"Sum": dist.ReduceOp.SUM, "Min": dist.ReduceOp.MIN, "Max": dist.ReduceOp
         "Prod": dist.ReduceOp.PRODUCT}
 
 
+def _engine_comm():
+    from . import comm
+    return comm.get()
+
+
 def all_reduce_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
+    """In-place all-reduce. Device tensors go through the engine's own
+    communicator (parallel/comm.py: one-shot IPC for <= 64 KB, its RCCL
+    communicator above) when it serves them, else torch.distributed."""
     if not is_distributed():
         return t
     _ensure_groups()
+    if t.is_cuda:
+        ec = _engine_comm()
+        if ec is not None and ec.can_all_reduce(t):
+            return ec.all_reduce_(t.contiguous() if not t.is_contiguous() else t, op)
     if t.is_cuda and not gpu_collectives():  # gloo rehearsal: stage through the host
         return t.copy_(all_reduce_(t.cpu(), op))
     group = _state["device_group"] if t.is_cuda else _state["cpu_group"]
@@ -444,6 +466,10 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
         return t.unsqueeze(0)
     _ensure_groups()
     t = t.contiguous()
+    if t.is_cuda:
+        ec = _engine_comm()
+        if ec is not None and ec.rccl is not None:
+            return ec.all_gather(t)
     if t.is_cuda and not gpu_collectives():
         return all_gather_tensor(t.cpu()).to(t.device)
     if t.is_cuda:

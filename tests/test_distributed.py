@@ -140,7 +140,8 @@ def _check_results(tmp_path, world, device):
     outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
     assert all(o["device"] == device for o in outs)
     for o in outs:  # collectives are counted (metrics) on every rank
-        assert o["coll"].get("collective_all_to_all", 0) >= 1 and o["coll"].get("collective_all_reduce", 0) >= 1
+        reduces = sum(o["coll"].get(k, 0) for k in ("collective_all_reduce", "collective_oneshot_all_reduce"))
+        assert o["coll"].get("collective_all_to_all", 0) >= 1 and reduces >= 1
         assert o["coll"]["collective_bytes"] > 0
     xs = [float(i) for i in range(20)]
     parts = sorted(p for o in outs for p in o["local_parts"])

@@ -55,7 +55,10 @@ def test_reduce_blocks_runs_one_rccl_allreduce_per_op(rccl_group):
             got = tfs.reduce_blocks(fn(xi, [0], name="x"), df)
         after = metrics.snapshot()
         np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-3)
-        assert _delta(before, after, "collective_all_reduce") == 1, op
+        # one device all-reduce, through the engine's own communicator: the
+        # partial (65 floats) takes the one-shot IPC path, not torch's RCCL
+        assert _delta(before, after, "collective_oneshot_all_reduce") == 1, op
+        assert _delta(before, after, "collective_all_reduce") == 0, op
         assert _delta(before, after, "collective_all_gather_object") == 0, op
     assert rccl_group.collective_device_ms() > 0
 
@@ -73,7 +76,7 @@ def test_reduce_blocks_two_fetches_share_one_allreduce(rccl_group):
         ra, rb = tfs.reduce_blocks([tf.reduce_sum(ai, [0], name="a"), tf.reduce_sum(bi, [0], name="b")], df)
     after = metrics.snapshot()
     assert ra == a.sum() and rb == 2 * a.sum()
-    assert _delta(before, after, "collective_all_reduce") == 1
+    assert _delta(before, after, "collective_oneshot_all_reduce") == 1
 
 
 def test_reduce_rows_and_generic_reduce_over_rccl(rccl_group):
@@ -92,7 +95,7 @@ def test_reduce_rows_and_generic_reduce_over_rccl(rccl_group):
         got = tfs.reduce_blocks(tf.identity(tf.reduce_sum(xi, [0]), name="x"), df)
     after = metrics.snapshot()
     assert got == 4950.0
-    assert _delta(before, after, "collective_all_gather") >= 1
+    assert _delta(before, after, "collective_rccl_all_gather") >= 1  # the engine's RCCL communicator
     assert _delta(before, after, "collective_all_gather_object") == 0
 
 
@@ -110,7 +113,7 @@ def test_aggregate_shuffle_over_rccl(rccl_group):
         out = tfs.aggregate(tf.reduce_sum(xi, [0], name="x"), df.groupBy("k"))
         rows = sorted(out.collect(), key=lambda r: r.k)
     after = metrics.snapshot()
-    assert _delta(before, after, "collective_all_to_all") >= 1
+    assert _delta(before, after, "collective_rccl_all_to_all") >= 1  # grouped send/recv of the engine's comm
     assert len(rows) == 37
     for r in rows:
         np.testing.assert_allclose(r.x, x[keys == r.k].sum(0), rtol=1e-10, atol=1e-9)
