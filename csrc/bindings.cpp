@@ -369,6 +369,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
     return py::make_tuple(ids, uniq.narrow(0, 0, nseg));
   }, "keys [n] -> (group id per row int64, distinct keys ascending)");
+  m.def("string_words", [](const at::Tensor& offsets, const at::Tensor& data, int64_t W) {
+    TFA_CHECK(offsets.scalar_type() == at::kLong && offsets.dim() == 1 && offsets.size(0) >= 1,
+              "string_words: offsets must be int64[n+1]");
+    TFA_CHECK(data.scalar_type() == at::kByte && data.dim() == 1, "string_words: data must be uint8[bytes]");
+    TFA_CHECK(W >= 1 && W <= 4096, "string_words: 1..4096 words");
+    TFA_CHECK(offsets.device() == data.device(), "string_words: offsets and data on different devices");
+    const int64_t n = offsets.size(0) - 1;
+    at::Tensor oc = offsets.contiguous(), dc = data.contiguous();
+    if (!oc.is_cuda()) {  // host: the same packing, a plain loop
+      at::Tensor out = at::empty({W + 1, n}, oc.options());
+      const int64_t* o = oc.data_ptr<int64_t>();
+      const uint8_t* d = dc.data_ptr<uint8_t>();
+      int64_t* y = out.data_ptr<int64_t>();
+      for (int64_t i = 0; i < n; ++i) {
+        const int64_t a = o[i], len = o[i + 1] - a;
+        for (int64_t w = 0; w < W; ++w) {
+          uint64_t v = 0;
+          for (int b = 0; b < 8; ++b) {
+            const int64_t j = w * 8 + b;
+            v |= static_cast<uint64_t>(j < len ? d[a + j] : 0) << (56 - 8 * b);
+          }
+          y[w * n + i] = static_cast<int64_t>(v ^ 0x8000000000000000ull);
+        }
+        y[W * n + i] = len;
+      }
+      return out;
+    }
+    c10::hip::HIPGuard guard(oc.device().index());
+    at::Tensor out = pool_empty({W + 1, n}, oc.options());
+    k::string_words(oc.data_ptr<int64_t>(), dc.data_ptr<uint8_t>(), n, static_cast<int>(W), out.data_ptr<int64_t>(),
+                    c10::hip::getCurrentHIPStream(oc.device().index()).stream());
+    return out;
+  }, py::arg("offsets"), py::arg("data"), py::arg("words"),
+        "string keys -> [words + 1, n] int64: big-endian 8-byte words (sign-flipped) + byte length; signed order "
+        "of the columns = lexicographic order of the strings");
   m.def("key_dest", [](const std::vector<at::Tensor>& keys, int64_t world) {
     TFA_CHECK(!keys.empty() && keys[0].is_cuda(), "key_dest: device key columns expected");
     c10::hip::HIPGuard guard(keys[0].device().index());

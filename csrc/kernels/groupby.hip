@@ -612,6 +612,42 @@ void unpack_rows(const PackCols& pc, const void* in, int64_t nrows, int64_t reco
   TFA_LAUNCH_CHECK("unpack_rows");
 }
 
+// ---- string keys: the bytes of every row packed into W big-endian 64-bit
+// words (zero padded) with the sign bit flipped, plus the byte length. Signed
+// comparison of (word 0, ..., word W-1, length) is then the lexicographic
+// order of the byte strings, so the numeric groupBy kernels group string keys
+// exactly (no hashing, no collisions) and in sorted order. One thread per
+// (row, word); the output is column-major [W + 1][n] (contiguous key columns).
+__global__ __launch_bounds__(kT) void string_words_kernel(const int64_t* __restrict__ offs,
+                                                          const uint8_t* __restrict__ data, int64_t n, int W,
+                                                          int64_t* __restrict__ out) {
+  const int64_t total = n * (W + 1);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int w = (int)(t / n);
+    const int64_t i = t - (int64_t)w * n;
+    const int64_t a = offs[i], len = offs[i + 1] - a;
+    if (w == W) {
+      out[t] = len;
+      continue;
+    }
+    uint64_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int64_t j = (int64_t)w * 8 + b;
+      const uint64_t byte = j < len ? data[a + j] : 0;
+      v |= byte << (56 - 8 * b);
+    }
+    out[t] = (int64_t)(v ^ 0x8000000000000000ull);
+  }
+}
+
+void string_words(const int64_t* offs, const uint8_t* data, int64_t n, int W, int64_t* out, hipStream_t s) {
+  TFA_CHECK(W >= 1 && n >= 0, "string_words: bad shape");
+  if (n == 0) return;
+  hipLaunchKernelGGL(string_words_kernel, dim3(ew_grid(n * (W + 1))), dim3(kT), 0, s, offs, data, n, W, out);
+  TFA_LAUNCH_CHECK("string_words");
+}
+
 void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s) {
   if (n == 0) return;
   TFA_CHECK(world >= 1, "hash_mod: world must be >= 1");

@@ -96,6 +96,8 @@ int64_t factorize(DType dt, const void* keys, int64_t n, int64_t* ids, void* uni
 // per-row 64-bit key hash (accumulate: combine with the hash already in h)
 void key_hash(DType dt, const void* keys, int64_t n, uint64_t* h, bool accumulate, hipStream_t s);
 void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s);
+// string keys as W big-endian words (sign-flipped) + length, column-major [W+1][n]
+void string_words(const int64_t* offs, const uint8_t* data, int64_t n, int W, int64_t* out, hipStream_t s);
 // ids [n] in [0, nseg) -> rows ordered by segment (stable) perm [n] and CSR
 // offsets [nseg + 1]; out-of-range ids are dropped
 size_t segment_csr_workspace_bytes(int64_t n, int64_t nseg);

@@ -1654,21 +1654,20 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         (hash-routed all-to-all over RCCL), and are reduced again per key."""
         from .ops import groupby as G
         # decided from the schema, so every rank takes the same (collective) path
-        if not numeric_keys:
+        if not device_keys_ok:
             return combine_host(blocks)
         dev = engine.compute_device()
         on_device = any(b.columns[n].is_cuda for b in blocks.values() if b.nrows for n in out_names) or \
             dev.type == "cuda"
         parts = [b for _, b in sorted(blocks.items()) if b.nrows]
-        kdt = [D.torch_dtype(tf_types[k]) for k in keys]
-        K: List[torch.Tensor] = [engine.device_empty(0, t, dev) for t in kdt]
+        K: List[torch.Tensor] = expand_keys(parts, dev)
         V: Dict[str, Optional[torch.Tensor]] = {n: None for n in out_names}
         if parts:
             # this rank's keys are factorised ONCE over all its partitions
             # (one id space), so every partition reduces straight into its
             # row of a [P, groups, ...] buffer and the partitions combine by an
             # elementwise fold: no second factorisation on a single rank
-            ids, K, ng = G.group_ids([engine.cat_rows([b.columns[k].to(dev) for b in parts]) for k in keys])
+            ids, K, ng = G.group_ids(K)
             bounds = np.cumsum([0] + [b.nrows for b in parts])
             for n in out_names:
                 vals = [b.columns[n].to(dev).contiguous() for b in parts]
@@ -1683,12 +1682,13 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         if not dist.is_distributed():
             if K[0].shape[0] == 0:
                 return {0: Block(0, _empty_agg_cols(df, keys, out_names))}
-            out_cols: Dict[str, Any] = dict(zip(keys, K))
-            out_cols.update(V)
+            ngk = int(K[0].shape[0])
+            out_cols: Dict[str, Any] = dict(V)
             if not on_device or not keep_on_device:
                 out_cols = {k: v.cpu() for k, v in out_cols.items()}
+            out_cols.update(collapse_keys(K, on_device and keep_on_device))
             metrics.add("aggregate_device_groupby" if dev.type == "cuda" else "aggregate_host_groupby")
-            return {0: Block(int(K[0].shape[0]), out_cols)}
+            return {0: Block(ngk, {c: out_cols[c] for c in all_cols})}
         if dist.is_distributed():
             cells = _agree_shapes({n: (V[n][0] if V[n] is not None and V[n].shape[0] else None) for n in out_names},
                                   {n: agg_static.get(n) for n in out_names}, dev) if any(
@@ -1697,22 +1697,79 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             for n in out_names:
                 if V[n] is None:
                     V[n] = engine.device_empty((0,) + tuple(cells[n]), D.torch_dtype(summary[n].tf_dtype), dev)
+            nk = len(K)  # expanded key columns (string keys: words + length)
             recv = G.route(K, [V[n] for n in out_names])
-            K, V = recv[:len(keys)], dict(zip(out_names, recv[len(keys):]))
+            K, V = recv[:nk], dict(zip(out_names, recv[nk:]))
         if K[0].shape[0] == 0:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, dist.world_size()))}
         ids, uniq, ng = G.group_ids(K)
-        out_cols: Dict[str, Any] = dict(zip(keys, uniq))
+        out_cols: Dict[str, Any] = {}
         for n in out_names:
             out_cols[n] = _C.unsorted_segment_reduce(monoid[n], V[n].contiguous(), ids, ng)
         if not on_device or not keep_on_device:
             out_cols = {k: v.cpu() for k, v in out_cols.items()}
+        out_cols.update(collapse_keys(uniq, on_device and keep_on_device))
         metrics.add("aggregate_device_groupby" if dev.type == "cuda" else "aggregate_host_groupby")
-        return {dist.rank(): Block(ng, out_cols)}
+        return {dist.rank(): Block(ng, {c: out_cols[c] for c in all_cols})}
 
-    numeric_keys = all(tf_types[k] in (D.DT_FLOAT, D.DT_DOUBLE, D.DT_INT32, D.DT_INT64) and
-                       (ColumnInformation(df.schema[k]).stf is not None and
-                        ColumnInformation(df.schema[k]).stf.shape.num_dims == 1) for k in keys)
+    def _key_kind(k: str) -> Optional[str]:
+        f = df.schema[k]
+        if isinstance(f.dataType, StringType):
+            return "str"
+        if isinstance(f.dataType, BinaryType):
+            return "bin"
+        stf = ColumnInformation(f).stf
+        if tf_types[k] in (D.DT_FLOAT, D.DT_DOUBLE, D.DT_INT32, D.DT_INT64) and stf is not None and \
+                stf.shape.num_dims == 1:
+            return "num"
+        return None
+
+    # numeric scalar keys group as they are; string / binary keys as their
+    # packed words (ops/groupby.string_key_words): both on the device
+    key_kinds = {k: _key_kind(k) for k in keys}
+    device_keys_ok = all(v is not None for v in key_kinds.values())
+    numeric_keys = device_keys_ok
+    key_width: Dict[str, int] = {}
+
+    def expand_keys(parts: List[Block], dev) -> List[torch.Tensor]:
+        """The key columns of these partitions as int64/numeric device columns
+        (string keys: W words + length each). Collective for string keys: the
+        word count is agreed by a Max all-reduce, every rank calls this."""
+        from .ops import groupby as G
+        out: List[torch.Tensor] = []
+        strs = {k: [G.as_string_column(b.columns[k], key_kinds[k] == "bin") for b in parts]
+                for k in keys if key_kinds[k] != "num"}
+        if strs:
+            widths = torch.tensor([G.string_width(strs[k]) for k in strs], dtype=torch.int64)
+            dist.all_reduce_host_(widths, "Max")
+            key_width.update({k: int(w) for k, w in zip(strs, widths.tolist())})
+        for k in keys:
+            if key_kinds[k] == "num":
+                kdt = D.torch_dtype(tf_types[k])
+                out.append(engine.cat_rows([b.columns[k].to(dev) for b in parts]) if parts
+                           else engine.device_empty(0, kdt, dev))
+                continue
+            w = key_width[k]
+            cols = [G.string_key_words(c, w, dev) for c in strs[k]]
+            for j in range(w + 1):
+                out.append(engine.cat_rows([c[j] for c in cols]) if cols
+                           else engine.device_empty(0, torch.int64, dev))
+        metrics.add("aggregate_string_key_words", sum(key_width.get(k, 0) for k in keys))
+        return out
+
+    def collapse_keys(cols: List[torch.Tensor], keep: bool) -> Dict[str, Any]:
+        """Expanded group key columns -> the output key columns."""
+        from .ops import groupby as G
+        out, j = {}, 0
+        for k in keys:
+            if key_kinds[k] == "num":
+                out[k] = cols[j] if keep else cols[j].cpu()
+                j += 1
+            else:
+                w = key_width[k]
+                out[k] = G.words_to_strings(cols[j:j + w + 1], key_kinds[k] == "bin")
+                j += w + 1
+        return out
     # static cell shapes of the reduced columns (from the schema), for ranks without rows
     agg_static = {}
     for n in out_names:
@@ -1779,18 +1836,17 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         from .ops import groupby as G
         dev = engine.compute_device()
         parts = [b for _, b in sorted(blocks.items()) if b.nrows]
-        kdt = [D.torch_dtype(tf_types[k]) for k in keys]
+        K = expand_keys(parts, dev)
         if parts:
-            K = [engine.cat_rows([b.columns[k].to(dev) for b in parts]) for k in keys]
             V = [engine.cat_rows([b.columns[n].to(dev).contiguous() for b in parts]) for n in out_names]
         else:
-            K = [engine.device_empty(0, t, dev) for t in kdt]
             cells = {n: agg_static_in.get(n) for n in out_names}
             V = [engine.device_empty((0,) + tuple(cells[n] or ()), D.torch_dtype(summary[n].tf_dtype), dev)
                  for n in out_names]
         if dist.is_distributed():
+            nk = len(K)
             recv = G.route(K, V)
-            K, V = recv[:len(keys)], recv[len(keys):]
+            K, V = recv[:nk], recv[nk:]
         if K[0].shape[0] == 0:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, dist.world_size()))}
         ids, uniq, ng = G.group_ids(K)
@@ -1827,11 +1883,11 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         metrics.add("aggregate_batched_groups", batched)
         metrics.add("aggregate_single_groups", ng - batched)
         metrics.add("aggregate_device_generic")
-        out_cols: Dict[str, Any] = dict(zip(keys, uniq))
-        out_cols.update(out)
+        out_cols: Dict[str, Any] = dict(out)
         if not keep_on_device:
             out_cols = {k: v.cpu() for k, v in out_cols.items()}
-        return {dist.rank(): Block(ng, out_cols)}
+        out_cols.update(collapse_keys(uniq, keep_on_device))
+        return {dist.rank(): Block(ng, {c: out_cols[c] for c in all_cols})}
 
     # static cell shapes of the input columns, for ranks without rows
     agg_static_in = {}

@@ -596,6 +596,8 @@ createDataFrame = create_dataframe  # noqa: N816
 def _field_for_array(name: str, arr) -> StructField:
     """Dense whole-column arrays know their cell shape: record it in the
     metadata (lead dim unknown), so no `analyze` pass is needed."""
+    if isinstance(arr, StringColumn):
+        return StructField(name, BinaryType() if arr.binary else StringType(), False)
     if isinstance(arr, torch.Tensor):
         tf = D.as_dtype(arr.dtype).enum
         shape = tuple(arr.shape)
@@ -625,7 +627,7 @@ def from_columns(columns: Dict[str, Any], num_partitions: Optional[int] = None,
     cols = {}
     n = None
     for k, v in columns.items():
-        if isinstance(v, torch.Tensor):
+        if isinstance(v, (torch.Tensor, StringColumn)):
             t = v
         else:
             a = np.asarray(v)
@@ -633,7 +635,7 @@ def from_columns(columns: Dict[str, Any], num_partitions: Optional[int] = None,
                 t = a  # fixed-width strings: Arrow-layout StringColumn per partition, vectorised
             else:
                 t = torch.from_numpy(np.asarray(a, order="C")) if a.dtype.kind not in ("U", "S", "O") else list(v)
-        ln = t.shape[0] if isinstance(t, (torch.Tensor, np.ndarray)) else len(t)
+        ln = t.shape[0] if isinstance(t, (torch.Tensor, np.ndarray)) else len(t)  # StringColumn: rows
         if n is None:
             n = ln
         elif ln != n:
@@ -654,6 +656,8 @@ def from_columns(columns: Dict[str, Any], num_partitions: Optional[int] = None,
                 bc[k] = s
             elif isinstance(t, np.ndarray):
                 bc[k] = StringColumn.from_numpy(t[a:b])
+            elif isinstance(t, StringColumn):
+                bc[k] = t.slice(a, b)
             else:
                 bc[k] = ObjectColumn(t[a:b])
         blocks[p] = Block(b - a, bc)

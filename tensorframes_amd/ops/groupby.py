@@ -5,7 +5,9 @@ kernels of csrc/kernels/groupby.hip (`_C.factorize`), on the host by the ATen
 oracle. Groups come out in ascending key order (lexicographic for several
 key columns), the order the reference's Spark groupBy results are compared in
 (reference: src/test/scala/org/tensorframes/BasicOperationsSuite.scala:200-210
-via compareRows). String keys are dictionary-encoded on the host once.
+via compareRows). String keys never become Python objects: their bytes are
+packed into big-endian 64-bit words + a length (`_C.string_words`), which the
+same numeric kernels group exactly and in lexicographic order.
 
 The cross-rank shuffle of per-key partials hashes the keys on the device
 (`_C.key_dest`: the same 64-bit hash on every rank), orders the rows by
@@ -99,3 +101,47 @@ def route(keys: List[torch.Tensor], cols: List[torch.Tensor]) -> List[torch.Tens
         ordered = [c[perm] for c in allc]
     recv_rows = dist.all_to_all_counts(send_rows)
     return [dist.all_to_all_rows(c, send_rows, recv_rows) for c in ordered]
+
+
+# ---------------------------------------------------------------- string keys
+def as_string_column(col, binary: bool = False):
+    """A key column of str / bytes values as an Arrow-layout StringColumn."""
+    from ..frame.block import StringColumn
+    if isinstance(col, StringColumn):
+        return col
+    return StringColumn.from_values(list(col.values), binary)
+
+
+def string_width(cols: Sequence) -> int:
+    """Words (8 bytes each) that hold the longest string of these columns, >= 1."""
+    longest = 0
+    for c in cols:
+        if len(c):
+            longest = max(longest, int(c.lengths().max()))
+    return max(1, -(-longest // 8))
+
+
+def string_key_words(col, words: int, dev: torch.device) -> List[torch.Tensor]:
+    """[word 0, ..., word W-1, length] int64 key columns of one string column
+    on `dev` (kernels/groupby.hip string_words): grouped by the numeric
+    factorisation they sort lexicographically and compare exactly."""
+    col = col.to(dev)
+    packed = _C.string_words(col.offsets, col.data, int(words))  # [W + 1, n]
+    return [packed[j] for j in range(words + 1)]
+
+
+def words_to_strings(cols: List[torch.Tensor], binary: bool = False):
+    """Inverse of string_key_words for the (few) group keys: -> StringColumn (host)."""
+    from ..frame.block import StringColumn
+    w = len(cols) - 1
+    lens = cols[w].cpu().numpy().astype(np.int64)
+    n = len(lens)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    if n == 0:
+        return StringColumn(torch.from_numpy(offs), torch.zeros(0, dtype=torch.uint8), binary)
+    words = torch.stack([c.cpu() for c in cols[:w]], 1).numpy()  # [n, W]
+    u = (words.view(np.uint64) ^ np.uint64(1 << 63)).astype(">u8")
+    raw = u.view(np.uint8).reshape(n, 8 * w)
+    mask = np.arange(8 * w)[None, :] < lens[:, None]
+    return StringColumn(torch.from_numpy(offs), torch.from_numpy(np.ascontiguousarray(raw[mask])), binary)

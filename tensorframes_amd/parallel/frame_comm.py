@@ -80,6 +80,9 @@ def column_kinds(blocks: Sequence, names: Sequence[str], schema) -> Dict[str, Ki
         for n, f in zip(cand, ok.tolist()):
             if f:
                 out[n] = pinned[n]
+    for n in names:  # string fields: never dense (their own tensor path), nothing to exchange
+        if n not in out and _is_string_field(schema[n]):
+            out[n] = None
     rest = [n for n in names if n not in out]
     if rest:
         # the schema does not pin these: a small metadata exchange (no data)
@@ -112,6 +115,38 @@ def _host_cat(cols: List[Any], kind: Kind) -> torch.Tensor:
     return ts[0].contiguous() if len(ts) == 1 else torch.cat(ts, 0)
 
 
+def _is_string_field(field) -> bool:
+    from ..frame.types import StringType
+    return isinstance(field.dataType, StringType)
+
+
+def _gather_strings(local, owned, counts, rows_of_rank, root, w) -> Optional[Dict[int, List[str]]]:
+    """String column of every partition (in pid order) as value lists, moved
+    as an int64 length tensor and a uint8 byte tensor per rank."""
+    from ..frame.block import StringColumn, concat_columns
+    from ..ops import groupby as G
+    cols = [G.as_string_column(c).to(torch.device("cpu")) for _, c in sorted(local, key=lambda x: x[0])]
+    cat = concat_columns(cols) if cols else StringColumn.from_values([])
+    nb = torch.zeros(w, dtype=torch.int64)
+    nb[dist.rank()] = int(cat.data.numel())
+    dist.all_reduce_host_(nb, "Sum")
+    lens = dist.gather_rows(cat.lengths().contiguous(), rows_of_rank, root)
+    data = dist.gather_rows(cat.data.contiguous(), nb.tolist(), root)
+    if lens is None:
+        return None
+    out: Dict[int, List[str]] = {}
+    for r in range(w):
+        ln = lens[r]
+        offs = torch.zeros(ln.shape[0] + 1, dtype=torch.int64)
+        torch.cumsum(ln, 0, out=offs[1:])
+        sc = StringColumn(offs, data[r])
+        a = 0
+        for p in owned[r]:
+            out[p] = sc.slice(a, a + counts[p]).values
+            a += counts[p]
+    return out
+
+
 def gather_blocks(local: List[Tuple[int, Any]], names: Sequence[str], schema, nparts: int,
                   root: Optional[int] = None) -> Optional[List[Tuple[int, int, List[Any]]]]:
     """[(pid, nrows, [column payload per name])] of EVERY partition, in pid
@@ -140,6 +175,12 @@ def gather_blocks(local: List[Tuple[int, Any]], names: Sequence[str], schema, np
                     byp[p] = arr[a:a + counts[p]]
                     a += counts[p]
             per_col[n] = byp
+        elif _is_string_field(schema[n]):
+            # strings as two tensors (lengths + bytes), no pickling
+            per_col[n] = _gather_strings([(p, b.columns[n]) for p, b in local if b.nrows], owned, counts,
+                                         rows_of_rank, root, w)
+            if per_col[n] is None:
+                del per_col[n]
         else:
             mine = [(p, column_values(b.columns[n])) for p, b in local if b.nrows]
             got = dist.all_gather_object(mine) if root is None else dist.gather_object(mine, root)
