@@ -238,8 +238,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            })
       .def("run", &Program::run, py::call_guard<py::gil_scoped_release>())
       .def("run_chunked", &Program::run_chunked, py::arg("seg_inputs"), py::arg("seg_outputs"),
-           py::arg("chunk_rows"), py::arg("device"), py::arg("depth") = 3,
+           py::arg("chunk_rows"), py::arg("device"), py::arg("depth") = 3, py::arg("wait") = true,
            py::call_guard<py::gil_scoped_release>())
+      .def("release_pipeline", &Program::release_pipeline, py::call_guard<py::gil_scoped_release>(),
+           "drain and free the persistent chunk pipeline (after a deferred run_chunked sequence)")
       .def("run_chunked_reduce", &Program::run_chunked_reduce, py::arg("seg_inputs"), py::arg("chunk_rows"),
            py::arg("device"), py::arg("depth") = 3, py::call_guard<py::gil_scoped_release>())
       .def("describe", &Program::describe_plan, py::arg("inputs"), py::arg("as_gpu") = false)
@@ -748,6 +750,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }, py::arg("tensor"), py::arg("op") = "Sum", GR())
         .def("check", &comm::OneShotComm::check, GR());
   }
+  m.def("pipeline_wait", &pipeline_wait, py::arg("handle"), py::call_guard<py::gil_scoped_release>(),
+        "wait for a run_chunked(wait=False) completion handle (and release it)");
   m.def("device_empty", [](const std::vector<int64_t>& sizes, at::ScalarType dt, int device) {
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
     return pool_empty(sizes, at::TensorOptions().dtype(dt).device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));

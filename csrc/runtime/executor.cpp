@@ -1176,6 +1176,10 @@ void Program::wait_consts(const at::Device& dev, void* stream) {
 }
 
 Program::~Program() {
+  {
+    std::lock_guard<std::mutex> lk(pipe_mu_);
+    drop_pipe(false);
+  }
   for (auto& kv : const_events_) (void)hipEventDestroy(static_cast<hipEvent_t>(kv.second));
 }
 
@@ -1565,9 +1569,31 @@ static void order_copy_after_compute(hipStream_t copy, hipStream_t compute) {
   HIP_OK(hipEventDestroy(e));
 }
 
-void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
-                          const std::vector<std::vector<at::Tensor>>& seg_outputs,
-                          int64_t chunk_rows, int device, int depth) {
+void Program::drop_pipe(bool synced) {
+  if (!pipe_) return;
+  if (pipe_->device >= 0) {
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(pipe_->device));
+    if (!synced) {
+      (void)hipStreamSynchronize(copy_stream(pipe_->device, 0));
+      (void)hipStreamSynchronize(copy_stream(pipe_->device, 1));
+      (void)hipDeviceSynchronize();  // the compute streams that read the ring
+    }
+    for (hipEvent_t e : pipe_->ev_comp) (void)hipEventDestroy(e);
+    for (hipEvent_t e : pipe_->ev_d2h) (void)hipEventDestroy(e);
+  }
+  pipe_.reset();
+}
+
+void pipeline_wait(int64_t handle) {
+  if (!handle) return;
+  hipEvent_t e = reinterpret_cast<hipEvent_t>(handle);
+  HIP_OK(hipEventSynchronize(e));
+  HIP_OK(hipEventDestroy(e));
+}
+
+int64_t Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
+                             const std::vector<std::vector<at::Tensor>>& seg_outputs,
+                             int64_t chunk_rows, int device, int depth, bool wait) {
   TFA_CHECK(host_op_error_.empty(), host_op_error_);
   TFA_CHECK(seg_inputs.size() == seg_outputs.size(), "segments mismatch");
   TFA_CHECK(chunk_rows > 0, "chunk_rows must be > 0");
@@ -1601,28 +1627,64 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
                 "run_chunked outputs must be contiguous host tensors with ", rows, " rows");
     for (int64_t st = 0; st < rows; st += chunk_rows) chunks.push_back({s, st, std::min(chunk_rows, rows - st)});
   }
-  if (chunks.empty()) return;
-  // device input ring
+  if (chunks.empty()) return 0;
+  std::lock_guard<std::mutex> plk(pipe_mu_);
+  // the persistent device input ring: reused while device, depth, feed dtypes
+  // and row shapes match and it holds chunk_rows rows; rebuilt (after a
+  // drain) otherwise
   size_t nin = feed_nodes_.size();
-  std::vector<std::vector<at::Tensor>> ring(depth);
-  for (int d = 0; d < depth; ++d)
+  {
+    std::vector<std::vector<int64_t>> shapes;
+    std::vector<at::ScalarType> dts;
     for (size_t i = 0; i < nin; ++i) {
-      auto sz = seg_inputs[0][i].sizes().vec();
-      sz[0] = chunk_rows;
-      ring[d].push_back(dev_empty(sz, seg_inputs[0][i].scalar_type(), dev, compute.stream()));
+      auto sz = seg_inputs[chunks[0].seg][i].sizes().vec();
+      sz.erase(sz.begin());
+      shapes.push_back(sz);
+      dts.push_back(seg_inputs[chunks[0].seg][i].scalar_type());
     }
-  order_copy_after_compute(h2d.stream(), compute.stream());
-  std::vector<hipEvent_t> ev_h2d(depth), ev_comp(depth), ev_d2h(depth);
-  for (int d = 0; d < depth; ++d) {
-    HIP_OK(hipEventCreateWithFlags(&ev_h2d[d], hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_comp[d], hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_d2h[d], hipEventDisableTiming));
+    const bool fits = pipe_ && pipe_->device == device && pipe_->depth == depth && pipe_->shapes == shapes &&
+                      pipe_->dtypes == dts && pipe_->rows >= chunk_rows;
+    if (!fits) {
+      drop_pipe(false);
+      pipe_ = std::make_unique<Pipe>();
+      pipe_->device = device;
+      pipe_->depth = depth;
+      pipe_->rows = chunk_rows;
+      pipe_->shapes = shapes;
+      pipe_->dtypes = dts;
+      pipe_->ring.resize(depth);
+      for (int d = 0; d < depth; ++d)
+        for (size_t i = 0; i < nin; ++i) {
+          std::vector<int64_t> sz = shapes[i];
+          sz.insert(sz.begin(), chunk_rows);
+          pipe_->ring[d].push_back(dev_empty(sz, dts[i], dev, compute.stream()));
+        }
+      // fresh pool blocks of the compute stream: work queued there earlier may
+      // still read them; the first H2D writes wait for it
+      order_copy_after_compute(h2d.stream(), compute.stream());
+      pipe_->ev_comp.resize(depth);
+      pipe_->ev_d2h.resize(depth);
+      for (int d = 0; d < depth; ++d) {
+        HIP_OK(hipEventCreateWithFlags(&pipe_->ev_comp[d], hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&pipe_->ev_d2h[d], hipEventDisableTiming));
+      }
+      pipe_->used.assign(depth, false);
+    }
   }
-  std::vector<bool> used(depth, false);
+  Pipe& P = *pipe_;
+  for (size_t s = 0; s < seg_inputs.size(); ++s)
+    for (size_t i = 0; i < nin; ++i) {
+      auto sz = seg_inputs[s][i].sizes().vec();
+      sz.erase(sz.begin());
+      TFA_CHECK(sz == P.shapes[i] && seg_inputs[s][i].scalar_type() == P.dtypes[i],
+                "run_chunked: segments disagree on the row shape / dtype of feed ", i);
+    }
+  std::vector<hipEvent_t> ev_h2d(depth);
+  for (int d = 0; d < depth; ++d) HIP_OK(hipEventCreateWithFlags(&ev_h2d[d], hipEventDisableTiming));
   int64_t h2d_bytes = 0, d2h_bytes = 0;
   // per-stage device time (hipEvent pairs bracketing each chunk's H2D, compute
   // and D2H on their streams; read once after the final synchronisation)
-  const bool timed = stage_timers_enabled();
+  const bool timed = stage_timers_enabled() && wait;
   std::vector<std::array<hipEvent_t, 6>> tev;
   auto stamp = [&](size_t ci, int k, hipStream_t s) {
     if (!timed) return;
@@ -1632,18 +1694,19 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
   if (timed) tev.assign(chunks.size(), std::array<hipEvent_t, 6>{});
   for (size_t ci = 0; ci < chunks.size(); ++ci) {
     const Chunk& ch = chunks[ci];
-    int slot = static_cast<int>(ci % depth);
-    // H2D: wait until the compute (and any D2H of outputs aliasing the ring) of this slot finished
-    if (used[slot]) {
-      HIP_OK(hipStreamWaitEvent(h2d.stream(), ev_comp[slot], 0));
-      HIP_OK(hipStreamWaitEvent(h2d.stream(), ev_d2h[slot], 0));
+    const int slot = static_cast<int>(P.next++ % depth);
+    // H2D: wait until the compute (and any D2H of outputs aliasing the ring)
+    // of the chunk that last used this slot finished (maybe in an earlier call)
+    if (P.used[slot]) {
+      HIP_OK(hipStreamWaitEvent(h2d.stream(), P.ev_comp[slot], 0));
+      HIP_OK(hipStreamWaitEvent(h2d.stream(), P.ev_d2h[slot], 0));
     }
     std::vector<at::Tensor> dev_in;
     stamp(ci, 0, h2d.stream());
     for (size_t i = 0; i < nin; ++i) {
       const at::Tensor& src = seg_inputs[ch.seg][i];
       int64_t row_bytes = src.numel() / std::max<int64_t>(src.size(0), 1) * src.element_size();
-      at::Tensor dst = ring[slot][i].narrow(0, 0, ch.rows);
+      at::Tensor dst = P.ring[slot][i].narrow(0, 0, ch.rows);
       const char* sp = static_cast<const char*>(src.data_ptr()) + ch.start * row_bytes;
       if (ch.rows * row_bytes)
         HIP_OK(hipMemcpyAsync(dst.data_ptr(), sp, ch.rows * row_bytes, hipMemcpyHostToDevice, h2d.stream()));
@@ -1662,9 +1725,9 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
       outs = execute(*p, dev_in, compute.stream());
     }
     stamp(ci, 3, compute.stream());
-    HIP_OK(hipEventRecord(ev_comp[slot], compute.stream()));
+    HIP_OK(hipEventRecord(P.ev_comp[slot], compute.stream()));
     // D2H
-    HIP_OK(hipStreamWaitEvent(d2h.stream(), ev_comp[slot], 0));
+    HIP_OK(hipStreamWaitEvent(d2h.stream(), P.ev_comp[slot], 0));
     stamp(ci, 4, d2h.stream());
     for (size_t j = 0; j < outs.size(); ++j) {
       at::Tensor o = outs[j];
@@ -1680,18 +1743,28 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
       d2h_bytes += ch.rows * row_bytes;
     }
     stamp(ci, 5, d2h.stream());
-    HIP_OK(hipEventRecord(ev_d2h[slot], d2h.stream()));
-    used[slot] = true;
+    HIP_OK(hipEventRecord(P.ev_d2h[slot], d2h.stream()));
+    P.used[slot] = true;
     stats_.chunks++;
   }
-  HIP_OK(hipStreamSynchronize(h2d.stream()));
-  HIP_OK(hipStreamSynchronize(compute.stream()));
-  HIP_OK(hipStreamSynchronize(d2h.stream()));
-  for (int d = 0; d < depth; ++d) {
-    hipEventDestroy(ev_h2d[d]);
-    hipEventDestroy(ev_comp[d]);
-    hipEventDestroy(ev_d2h[d]);
+  int64_t handle = 0;
+  if (wait) {
+    HIP_OK(hipStreamSynchronize(h2d.stream()));
+    HIP_OK(hipStreamSynchronize(compute.stream()));
+    HIP_OK(hipStreamSynchronize(d2h.stream()));
+    // drained: the ring goes back to the pool (only a deferred sequence of
+    // calls keeps it, to continue the slot rotation)
+    drop_pipe(true);
+  } else {
+    // completion of this call = its last D2H (which waited for the last
+    // compute, which waited for the last H2D)
+    hipEvent_t done;
+    HIP_OK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(done, d2h.stream()));
+    handle = reinterpret_cast<int64_t>(done);
   }
+  // ev_h2d: compute already waits on them; destroying a recorded event is safe
+  for (int d = 0; d < depth; ++d) hipEventDestroy(ev_h2d[d]);
   double stage_ms[3] = {0, 0, 0};
   for (auto& e : tev) {
     for (int k = 0; k < 3; ++k) {
@@ -1708,6 +1781,7 @@ void Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs
   stats_.h2d_ms += stage_ms[0];
   stats_.compute_ms += stage_ms[1];
   stats_.d2h_ms += stage_ms[2];
+  return handle;
 }
 
 std::vector<at::Tensor> Program::run_chunked_reduce(const std::vector<std::vector<at::Tensor>>& seg_inputs,

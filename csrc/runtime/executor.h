@@ -74,9 +74,23 @@ class Program {
   // Pipelined host->device->host execution over row chunks of several segments.
   // seg_inputs[s][i]: pinned host tensor for feed i of segment s (leading dim = rows).
   // seg_outputs[s][j]: preallocated pinned host tensor for fetch j.
-  void run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
-                   const std::vector<std::vector<at::Tensor>>& seg_outputs, int64_t chunk_rows,
-                   int device, int depth);
+  //
+  // The ring of device input slots and the per-slot events persist across
+  // calls (one pipeline per program and device): a call continues the slot
+  // rotation of the previous one, so its first H2D waits only for the compute
+  // of the chunk that last used that slot, not for the whole previous call.
+  // wait = false: return as soon as every copy and kernel is enqueued (no
+  // synchronisation); the result is an event handle that completes when the
+  // last D2H has landed (pipeline_wait). The caller keeps seg_inputs and
+  // seg_outputs alive until then. wait = true: returns 0 after the drain.
+  int64_t run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inputs,
+                      const std::vector<std::vector<at::Tensor>>& seg_outputs, int64_t chunk_rows,
+                      int device, int depth, bool wait = true);
+
+  void release_pipeline() {
+    std::lock_guard<std::mutex> lk(pipe_mu_);
+    drop_pipe(false);
+  }
 
   // Pipelined host->device reduction over row chunks (reduce_blocks of host
   // partitions): every chunk's fetches are copied into slot c of a device
@@ -122,7 +136,26 @@ class Program {
   // needs them first; a run on another stream waits for that copy's event
   std::map<std::pair<int, void*>, void*> const_events_;  // (device, upload stream) -> hipEvent_t
   ExecStats stats_;
+  // persistent chunk pipeline of run_chunked (see there)
+  struct Pipe {
+    int device = -1, depth = 0;
+    int64_t rows = 0;                          // ring capacity in rows
+    std::vector<std::vector<int64_t>> shapes;  // per feed: row shape
+    std::vector<at::ScalarType> dtypes;
+    std::vector<std::vector<at::Tensor>> ring; // [slot][feed]
+    std::vector<hipEvent_t> ev_comp, ev_d2h;   // per slot: last compute / D2H that used it
+    std::vector<bool> used;
+    int64_t next = 0;                          // chunk counter (slot = next % depth)
+  };
+  std::mutex pipe_mu_;
+  std::unique_ptr<Pipe> pipe_;
+  // caller holds pipe_mu_: free ring and events (draining the streams first
+  // unless `synced`)
+  void drop_pipe(bool synced);
 };
+
+// waits for (and releases) an event handle returned by run_chunked(wait=false)
+void pipeline_wait(int64_t handle);
 
 // pinned host memory (hipHostMalloc, exact size; freed with hipHostFree)
 at::Tensor empty_pinned(const std::vector<int64_t>& sizes, at::ScalarType dt);

@@ -322,11 +322,44 @@ def chunk_rows_for(inputs: List[torch.Tensor], total_rows: Optional[int] = None)
     return max(1, (4 << 20) // row_bytes, rows)
 
 
+_defer = threading.local()
+
+
+class deferred_pipelines:
+    """Inside this context, pipelined runs (run_segments_pipelined) return as
+    soon as their copies and kernels are enqueued; their completions collect
+    in the yielded list. A streaming action enqueues the next group of
+    partitions before it waits for the previous one (wait_pipelines), so the
+    chunk pipeline runs on across group boundaries (the next group's first H2D
+    overlaps the previous group's last chunks) instead of draining and
+    ramping up once per group."""
+
+    def __enter__(self):
+        self.prev = getattr(_defer, "handles", None)
+        self.handles = []
+        _defer.handles = self.handles
+        return self.handles
+
+    def __exit__(self, *exc):
+        _defer.handles = self.prev
+        if exc[0] is not None:
+            wait_pipelines(self.handles)  # nothing may outlive its DMA
+        return False
+
+
+def wait_pipelines(handles: list) -> None:
+    """Block until the deferred pipelined runs in `handles` have landed."""
+    while handles:
+        _prog, h, _keep = handles.pop(0)
+        _C.pipeline_wait(h)
+
+
 def run_segments_pipelined(prog, segments: List[List[torch.Tensor]],
                            out_specs: List[List[Tuple[tuple, torch.dtype]]]) -> List[List[torch.Tensor]]:
     """Pipelined H2D/compute/D2H over row chunks of several host segments.
 
     out_specs[s][j] = (full output shape, dtype) of fetch j for segment s.
+    Inside `deferred_pipelines()` it returns before the outputs have landed.
     """
     dev = compute_device()
     segs = [[pin(t.contiguous()) for t in seg] for seg in segments]
@@ -334,8 +367,13 @@ def run_segments_pipelined(prog, segments: List[List[torch.Tensor]],
     total = sum(seg[0].shape[0] for seg in segs if seg)
     chunk = chunk_rows_for(segs[0], total) if segs and segs[0] else 1 << 16
     before = prog.stats()
+    handles = getattr(_defer, "handles", None)
     with metrics.timer("pipelined"):
-        prog.run_chunked(segs, outs, chunk, dev.index or 0, config.pipeline_depth)
+        h = prog.run_chunked(segs, outs, chunk, dev.index or 0, config.pipeline_depth, handles is None)
+    if handles is not None:
+        # the staged inputs and the outputs stay referenced until the wait
+        handles.append((prog, h, (segs, outs)))
+        metrics.add("pipelines_deferred")
     st = prog.stats()
     # this call's share of the program's cumulative counters; the *_device_ms
     # stage times come from hipEvent pairs around each chunk's copies/kernels

@@ -76,19 +76,48 @@ class _Derived(_Source):
         call spans several partitions (one H2D ramp-up per group, not per
         partition) while memory stays bounded."""
         from ..config import config
+        from .. import engine
         group: Dict[int, Block] = {}
         nbytes = 0
-        for pid, b in self._parent._iter_blocks():
-            group[pid] = b
-            nbytes += _block_bytes(b)
-            if nbytes >= config.stream_group_bytes or len(group) >= _MAX_GROUP_PARTITIONS:
-                yield from self._run_group(group)
-                group, nbytes = {}, 0
-        if group:
-            yield from self._run_group(group)
+        pending = None  # (group, results, completion handles) enqueued, not yet waited
+        progs = set()
+        try:
+            for pid, b in self._parent._iter_blocks():
+                group[pid] = b
+                nbytes += _block_bytes(b)
+                if nbytes >= config.stream_group_bytes or len(group) >= _MAX_GROUP_PARTITIONS:
+                    # enqueue this group, THEN wait for (and hand out) the
+                    # previous one: the chunk pipeline never drains between groups
+                    nxt = self._start_group(group, progs)
+                    if pending is not None:
+                        yield from self._finish_group(pending)
+                    pending = nxt
+                    group, nbytes = {}, 0
+            if group:
+                nxt = self._start_group(group, progs)
+                if pending is not None:
+                    yield from self._finish_group(pending)
+                pending = nxt
+            if pending is not None:
+                done, pending = pending, None
+                yield from self._finish_group(done)
+        finally:
+            if pending is not None:
+                engine.wait_pipelines(pending[2])
+            for prog in progs:
+                prog.release_pipeline()
 
-    def _run_group(self, group: Dict[int, Block]):
-        res = self._fn(group)
+    def _start_group(self, group: Dict[int, Block], progs: set):
+        from .. import engine
+        with engine.deferred_pipelines() as handles:
+            res = self._fn(group)
+        progs.update(h[0] for h in handles)
+        return group, res, list(handles)
+
+    def _finish_group(self, pending):
+        from .. import engine
+        group, res, handles = pending
+        engine.wait_pipelines(handles)
         for pid in sorted(group):
             yield pid, res[pid]
 
