@@ -1612,12 +1612,28 @@ def _shuffle_blocks(send: List[List[Block]], names: List[str], tf_types: Dict[st
     dev = engine.compute_device() if engine.compute_device().type == "cuda" and dist.gpu_collectives() \
         else torch.device("cpu")
     cols: Dict[str, Any] = {}
+    dense = [n for n in names if kinds[n] is not None]
+    if dense:
+        # every dense column of a row packed into one byte record: the rows
+        # move in ONE all_to_all, not one per column
+        widths = [int(np.prod(kinds[n][1] or (1,))) * torch.empty((), dtype=kinds[n][0]).element_size()
+                  for n in dense]
+        chunks = []
+        for p in per:
+            if p is not None and p.nrows:
+                chunks.append(torch.cat([p.columns[n].to(dev).contiguous().reshape(p.nrows, -1).view(torch.uint8)
+                                         for n in dense], 1))
+            else:
+                chunks.append(engine.device_empty((0, sum(widths)), torch.uint8, dev))
+        rec = dist.all_to_all_tensors(chunks, recv_rows)
+        off = 0
+        for n, wb in zip(dense, widths):
+            dtype, cell = kinds[n]
+            cols[n] = rec[:, off:off + wb].contiguous().view(dtype).reshape((rec.shape[0],) + tuple(cell))
+            off += wb
     for j, n in enumerate(names):
         if kinds[n] is not None:
-            dtype, cell = kinds[n]
-            chunks = [p.columns[n].to(dev) if p is not None and p.nrows else
-                      engine.device_empty((0,) + cell, dtype, dev) for p in per]
-            cols[n] = dist.all_to_all_tensors(chunks, recv_rows)
+            continue
         else:
             got = dist.all_to_all_objects([column_values(p.columns[n]) if p is not None and p.nrows else []
                                            for p in per])
