@@ -126,10 +126,7 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
   // cycles, profiles/r4_pmc/). Float4-stored images keep a 16-byte pitch.
   constexpr int LDA = AL == A_MCONTIG ? BM + 4 : BM + 2;
   constexpr int LDB = TB ? BN + 2 : BN + 4;
-  const int vepi = flags & 1;
-  // flags bit 1: static priority for the second half of an 8-wave block (the
-  // younger waves lose every issue arbitration to their SIMD partner)
-  if (NT == 512 && (flags & 2) && (threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
+  const int vepi = flags & 1;  // bit 0: vector epilogue
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves, >= one 32x32 tile each");
   constexpr int KQ = BK / 4;  // float4 pieces along k
@@ -623,18 +620,9 @@ int vector_epilogue(const GemmArgs& g) {
   return 1;
 }
 
-// TFA_GEMM_PRIO=1: static s_setprio(1) for waves 4-7 of the 8-wave tiles
-int prio_flag() {
-  static const int v = [] {
-    const char* e = std::getenv("TFA_GEMM_PRIO");
-    return e && std::atoi(e) ? 2 : 0;
-  }();
-  return v;
-}
-
 template <int AL, bool TB, bool VEC>
 void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s) {
-  const int vepi = (p.splits == 1 ? vector_epilogue(g) : 0) | prio_flag();
+  const int vepi = p.splits == 1 ? vector_epilogue(g) : 0;
   const int64_t tm = (g.M + p.bm - 1) / p.bm, tn = (g.N + p.bn - 1) / p.bn;
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
   TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");

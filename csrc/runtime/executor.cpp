@@ -1,5 +1,7 @@
 // Planner + executor (see executor.h).
 #include "executor.h"
+
+#include <optional>
 #include "device_pool.h"
 
 
@@ -234,6 +236,26 @@ struct Program::Plan {
       if (stream) (void)hipStreamDestroy(stream);
     }
   } cap;
+  // zero-copy replays for device inputs that come back at the same addresses
+  // (device-cached partitions of an iterative workload): the graph is
+  // captured on the caller's own input tensors, so a replay copies nothing in;
+  // keyed by the input data pointers (same plan => same shapes and dtypes)
+  struct PtrCap {
+    std::unique_ptr<HipGraph> graph;
+    std::vector<at::Tensor> static_out;
+    hipStream_t stream = nullptr;
+    int64_t last_use = 0;
+    ~PtrCap() {
+      graph.reset();
+      if (stream) (void)hipStreamDestroy(stream);
+    }
+  };
+  std::mutex ptr_mu;
+  std::map<std::vector<const void*>, int> ptr_seen;  // pointer set -> runs seen (bounded)
+  std::map<std::vector<const void*>, std::unique_ptr<PtrCap>> ptr_caps;
+  int64_t ptr_tick = 0;
+  bool ptr_declined = false;
+  int64_t ptr_eager_ns = 0, ptr_eager_n = 0, ptr_replay_ns = 0, ptr_replay_n = 0;
 };
 
 Program::Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetches,
@@ -1496,6 +1518,101 @@ std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor
   return outs;
 }
 
+namespace {
+constexpr int kPtrWarmRuns = 2;       // eager runs of a pointer set before it is captured
+constexpr size_t kPtrMinSteps = 4;    // no input copies: worth it from a few kernels on
+constexpr size_t kPtrMaxCaps = 8;     // captures per plan (each owns its intermediates)
+constexpr size_t kPtrMaxSeen = 32;
+int64_t ptr_graph_max_bytes() {
+  static const int64_t v = env_positive("TFA_HIP_GRAPH_PTR_MAX_BYTES", int64_t(256) << 20);
+  return v;
+}
+}  // namespace
+
+std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std::vector<at::Tensor>& inputs,
+                                                               int64_t bytes) {
+  if (hip_graphs_mode() != 1 || p.ptr_declined || p.cap_reset || bytes > ptr_graph_max_bytes() ||
+      p.steps.size() < kPtrMinSteps || inputs.empty())
+    return std::nullopt;
+  for (auto& t : inputs)
+    if (!t.is_cuda() || !t.is_contiguous()) return std::nullopt;
+  std::vector<const void*> key;
+  key.reserve(inputs.size());
+  for (auto& t : inputs) key.push_back(t.data_ptr());
+  std::lock_guard<std::mutex> lk(p.ptr_mu);
+  const int dev = inputs[0].device().index();
+  hipStream_t cur = c10::hip::getCurrentHIPStream(dev).stream();
+  auto it = p.ptr_caps.find(key);
+  if (it == p.ptr_caps.end()) {
+    int& seen = p.ptr_seen[key];
+    if (p.ptr_seen.size() > kPtrMaxSeen) {  // a stream of fresh pointers: not an iterative workload
+      p.ptr_seen.clear();
+      return std::nullopt;
+    }
+    if (++seen <= kPtrWarmRuns || !graphable(p)) {
+      if (seen > 1) {  // warm eager run: the baseline a replay must beat
+        const int64_t t0 = now_ns();
+        auto outs = execute(p, inputs, cur);
+        p.ptr_eager_ns += now_ns() - t0;
+        p.ptr_eager_n++;
+        return outs;
+      }
+      return std::nullopt;
+    }
+    // capture on a private stream, on the caller's own tensors
+    if (p.ptr_caps.size() >= kPtrMaxCaps) {  // evict the least recently used
+      auto lru = p.ptr_caps.begin();
+      for (auto j = p.ptr_caps.begin(); j != p.ptr_caps.end(); ++j)
+        if (j->second->last_use < lru->second->last_use) lru = j;
+      if (lru->second->stream) (void)hipStreamSynchronize(lru->second->stream);
+      (void)hipStreamSynchronize(cur);  // its replays (on cur) are done before its pool goes
+      p.ptr_caps.erase(lru);
+    }
+    auto pc = std::make_unique<Plan::PtrCap>();
+    TFA_CHECK(hipStreamCreateWithFlags(&pc->stream, hipStreamNonBlocking) == hipSuccess, "hipStreamCreate failed");
+    hipEvent_t ev;
+    TFA_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+    (void)hipEventRecord(ev, cur);
+    (void)hipStreamWaitEvent(pc->stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    auto g = std::make_unique<HipGraph>();
+    try {
+      c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromExternal(pc->stream, dev));
+      g->begin(pc->stream, dev);
+      pc->static_out = execute(p, inputs, pc->stream);
+      g->end();
+    } catch (const std::exception&) {
+      g->abort();
+      g.release();  // its pool may back tensors of the failed capture; leak it
+      p.ptr_declined = true;
+      stats_.graph_failures++;
+      return std::nullopt;
+    }
+    pc->graph = std::move(g);
+    stats_.graphs_captured++;
+    it = p.ptr_caps.emplace(key, std::move(pc)).first;
+    p.ptr_seen.erase(key);
+  }
+  Plan::PtrCap& pc = *it->second;
+  pc.last_use = ++p.ptr_tick;
+  const int64_t t0 = now_ns();
+  pc.graph->replay(cur);
+  std::vector<at::Tensor> outs;
+  outs.reserve(pc.static_out.size());
+  for (auto& o : pc.static_out) outs.push_back(dev_clone(o.contiguous(), cur));
+  stats_.graph_replays++;
+  // the first replays are timed against the warm eager runs; a plan whose
+  // replays cost more host time than launching its kernels keeps running eagerly
+  if (p.ptr_eager_n > 0 && p.ptr_replay_n < kGraphProbeRuns) {
+    p.ptr_replay_ns += now_ns() - t0;
+    if (++p.ptr_replay_n == kGraphProbeRuns && p.ptr_replay_ns * p.ptr_eager_n > p.ptr_eager_ns * p.ptr_replay_n) {
+      p.ptr_declined = true;
+      stats_.graphs_declined++;
+    }
+  }
+  return outs;
+}
+
 std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
   TFA_CHECK(host_op_error_.empty(), host_op_error_);
   auto p = plan_for(inputs);
@@ -1512,10 +1629,22 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
     if (hip_graphs_enabled()) {
       int64_t bytes = 0;
       for (auto& t : inputs) bytes += t.numel() * t.element_size();
+      if (auto outs = run_ptr_graph(*p, inputs, bytes)) {
+        stats_.runs++;
+        return std::move(*outs);
+      }
       auto& c = p->cap;
       std::lock_guard<std::mutex> lk(c.mu);
       if (p->cap_reset) {
         p->cap_reset = false;
+        {
+          std::lock_guard<std::mutex> pl(p->ptr_mu);
+          for (auto& kv : p->ptr_caps)
+            if (kv.second->stream) (void)hipStreamSynchronize(kv.second->stream);
+          if (!p->ptr_caps.empty()) (void)hipDeviceSynchronize();
+          p->ptr_caps.clear();
+          p->ptr_seen.clear();
+        }
         if (c.graph) {
           if (c.stream) (void)hipStreamSynchronize(c.stream);
           c.graph.reset();

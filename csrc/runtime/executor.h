@@ -15,6 +15,7 @@
 #include <tuple>
 #include <memory>
 #include <mutex>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -121,6 +122,8 @@ class Program {
   void refresh_consts(Plan& p, int di, void* stream);
   bool graphable(const Plan& p) const;
   std::vector<at::Tensor> run_graph(Plan& p, const std::vector<at::Tensor>& inputs);
+  std::optional<std::vector<at::Tensor>> run_ptr_graph(Plan& p, const std::vector<at::Tensor>& inputs,
+                                                       int64_t bytes);
 
   std::shared_ptr<Graph> g_;
   std::vector<std::string> fetch_names_, feed_names_;

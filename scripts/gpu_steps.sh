@@ -23,7 +23,6 @@ for s in ${STEPS:-tests}; do
   case $s in
     pmc) run pmc 900 bash scripts/pmc_gemm.sh ;;
     comm) run comm 300 python -u -m pytest tests/test_gpu_comm.py tests/test_rccl.py tests/test_multirank_gpu.py -x -v --timeout 120 --timeout-method thread ;;
-    prio_ab) for p in 0 1 0 1; do TFA_GEMM_PRIO=$p TFA_GEMM_TILE=13 run prio_g_$p 120 python scripts/gemm_one.py gemm 4096 4096 4096 --iters 50; grep '{' gpurun_out/prio_g_$p.log; TFA_GEMM_PRIO=$p TFA_GEMM_TILE=15 run prio_c_$p 120 python scripts/gemm_one.py conv 2048 25 25 288 3 3 384 2 VALID --iters 20; grep '{' gpurun_out/prio_c_$p.log; done ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_plan_reuse.py tests/test_gpu_engine.py tests/test_models.py tests/test_gpu_models.py tests/test_fusion.py -x -q --timeout 120 --timeout-method thread ;;
     ab) for i in 1 2; do run ab_old_$i 300 python ab_old/scripts/gemm_bench.py --json gpurun_out/ab_old_$i.json; run ab_new_$i 300 python scripts/gemm_bench.py --json gpurun_out/ab_new_$i.json; done ;;

@@ -108,10 +108,45 @@ def test_hip_graph_replay_matches_eager_and_outputs_do_not_alias():
         refs.append(engine.run_program(prog, [xin], torch.device("cpu")))
     torch.cuda.synchronize()
     st = prog.stats()
-    assert st["graphs_captured"] == 1 and st["graph_replays"] >= 4 and st["graph_failures"] == 0
+    assert st["graphs_captured"] >= 1 and st["graph_replays"] >= 4 and st["graph_failures"] == 0
     for o, r in zip(outs, refs):
         for a, b in zip(o, r):
             torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-4)
+
+
+def test_zero_copy_replay_for_device_inputs_at_stable_addresses():
+    """Device inputs that come back at the same addresses (the partitions of a
+    device-cached frame, run every iteration) are captured on the caller's own
+    tensors and replayed with no input copy: the replay must read the CURRENT
+    contents of those tensors (updated in place between runs), outputs of
+    earlier runs must stay intact, and a 20 MB input is no obstacle."""
+    import numpy as np
+    from tensorframes_amd import engine, tf
+    rng = np.random.default_rng(4)
+    c = rng.standard_normal((10, 100))
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.double, [None, 100], name="x")
+        d = tf.reduce_sum(tf.square(x), [1], keep_dims=True) - 2 * tf.matmul(x, tf.constant(c), transpose_b=True)
+        tf.argmin(d, 1, name="i")
+        tf.reduce_min(d, [1], name="m")
+    prog = engine.program(g.serialize(), ["i", "m"], ["x"])
+    dev = torch.device("cuda", 0)
+    parts = [torch.randn((25000, 100), dtype=torch.float64, device=dev) for _ in range(2)]
+    before = prog.stats()
+    outs = []
+    for it in range(6):
+        for p in parts:
+            p.mul_(1.01)  # in place: same address, new values
+            outs.append((engine.run_program(prog, [p], dev), p.cpu().numpy().copy()))
+    torch.cuda.synchronize()
+    st = prog.stats()
+    assert st["graph_replays"] - before["graph_replays"] >= 6
+    assert st["graphs_captured"] - before["graphs_captured"] == 2  # one per partition address
+    for (i, m), xin in outs:
+        dd = (xin ** 2).sum(1, keepdims=True) - 2 * xin @ c.T
+        np.testing.assert_array_equal(i.cpu().numpy(), dd.argmin(1))
+        np.testing.assert_allclose(m.cpu().numpy(), dd.min(1), rtol=1e-9, atol=1e-9)
 
 
 def test_pipeline_stage_device_timers():

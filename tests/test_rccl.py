@@ -28,6 +28,10 @@ def rccl_group(monkeypatch):
         assert dist.init(backend="nccl", force=True)
         assert tdist.get_backend() == "nccl" and tdist.get_world_size() == 1
         assert dist.gpu_collectives()
+        from tensorframes_amd.parallel import comm
+        # the engine communicator is built once, collectively (its one-time
+        # setup exchanges device ids and IPC handles over the host group)
+        assert comm.get() is not None
         yield dist
     finally:
         dist.shutdown()
