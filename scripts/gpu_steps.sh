@@ -22,6 +22,7 @@ run() {
 for s in ${STEPS:-tests}; do
   case $s in
     pmc) run pmc 900 bash scripts/pmc_gemm.sh ;;
+    engine) run engine 300 python -u -m pytest tests/test_gpu_engine.py tests/test_streaming.py tests/test_gpu_string_keys.py -x -v --timeout 120 --timeout-method thread ;;
     comm) run comm 300 python -u -m pytest tests/test_gpu_comm.py tests/test_rccl.py tests/test_multirank_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_plan_reuse.py tests/test_gpu_engine.py tests/test_models.py tests/test_gpu_models.py tests/test_fusion.py -x -q --timeout 120 --timeout-method thread ;;

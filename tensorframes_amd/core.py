@@ -1231,22 +1231,26 @@ def _to_host_batched(vals: Dict[str, torch.Tensor]) -> Dict[str, np.ndarray]:
     """Device results to numpy with one device->host copy per dtype (each copy
     is a synchronisation) instead of one per fetch."""
     out: Dict[str, np.ndarray] = {}
-    by_dtype: Dict[Any, List[str]] = {}
+    dev_names = []
     for n, v in vals.items():
         if v.is_cuda:
-            by_dtype.setdefault(v.dtype, []).append(n)
+            dev_names.append(n)
         else:
             out[n] = v.numpy()
-    for names in by_dtype.values():
-        if len(names) == 1:
-            out[names[0]] = vals[names[0]].cpu().numpy()
-            continue
-        flat = engine.cat_rows([vals[n].reshape(-1) for n in names]).cpu().numpy()
+    if len(dev_names) == 1:
+        n = dev_names[0]
+        out[n] = vals[n].cpu().numpy()
+    elif dev_names:
+        # every result as raw bytes in ONE buffer: one device->host copy (one
+        # synchronisation) whatever the mix of dtypes
+        flat = engine.cat_rows([vals[n].contiguous().reshape(-1).view(torch.uint8) for n in dev_names]).cpu().numpy()
         off = 0
-        for n in names:
-            k = vals[n].numel()
-            out[n] = flat[off:off + k].reshape(tuple(vals[n].shape))
-            off += k
+        for n in dev_names:
+            v = vals[n]
+            nb = v.numel() * v.element_size()
+            npdt = torch.empty((), dtype=v.dtype).numpy().dtype
+            out[n] = flat[off:off + nb].view(npdt).reshape(tuple(v.shape))
+            off += nb
     return out
 
 
@@ -1280,10 +1284,13 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     def task(blocks):
         res = {}
         dense_of = {}
-        if uniform and len(blocks) > 1:
-            # every fetch is op(x_input, axis=0): this rank's device-resident
-            # partitions are one block for the graph, so a concatenation per
-            # column replaces a reduction per partition per fetch plus a stack
+        if len(blocks) > 1:
+            # this rank's device-resident partitions are one block for the
+            # graph: a concatenation per column replaces a run per partition
+            # plus a run over the stacked partials. Valid for ANY reducer graph
+            # under the reduce_blocks contract (the graph takes any lead dim
+            # and is associative over stacked partials: reference
+            # DebugRowOps.scala:503-526, :741-750)
             dense = [(pid, _dense_inputs(b, cols, "reduce_blocks")) for pid, b in sorted(blocks.items())
                      if b.nrows > 0]
             dense_of = dict(dense)

@@ -128,9 +128,12 @@ def test_zero_copy_replay_for_device_inputs_at_stable_addresses():
     with g.as_default():
         x = tf.placeholder(tf.double, [None, 100], name="x")
         d = tf.reduce_sum(tf.square(x), [1], keep_dims=True) - 2 * tf.matmul(x, tf.constant(c), transpose_b=True)
-        tf.argmin(d, 1, name="i")
+        idx = tf.argmin(d, 1, name="i")
         tf.reduce_min(d, [1], name="m")
-    prog = engine.program(g.serialize(), ["i", "m"], ["x"])
+        # the K-Means per-cluster sums: a few more kernels (>= 4 steps)
+        tf.unsorted_segment_sum(x, idx, 10, name="s")
+        tf.reduce_sum(tf.unsorted_segment_sum(tf.ones_like(d), idx, 10), [1], name="n")
+    prog = engine.program(g.serialize(), ["i", "m", "s", "n"], ["x"])
     dev = torch.device("cuda", 0)
     parts = [torch.randn((25000, 100), dtype=torch.float64, device=dev) for _ in range(2)]
     before = prog.stats()
@@ -141,12 +144,17 @@ def test_zero_copy_replay_for_device_inputs_at_stable_addresses():
             outs.append((engine.run_program(prog, [p], dev), p.cpu().numpy().copy()))
     torch.cuda.synchronize()
     st = prog.stats()
-    assert st["graph_replays"] - before["graph_replays"] >= 6
     assert st["graphs_captured"] - before["graphs_captured"] == 2  # one per partition address
-    for (i, m), xin in outs:
+    assert st["graph_replays"] - before["graph_replays"] >= 4
+    for (i, m, sm, n), xin in outs:
         dd = (xin ** 2).sum(1, keepdims=True) - 2 * xin @ c.T
-        np.testing.assert_array_equal(i.cpu().numpy(), dd.argmin(1))
+        want_i = dd.argmin(1)
+        np.testing.assert_array_equal(i.cpu().numpy(), want_i)
         np.testing.assert_allclose(m.cpu().numpy(), dd.min(1), rtol=1e-9, atol=1e-9)
+        want_s = np.zeros((10, 100))
+        np.add.at(want_s, want_i, xin)
+        np.testing.assert_allclose(sm.cpu().numpy(), want_s, rtol=1e-9, atol=1e-8)
+        np.testing.assert_allclose(n.cpu().numpy(), np.bincount(want_i, minlength=10) * 10.0)
 
 
 def test_pipeline_stage_device_timers():
