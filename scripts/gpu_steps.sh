@@ -23,6 +23,13 @@ for s in ${STEPS:-tests}; do
   case $s in
     pmc) run pmc 900 bash scripts/pmc_gemm.sh ;;
     engine) run engine 300 python -u -m pytest tests/test_gpu_engine.py tests/test_streaming.py tests/test_gpu_string_keys.py -x -v --timeout 120 --timeout-method thread ;;
+    comm_bench) run comm_bench 300 python scripts/comm_bench.py ;;
+    comm_bench2) TFA_DIST_BACKEND=gloo run comm_bench2 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 scripts/comm_bench.py ;;
+    read_image) run read_image 600 python examples/read_image.py --images 2048 ;;
+    incep_bf16x3) run incep_bf16x3 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --precision bf16x3 ;;
+    incep_bf16) run incep_bf16 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --precision bf16 ;;
+    f64gemm) run f64gemm 600 python scripts/gemm_bench.py --f64-only ;;
+    strkeys) run strkeys 300 python -u -m pytest tests/test_gpu_string_keys.py -x -v -s --timeout 120 --timeout-method thread ;;
     comm) run comm 300 python -u -m pytest tests/test_gpu_comm.py tests/test_rccl.py tests/test_multirank_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     newtests) run newtests 600 python -u -m pytest tests/test_plan_reuse.py tests/test_gpu_engine.py tests/test_models.py tests/test_gpu_models.py tests/test_fusion.py -x -q --timeout 120 --timeout-method thread ;;
