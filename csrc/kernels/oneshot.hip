@@ -31,38 +31,6 @@ namespace k {
 
 namespace {
 
-template <typename T>
-struct Bits;
-template <>
-struct Bits<float> {
-  using U = uint32_t;
-};
-template <>
-struct Bits<int32_t> {
-  using U = uint32_t;
-};
-template <>
-struct Bits<double> {
-  using U = uint64_t;
-};
-template <>
-struct Bits<int64_t> {
-  using U = uint64_t;
-};
-
-template <typename T>
-__device__ __forceinline__ T sys_load(const T* p) {
-  using U = typename Bits<T>::U;
-  const U u = __hip_atomic_load(reinterpret_cast<const U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return __builtin_bit_cast(T, u);
-}
-
-template <typename T>
-__device__ __forceinline__ void sys_store(T* p, T v) {
-  using U = typename Bits<T>::U;
-  __hip_atomic_store(reinterpret_cast<U*>(p), __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 template <typename T, int OP>
 __device__ __forceinline__ T fold(T a, T b) {
   if constexpr (OP == (int)RedOp::SUM) return a + b;
@@ -71,17 +39,34 @@ __device__ __forceinline__ T fold(T a, T b) {
   return b > a ? b : a;
 }
 
-constexpr int kThreads = 512;
+constexpr int kThreads = 1024;
 constexpr uint64_t kSpinTicks = 10ull * 100000000ull;  // 10 s of the 100 MHz realtime counter
+
+// 8-byte granules: the shared buffers are touched with 64-bit system-scope
+// atomics (half the transactions of 4-byte ones for f32 / i32 payloads)
+template <typename T>
+union Granule {
+  uint64_t u;
+  T v[8 / sizeof(T)];
+};
 
 template <typename T, int OP>
 __global__ __launch_bounds__(kThreads) void oneshot_kernel(const T* in, T* out, int64_t n,
                                                           int rank, int world, OneShotPeers p, uint32_t epoch,
                                                           int slot) {
+  constexpr int E = 8 / sizeof(T);  // elements per granule
   const int tid = threadIdx.x;
+  const int64_t ng = (n + E - 1) / E;
   // 1. publish this rank's partial in its own buffer
-  T* mine = reinterpret_cast<T*>(static_cast<char*>(p.buf[rank]) + slot * kOneShotSlotBytes);
-  for (int64_t i = tid; i < n; i += kThreads) sys_store(mine + i, in[i]);
+  uint64_t* mine = reinterpret_cast<uint64_t*>(static_cast<char*>(p.buf[rank]) + slot * kOneShotSlotBytes);
+  for (int64_t g = tid; g < ng; g += kThreads) {
+    Granule<T> x;
+    x.u = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (g * E + e < n) x.v[e] = in[g * E + e];
+    __hip_atomic_store(mine + g, x.u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // 2. tell every peer (lane r writes rank r's flag word for this rank)
@@ -109,12 +94,22 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(const T* in, T* out, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // 4. fold the N partials in rank order
-  for (int64_t i = tid; i < n; i += kThreads) {
-    T acc = sys_load(reinterpret_cast<const T*>(static_cast<const char*>(p.buf[0]) + slot * kOneShotSlotBytes) + i);
-    for (int r = 1; r < world; ++r)
-      acc = fold<T, OP>(acc, sys_load(reinterpret_cast<const T*>(static_cast<const char*>(p.buf[r]) +
-                                                                  slot * kOneShotSlotBytes) + i));
-    out[i] = acc;
+  for (int64_t g = tid; g < ng; g += kThreads) {
+    Granule<T> acc;
+    acc.u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(static_cast<const char*>(p.buf[0]) +
+                                                                 slot * kOneShotSlotBytes) + g,
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int r = 1; r < world; ++r) {
+      Granule<T> x;
+      x.u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(static_cast<const char*>(p.buf[r]) +
+                                                                 slot * kOneShotSlotBytes) + g,
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc.v[e] = fold<T, OP>(acc.v[e], x.v[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (g * E + e < n) out[g * E + e] = acc.v[e];
   }
 }
 

@@ -27,7 +27,8 @@ pts = rng.uniform(0.0, 1.0, size=(a.points, 100))
 df = tfs.analyze(tfs.from_columns({"features": pts}, num_partitions=4)).cache_on_device(engine.compute_device())
 c0 = np.random.default_rng(2).standard_normal((10, 100))
 agg = a.variant == "in_graph"
-kmeans.kmeans(df, c0, num_iters=1, tf_aggregate=agg)  # warm: plans, JIT, tile tuning
+for _ in range(5):  # warm: plans, JIT, tile tuning, HIP-graph captures of the per-partition runs
+    (kmeans.run_one_step2 if agg else kmeans.run_one_step)(df, c0)
 torch.cuda.synchronize() if torch.cuda.is_available() else None
 prof = None
 if a.cprofile:
@@ -46,5 +47,9 @@ if prof is not None:
     pstats.Stats(prof).sort_stats("tottime").print_stats(25)
     pstats.Stats(prof).sort_stats("cumulative").print_stats(60)
 from tensorframes_amd._native import _C  # noqa: E402
+graphs = {}
+for p in list(engine._prog_cache.values()):
+    for k in ("graphs_captured", "graph_replays", "graphs_declined", "runs"):
+        graphs[k] = graphs.get(k, 0) + p.stats()[k]
 print(json.dumps({"variant": a.variant, "iters": a.iters, "ms_per_iter": dt * 1e3,
-                  "fusion": os.environ.get("TFA_FUSION", "1"), "jit": _C.jit_stats()}))
+                  "fusion": os.environ.get("TFA_FUSION", "1"), "jit": _C.jit_stats(), "programs": graphs}))

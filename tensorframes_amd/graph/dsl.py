@@ -345,6 +345,9 @@ def with_graph():
 
 
 class Operation:
+    # graphs rebuilt per iteration (K-Means) create thousands of these
+    __slots__ = ("graph", "node_def", "_inputs", "outputs", "__weakref__")
+
     def __init__(self, graph: Graph, node: P.NodeDef, n_out: int, out_dtypes: List[DType]):
         self.graph = graph
         self.node_def = node
@@ -386,6 +389,8 @@ class Operation:
 
 
 class Tensor:
+    __slots__ = ("op", "value_index", "_dtype", "_rank", "__weakref__")
+
     def __init__(self, op: Operation, value_index: int, dtype: Optional[DType]):
         self.op = op
         self.value_index = value_index

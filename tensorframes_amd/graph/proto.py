@@ -75,6 +75,8 @@ class TensorProto:
 class AttrValue:
     """kind in {list, s, i, f, b, type, shape, tensor, placeholder, func}."""
 
+    __slots__ = ("kind", "value")
+
     def __init__(self, kind: str, value):
         self.kind = kind
         self.value = value
@@ -146,6 +148,8 @@ _B_ATTRS = {False: AttrValue("b", False), True: AttrValue("b", True)}
 
 
 class NodeDef:
+    __slots__ = ("name", "op", "input", "attr", "device")
+
     def __init__(self, name: str, op: str, input: Optional[List[str]] = None,  # noqa: A002
                  attr: Optional[Dict[str, AttrValue]] = None, device: str = ""):
         self.name = name
