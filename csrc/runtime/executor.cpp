@@ -1447,7 +1447,10 @@ int64_t hip_graph_max_bytes() {
 }
 }  // namespace
 
-bool Program::graphable(const Plan& p) const {
+bool Program::graphable(const Plan& p) const { return graph_blocker(p).empty(); }
+
+// why a plan cannot be captured into a HIP graph ("" = it can)
+std::string Program::graph_blocker(const Plan& p) const {
   // every plan-time (host) input must be a known constant: a data-dependent
   // one would need a device->host sync, which a capture cannot contain
   static const std::set<std::string> kRuntimeHostCopies = {
@@ -1455,17 +1458,22 @@ bool Program::graphable(const Plan& p) const {
   const OpRegistry& reg = OpRegistry::get();
   for (auto& st : p.steps) {
     const std::string& op = g_->node(st.node).op;
-    if (kRuntimeHostCopies.count(op)) return false;  // host->device copies at run time
+    const std::string& nm = g_->node(st.node).name;
+    if (kRuntimeHostCopies.count(op)) return str_cat(op, " '", nm, "' copies host data at run time");
+    // a fused region / GEMM / conv step launches generated or fixed kernels
+    // on device operands only: its op's host inputs were consumed at plan time
+    if (st.kind != Step::OP) continue;
     const OpDef* od = reg.find(op);
-    if (!od) return false;
+    if (!od) return str_cat(op, " '", nm, "' has no registered op");
     for (int hi : od->host_inputs) {
       if (hi < 0 || hi >= static_cast<int>(st.in_info.size())) continue;
-      if (!st.in_info[hi]->value) return false;
+      if (!st.in_info[hi]->value) return str_cat(op, " '", nm, "': host input ", hi, " is not a plan-time constant");
     }
     // scalar operands read on the host at run time when not constant
-    if (op == "Fill" && st.in_info.size() > 1 && !st.in_info[1]->value) return false;
+    if (op == "Fill" && st.in_info.size() > 1 && !st.in_info[1]->value)
+      return str_cat("Fill '", nm, "': value read on the host");
   }
-  return !p.steps.empty();
+  return p.steps.empty() ? "no steps" : "";
 }
 
 std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor>& inputs) {
@@ -2027,6 +2035,10 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
   os << "plan: " << p->steps.size() << " steps, " << p->const_slots.size() << " constants, "
      << p->fused << " fused epilogues, " << p->fused_regions.size() << " fused regions";
   if (p->fused_siblings) os << ", " << p->fused_siblings << " sibling convs fused";
+  {
+    const std::string why = graph_blocker(*p);
+    os << (why.empty() ? ", graphable" : ", not graphable (" + why + ")");
+  }
   os << "\n";
   for (auto& st : p->steps) {
     const Node& nd = g_->node(st.node);

@@ -121,6 +121,7 @@ class Program {
   void wait_consts(const at::Device& dev, void* stream);
   void refresh_consts(Plan& p, int di, void* stream);
   bool graphable(const Plan& p) const;
+  std::string graph_blocker(const Plan& p) const;
   std::vector<at::Tensor> run_graph(Plan& p, const std::vector<at::Tensor>& inputs);
   std::optional<std::vector<at::Tensor>> run_ptr_graph(Plan& p, const std::vector<at::Tensor>& inputs,
                                                        int64_t bytes);
