@@ -750,6 +750,45 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }, py::arg("tensor"), py::arg("op") = "Sum", GR())
         .def("check", &comm::OneShotComm::check, GR());
   }
+  m.def("cat_rows", [](const std::vector<at::Tensor>& ts) {
+    TFA_CHECK(!ts.empty(), "cat_rows: no tensors");
+    const at::Tensor& t0 = ts[0];
+    TFA_CHECK(t0.is_cuda() && t0.dim() >= 1, "cat_rows: device tensors of rank >= 1 expected");
+    std::vector<int64_t> sz = t0.sizes().vec();
+    int64_t rows = 0;
+    for (auto& t : ts) {
+      TFA_CHECK(t.is_cuda() && t.device() == t0.device() && t.scalar_type() == t0.scalar_type() &&
+                    t.dim() == t0.dim() && t.sizes().slice(1) == t0.sizes().slice(1),
+                "cat_rows: tensors must share device, dtype and trailing shape");
+      rows += t.size(0);
+    }
+    sz[0] = rows;
+    c10::hip::HIPGuard guard(t0.device().index());
+    at::Tensor out = pool_empty(sz, t0.options());
+    hipStream_t st = c10::hip::getCurrentHIPStream(t0.device().index()).stream();
+    std::vector<at::Tensor> keep;  // contiguous copies of strided inputs, alive until launched
+    k::CopyPieces pc;
+    int64_t off = 0;
+    auto flush = [&]() {
+      k::batched_copy(pc, out.data_ptr(), st);
+      pc.n = 0;
+    };
+    for (auto& t0i : ts) {
+      at::Tensor t = t0i.is_contiguous() ? t0i : t0i.contiguous();
+      if (!t0i.is_contiguous()) keep.push_back(t);
+      const int64_t nb = t.numel() * t.element_size();
+      if (nb) {
+        pc.src[pc.n] = t.data_ptr();
+        pc.dst_off[pc.n] = off;
+        pc.bytes[pc.n] = nb;
+        if (++pc.n == k::kMaxCopyPieces) flush();
+      }
+      off += nb;
+    }
+    flush();
+    for (auto& t : keep) dev_record_stream(t, st);
+    return out;
+  }, py::arg("tensors"), "row concatenation of device tensors into one pool buffer: one batched-copy kernel");
   m.def("pipeline_wait", &pipeline_wait, py::arg("handle"), py::call_guard<py::gil_scoped_release>(),
         "wait for a run_chunked(wait=False) completion handle (and release it)");
   m.def("device_empty", [](const std::vector<int64_t>& sizes, at::ScalarType dt, int device) {

@@ -4,6 +4,7 @@
 //
 // All grid-stride over <= 2048 blocks of 256 threads; scans along the last
 // axis use one block per row with wave-level (64-lane) prefix sums.
+#include <algorithm>
 #include <cmath>
 #include <type_traits>
 
@@ -314,6 +315,40 @@ void gather_nd(int64_t elem_size, DType idt, const void* params, const void* idx
   }
 #undef TFA_GND
   TFA_LAUNCH_CHECK("gather_nd");
+}
+
+// ---- batched copy: up to kMaxCopyPieces contiguous pieces into one buffer
+// in ONE launch (a row concatenation of many small device tensors costs one
+// kernel, not one DMA call per piece). blockIdx.y = piece; 16-byte accesses
+// when the piece's source and destination are 16-byte aligned.
+__global__ __launch_bounds__(256) void batched_copy_kernel(CopyPieces pc, char* __restrict__ dst) {
+  const int p = blockIdx.y;
+  const char* src = static_cast<const char*>(pc.src[p]);
+  char* d = dst + pc.dst_off[p];
+  const int64_t nb = pc.bytes[p];
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+    const int64_t n16 = nb / 16;
+    for (int64_t i = tid; i < n16; i += stride)
+      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (int64_t i = n16 * 16 + tid; i < nb; i += stride) d[i] = src[i];
+  } else {
+    for (int64_t i = tid; i < nb; i += stride) d[i] = src[i];
+  }
+}
+
+void batched_copy(const CopyPieces& pc, void* dst, hipStream_t s) {
+  TFA_CHECK(pc.n >= 0 && pc.n <= kMaxCopyPieces, "batched_copy: at most ", kMaxCopyPieces, " pieces");
+  if (pc.n == 0) return;
+  int64_t mx = 0;
+  for (int i = 0; i < pc.n; ++i) {
+    TFA_CHECK(pc.bytes[i] >= 0, "batched_copy: negative size");
+    mx = std::max(mx, pc.bytes[i]);
+  }
+  if (mx == 0) return;
+  const int gx = static_cast<int>(std::min<int64_t>((mx / 16 + 255) / 256 + 1, 1024));
+  hipLaunchKernelGGL(batched_copy_kernel, dim3(gx, pc.n), dim3(256), 0, s, pc, static_cast<char*>(dst));
+  TFA_LAUNCH_CHECK("batched_copy");
 }
 
 void mask_prefix(const uint8_t* mask, int64_t* pos, int64_t n, hipStream_t s) {

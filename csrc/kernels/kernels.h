@@ -134,6 +134,14 @@ void partition_rows(const int64_t* dest, int64_t n, int64_t world, int64_t* perm
 // ------------------------------------------------------------ data movement
 // dst[idx] = src[idx] over `dims`, both operands addressed by element strides
 // (src strides may be 0 or negative; pointers already include the offsets).
+constexpr int kMaxCopyPieces = 32;
+struct CopyPieces {
+  const void* src[kMaxCopyPieces];
+  int64_t dst_off[kMaxCopyPieces];
+  int64_t bytes[kMaxCopyPieces];
+  int n = 0;
+};
+void batched_copy(const CopyPieces& pc, void* dst, hipStream_t s);
 void strided_copy(int64_t elem_size, int rank, const int64_t* dims, const void* src,
                   const int64_t* src_strides, void* dst, const int64_t* dst_strides,
                   hipStream_t s);

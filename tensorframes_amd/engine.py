@@ -216,6 +216,9 @@ def cat_rows(ts: Sequence[torch.Tensor]) -> torch.Tensor:
     t0 = ts[0]
     if not t0.is_cuda:
         return torch.cat(ts, 0)
+    if t0.dim() >= 1 and len(ts) <= 256 and sum(t.numel() * t.element_size() for t in ts) <= (64 << 20):
+        # many small pieces (per-partition partials): one batched-copy kernel
+        return _C.cat_rows(ts)
     out = device_empty((sum(int(t.shape[0]) for t in ts),) + tuple(t0.shape[1:]), t0.dtype, t0.device)
     a = 0
     for t in ts:
@@ -250,6 +253,8 @@ def run_program(prog, inputs: List[torch.Tensor], dev: Optional[torch.device] = 
     dev = dev or compute_device()
     ins = [to_device(t.contiguous(), dev) for t in inputs]
     if dev.type == "cuda":
+        if dev.index is None or dev.index == torch.cuda.current_device():
+            return list(prog.run(ins))  # (Program::run guards the inputs' device itself)
         with torch.cuda.device(dev):
             return list(prog.run(ins))
     if sum(t.numel() for t in ins) < config.cpu_parallel_min_elems:

@@ -265,3 +265,19 @@ def test_const_upload_is_async_and_ordered_across_streams():
     ref = (xin.double() @ torch.from_numpy(w).double().to(dev)).float()
     assert torch.allclose(y1, ref, atol=1e-3, rtol=1e-4)
     assert torch.allclose(y2, ref, atol=1e-3, rtol=1e-4)
+
+
+def test_cat_rows_batched_copy_matches_torch_cat():
+    """engine.cat_rows of many small device pieces (one batched-copy kernel,
+    kernels/extra.hip): equal to torch.cat, for aligned, unaligned, empty and
+    strided pieces, and above the 32-piece launch batch."""
+    from tensorframes_amd import engine
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    for dt in (torch.float64, torch.float32, torch.int32, torch.uint8):
+        for trail in ((), (3,), (10, 100)):
+            pieces = [torch.randint(0, 100, (n,) + trail, device=dev, generator=g).to(dt) for n in
+                      [1, 0, 7, 2, 33, 5] * 7]
+            pieces[4] = pieces[4][::2]  # a strided piece
+            got = engine.cat_rows(pieces)
+            assert torch.equal(got, torch.cat(pieces, 0)), (dt, trail)
