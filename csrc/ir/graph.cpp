@@ -531,6 +531,17 @@ static constexpr int64_t kDynFoldLimit = 1024;
 
 Graph::Infos Graph::infer(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds,
                           bool concrete) const {
+  return infer_impl(order, feeds, concrete, nullptr, nullptr);
+}
+
+Graph::Infos Graph::infer_update(const std::vector<int>& order, const Infos& base, const std::vector<char>& redo,
+                                 bool concrete) const {
+  TFA_CHECK(base.size() == nodes_.size() && redo.size() == nodes_.size(), "infer_update: size mismatch");
+  return infer_impl(order, {}, concrete, &base, &redo);
+}
+
+Graph::Infos Graph::infer_impl(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds,
+                               bool concrete, const Infos* base, const std::vector<char>* redo) const {
   const OpRegistry& reg = OpRegistry::get();
   Infos infos(nodes_.size());
   // dyn[n]: n depends on a placeholder or a stateful op (its info may change
@@ -546,6 +557,16 @@ Graph::Infos Graph::infer(const std::vector<int>& order, const std::map<int, Ten
   }
   for (int ni : order) {
     const Node& n = nodes_[ni];
+    if (base && !(*redo)[ni]) {  // unchanged by the update: the base graph's infos
+      infos[ni] = (*base)[ni];
+      bool d = n.op == "Placeholder" || n.op == "PlaceholderV2";
+      if (const OpDef* od0 = reg.find(n.op)) d = d || od0->stateful;
+      for (auto& r : n.inputs) d = d || dyn[r.node];
+      // a fed node (a cut point) carries no value: dynamic
+      d = d || (!infos[ni].empty() && !infos[ni][0].value && infos[ni][0].row == RowClass::ROW);
+      dyn[ni] = d;
+      continue;
+    }
     auto fit = feeds.find(ni);
     if (fit != feeds.end()) {
       infos[ni] = {fit->second};

@@ -171,6 +171,12 @@ class Graph {
   using Infos = std::vector<std::vector<TensorInfo>>;
   Infos infer(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds,
               bool concrete) const;
+  // The same inference, recomputing only the nodes marked in `redo` and taking
+  // every other node's infos from `base` (the infos of a graph of the same
+  // structure: a rebuilt graph whose parameter constants changed redoes only
+  // the nodes those constants reach).
+  Infos infer_update(const std::vector<int>& order, const Infos& base, const std::vector<char>& redo,
+                     bool concrete) const;
 
   // Hash of the graph's structure: every node, input and attribute, except
   // the payloads of PARAMETER constants (floating-point Consts of >= 2
@@ -198,6 +204,8 @@ class Graph {
   mutable std::mutex key_mu_;
   mutable std::optional<uint64_t> key_;
   mutable std::vector<char> params_;
+  Infos infer_impl(const std::vector<int>& order, const std::map<int, TensorInfo>& feeds, bool concrete,
+                   const Infos* base, const std::vector<char>* redo) const;
 };
 
 // dtype <-> ATen

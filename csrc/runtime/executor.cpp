@@ -198,6 +198,9 @@ struct Program::Plan {
   std::vector<int> fetch_slots;
   std::map<int, std::map<int, at::Tensor>> dev_consts;  // device index -> slot -> tensor
   std::map<int, TensorInfo> feed_infos;                  // what the plan was inferred with
+  // the graph the plan was built from: infos values may view its constant
+  // payloads, and adopt() carries the infos of unchanged nodes over from it
+  std::shared_ptr<Graph> base_graph;
   // one device arena per device (upload_consts): the slots it holds, for an
   // in-place refresh after adopt()
   struct Arena {
@@ -398,6 +401,7 @@ std::shared_ptr<Program::Plan> Program::plan_for(const std::vector<at::Tensor>& 
 
 std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>& inputs, bool force_gpu) {
   auto p = std::make_shared<Plan>();
+  p->base_graph = g_;
   const bool gpu_plan = force_gpu || (!inputs.empty() && inputs[0].is_cuda());
   std::map<int, TensorInfo> feeds;
   for (size_t i = 0; i < inputs.size(); ++i) {
@@ -1137,9 +1141,19 @@ bool Program::adopt(Program& old) {
   // new values of every constant slot (the same nodes: equal structure);
   // shapes and dtypes must match (the parameter rule guarantees it)
   std::vector<std::pair<std::shared_ptr<Plan>, Graph::Infos>> fresh;
+  // only the nodes the (changed) parameter constants reach are re-inferred;
+  // every other node's info is the old plan's (same structure)
+  const std::vector<char>& prm = g_->parameter_consts();
+  std::vector<char> redo(g_->nodes().size(), 0);
+  for (int n : order_) {
+    char t = prm[n];
+    for (auto& r : g_->node(n).inputs) t = t || redo[r.node];
+    redo[n] = t;
+  }
   for (auto& kv : old.plans_) {
     Plan& p = *kv.second;
-    Graph::Infos ni = g_->infer(order_, p.feed_infos, true);
+    Graph::Infos ni = p.infos.size() == g_->nodes().size() ? g_->infer_update(order_, p.infos, redo, true)
+                                                           : g_->infer(order_, p.feed_infos, true);
     for (auto& cs : p.const_slots) {
       const TensorRef& r = cs.second;
       const TensorInfo& a = p.infos[r.node][r.index];
@@ -1156,6 +1170,11 @@ bool Program::adopt(Program& old) {
       const TensorRef& r = cs.second;
       p.infos[r.node][r.index].value = ni[r.node][r.index].value;
     }
+    // every node the parameters reach takes the new values (the next adopt
+    // starts from them); the others keep their base-graph values
+    for (size_t n = 0; n < redo.size() && n < p.infos.size(); ++n)
+      if (redo[n])
+        for (size_t k = 0; k < p.infos[n].size() && k < ni[n].size(); ++k) p.infos[n][k].value = ni[n][k].value;
     for (auto& kv : p.dev_consts)
       if (!kv.second.empty()) p.stale.insert(kv.first);
   }

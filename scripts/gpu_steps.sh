@@ -44,6 +44,8 @@ for s in ${STEPS:-tests}; do
     sib) run sib 600 python -u -m pytest tests/test_sibling_fusion.py -x -q --timeout 120 --timeout-method thread ;;
     kparts) run kparts 300 python scripts/kmeans_parts.py gpurun_out/kparts_cprofile.txt ;;
     kparts_plan) TFA_PLAN_TIMING=1 run kparts_plan 300 python scripts/kmeans_parts.py ;;
+    kmeans_agg) run kmeans_agg 300 python scripts/kmeans_profile.py --iters 50 --variant aggregate ;;
+    kbreak) run kbreak 300 python scripts/kmeans_breakdown.py --iters 200 ;;
     kmeans) run kmeans 300 python scripts/kmeans_profile.py --iters 50 ;;
     kmeans_cprof) run kmeans_cprof 300 python scripts/kmeans_profile.py --iters 20 --cprofile ;;
     refperf) run refperf 600 python bench/configs.py refperf ;;

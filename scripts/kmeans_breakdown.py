@@ -55,7 +55,7 @@ def main():
         c, _ = kmeans.run_one_step2(df, c)
     for mod, name in [(core, "map_blocks"), (core, "reduce_blocks"), (core, "_resolve"), (core, "analyze_graph"),
                       (engine, "program"), (engine, "run_program"), (core, "_combine_monoids"),
-                      (core, "_to_host_batched")]:
+                      (core, "_to_host_batched"), (engine, "cat_rows"), (kmeans, "tf_compute_distances")]:
         timed(mod, name)
     if gpu:
         torch.cuda.synchronize()
