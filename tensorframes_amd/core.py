@@ -1263,6 +1263,40 @@ def _identity(op: str, shape, dtype, dev) -> torch.Tensor:
     return torch.full(shape, info.max if op == "Min" else info.min, dtype=dtype, device=dev)
 
 
+_REDUCE_SETUP: "OrderedDict[tuple, tuple]" = OrderedDict()
+
+
+def _schema_key(schema: StructType) -> tuple:
+    return tuple((f.name, f.dataType.simpleString(), repr(sorted(f.metadata.items()))) for f in schema.fields)
+
+
+def _reduce_setup(spec: GraphSpec, schema: StructType) -> tuple:
+    """Analysis, validation, program and static shapes of a reduce_blocks
+    call, memoised by (graph bytes, fetches, hints, schema): an iterative
+    workload (K-Means) calls reduce_blocks with the same reducer graph on a
+    frame of the same schema every step."""
+    key = (engine._key(spec.graph_bytes), tuple(spec.fetch_refs), tuple(spec.fetch_names),
+           repr(sorted(spec.hints.items())), _schema_key(schema))
+    hit = _REDUCE_SETUP.get(key)
+    if hit is not None:
+        _REDUCE_SETUP.move_to_end(key)
+        return hit
+    summary = analyze_graph(spec)
+    out_names, in_names = _reduce_blocks_schema(schema, summary)
+    fetch_refs = [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names]
+    prog = engine.program(spec.graph_bytes, fetch_refs, in_names)
+    monoid = {m[0]: m[2] for m in prog.monoids()}  # fetch -> op
+    col_hints = {n + "_input": (summary[n].tf_dtype, list(_col_info(schema[n]).shape.tail().prepend(UNKNOWN).dims))
+                 for n in out_names}
+    static = _static_shapes(spec.graph_bytes, fetch_refs, out_names, in_names, col_hints)
+    dtypes = {n: summary[n].tf_dtype for n in out_names}
+    res = (summary, out_names, in_names, prog, monoid, static, dtypes)
+    _REDUCE_SETUP[key] = res
+    while len(_REDUCE_SETUP) > 64:
+        _REDUCE_SETUP.popitem(last=False)
+    return res
+
+
 def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     """Reduces blocks to one value per fetch. For each fetch `x` the graph
     reads a placeholder `x_input` holding a block of column `x`; the graph is
@@ -1271,11 +1305,7 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     Sum/Min/Max/Prod over axis 0 take the native reduction + RCCL all-reduce path."""
     dframe = _frame(dframe)
     spec = _resolve(fetches, graph, shape_hints)
-    summary = analyze_graph(spec)
-    out_names, in_names = _reduce_blocks_schema(dframe.schema, summary)
-    prog = engine.program(spec.graph_bytes, [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names],
-                          in_names)
-    monoid = {m[0]: m[2] for m in prog.monoids()}  # fetch -> op
+    summary, out_names, in_names, prog, monoid, static, dtypes = _reduce_setup(spec, dframe.schema)
     uniform = monoid if set(monoid) == set(out_names) else None
 
     partials: List[List[torch.Tensor]] = [[] for _ in out_names]
@@ -1327,11 +1357,6 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
         for j, o in enumerate(per_part[pid]):
             partials[j].append(o)
 
-    fetch_refs = [dict(zip(spec.fetch_names, spec.fetch_refs))[n] for n in out_names]
-    col_hints = {n + "_input": (summary[n].tf_dtype, list(_col_info(dframe.schema[n]).shape.tail().prepend(UNKNOWN).dims))
-                 for n in out_names}
-    static = _static_shapes(spec.graph_bytes, fetch_refs, out_names, in_names, col_hints)
-    dtypes = {n: summary[n].tf_dtype for n in out_names}
     if uniform:
         # partials reduced on device, then one all-reduce per (op, dtype) over RCCL
         comb = _combine_monoids({n: partials[j] for j, n in enumerate(out_names)}, uniform, static, dtypes)

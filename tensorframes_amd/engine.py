@@ -142,6 +142,8 @@ def clear_program_cache():
     with _lock:
         _prog_cache.clear()
         _struct_cache.clear()
+    from . import core  # memoised operator setups hold programs too
+    core._REDUCE_SETUP.clear()
 
 
 # ------------------------------------------------------------------ devices
