@@ -286,6 +286,20 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
     """
     dframe = _frame(dframe)
     spec = _resolve(fetches, graph, shape_hints)
+    setup_key = None
+    if config.plan_reuse:
+        setup_key = (engine.structure_key(spec.graph_bytes), tuple(spec.fetch_refs), tuple(spec.fetch_names),
+                     repr(sorted(spec.hints.items())), repr(sorted((feed_dict or {}).items())), bool(trim),
+                     _schema_key(dframe.schema))
+        hit = _MAP_SETUP.get(setup_key)
+        if hit is not None:
+            # a rebuilt graph of a known structure on a frame of a known
+            # schema (iterative workloads): validation and output schema are
+            # the same; only the program (new constants) is looked up
+            out_schema, feed_names, feed_cols, fetch_refs, separable, out_meta = hit
+            prog = engine.program(spec.graph_bytes, fetch_refs, feed_names)
+            return _map_blocks_frame(dframe, spec, prog, out_schema, feed_names, feed_cols, fetch_refs, separable,
+                                     out_meta, trim)
     summary = analyze_graph(spec)
     inputs = [s for s in summary.values() if s.is_input]
     outputs = sorted([s for s in summary.values() if s.is_output], key=lambda s: s.name)
@@ -328,6 +342,21 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
         ("separable", tuple(fetch_refs), tuple(feed_names), repr(sorted(hints.items()))), spec.graph_bytes,
         lambda: prog.row_separable(hints))
     out_meta = [(o.name, o.tf_dtype, o.shape) for o in outputs]
+    if setup_key is not None:
+        _MAP_SETUP[setup_key] = (out_schema, feed_names, feed_cols, fetch_refs, separable, out_meta)
+        while len(_MAP_SETUP) > 64:
+            _MAP_SETUP.popitem(last=False)
+    return _map_blocks_frame(dframe, spec, prog, out_schema, feed_names, feed_cols, fetch_refs, separable,
+                             out_meta, trim)
+
+
+_MAP_SETUP: "OrderedDict[tuple, tuple]" = OrderedDict()
+
+
+def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: StructType, feed_names: List[str],
+                      feed_cols: List[str], fetch_refs: List[str], separable: bool, out_meta,
+                      trim: bool) -> DataFrame:
+    """The lazy map_blocks frame over `dframe` for a validated graph."""
 
     def compute(blocks: Dict[int, Block]) -> Dict[int, Block]:
         res: Dict[int, Block] = {}
