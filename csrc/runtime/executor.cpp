@@ -211,6 +211,9 @@ struct Program::Plan {
   std::set<int> stale;                  // devices whose constants predate adopt()
   bool cap_reset = false;               // the capture reads constants that were replaced
   std::map<int, void*> last_stream;     // device -> stream of the last run
+  // device -> every stream a run or replay of this plan was issued on (the
+  // arena refresh waits for all of them: partitions may run concurrently)
+  std::map<int, std::set<void*>> used_streams;
   int fused = 0;
   int fused_siblings = 0;  // convs folded into sibling-fused steps
   // fused elementwise regions (GPU plans): generated source + loaded kernel per device
@@ -222,6 +225,26 @@ struct Program::Plan {
   std::vector<std::unique_ptr<Fused>> fused_regions;
   // HIP-graph replay of this plan (small, repeated launches): static input
   // buffers the inputs are copied into, the captured graph, its outputs
+  // replays of one capture share its buffers: a replay on another stream than
+  // the last one waits for it (concurrent partitions run on several streams)
+  struct ReplayOrder {
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+    void before(hipStream_t cur) {
+      if (done && last != cur) (void)hipStreamWaitEvent(cur, done, 0);
+    }
+    void after(hipStream_t cur) {
+      if (!done) TFA_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+      (void)hipEventRecord(done, cur);
+      last = cur;
+    }
+    void drain() {
+      if (done) (void)hipEventSynchronize(done);
+    }
+    ~ReplayOrder() {
+      if (done) (void)hipEventDestroy(done);
+    }
+  };
   struct Captured {
     std::mutex mu;
     int64_t gpu_runs = 0;
@@ -234,7 +257,9 @@ struct Program::Plan {
     hipStream_t stream = nullptr;  // our own capture stream (never shared)
     std::unique_ptr<HipGraph> graph;
     std::vector<at::Tensor> static_in, static_out;
+    ReplayOrder order;
     ~Captured() {
+      order.drain();
       graph.reset();
       if (stream) (void)hipStreamDestroy(stream);
     }
@@ -248,7 +273,9 @@ struct Program::Plan {
     std::vector<at::Tensor> static_out;
     hipStream_t stream = nullptr;
     int64_t last_use = 0;
+    ReplayOrder order;
     ~PtrCap() {
+      order.drain();
       graph.reset();
       if (stream) (void)hipStreamDestroy(stream);
     }
@@ -1105,10 +1132,10 @@ void Program::refresh_consts(Plan& p, int di, void* stream) {
     std::memcpy(hp + std::get<2>(it), c.data_ptr(), c.nbytes());
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  auto ls = p.last_stream.find(di);
-  // the previous runs may still read the arena: same stream = ordered, else wait
-  if (ls != p.last_stream.end() && ls->second && ls->second != stream)
-    (void)hipStreamSynchronize(static_cast<hipStream_t>(ls->second));
+  // the previous runs and replays may still read the arena: the same stream
+  // is ordered, every other stream they used is waited for
+  for (void* us : p.used_streams[di])
+    if (us && us != stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(us));
   {
     c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromExternal(s, static_cast<c10::DeviceIndex>(di)));
     ar.dev.copy_(host, /*non_blocking=*/true);
@@ -1257,6 +1284,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
     wait_consts(dev, stream);
     std::lock_guard<std::mutex> lk(const_mu_);
     p.last_stream[dev.index()] = stream;
+    if (!dev_stream_capturing(static_cast<hipStream_t>(stream))) p.used_streams[dev.index()].insert(stream);
   }
   for (auto& sc : p.synth_consts) {
     std::lock_guard<std::mutex> lk(const_mu_);
@@ -1534,13 +1562,20 @@ std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor
     // the capture stream's work (none executed yet) is ordered before replays on `cur`
     stats_.graphs_captured++;
   }
+  c.order.before(cur);  // the last replay (maybe on another stream) is done with the buffers
   for (size_t i = 0; i < inputs.size(); ++i) c.static_in[i].copy_(inputs[i], true);
+  wait_consts(inputs[0].device(), cur);
+  {
+    std::lock_guard<std::mutex> cl(const_mu_);
+    p.used_streams[dev].insert(cur);
+  }
   // the replay is ordered after the input copies on the caller's stream
   c.graph->replay(cur);
   std::vector<at::Tensor> outs;
   outs.reserve(c.static_out.size());
   // replay outputs are copied out of the graph's static buffers by DMA
   for (auto& o : c.static_out) outs.push_back(dev_clone(o.contiguous(), cur));
+  c.order.after(cur);
   stats_.graph_replays++;
   return outs;
 }
@@ -1592,7 +1627,7 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
       for (auto j = p.ptr_caps.begin(); j != p.ptr_caps.end(); ++j)
         if (j->second->last_use < lru->second->last_use) lru = j;
       if (lru->second->stream) (void)hipStreamSynchronize(lru->second->stream);
-      (void)hipStreamSynchronize(cur);  // its replays (on cur) are done before its pool goes
+      lru->second->order.drain();  // its replays are done before its pool goes
       p.ptr_caps.erase(lru);
     }
     auto pc = std::make_unique<Plan::PtrCap>();
@@ -1623,10 +1658,17 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
   Plan::PtrCap& pc = *it->second;
   pc.last_use = ++p.ptr_tick;
   const int64_t t0 = now_ns();
+  wait_consts(inputs[0].device(), cur);  // a refresh on another stream lands first
+  {
+    std::lock_guard<std::mutex> cl(const_mu_);
+    p.used_streams[dev].insert(cur);
+  }
+  pc.order.before(cur);
   pc.graph->replay(cur);
   std::vector<at::Tensor> outs;
   outs.reserve(pc.static_out.size());
   for (auto& o : pc.static_out) outs.push_back(dev_clone(o.contiguous(), cur));
+  pc.order.after(cur);
   stats_.graph_replays++;
   // the first replays are timed against the warm eager runs; a plan whose
   // replays cost more host time than launching its kernels keeps running eagerly
@@ -1668,12 +1710,12 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
           std::lock_guard<std::mutex> pl(p->ptr_mu);
           for (auto& kv : p->ptr_caps)
             if (kv.second->stream) (void)hipStreamSynchronize(kv.second->stream);
-          if (!p->ptr_caps.empty()) (void)hipDeviceSynchronize();
           p->ptr_caps.clear();
           p->ptr_seen.clear();
         }
         if (c.graph) {
           if (c.stream) (void)hipStreamSynchronize(c.stream);
+          c.order.drain();
           c.graph.reset();
           c.static_in.clear();
           c.static_out.clear();

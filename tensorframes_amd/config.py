@@ -73,6 +73,9 @@ class Config:
     collective_backend: str = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_BACKEND", "engine", str))
     # the single-hop IPC all-reduce for small payloads (kernels/oneshot.hip)
     oneshot_allreduce: bool = dataclasses.field(default_factory=lambda: _env("TFA_ONESHOT_ALLREDUCE", True, bool))
+    # small device-resident partitions of one map_blocks run side by side on
+    # up to 4 streams (engine.run_programs_concurrent)
+    concurrent_partitions: bool = dataclasses.field(default_factory=lambda: _env("TFA_CONCURRENT_PARTITIONS", True, bool))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 

@@ -351,6 +351,9 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
 
 
 _MAP_SETUP: "OrderedDict[tuple, tuple]" = OrderedDict()
+# device partitions up to this size run concurrently on side streams (bigger
+# ones fill the GPU alone, and running two would double the peak memory)
+_CONCURRENT_MAX_BYTES = 256 << 20
 
 
 def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: StructType, feed_names: List[str],
@@ -361,6 +364,7 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
     def compute(blocks: Dict[int, Block]) -> Dict[int, Block]:
         res: Dict[int, Block] = {}
         host_jobs = []
+        dev_jobs = []  # small device-resident partitions: run side by side
         for pid in sorted(blocks):
             b = blocks[pid]
             if b.nrows == 0:
@@ -371,6 +375,11 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
                 continue
             ins = _dense_inputs(b, feed_cols, "map_blocks")
             on_device = bool(ins) and all(t.is_cuda for t in ins)
+            if on_device and config.concurrent_partitions and \
+                    sum(t.numel() * t.element_size() for t in ins) <= _CONCURRENT_MAX_BYTES and \
+                    len({t.device for t in ins}) == 1:
+                dev_jobs.append((pid, b, ins))
+                continue
             if on_device or not engine.gpu_available() or not ins:
                 outs = engine.run_program(prog, ins, ins[0].device if on_device else None)
                 if not on_device and any(o.is_cuda for o in outs):
@@ -378,6 +387,13 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
                 res[pid] = _assemble(b, outs, out_meta, trim)
             else:
                 host_jobs.append((pid, b, ins))
+        if len(dev_jobs) > 1 and len({j[2][0].device for j in dev_jobs}) == 1:
+            outs_all = engine.run_programs_concurrent(prog, [j[2] for j in dev_jobs], dev_jobs[0][2][0].device)
+            for (pid, b, _), outs in zip(dev_jobs, outs_all):
+                res[pid] = _assemble(b, outs, out_meta, trim)
+        else:
+            for pid, b, ins in dev_jobs:
+                res[pid] = _assemble(b, engine.run_program(prog, ins, ins[0].device), out_meta, trim)
         if host_jobs:
             _run_host_jobs(host_jobs, res)
         metrics.add("map_blocks_rows", sum(b.nrows for b in blocks.values()))

@@ -265,6 +265,39 @@ def run_program(prog, inputs: List[torch.Tensor], dev: Optional[torch.device] = 
     return list(prog.run(ins))
 
 
+_side_streams: Dict[int, List[torch.cuda.Stream]] = {}
+
+
+def run_programs_concurrent(prog, inputs_list: List[List[torch.Tensor]], dev: torch.device) -> List[List[torch.Tensor]]:
+    """Several independent runs of one program (the device-resident partitions
+    of a map_blocks) issued on up to 4 streams at once, so a GPU that one small
+    partition cannot fill runs them side by side (K-Means: 4 partitions of
+    25k rows, each a chain of small kernels). The results are ordered back
+    onto the caller's stream before they are returned."""
+    main = torch.cuda.current_stream(dev)
+    pool = _side_streams.setdefault(dev.index, [])
+    k = min(len(inputs_list), 4)
+    while len(pool) < k:
+        pool.append(torch.cuda.Stream(dev))
+    ready = main.record_event()
+    outs: List[List[torch.Tensor]] = []
+    for i, ins in enumerate(inputs_list):
+        st = pool[i % k]
+        st.wait_event(ready)
+        with torch.cuda.stream(st):
+            outs.append(run_program(prog, ins, dev))
+        for t in ins:
+            record_stream(t, st)  # read on the side stream
+    for st in pool[:k]:
+        main.wait_stream(st)
+    for o in outs:
+        for t in o:
+            if t.is_cuda:
+                record_stream(t, main)  # side-stream memory, used on main from here on
+    metrics.add("concurrent_partition_runs", len(inputs_list))
+    return outs
+
+
 _thread_lock = threading.Lock()
 
 

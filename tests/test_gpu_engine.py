@@ -281,3 +281,52 @@ def test_cat_rows_batched_copy_matches_torch_cat():
             pieces[4] = pieces[4][::2]  # a strided piece
             got = engine.cat_rows(pieces)
             assert torch.equal(got, torch.cat(pieces, 0)), (dt, trail)
+
+
+def test_concurrent_partition_runs_match_sequential():
+    """engine.run_programs_concurrent issues the partitions of one program on
+    up to 4 side streams: results must equal a plain sequential run, over
+    repeated iterations where the zero-copy captures are replayed from a
+    different stream each time (partition i lands on stream (i + it) % 4)."""
+    rng = np.random.default_rng(7)
+    c = rng.standard_normal((16, 32))
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.double, [None, 32], name="x")
+        d = tf.reduce_sum(tf.square(x), [1], keep_dims=True) - 2 * tf.matmul(x, tf.constant(c), transpose_b=True)
+        idx = tf.argmin(d, 1, name="i")
+        tf.unsorted_segment_sum(x, idx, 16, name="s")
+        tf.reduce_sum(tf.unsorted_segment_sum(tf.ones_like(d), idx, 16), [1], name="n")
+        tf.reduce_min(d, [1], name="m")
+    prog = engine.program(g.serialize(), ["i", "s", "n", "m"], ["x"])
+    dev = torch.device("cuda", 0)
+    parts = [torch.randn((20000 + 1000 * k, 32), dtype=torch.float64, device=dev) for k in range(5)]
+    for it in range(6):
+        order = parts[it % 5:] + parts[:it % 5]  # rotate: each partition changes stream
+        got = engine.run_programs_concurrent(prog, [[p] for p in order], dev)
+        for p, outs in zip(order, got):
+            xin = p.cpu().numpy()
+            dd = (xin ** 2).sum(1, keepdims=True) - 2 * xin @ c.T
+            want_i = dd.argmin(1)
+            np.testing.assert_array_equal(outs[0].cpu().numpy(), want_i)
+            want_s = np.zeros((16, 32))
+            np.add.at(want_s, want_i, xin)
+            np.testing.assert_allclose(outs[1].cpu().numpy(), want_s, rtol=1e-9, atol=1e-8)
+            np.testing.assert_allclose(outs[3].cpu().numpy(), dd.min(1), rtol=1e-9, atol=1e-9)
+        for p in parts:
+            p.mul_(0.99)
+
+
+def test_map_blocks_concurrent_partitions_frame():
+    """A device-cached frame of 4 partitions: map_blocks runs them side by side
+    and the frame result equals the CPU result."""
+    xs = np.random.default_rng(8).standard_normal((40000, 8))
+    df = tfs.from_columns({"x": xs}, num_partitions=4).cache_on_device()
+    before = engine.metrics.snapshot().get("concurrent_partition_runs", 0)
+    with tf.Graph().as_default():
+        xb = tf.placeholder(tf.float64, [None, 8], name="x")
+        z = tf.reduce_sum(xb * xb, [1], name="z")
+        out = tfs.map_blocks(z, df)
+        got = out.to_numpy("z")
+    assert engine.metrics.snapshot().get("concurrent_partition_runs", 0) - before == 4
+    np.testing.assert_allclose(got, (xs * xs).sum(1), rtol=1e-12)
