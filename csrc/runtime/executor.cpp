@@ -1523,6 +1523,44 @@ std::string Program::graph_blocker(const Plan& p) const {
   return p.steps.empty() ? "no steps" : "";
 }
 
+namespace {
+// the outputs of a replay leave the graph's static buffers in ONE batched-copy
+// launch into one pool buffer (the outputs are views of it) instead of one
+// DMA call per output: a K-Means partition run returns 4 small outputs
+std::vector<at::Tensor> clone_outputs(const std::vector<at::Tensor>& outs, hipStream_t s) {
+  std::vector<at::Tensor> r;
+  r.reserve(outs.size());
+  if (outs.size() < 2 || outs.size() > static_cast<size_t>(k::kMaxCopyPieces)) {
+    for (auto& o : outs) r.push_back(dev_clone(o.contiguous(), s));
+    return r;
+  }
+  std::vector<at::Tensor> src;
+  std::vector<int64_t> off;
+  int64_t total = 0;
+  for (auto& o : outs) {
+    src.push_back(o.contiguous());
+    off.push_back(total);
+    total += (src.back().numel() * src.back().element_size() + 255) / 256 * 256;
+  }
+  at::Tensor buf = dev_empty({std::max<int64_t>(total, 1)}, at::kByte, outs[0].device(), s);
+  k::CopyPieces pc;
+  for (size_t i = 0; i < src.size(); ++i) {
+    const int64_t nb = src[i].numel() * src[i].element_size();
+    if (!nb) continue;
+    pc.src[pc.n] = src[i].data_ptr();
+    pc.dst_off[pc.n] = off[i];
+    pc.bytes[pc.n] = nb;
+    pc.n++;
+  }
+  k::batched_copy(pc, buf.data_ptr(), s);
+  for (size_t i = 0; i < src.size(); ++i) {
+    const int64_t nb = src[i].numel() * src[i].element_size();
+    r.push_back(buf.narrow(0, off[i], nb).view(src[i].scalar_type()).view(src[i].sizes()));
+  }
+  return r;
+}
+}  // namespace
+
 std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor>& inputs) {
   auto& c = p.cap;  // caller holds c.mu
   const int dev = inputs[0].device().index();
@@ -1571,10 +1609,8 @@ std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor
   }
   // the replay is ordered after the input copies on the caller's stream
   c.graph->replay(cur);
-  std::vector<at::Tensor> outs;
-  outs.reserve(c.static_out.size());
-  // replay outputs are copied out of the graph's static buffers by DMA
-  for (auto& o : c.static_out) outs.push_back(dev_clone(o.contiguous(), cur));
+  // replay outputs are copied out of the graph's static buffers
+  std::vector<at::Tensor> outs = clone_outputs(c.static_out, cur);
   c.order.after(cur);
   stats_.graph_replays++;
   return outs;
@@ -1665,9 +1701,7 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
   }
   pc.order.before(cur);
   pc.graph->replay(cur);
-  std::vector<at::Tensor> outs;
-  outs.reserve(pc.static_out.size());
-  for (auto& o : pc.static_out) outs.push_back(dev_clone(o.contiguous(), cur));
+  std::vector<at::Tensor> outs = clone_outputs(pc.static_out, cur);
   pc.order.after(cur);
   stats_.graph_replays++;
   // the first replays are timed against the warm eager runs; a plan whose

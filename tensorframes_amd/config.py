@@ -74,8 +74,11 @@ class Config:
     # the single-hop IPC all-reduce for small payloads (kernels/oneshot.hip)
     oneshot_allreduce: bool = dataclasses.field(default_factory=lambda: _env("TFA_ONESHOT_ALLREDUCE", True, bool))
     # small device-resident partitions of one map_blocks run side by side on
-    # up to 4 streams (engine.run_programs_concurrent)
-    concurrent_partitions: bool = dataclasses.field(default_factory=lambda: _env("TFA_CONCURRENT_PARTITIONS", True, bool))
+    # up to 4 streams (engine.run_programs_concurrent). Off by default: on the
+    # K-Means demo (4 x 25k rows, host-bound) the stream switches and events
+    # cost more host time than the overlap saves (0.92 -> 1.12 ms/iteration,
+    # profiles/r4_validation/kmeans_concurrency.md)
+    concurrent_partitions: bool = dataclasses.field(default_factory=lambda: _env("TFA_CONCURRENT_PARTITIONS", False, bool))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 

@@ -323,10 +323,14 @@ def test_map_blocks_concurrent_partitions_frame():
     xs = np.random.default_rng(8).standard_normal((40000, 8))
     df = tfs.from_columns({"x": xs}, num_partitions=4).cache_on_device()
     before = engine.metrics.snapshot().get("concurrent_partition_runs", 0)
-    with tf.Graph().as_default():
-        xb = tf.placeholder(tf.float64, [None, 8], name="x")
-        z = tf.reduce_sum(xb * xb, [1], name="z")
-        out = tfs.map_blocks(z, df)
-        got = out.to_numpy("z")
+    tfs.set_config(concurrent_partitions=True)
+    try:
+        with tf.Graph().as_default():
+            xb = tf.placeholder(tf.float64, [None, 8], name="x")
+            z = tf.reduce_sum(xb * xb, [1], name="z")
+            out = tfs.map_blocks(z, df)
+            got = out.to_numpy("z")
+    finally:
+        tfs.set_config(concurrent_partitions=False)
     assert engine.metrics.snapshot().get("concurrent_partition_runs", 0) - before == 4
     np.testing.assert_allclose(got, (xs * xs).sum(1), rtol=1e-12)
