@@ -267,6 +267,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["graph_replays"] = s.graph_replays;
         d["graph_failures"] = s.graph_failures;
         d["graphs_declined"] = s.graphs_declined;
+        d["graph_busy"] = s.graph_busy;
         return d;
       });
 

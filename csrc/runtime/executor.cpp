@@ -225,24 +225,18 @@ struct Program::Plan {
   std::vector<std::unique_ptr<Fused>> fused_regions;
   // HIP-graph replay of this plan (small, repeated launches): static input
   // buffers the inputs are copied into, the captured graph, its outputs
-  // replays of one capture share its buffers: a replay on another stream than
-  // the last one waits for it (concurrent partitions run on several streams)
+  // replays of one capture share its buffers: a replay on another stream
+  // than the last one first waits for that stream (rare: concurrent
+  // partitions; a per-replay event record cost 3 us of host time)
   struct ReplayOrder {
-    hipEvent_t done = nullptr;
     hipStream_t last = nullptr;
     void before(hipStream_t cur) {
-      if (done && last != cur) (void)hipStreamWaitEvent(cur, done, 0);
+      if (last && last != cur) (void)hipStreamSynchronize(last);
     }
-    void after(hipStream_t cur) {
-      if (!done) TFA_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
-      (void)hipEventRecord(done, cur);
-      last = cur;
-    }
+    void after(hipStream_t cur) { last = cur; }
     void drain() {
-      if (done) (void)hipEventSynchronize(done);
-    }
-    ~ReplayOrder() {
-      if (done) (void)hipEventDestroy(done);
+      if (last) (void)hipStreamSynchronize(last);
+      last = nullptr;
     }
   };
   struct Captured {
@@ -268,12 +262,25 @@ struct Program::Plan {
   // (device-cached partitions of an iterative workload): the graph is
   // captured on the caller's own input tensors, so a replay copies nothing in;
   // keyed by the input data pointers (same plan => same shapes and dtypes)
+  // The outputs of the first instance of a pointer set are handed out as
+  // aliases of the graph's own output buffers (no copy): it replays only once
+  // the caller has dropped every output of its last replay (storage use
+  // counts back at their values right after the capture). While they are
+  // held, a second, `cloning` instance replays and copies its outputs out.
   struct PtrCap {
+    bool cloning = false;
     std::unique_ptr<HipGraph> graph;
     std::vector<at::Tensor> static_out;
+    std::vector<long> base_uc;      // storage use count of each output after capture
+    std::vector<bool> input_alias;  // output is (a view of) an input: never written
     hipStream_t stream = nullptr;
     int64_t last_use = 0;
     ReplayOrder order;
+    bool outputs_free() const {
+      for (size_t i = 0; i < static_out.size(); ++i)
+        if (!input_alias[i] && static_out[i].storage().use_count() > base_uc[i]) return false;
+      return true;
+    }
     ~PtrCap() {
       order.drain();
       graph.reset();
@@ -282,7 +289,7 @@ struct Program::Plan {
   };
   std::mutex ptr_mu;
   std::map<std::vector<const void*>, int> ptr_seen;  // pointer set -> runs seen (bounded)
-  std::map<std::vector<const void*>, std::unique_ptr<PtrCap>> ptr_caps;
+  std::map<std::vector<const void*>, std::vector<std::unique_ptr<PtrCap>>> ptr_caps;
   int64_t ptr_tick = 0;
   bool ptr_declined = false;
   int64_t ptr_eager_ns = 0, ptr_eager_n = 0, ptr_replay_ns = 0, ptr_replay_n = 0;
@@ -1641,30 +1648,55 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
   const int dev = inputs[0].device().index();
   hipStream_t cur = c10::hip::getCurrentHIPStream(dev).stream();
   auto it = p.ptr_caps.find(key);
-  if (it == p.ptr_caps.end()) {
-    int& seen = p.ptr_seen[key];
-    if (p.ptr_seen.size() > kPtrMaxSeen) {  // a stream of fresh pointers: not an iterative workload
-      p.ptr_seen.clear();
-      return std::nullopt;
-    }
-    if (++seen <= kPtrWarmRuns || !graphable(p)) {
-      if (seen > 1) {  // warm eager run: the baseline a replay must beat
-        const int64_t t0 = now_ns();
-        auto outs = execute(p, inputs, cur);
-        p.ptr_eager_ns += now_ns() - t0;
-        p.ptr_eager_n++;
-        return outs;
+  Plan::PtrCap* use = nullptr;
+  if (it != p.ptr_caps.end()) {
+    for (auto& c : it->second)
+      if (!c->cloning && c->outputs_free()) use = c.get();
+    if (!use)
+      for (auto& c : it->second)
+        if (c->cloning) use = c.get();
+  }
+  const bool cloning = it != p.ptr_caps.end() && (use ? use->cloning : true);
+  if (!use) {
+    if (it == p.ptr_caps.end()) {
+      int& seen = p.ptr_seen[key];
+      if (p.ptr_seen.size() > kPtrMaxSeen) {  // a stream of fresh pointers: not an iterative workload
+        p.ptr_seen.clear();
+        return std::nullopt;
       }
-      return std::nullopt;
+      if (++seen <= kPtrWarmRuns || !graphable(p)) {
+        if (seen > 1) {  // warm eager run: the baseline a replay must beat
+          const int64_t t0 = now_ns();
+          auto outs = execute(p, inputs, cur);
+          p.ptr_eager_ns += now_ns() - t0;
+          p.ptr_eager_n++;
+          return outs;
+        }
+        return std::nullopt;
+      }
     }
     // capture on a private stream, on the caller's own tensors
-    if (p.ptr_caps.size() >= kPtrMaxCaps) {  // evict the least recently used
-      auto lru = p.ptr_caps.begin();
-      for (auto j = p.ptr_caps.begin(); j != p.ptr_caps.end(); ++j)
-        if (j->second->last_use < lru->second->last_use) lru = j;
-      if (lru->second->stream) (void)hipStreamSynchronize(lru->second->stream);
-      lru->second->order.drain();  // its replays are done before its pool goes
-      p.ptr_caps.erase(lru);
+    size_t total = 0;
+    for (auto& kv : p.ptr_caps) total += kv.second.size();
+    if (total >= kPtrMaxCaps) {  // evict the least recently used instance
+      std::vector<std::unique_ptr<Plan::PtrCap>>* lv = nullptr;
+      size_t li = 0;
+      int64_t best = INT64_MAX;
+      for (auto& kv : p.ptr_caps)
+        for (size_t i = 0; i < kv.second.size(); ++i)
+          if (kv.second[i]->last_use < best) {
+            best = kv.second[i]->last_use;
+            lv = &kv.second;
+            li = i;
+          }
+      if (lv) {
+        auto& victim = (*lv)[li];
+        if (victim->stream) (void)hipStreamSynchronize(victim->stream);
+        victim->order.drain();  // its replays are done before its pool goes
+        lv->erase(lv->begin() + static_cast<long>(li));
+        for (auto j = p.ptr_caps.begin(); j != p.ptr_caps.end();)
+          j = j->second.empty() ? p.ptr_caps.erase(j) : std::next(j);
+      }
     }
     auto pc = std::make_unique<Plan::PtrCap>();
     TFA_CHECK(hipStreamCreateWithFlags(&pc->stream, hipStreamNonBlocking) == hipSuccess, "hipStreamCreate failed");
@@ -1687,22 +1719,36 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
       return std::nullopt;
     }
     pc->graph = std::move(g);
+    pc->cloning = cloning;
+    for (auto& o : pc->static_out) {
+      bool in_alias = false;
+      for (auto& t : inputs) in_alias = in_alias || o.storage().is_alias_of(t.storage());
+      pc->input_alias.push_back(in_alias);
+      pc->base_uc.push_back(o.storage().use_count());
+    }
     stats_.graphs_captured++;
-    it = p.ptr_caps.emplace(key, std::move(pc)).first;
+    use = pc.get();
+    p.ptr_caps[key].push_back(std::move(pc));
     p.ptr_seen.erase(key);
   }
-  Plan::PtrCap& pc = *it->second;
-  pc.last_use = ++p.ptr_tick;
+  use->last_use = ++p.ptr_tick;
   const int64_t t0 = now_ns();
   wait_consts(inputs[0].device(), cur);  // a refresh on another stream lands first
   {
     std::lock_guard<std::mutex> cl(const_mu_);
     p.used_streams[dev].insert(cur);
   }
-  pc.order.before(cur);
-  pc.graph->replay(cur);
-  std::vector<at::Tensor> outs = clone_outputs(pc.static_out, cur);
-  pc.order.after(cur);
+  use->order.before(cur);
+  use->graph->replay(cur);
+  use->order.after(cur);
+  std::vector<at::Tensor> outs;
+  if (use->cloning) {
+    outs = clone_outputs(use->static_out, cur);
+    stats_.graph_busy++;
+  } else {
+    outs.reserve(use->static_out.size());
+    for (auto& o : use->static_out) outs.push_back(o.alias());  // no copy: see PtrCap
+  }
   stats_.graph_replays++;
   // the first replays are timed against the warm eager runs; a plan whose
   // replays cost more host time than launching its kernels keeps running eagerly
@@ -1743,7 +1789,8 @@ std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
         {
           std::lock_guard<std::mutex> pl(p->ptr_mu);
           for (auto& kv : p->ptr_caps)
-            if (kv.second->stream) (void)hipStreamSynchronize(kv.second->stream);
+            for (auto& pc : kv.second)
+              if (pc->stream) (void)hipStreamSynchronize(pc->stream);
           p->ptr_caps.clear();
           p->ptr_seen.clear();
         }

@@ -41,6 +41,7 @@ struct ExecStats {
   double plan_ms = 0;     // host time building plans (inference, fusion, kernel choice)
   double exec_ms = 0;     // host time issuing a plan's steps (launch overhead on a GPU)
   int64_t graphs_captured = 0, graph_replays = 0, graph_failures = 0, graphs_declined = 0;
+  int64_t graph_busy = 0;  // pointer-keyed replays that copied their outputs out (the caller held the aliases)
 };
 
 class Program {

@@ -17,6 +17,7 @@ Block execution on a GPU:
 from __future__ import annotations
 
 import hashlib
+import os
 import threading
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -147,14 +148,32 @@ def clear_program_cache():
 
 
 # ------------------------------------------------------------------ devices
+_cuda_ok: Optional[bool] = None
+_dev_memo: Dict[Tuple[str, str], torch.device] = {}
+
+
 def gpu_available() -> bool:
-    return config.device != "cpu" and torch.cuda.is_available()
+    # torch.cuda.is_available() asks the runtime each time (~2 us; an
+    # iterative workload asked it 17 times per step): whether this process
+    # sees a GPU does not change, so it is asked once
+    global _cuda_ok
+    if config.device == "cpu":
+        return False
+    if _cuda_ok is None:
+        _cuda_ok = torch.cuda.is_available()
+    return _cuda_ok
 
 
 def compute_device() -> torch.device:
     if gpu_available():
-        n = torch.cuda.device_count()
-        return torch.device("cuda", dist.local_rank() % max(n, 1))
+        lr = os.environ.get("LOCAL_RANK", "")
+        d = _dev_memo.get((config.device, lr)) if lr else None
+        if d is None:
+            n = torch.cuda.device_count()
+            d = torch.device("cuda", dist.local_rank() % max(n, 1))
+            if lr:  # (without LOCAL_RANK the rank comes from a group that may start later)
+                _dev_memo[(config.device, lr)] = d
+        return d
     if config.device == "cuda":
         raise RuntimeError("TFA_DEVICE=cuda but no GPU is visible")
     return torch.device("cpu")

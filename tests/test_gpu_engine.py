@@ -144,8 +144,12 @@ def test_zero_copy_replay_for_device_inputs_at_stable_addresses():
             outs.append((engine.run_program(prog, [p], dev), p.cpu().numpy().copy()))
     torch.cuda.synchronize()
     st = prog.stats()
-    assert st["graphs_captured"] - before["graphs_captured"] == 2  # one per partition address
-    assert st["graph_replays"] - before["graph_replays"] >= 4
+    # every output is kept alive here: after the first replay (outputs are
+    # aliases of the graph's buffers) each address gets a second, cloning
+    # instance whose replays copy their outputs out
+    assert st["graphs_captured"] - before["graphs_captured"] == 4
+    assert st["graph_replays"] - before["graph_replays"] >= 6
+    assert st["graph_busy"] - before["graph_busy"] >= 4
     for (i, m, sm, n), xin in outs:
         dd = (xin ** 2).sum(1, keepdims=True) - 2 * xin @ c.T
         want_i = dd.argmin(1)
@@ -334,3 +338,34 @@ def test_map_blocks_concurrent_partitions_frame():
         tfs.set_config(concurrent_partitions=False)
     assert engine.metrics.snapshot().get("concurrent_partition_runs", 0) - before == 4
     np.testing.assert_allclose(got, (xs * xs).sum(1), rtol=1e-12)
+
+
+def test_zero_copy_replay_outputs_alias_graph_buffers_when_released():
+    """The iterative pattern (outputs dropped before the next run): one
+    instance per address, replayed every time with no output copy, and the
+    results stay right while inputs change in place."""
+    rng = np.random.default_rng(9)
+    c = rng.standard_normal((10, 64))
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.double, [None, 64], name="x")
+        d = tf.reduce_sum(tf.square(x), [1], keep_dims=True) - 2 * tf.matmul(x, tf.constant(c), transpose_b=True)
+        idx = tf.argmin(d, 1, name="i")
+        tf.unsorted_segment_sum(x, idx, 10, name="s")
+        tf.reduce_min(d, [1], name="m")
+    prog = engine.program(g.serialize(), ["i", "s", "m"], ["x"])
+    dev = torch.device("cuda", 0)
+    p = torch.randn((30000, 64), dtype=torch.float64, device=dev)
+    before = prog.stats()
+    for it in range(10):
+        p.mul_(1.02)
+        i, sm, m = engine.run_program(prog, [p], dev)
+        xin = p.cpu().numpy()
+        dd = (xin ** 2).sum(1, keepdims=True) - 2 * xin @ c.T
+        np.testing.assert_array_equal(i.cpu().numpy(), dd.argmin(1))
+        np.testing.assert_allclose(m.cpu().numpy(), dd.min(1), rtol=1e-9, atol=1e-9)
+        del i, sm, m
+    st = prog.stats()
+    assert st["graphs_captured"] - before["graphs_captured"] == 1
+    assert st["graph_replays"] - before["graph_replays"] >= 7
+    assert st["graph_busy"] - before["graph_busy"] == 0
