@@ -228,6 +228,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("feed_names", &Program::feed_names)
       .def("row_separable",
            [](const Program& p, py::dict hints) { return p.row_separable(infos_from_py(hints)); })
+      .def("rebind", &Program::rebind, py::arg("values"), py::call_guard<py::gil_scoped_release>(),
+           "a program with new parameter-constant payloads that takes over this one's plans")
       .def("adopt", &Program::adopt, py::arg("old"), py::call_guard<py::gil_scoped_release>(),
            "take over the plans of a structurally equal program (see executor.h)")
       .def("monoids",
@@ -790,6 +792,69 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (auto& t : keep) dev_record_stream(t, st);
     return out;
   }, py::arg("tensors"), "row concatenation of device tensors into one pool buffer: one batched-copy kernel");
+  m.def("cat_rows_many", [](const std::vector<std::vector<at::Tensor>>& cols) {
+    // several row concatenations (the columns of merged partitions) into ONE
+    // pool buffer with one batched-copy launch per 32 pieces; each result is
+    // a view of that buffer at a 256-byte aligned offset
+    TFA_CHECK(!cols.empty() && !cols[0].empty(), "cat_rows_many: no tensors");
+    const at::Tensor& t00 = cols[0][0];
+    TFA_CHECK(t00.is_cuda(), "cat_rows_many: device tensors expected");
+    std::vector<std::vector<int64_t>> shapes;
+    std::vector<int64_t> offs;
+    int64_t total = 0;
+    for (auto& ts : cols) {
+      TFA_CHECK(!ts.empty(), "cat_rows_many: empty column");
+      const at::Tensor& t0 = ts[0];
+      TFA_CHECK(t0.dim() >= 1, "cat_rows_many: tensors of rank >= 1 expected");
+      std::vector<int64_t> sz = t0.sizes().vec();
+      int64_t rows = 0, nb = 0;
+      for (auto& t : ts) {
+        TFA_CHECK(t.is_cuda() && t.device() == t00.device() && t.scalar_type() == t0.scalar_type() &&
+                      t.dim() == t0.dim() && t.sizes().slice(1) == t0.sizes().slice(1),
+                  "cat_rows_many: the tensors of a column must share device, dtype and trailing shape");
+        rows += t.size(0);
+        nb += t.numel() * t.element_size();
+      }
+      sz[0] = rows;
+      shapes.push_back(sz);
+      offs.push_back(total);
+      total += (nb + 255) / 256 * 256;
+    }
+    c10::hip::HIPGuard guard(t00.device().index());
+    at::Tensor buf = pool_empty({std::max<int64_t>(total, 1)}, t00.options().dtype(at::kByte));
+    hipStream_t st = c10::hip::getCurrentHIPStream(t00.device().index()).stream();
+    std::vector<at::Tensor> keep;
+    k::CopyPieces pc;
+    auto flush = [&]() {
+      k::batched_copy(pc, buf.data_ptr(), st);
+      pc.n = 0;
+    };
+    for (size_t c = 0; c < cols.size(); ++c) {
+      int64_t off = offs[c];
+      for (auto& t0i : cols[c]) {
+        at::Tensor t = t0i.is_contiguous() ? t0i : t0i.contiguous();
+        if (!t0i.is_contiguous()) keep.push_back(t);
+        const int64_t nb = t.numel() * t.element_size();
+        if (nb) {
+          pc.src[pc.n] = t.data_ptr();
+          pc.dst_off[pc.n] = off;
+          pc.bytes[pc.n] = nb;
+          if (++pc.n == k::kMaxCopyPieces) flush();
+        }
+        off += nb;
+      }
+    }
+    flush();
+    for (auto& t : keep) dev_record_stream(t, st);
+    std::vector<at::Tensor> out;
+    for (size_t c = 0; c < cols.size(); ++c) {
+      const auto dt = cols[c][0].scalar_type();
+      int64_t n = 1;
+      for (int64_t d : shapes[c]) n *= d;
+      out.push_back(buf.narrow(0, offs[c], n * c10::elementSize(dt)).view(dt).view(shapes[c]));
+    }
+    return out;
+  }, py::arg("columns"), "row concatenations of several columns into one pool buffer (views of it)");
   m.def("pipeline_wait", &pipeline_wait, py::arg("handle"), py::call_guard<py::gil_scoped_release>(),
         "wait for a run_chunked(wait=False) completion handle (and release it)");
   m.def("device_empty", [](const std::vector<int64_t>& sizes, at::ScalarType dt, int device) {

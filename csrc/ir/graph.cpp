@@ -446,6 +446,34 @@ uint64_t Graph::hash_nodes(const std::vector<char>& param) const {
   return k.h;
 }
 
+std::shared_ptr<Graph> Graph::with_values(const std::map<std::string, at::Tensor>& values) const {
+  const std::vector<char>& params = parameter_consts();
+  GraphDef d = def_;  // node copies; tensor payloads stay shared (shared_ptr<HostTensor>)
+  for (const auto& [name, t] : values) {
+    const int i = find(name);
+    TFA_CHECK(i >= 0 && params[i], "with_values: '", name, "' is not a parameter constant of the graph");
+    auto it = d.nodes[i].attr.find("value");
+    TFA_CHECK(it != d.nodes[i].attr.end() && it->second.kind == AttrValue::TENSOR && it->second.tensor,
+              "with_values: '", name, "' has no tensor value");
+    const HostTensor& old = *it->second.tensor;
+    at::Tensor c = t.contiguous();
+    if (c.is_cuda()) c = c.cpu();
+    TFA_CHECK(c.scalar_type() == to_scalar_type(old.dtype) && c.numel() == old.num_elements(),
+              "with_values: '", name, "' needs ", old.num_elements(), " values of its dtype");
+    auto ht = std::make_shared<HostTensor>();
+    ht->dtype = old.dtype;
+    ht->shape = old.shape;
+    const auto* b = static_cast<const uint8_t*>(c.data_ptr());
+    ht->bytes.assign(b, b + c.numel() * c.element_size());
+    it->second.tensor = std::move(ht);
+  }
+  auto g = std::make_shared<Graph>(std::move(d));
+  std::lock_guard<std::mutex> lk(key_mu_);
+  g->key_ = key_;
+  g->params_ = params_;
+  return g;
+}
+
 uint64_t Graph::structure_key() const {
   std::lock_guard<std::mutex> lk(key_mu_);
   if (key_) return *key_;

@@ -189,6 +189,10 @@ class Graph {
   uint64_t hash_nodes(const std::vector<char>& param) const;
   // node -> is a parameter constant (as used by structure_key)
   const std::vector<char>& parameter_consts() const;
+  // The same graph with new payloads for some of its parameter constants
+  // (same dtype and element count), built from the decoded GraphDef: no
+  // serialisation or parse. The structure key carries over.
+  std::shared_ptr<Graph> with_values(const std::map<std::string, at::Tensor>& values) const;
 
  private:
   GraphDef def_;

@@ -91,6 +91,39 @@ __global__ __launch_bounds__(256) void row_reduce_wave(const T* __restrict__ x, 
   }
 }
 
+// ---- short rows (inner == 1, r <= kBlockRowBytes): one 1024-thread block per
+// row, so a small full reduction (a per-partition Sum of 25k values) is one
+// launch instead of a split pass plus a final pass
+constexpr int64_t kBlockRowBytes = 256 << 10;
+template <typename T, int OP>
+__global__ __launch_bounds__(1024) void row_reduce_block(const T* __restrict__ x, T* __restrict__ y, int64_t r) {
+  using A = typename AccT<T>::type;
+  __shared__ A red[16];
+  const T* p = x + (int64_t)blockIdx.x * r;
+  A acc = ident<OP, A>();
+  // 8 independent loads in flight per thread: one block has no other waves
+  // to hide the HBM latency behind
+  constexpr int U = 8;
+  int64_t i = threadIdx.x;
+  for (; i + (U - 1) * 1024 < r; i += U * 1024) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p[i + u * 1024];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = combine<OP, A>(acc, A(v[u]));
+  }
+  for (; i < r; i += 1024) acc = combine<OP, A>(acc, A(p[i]));
+  acc = wave_reduce<OP, A>(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    A t = red[0];
+#pragma unroll
+    for (int w = 1; w < 16; ++w) t = combine<OP, A>(t, red[w]);
+    y[blockIdx.x] = finish<OP, T, A>(t, r);
+  }
+}
+
 // ---- column-style reduce over [outer, r, inner]; grid = (col_blocks, outer, S)
 // Each thread owns one column and a contiguous slice of r. S > 1 writes
 // partials part[s][outer][inner] (accumulator type), combined by col_final.
@@ -291,6 +324,10 @@ void reduce_typed(const void* xv, void* yv, int64_t outer, int64_t r, int64_t in
   }
   int64_t rows_per_split = (r + p.S - 1) / p.S;
   int64_t S = (r + rows_per_split - 1) / rows_per_split;
+  if (inner == 1 && S > 1 && outer <= 64 && r * (int64_t)sizeof(T) <= kBlockRowBytes) {
+    hipLaunchKernelGGL((row_reduce_block<T, OP>), dim3((unsigned)outer), dim3(1024), 0, s, x, y, r);
+    return;
+  }
   if (inner == 1) {
     TFA_CHECK(ws != nullptr || S == 1, "reduce: missing workspace");
     TFA_CHECK(outer <= 65535, "reduce: outer dim ", outer, " too large for the split-row path");
@@ -750,10 +787,62 @@ void segment_reduce_perm(RedOp op, DType dt, const void* x, const int64_t* perm,
   TFA_LAUNCH_CHECK("segment_reduce_perm");
 }
 
+// ---- small integer segment reduce (inner == 1): one 1024-thread block folds
+// every row into an LDS table with integer atomics (exact, so the order does
+// not matter) -- one launch instead of private slabs plus a final pass (the
+// per-cluster counts of K-Means)
+constexpr int64_t kUsegSmallRows = 1 << 18;
+constexpr int64_t kUsegSmallSegs = 4096;
+template <typename T, typename I, int OP>
+__global__ __launch_bounds__(1024) void useg_small_int(const T* __restrict__ x, const I* __restrict__ ids,
+                                                       T* __restrict__ y, int64_t n, int64_t nseg) {
+  __shared__ long long acc[kUsegSmallSegs];
+  for (int64_t g = threadIdx.x; g < nseg; g += 1024) acc[g] = ident<OP, long long>();
+  __syncthreads();
+  // 8 rows of ids and values in flight per thread (latency, as above)
+  constexpr int U = 8;
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += U * 1024) {
+    int64_t g[U];
+    long long v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * 1024;
+      const bool ok = i < n;
+      g[u] = ok ? (int64_t)ids[i] : -1;
+      v[u] = ok ? (long long)x[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (g[u] < 0 || g[u] >= nseg) continue;
+      if constexpr (OP == (int)RedOp::SUM)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[g[u]]), (unsigned long long)v[u]);
+      else if constexpr (OP == (int)RedOp::MIN) atomicMin(&acc[g[u]], v[u]);
+      else atomicMax(&acc[g[u]], v[u]);
+    }
+  }
+  __syncthreads();
+  for (int64_t g = threadIdx.x; g < nseg; g += 1024) {
+    long long a = acc[g];
+    if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
+      // TF: empty segments get the type's highest (min) / lowest (max) value
+      if (a == ident<OP, long long>())
+        a = OP == (int)RedOp::MAX ? (long long)std::numeric_limits<T>::lowest() : (long long)std::numeric_limits<T>::max();
+    }
+    y[g] = T(a);
+  }
+}
+
 template <typename T, typename I, int OP>
 static void useg_typed(const void* x, const void* ids, void* y, int64_t n, int64_t inner, int64_t nseg,
                        void* ws, hipStream_t s) {
   using A = typename AccT<T>::type;
+  if constexpr (std::is_integral<T>::value && OP != (int)RedOp::PROD) {
+    if (inner == 1 && n <= kUsegSmallRows && nseg <= kUsegSmallSegs) {
+      hipLaunchKernelGGL((useg_small_int<T, I, OP>), dim3(1), dim3(1024), 0, s, (const T*)x, (const I*)ids, (T*)y, n,
+                         nseg);
+      return;
+    }
+  }
   int64_t tile = useg_tile(inner);
   size_t lds = static_cast<size_t>(nseg * tile * sizeof(A));
   TFA_CHECK(lds <= kUsegLds, "unsorted segment reduce: ", nseg, " segments x ", tile,

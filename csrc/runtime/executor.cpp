@@ -1156,6 +1156,12 @@ void Program::refresh_consts(Plan& p, int di, void* stream) {
   (void)hipEventRecord(static_cast<hipEvent_t>(ev), s);
 }
 
+std::shared_ptr<Program> Program::rebind(const std::map<std::string, at::Tensor>& values) {
+  auto p = std::make_shared<Program>(g_->with_values(values), fetch_names_, feed_names_);
+  p->adopt(*this);
+  return p;
+}
+
 bool Program::adopt(Program& old) {
   if (&old == this) return false;
   if (g_->structure_key() != old.g_->structure_key() || g_->nodes().size() != old.g_->nodes().size())

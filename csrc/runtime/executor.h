@@ -69,6 +69,10 @@ class Program {
   // afresh if it runs again (a lazy frame built on it still sees its own
   // constants). False (nothing moved) when the structures differ.
   bool adopt(Program& old);
+  // A program for this graph with new parameter-constant payloads
+  // (Graph::with_values) that takes over this program's plans: the per-step
+  // rebuild of an iterative workload without serialising or parsing a graph.
+  std::shared_ptr<Program> rebind(const std::map<std::string, at::Tensor>& values);
 
   // Run on concrete inputs (all on one device: CPU or a GPU). Returns the fetches.
   std::vector<at::Tensor> run(const std::vector<at::Tensor>& inputs);

@@ -73,6 +73,13 @@ class Config:
     collective_backend: str = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_BACKEND", "engine", str))
     # the single-hop IPC all-reduce for small payloads (kernels/oneshot.hip)
     oneshot_allreduce: bool = dataclasses.field(default_factory=lambda: _env("TFA_ONESHOT_ALLREDUCE", True, bool))
+    # map_blocks over a frame cached in HBM (cache_on_device) launches its
+    # partitions at the call instead of at the first action, when the feed
+    # columns total at most `eager_device_map_bytes`: the GPU runs them while
+    # the host builds what comes next (iterative workloads)
+    eager_device_map: bool = dataclasses.field(default_factory=lambda: _env("TFA_EAGER_DEVICE_MAP", True, bool))
+    eager_device_map_bytes: int = dataclasses.field(
+        default_factory=lambda: _env("TFA_EAGER_DEVICE_MAP_BYTES", 1 << 30, int))
     # small device-resident partitions of one map_blocks run side by side on
     # up to 4 streams (engine.run_programs_concurrent). Off by default: on the
     # K-Means demo (4 x 25k rows, host-bound) the stream switches and events

@@ -77,13 +77,35 @@ def _check_dim(cond: bool, msg: str):
 
 
 # ------------------------------------------------------------------ graph specs
-@dataclass
 class GraphSpec:
-    graph_bytes: bytes
-    fetch_names: List[str]           # column names (":0" stripped)
-    fetch_refs: List[str]            # tensor names as given to the runtime
-    hints: Dict[str, Shape]          # shape hints (fetches, zero-input nodes)
-    dsl_fetches: Optional[list] = None
+    """A resolved graph + fetches. For a DSL graph the GraphDef bytes are made
+    on first use: a rebuilt graph of a known structure (K-Means, every
+    iteration) gets its program from Graph.fast_key + Program.rebind and is
+    never serialised or parsed (engine.program_for_spec)."""
+
+    __slots__ = ("_bytes", "fetch_names", "fetch_refs", "hints", "dsl_fetches", "dsl_graph", "dsl_nodes")
+
+    def __init__(self, graph_bytes: Optional[bytes], fetch_names: List[str], fetch_refs: List[str],
+                 hints: Dict[str, Shape], dsl_fetches: Optional[list] = None, dsl_graph=None, dsl_nodes: int = 0):
+        self._bytes = graph_bytes
+        self.fetch_names = fetch_names  # column names (":0" stripped)
+        self.fetch_refs = fetch_refs    # tensor names as given to the runtime
+        self.hints = hints              # shape hints (fetches, zero-input nodes)
+        self.dsl_fetches = dsl_fetches
+        self.dsl_graph = dsl_graph      # the DSL graph and its node count when resolved
+        self.dsl_nodes = dsl_nodes
+
+    @property
+    def graph_bytes(self) -> bytes:
+        if self._bytes is None:
+            self._bytes = self.dsl_graph.serialize(self.dsl_nodes)
+        return self._bytes
+
+    def fast_key(self):
+        """(key, params) of a DSL graph (dsl.Graph.fast_key), else None."""
+        if self.dsl_graph is None or not config.plan_reuse:
+            return None
+        return self.dsl_graph.fast_key(self.dsl_nodes)
 
 
 def _frame(df):
@@ -158,17 +180,19 @@ def _resolve(fetches, graph=None, shape_hints: Optional[Dict[str, Any]] = None) 
                 g.as_graph_element(n if ":" in n else n + ":0")
             except (KeyError, ValueError) as e:
                 raise ValueError(f"Fetch argument {n!r} cannot be interpreted as a Tensor. ({e})")
-        gbytes = g.serialize()
+        gbytes = None  # serialised on first use (GraphSpec.graph_bytes)
+        dsl_graph, dsl_nodes = g, len(g._nodes)
         dsl_fetches = [g.get_tensor_by_name(n if ":" in n else n + ":0") for n in names]
     else:
         gbytes = _graph_bytes(graph)
+        dsl_graph, dsl_nodes = None, 0
         names = [f.name if isinstance(f, dsl.Tensor) else str(f) for f in fl]
     cols = [_strip(n).split(":")[0] for n in names]
     if len(set(cols)) != len(cols):
         raise ValueError(f"Could not infer a list of unique names for the columns: {names}")
     for k, v in (shape_hints or {}).items():
         hints[_strip(k)] = v if isinstance(v, Shape) else Shape([UNKNOWN if d is None else d for d in v])
-    return GraphSpec(gbytes, cols, names, hints, dsl_fetches)
+    return GraphSpec(gbytes, cols, names, hints, dsl_fetches, dsl_graph, dsl_nodes)
 
 
 @dataclass
@@ -288,16 +312,17 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
     spec = _resolve(fetches, graph, shape_hints)
     setup_key = None
     if config.plan_reuse:
-        setup_key = (engine.structure_key(spec.graph_bytes), tuple(spec.fetch_refs), tuple(spec.fetch_names),
-                     repr(sorted(spec.hints.items())), repr(sorted((feed_dict or {}).items())), bool(trim),
-                     _schema_key(dframe.schema))
+        fk = spec.fast_key()
+        setup_key = (fk[0] if fk is not None else engine.structure_key(spec.graph_bytes), tuple(spec.fetch_refs),
+                     tuple(spec.fetch_names), repr(sorted(spec.hints.items())),
+                     repr(sorted((feed_dict or {}).items())), bool(trim), _schema_key(dframe.schema))
         hit = _MAP_SETUP.get(setup_key)
         if hit is not None:
             # a rebuilt graph of a known structure on a frame of a known
             # schema (iterative workloads): validation and output schema are
             # the same; only the program (new constants) is looked up
             out_schema, feed_names, feed_cols, fetch_refs, separable, out_meta = hit
-            prog = engine.program(spec.graph_bytes, fetch_refs, feed_names)
+            prog = engine.program_for_spec(spec, fetch_refs, feed_names)
             return _map_blocks_frame(dframe, spec, prog, out_schema, feed_names, feed_cols, fetch_refs, separable,
                                      out_meta, trim)
     summary = analyze_graph(spec)
@@ -336,7 +361,7 @@ def map_blocks(fetches, dframe: DataFrame, trim: bool = False, feed_dict: Option
     # fetches in output-column order
     ref_of = dict(zip(spec.fetch_names, spec.fetch_refs))
     fetch_refs = [ref_of[o.name] for o in outputs]
-    prog = engine.program(spec.graph_bytes, fetch_refs, feed_names)
+    prog = engine.program_for_spec(spec, fetch_refs, feed_names)
     hints = {n: (summary[n].tf_dtype, list(_col_info(fields[c]).shape.dims)) for n, c in zip(feed_names, feed_cols)}
     separable = bool(feed_names) and _structural(
         ("separable", tuple(fetch_refs), tuple(feed_names), repr(sorted(hints.items()))), spec.graph_bytes,
@@ -414,8 +439,32 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
             outs = engine.run_block_host(prog, ins, False)
             res[pid] = _assemble(b, outs, out_meta, trim)
 
-    return DataFrame(out_schema, _Derived(dframe, faults.with_retries("map_blocks", compute)),
-                     dframe.num_partitions)
+    run = faults.with_retries("map_blocks", compute)
+    src = dframe._cached
+    if config.eager_device_map and src and feed_cols and _device_resident(src, feed_cols):
+        # the parent is cached in HBM: launch the partitions now (they are
+        # asynchronous GPU work) so the host goes on -- building the next graph,
+        # setting up the next operator -- while the GPU runs them; an iterative
+        # workload's consumer then finds them computed (K-Means: the reduce
+        # graph is built under the partition kernels)
+        res = run(src)
+        df = DataFrame(out_schema, _Materialized(res), dframe.num_partitions)
+        df._persist = True
+        df._cached = res
+        return df
+    return DataFrame(out_schema, _Derived(dframe, run), dframe.num_partitions)
+
+
+def _device_resident(blocks: Dict[int, Block], cols: List[str]) -> bool:
+    """Every block's feed columns are device tensors, within the eager budget."""
+    n = 0
+    for b in blocks.values():
+        for c in cols:
+            t = b.columns.get(c)
+            if not isinstance(t, torch.Tensor) or not t.is_cuda:
+                return False
+            n += t.numel() * t.element_size()
+    return n <= config.eager_device_map_bytes
 
 
 def _assemble(b: Block, outs: List[torch.Tensor], out_meta, trim: bool) -> Block:
@@ -1373,7 +1422,7 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
             nbytes = sum(t.numel() * t.element_size() for _, ins in dense for t in ins)
             if (len(dense) > 1 and len(devs) == 1 and next(iter(devs)).type == "cuda"
                     and nbytes <= config.chunk_bytes):
-                ins = [engine.cat_rows([d[1][j] for d in dense]) for j in range(len(cols))]
+                ins = engine.cat_rows_many([[d[1][j] for d in dense] for j in range(len(cols))])
                 res[dense[0][0]] = engine.run_program(prog, ins, ins[0].device)
                 metrics.add("reduce_blocks_merged_partitions", len(dense))
                 return res

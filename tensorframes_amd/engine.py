@@ -117,6 +117,56 @@ def program(graph_bytes: bytes, fetches: Sequence[str], feeds: Sequence[str]):
     return p
 
 
+# (Graph.fast_key structure, fetches, feeds) -> [program, parameter names,
+# payloads of the other float constants, payloads the program was built with]
+_fast_progs: "OrderedDict[tuple, list]" = OrderedDict()
+
+
+def program_for_spec(spec, fetches: Sequence[str], feeds: Sequence[str]):
+    """`program(spec.graph_bytes, fetches, feeds)` for a resolved graph. A DSL
+    graph whose structure (Graph.fast_key: everything but the payloads of its
+    floating constants) is known gets the known program with the new
+    parameter payloads swapped in (Program.rebind: plans, fused kernels and
+    HIP-graph captures carried over) -- no serialisation, hash or parse of the
+    rebuilt graph (an iterative workload: reference kmeans_demo.py:101-168)."""
+    fk = spec.fast_key()
+    if fk is None:
+        return program(spec.graph_bytes, fetches, feeds)
+    skey, params = fk
+    k = (skey, tuple(fetches), tuple(feeds))
+    with _lock:
+        ent = _fast_progs.get(k)
+        if ent is not None:
+            _fast_progs.move_to_end(k)
+    if ent is not None:
+        prog, pnames, fixed, built = ent
+        if all(params[n].content == b for n, b in fixed.items()):
+            if all(params[n].content == built[n] for n in pnames):
+                return prog  # the same payloads: the same program
+            vals = {n: _tensor_of(params[n]) for n in pnames}
+            p = prog.rebind(vals)
+            metrics.add("programs_rebound")
+            with _lock:
+                _fast_progs[k] = [p, pnames, fixed, {n: params[n].content for n in pnames}]
+            return p
+    gb = spec.graph_bytes
+    p = program(gb, fetches, feeds)
+    if _planned_bytes(gb) is gb:  # no rewrite changed the graph: its constants are the user's
+        pnames = set(native_graph(gb).parameter_consts()) & set(params)
+        with _lock:
+            _fast_progs[k] = [p, pnames, {n: tp.content for n, tp in params.items() if n not in pnames},
+                              {n: params[n].content for n in pnames}]
+            while len(_fast_progs) > _MAX_CACHE:
+                _fast_progs.popitem(last=False)
+    return p
+
+
+def _tensor_of(tp) -> torch.Tensor:
+    from .utils import dtypes as D
+    npdt = np.dtype(D.numpy_dtype(tp.dtype)).newbyteorder("<")
+    return torch.from_numpy(np.frombuffer(tp.content, dtype=npdt).reshape(tp.shape).copy())
+
+
 _rewritten: "OrderedDict[str, bytes]" = OrderedDict()
 
 
@@ -143,6 +193,7 @@ def clear_program_cache():
     with _lock:
         _prog_cache.clear()
         _struct_cache.clear()
+        _fast_progs.clear()
     from . import core  # memoised operator setups hold programs too
     core._REDUCE_SETUP.clear()
 
@@ -225,6 +276,18 @@ def record_stream(t: torch.Tensor, stream) -> None:
     and for framework tensors alike."""
     if t.is_cuda:
         _C.record_stream(t, int(stream.cuda_stream))
+
+
+def cat_rows_many(cols: Sequence[Sequence[torch.Tensor]]) -> List[torch.Tensor]:
+    """`[cat_rows(c) for c in cols]` for device columns, in one pool buffer
+    and one batched-copy launch (the merged partitions of reduce_blocks: one
+    launch instead of one per column)."""
+    cols = [list(c) for c in cols]
+    if (cols and all(c and c[0].is_cuda and c[0].dim() >= 1 for c in cols)
+            and sum(len(c) for c in cols) <= 256
+            and sum(t.numel() * t.element_size() for c in cols for t in c) <= (64 << 20)):
+        return list(_C.cat_rows_many(cols))
+    return [cat_rows(c) for c in cols]
 
 
 def cat_rows(ts: Sequence[torch.Tensor]) -> torch.Tensor:

@@ -210,18 +210,52 @@ class Graph:
             g = P.GraphDef(nodes, producer=24)
         return g
 
-    def serialize(self) -> bytes:
-        """GraphDef bytes; cached while the graph is unchanged (nodes are only
-        ever appended, so the node count identifies the version)."""
-        n = len(self._nodes)
+    def serialize(self, upto: Optional[int] = None) -> bytes:
+        """GraphDef bytes (of the first `upto` nodes); cached while the graph is
+        unchanged (nodes are only ever appended, so the node count identifies
+        the version)."""
+        n = len(self._nodes) if upto is None else upto
         cached = getattr(self, "_ser_cache", None)
         if cached is not None and cached[0] == n:
             return cached[1]
-        parts = [p for e in self._node_parts(False) for p in e]
+        parts = [p for e in self._node_parts(False)[:n] for p in e]
         parts.append(P._ld(4, P._key(1, 0) + P._varint(24)))  # versions { producer: 24 }
         b = b"".join(parts)
         self._ser_cache = (n, b)
         return b
+
+    def fast_key(self, upto: int):
+        """(key, params) of the first `upto` nodes without serialising them:
+        `key` is every node, input and attribute except the payloads of the
+        candidate parameter constants (floating Consts of >= 2 elements, the
+        candidates of the native Graph::structure_key), `params` maps those
+        constants' names to their TensorProtos. A graph rebuilt with new
+        parameter values (K-Means centres) has the same key, so its program
+        is the known one with the payloads swapped (engine.program_for_spec)."""
+        cached = getattr(self, "_fk_cache", None)
+        if cached is not None and cached[0] == upto:
+            return cached[1]
+        parts = []
+        params = {}
+        # the per-node wire encodings (native encoder, cached: a later
+        # serialize() reuses them); a parameter candidate contributes its name,
+        # dtype and shape instead
+        for nd, e in zip(self._nodes[:upto], self._node_parts(False)[:upto]):
+            if nd.op == "Const":
+                v = nd.attr.get("value")
+                tp = v.value if v is not None and v.kind == "tensor" else None
+                if tp is not None and tp.dtype in _PARAM_DTYPES and tp.strings is None:
+                    n = 1
+                    for d in tp.shape:
+                        n *= d
+                    if n >= 2:
+                        params[nd.name] = tp
+                        parts.append((nd.name, tp.dtype, tuple(tp.shape)))
+                        continue
+            parts.append(e[0] if len(e) == 1 else b"".join(e))
+        r = (tuple(parts), params)
+        self._fk_cache = (upto, r)
+        return r
 
     @staticmethod
     def _view_node(n: P.NodeDef) -> P.NodeDef:
@@ -342,6 +376,9 @@ def variable_scope(name_or_scope, default_name=None, reuse=None):
 def with_graph():
     with Graph().as_default() as g:
         yield g
+
+
+_PARAM_DTYPES = frozenset((D.DT_FLOAT, D.DT_DOUBLE, D.DT_HALF, D.DT_BFLOAT16))
 
 
 class Operation:

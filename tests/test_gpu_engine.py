@@ -369,3 +369,17 @@ def test_zero_copy_replay_outputs_alias_graph_buffers_when_released():
     assert st["graphs_captured"] - before["graphs_captured"] == 1
     assert st["graph_replays"] - before["graph_replays"] >= 7
     assert st["graph_busy"] - before["graph_busy"] == 0
+
+
+def test_cat_rows_many_matches_torch_cat():
+    """Several columns concatenated in one launch: each result equals
+    torch.cat of its pieces (mixed dtypes, trailing shapes, a strided piece)."""
+    dev = torch.device("cuda", 0)
+    a = [torch.randn((n, 3, 5), dtype=torch.float64, device=dev) for n in (7, 1, 30, 2)]
+    b = [torch.randint(-9, 9, (n,), dtype=torch.int32, device=dev) for n in (7, 1, 30, 2)]
+    c = [torch.randn((5, n), device=dev).t() for n in (7, 1, 30, 2)]  # non-contiguous pieces
+    got = engine.cat_rows_many([a, b, c])
+    for g, parts in zip(got, (a, b, c)):
+        want = torch.cat(parts, 0)
+        assert g.shape == want.shape and g.dtype == want.dtype
+        torch.testing.assert_close(g, want, rtol=0, atol=0)

@@ -126,6 +126,44 @@ def test_unsorted_segment_sum_and_gather():
         torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-9)
 
 
+@pytest.mark.parametrize("dtype", [np.int32, np.int64])
+@pytest.mark.parametrize("n", [1, 777, 25000, 262144])
+def test_small_int_segment_reduce_single_block(dtype, n):
+    """The one-block LDS-atomic path (inner == 1, integer data, n <= 256k):
+    negative and out-of-range ids are dropped, empty segments of Min/Max get
+    the type's extreme value, Sum of int32 wraps like the slab path."""
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(dtype, [None], name="x")
+        ids = tf.placeholder(tf.int64, [None], name="ids")
+        tf.unsorted_segment_sum(x, ids, 37, name="s")
+        tf.unsorted_segment_min(x, ids, 37, name="lo")
+        tf.unsorted_segment_max(x, ids, 37, name="hi")
+    x_ = rng.integers(-1000, 1000, n).astype(dtype)
+    ids_ = rng.integers(-2, 30, n).astype(np.int64)  # segments 30..36 stay empty
+    gpu, cpu = both(g, ["s", "lo", "hi"], {"x": x_, "ids": ids_})
+    for a, b in zip(gpu, cpu):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32])
+@pytest.mark.parametrize("shape", [(25000,), (3, 40000), (64, 1000), (5000,)])
+def test_short_row_full_reduce_single_block(dtype, shape):
+    """Rows that fit the one-block-per-row path (<= 256 KB, <= 64 rows)."""
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(dtype, [None] * len(shape), name="x")
+        ax = len(shape) - 1
+        tf.reduce_sum(x, [ax], name="s")
+        tf.reduce_max(x, [ax], name="mx")
+        tf.reduce_mean(x, [ax], name="mean")
+    x_ = (rng.standard_normal(shape) * 100).astype(dtype)
+    gpu, cpu = both(g, ["s", "mx", "mean"], {"x": x_})
+    tol = 1e-5 if dtype == np.float32 else 1e-12
+    for a, b in zip(gpu, cpu):
+        torch.testing.assert_close(a, b, rtol=tol, atol=tol * 100)
+
+
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("m,n,k", [(1000, 512, 512), (129, 77, 33), (4096, 10, 100), (64, 128, 1000)])
 def test_matmul_f32_mfma(m, n, k, ta, tb):

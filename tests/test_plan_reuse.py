@@ -102,7 +102,8 @@ def test_kmeans_iterations_adopt_plans_and_match_numpy():
         np.testing.assert_allclose(c1, ref, rtol=1e-6, atol=1e-9)
         assert abs(d1 - dref) <= 1e-9 * abs(dref)
         c = c1
-    assert metrics.snapshot().get("programs_adopted", 0) >= 3
+    snap = metrics.snapshot()
+    assert snap.get("programs_adopted", 0) + snap.get("programs_rebound", 0) >= 3
 
 
 def test_plan_reuse_can_be_disabled():
@@ -116,3 +117,47 @@ def test_plan_reuse_can_be_disabled():
     finally:
         tfs.set_config(plan_reuse=True)
     assert metrics.snapshot().get("programs_adopted", 0) == 0
+
+
+def _spec_graph(w, ints, name_suffix=""):
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float64, [None, w.shape[0]], name="x")
+        y = tf.matmul(x, tf.constant(w))
+        y = tf.tile(y, tf.constant(ints))  # an integer constant: structure, never a parameter
+        tf.identity(y * 0.5, name="y")
+    return g
+
+
+@pytest.mark.parametrize("device", _devices())
+def test_program_for_spec_rebinds_parameters_and_checks_the_rest(device):
+    """DSL graphs rebuilt with new float payloads get the known program with
+    the payloads swapped (Program.rebind, no serialise/parse); a change in an
+    integer constant is a different structure and must not reuse it."""
+    from tensorframes_amd import core
+    engine.clear_program_cache()
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((64, 4))
+    dev = torch.device(device)
+    before = metrics.snapshot().get("programs_rebound", 0)
+    for it in range(4):
+        w = rng.standard_normal((4, 3))
+        ints = [1, 2] if it < 3 else [2, 1]
+        g = _spec_graph(w, ints)
+        spec = core._resolve([g.get_tensor_by_name("y:0")])
+        prog = engine.program_for_spec(spec, ["y:0"], ["x"])
+        got = engine.run_program(prog, [torch.as_tensor(x)], dev)[0].cpu().numpy()
+        want = np.tile(x @ w, ints) * 0.5
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+    # iterations 1 and 2 rebind; iteration 3 changed the int constant: a new program
+    assert metrics.snapshot().get("programs_rebound", 0) - before == 2
+
+
+def test_rebind_refuses_non_parameters():
+    rng = np.random.default_rng(6)
+    g = _spec_graph(rng.standard_normal((4, 3)), [1, 2])
+    prog = engine.program(g.serialize(), ["y:0"], ["x"])
+    with pytest.raises(Exception, match="not a parameter constant"):
+        prog.rebind({"x": torch.zeros(4, 3, dtype=torch.float64)})
+    with pytest.raises(Exception, match="values of its dtype"):
+        prog.rebind({"Const": torch.zeros(5, 3, dtype=torch.float64)})
