@@ -1631,7 +1631,7 @@ std::vector<at::Tensor> Program::run_graph(Plan& p, const std::vector<at::Tensor
 
 namespace {
 constexpr int kPtrWarmRuns = 2;       // eager runs of a pointer set before it is captured
-constexpr size_t kPtrMinSteps = 4;    // no input copies: worth it from a few kernels on
+constexpr size_t kPtrMinSteps = 3;    // no input copies: worth it from a few kernels on
 constexpr size_t kPtrMaxCaps = 8;     // captures per plan (each owns its intermediates)
 constexpr size_t kPtrMaxSeen = 32;
 int64_t ptr_graph_max_bytes() {

@@ -47,6 +47,12 @@ for s in ${STEPS:-tests}; do
     kmeans_agg) run kmeans_agg 300 python scripts/kmeans_profile.py --iters 50 --variant aggregate ;;
     kbreak) run kbreak 300 python scripts/kmeans_breakdown.py --iters 200 ;;
     kmeans) run kmeans 300 python scripts/kmeans_profile.py --iters 50 ;;
+    r4_kmeans) mkdir -p gpurun_out/r4_kmeans; export TMPDIR=/tmp
+      run r4_kmeans/in_graph 300 python scripts/kmeans_profile.py --iters 200 &&
+      run r4_kmeans/aggregate 300 python scripts/kmeans_profile.py --iters 200 --variant aggregate &&
+      run r4_kmeans/phases 300 python scripts/kmeans_phases.py --iters 300 &&
+      run r4_kmeans/cprofile 300 python scripts/kmeans_profile.py --iters 50 --cprofile &&
+      run r4_kmeans/rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r4_kmeans/rocprof" -o run -- python scripts/kmeans_profile.py --iters 20 ;;
     kmeans_cprof) run kmeans_cprof 300 python scripts/kmeans_profile.py --iters 20 --cprofile ;;
     refperf) run refperf 600 python bench/configs.py refperf ;;
     cfg_add) run cfg_add 600 python bench/configs.py add ;;

@@ -327,12 +327,18 @@ def gather_rows(x: torch.Tensor, rows_per_rank: List[int], root: Optional[int] =
     """Variable-length row blocks of every rank (x: this rank's [rows, ...]
     host tensor, rows_per_rank known everywhere): each rank's block, in rank
     order, on every rank (root None) or only on `root` (None elsewhere).
-    One padded all_gather / gather of the tensor itself: no pickling."""
+    Balanced blocks go in one padded all_gather / gather of the tensor itself;
+    skewed ones (padding would move > 25 % extra bytes) go rank by rank at
+    their exact sizes (point-to-point to `root`, or one broadcast per rank).
+    No pickling either way."""
     if not is_distributed():
         return [x]
     _ensure_groups()
     x = x.contiguous()
-    mx = max(int(r) for r in rows_per_rank) if rows_per_rank else 0
+    rows = [int(r) for r in rows_per_rank]
+    mx = max(rows) if rows else 0
+    if mx * len(rows) * 4 > sum(rows) * 5:
+        return _gather_rows_exact(x, rows, root)
     pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype)
     if x.shape[0]:
         pad[:x.shape[0]].copy_(x)
@@ -347,6 +353,36 @@ def gather_rows(x: torch.Tensor, rows_per_rank: List[int], root: Optional[int] =
     if parts is None:
         return None
     return [p[:int(r)] for p, r in zip(parts, rows_per_rank)]
+
+
+def _gather_rows_exact(x: torch.Tensor, rows: List[int], root: Optional[int]) -> Optional[List[torch.Tensor]]:
+    """gather_rows without padding: every block travels at its own size
+    (zero-row ranks send nothing; every rank knows `rows`)."""
+    group = _state["cpu_group"]
+    me, tail = rank(), tuple(x.shape[1:])
+    with _traced("gather_rows_exact", _nbytes(x)):
+        if root is not None:
+            if me != root:
+                if rows[me]:
+                    dist.send(x, dst=root, group=group)
+                return None
+            parts = []
+            for r, n in enumerate(rows):
+                if r == me:
+                    parts.append(x)
+                    continue
+                buf = torch.empty((n,) + tail, dtype=x.dtype)
+                if n:
+                    dist.recv(buf, src=r, group=group)
+                parts.append(buf)
+            return parts
+        parts = []
+        for r, n in enumerate(rows):
+            buf = x if r == me else torch.empty((n,) + tail, dtype=x.dtype)
+            if n:
+                dist.broadcast(buf, src=r, group=group)
+            parts.append(buf)
+        return parts
 
 
 def broadcast_tensor(t: Optional[torch.Tensor], shape: tuple, dtype: torch.dtype, src: int) -> torch.Tensor:
