@@ -832,11 +832,65 @@ __global__ __launch_bounds__(1024) void useg_small_int(const T* __restrict__ x, 
   }
 }
 
+// ---- very few segments (nseg <= 16, inner == 1, integer data): each thread
+// keeps one accumulator per segment in registers (compile-time indexed: a
+// compare-select per segment and row, no LDS atomics, no contention), then a
+// wave reduction and one LDS slot per wave and segment. The K-Means counts
+// (k = 10 clusters) are this shape.
+constexpr int kUsegRegSegs = 16;
+template <typename T, typename I, int OP>
+__global__ __launch_bounds__(1024) void useg_tiny_int(const T* __restrict__ x, const I* __restrict__ ids,
+                                                      T* __restrict__ y, int64_t n, int nseg) {
+  __shared__ long long part[16][kUsegRegSegs];
+  long long acc[kUsegRegSegs];
+#pragma unroll
+  for (int g = 0; g < kUsegRegSegs; ++g) acc[g] = ident<OP, long long>();
+  constexpr int U = 8;
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += U * 1024) {
+    int64_t gv[U];
+    long long v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * 1024;
+      const bool ok = i < n;
+      gv[u] = ok ? (int64_t)ids[i] : -1;
+      v[u] = ok ? (long long)x[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int g = 0; g < kUsegRegSegs; ++g)
+        if (gv[u] == g) acc[g] = combine<OP, long long>(acc[g], v[u]);
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < kUsegRegSegs; ++g) {
+    const long long t = wave_reduce<OP, long long>(acc[g]);
+    if (lane == 0) part[wave][g] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < nseg) {
+    const int g = threadIdx.x;
+    long long a = part[0][g];
+    for (int w = 1; w < 16; ++w) a = combine<OP, long long>(a, part[w][g]);
+    if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
+      if (a == ident<OP, long long>())
+        a = OP == (int)RedOp::MAX ? (long long)std::numeric_limits<T>::lowest() : (long long)std::numeric_limits<T>::max();
+    }
+    y[g] = T(a);
+  }
+}
+
 template <typename T, typename I, int OP>
 static void useg_typed(const void* x, const void* ids, void* y, int64_t n, int64_t inner, int64_t nseg,
                        void* ws, hipStream_t s) {
   using A = typename AccT<T>::type;
   if constexpr (std::is_integral<T>::value && OP != (int)RedOp::PROD) {
+    if (inner == 1 && n <= kUsegSmallRows && nseg <= kUsegRegSegs) {
+      hipLaunchKernelGGL((useg_tiny_int<T, I, OP>), dim3(1), dim3(1024), 0, s, (const T*)x, (const I*)ids, (T*)y, n,
+                         (int)nseg);
+      return;
+    }
     if (inner == 1 && n <= kUsegSmallRows && nseg <= kUsegSmallSegs) {
       hipLaunchKernelGGL((useg_small_int<T, I, OP>), dim3(1), dim3(1024), 0, s, (const T*)x, (const I*)ids, (T*)y, n,
                          nseg);

@@ -126,21 +126,23 @@ def test_unsorted_segment_sum_and_gather():
         torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-9)
 
 
+@pytest.mark.parametrize("nseg", [10, 16, 37])
 @pytest.mark.parametrize("dtype", [np.int32, np.int64])
 @pytest.mark.parametrize("n", [1, 777, 25000, 262144])
-def test_small_int_segment_reduce_single_block(dtype, n):
-    """The one-block LDS-atomic path (inner == 1, integer data, n <= 256k):
+def test_small_int_segment_reduce_single_block(dtype, n, nseg):
+    """The one-block paths (inner == 1, integer data, n <= 256k: registers for
+    <= 16 segments, LDS atomics above):
     negative and out-of-range ids are dropped, empty segments of Min/Max get
     the type's extreme value, Sum of int32 wraps like the slab path."""
     g = tf.Graph()
     with g.as_default():
         x = tf.placeholder(dtype, [None], name="x")
         ids = tf.placeholder(tf.int64, [None], name="ids")
-        tf.unsorted_segment_sum(x, ids, 37, name="s")
-        tf.unsorted_segment_min(x, ids, 37, name="lo")
-        tf.unsorted_segment_max(x, ids, 37, name="hi")
+        tf.unsorted_segment_sum(x, ids, nseg, name="s")
+        tf.unsorted_segment_min(x, ids, nseg, name="lo")
+        tf.unsorted_segment_max(x, ids, nseg, name="hi")
     x_ = rng.integers(-1000, 1000, n).astype(dtype)
-    ids_ = rng.integers(-2, 30, n).astype(np.int64)  # segments 30..36 stay empty
+    ids_ = rng.integers(-2, nseg + 3, n).astype(np.int64)  # some out of range; the top segments may stay empty
     gpu, cpu = both(g, ["s", "lo", "hi"], {"x": x_, "ids": ids_})
     for a, b in zip(gpu, cpu):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
