@@ -694,12 +694,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     d["allocs"] = v.allocs;
     d["frees"] = v.frees;
     d["fallbacks"] = v.fallbacks;
+    d["capture_allocs"] = v.capture_allocs;
     d["device_mallocs"] = v.device_mallocs;
     d["live"] = v.live_bytes;
     d["peak"] = v.peak_bytes;
     d["cached"] = v.cached_bytes;
     return d;
-  }, "engine-owned device pool: allocations, frees, c10 fallbacks, hipMallocs, live / peak / cached bytes");
+  }, "engine-owned device pool: allocations, frees, c10 fallbacks, HIP-graph capture allocations, hipMallocs, live / peak / cached bytes");
   m.def("trim_device_pool", &dev_pool_trim);
   // ---- engine-owned communicators (csrc/comm/comm.h)
   {

@@ -67,6 +67,10 @@ State& st() {
   return *s;
 }
 std::atomic<int64_t> g_allocs{0}, g_frees{0}, g_fallbacks{0}, g_live{0}, g_peak{0}, g_device_mallocs{0};
+// allocations made while one of the engine's HIP graphs captures their stream:
+// they belong to the graph (its private memory pool), not to this pool, and
+// are counted apart from the fallbacks (pool disabled / out of memory)
+std::atomic<int64_t> g_capture_allocs{0};
 
 // streams being captured by the engine's own HIP graphs (HipGraph::begin /
 // end report them): the common case, no capture anywhere, costs one atomic
@@ -202,7 +206,11 @@ bool dev_pool_enabled() {
 
 at::Tensor dev_empty(at::IntArrayRef sizes, at::ScalarType dt, const at::Device& dev, hipStream_t stream) {
   auto opts = at::TensorOptions().dtype(dt).device(dev);
-  if (!dev.is_cuda() || !dev_pool_enabled() || capturing(stream)) {
+  if (dev.is_cuda() && dev_pool_enabled() && capturing(stream)) {
+    g_capture_allocs++;
+    return at::empty(sizes, opts);
+  }
+  if (!dev.is_cuda() || !dev_pool_enabled()) {
     if (dev.is_cuda()) g_fallbacks++;
     return at::empty(sizes, opts);
   }
@@ -317,6 +325,7 @@ DevPoolStats dev_pool_stats() {
   s.allocs = g_allocs.load();
   s.frees = g_frees.load();
   s.fallbacks = g_fallbacks.load();
+  s.capture_allocs = g_capture_allocs.load();
   s.live_bytes = g_live.load();
   s.peak_bytes = g_peak.load();
   s.device_mallocs = g_device_mallocs.load();

@@ -31,7 +31,7 @@ at::Tensor pool_empty_like(const at::Tensor& t);
 at::Tensor pool_zeros(at::IntArrayRef sizes, const at::TensorOptions& opts);
 
 struct DevPoolStats {
-  int64_t allocs = 0, frees = 0, fallbacks = 0, device_mallocs = 0;
+  int64_t allocs = 0, frees = 0, fallbacks = 0, device_mallocs = 0, capture_allocs = 0;
   int64_t live_bytes = 0, peak_bytes = 0, cached_bytes = 0;
 };
 DevPoolStats dev_pool_stats();
