@@ -562,8 +562,22 @@ __global__ __launch_bounds__(256) void useg_final(const typename AccT<T>::type* 
   for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * per_wave; base < m; base += waves * per_wave) {
     const int64_t i = base + lane / G;
     A acc = ident<OP, A>();
-    if (i < m)
-      for (int64_t b = sub; b < B; b += G) acc = combine<OP, A>(acc, part[b * m + i]);
+    if (i < m) {
+      // 8 slabs' loads in flight per lane, folded in slab order (the same
+      // order as one at a time: deterministic, bit-identical)
+      constexpr int R = 8;
+      for (int64_t b0 = sub; b0 < B; b0 += (int64_t)R * G) {
+        A t[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int64_t b = b0 + (int64_t)r * G;
+          t[r] = b < B ? part[b * m + i] : ident<OP, A>();
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (b0 + (int64_t)r * G < B) acc = combine<OP, A>(acc, t[r]);  // no padding term (-0.0 stays -0.0)
+      }
+    }
     for (int s = G / 2; s >= 1; s >>= 1) acc = combine<OP, A>(acc, __shfl_xor(acc, s, 64));
     if (i >= m || sub != 0) continue;
     if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
@@ -835,50 +849,75 @@ __global__ __launch_bounds__(1024) void useg_small_int(const T* __restrict__ x, 
 // ---- very few segments (nseg <= 16, inner == 1, integer data): each thread
 // keeps one accumulator per segment in registers (compile-time indexed: a
 // compare-select per segment and row, no LDS atomics, no contention), then a
-// wave reduction and one LDS slot per wave and segment. The K-Means counts
-// (k = 10 clusters) are this shape.
+// wave reduction and one LDS slot per wave and segment. Many blocks of 1024
+// rows each write one partial row [nseg]; one wave folds the partials in block
+// order (integers: exact). The K-Means counts (k = 10 clusters, 25k rows per
+// partition) are this shape: a single 1024-thread block took 23.5 us of
+// compare-selects on one CU (profiles/r4_kmeans/kernel_stats.csv).
 constexpr int kUsegRegSegs = 16;
+constexpr int kUsegTinyThreads = 256, kUsegTinyU = 4;
+constexpr int64_t kUsegTinyRows = kUsegTinyThreads * kUsegTinyU;  // rows per block
 template <typename T, typename I, int OP>
-__global__ __launch_bounds__(1024) void useg_tiny_int(const T* __restrict__ x, const I* __restrict__ ids,
-                                                      T* __restrict__ y, int64_t n, int nseg) {
-  __shared__ long long part[16][kUsegRegSegs];
+__global__ __launch_bounds__(kUsegTinyThreads) void useg_tiny_int(const T* __restrict__ x, const I* __restrict__ ids,
+                                                                  long long* __restrict__ part, int64_t n, int nseg) {
+  // per-thread histograms, then transposed through LDS: wave w folds
+  // segments w, w+4, ... (4 values per lane, one wave reduction per segment)
+  // instead of every wave reducing every segment
+  __shared__ long long tab[kUsegRegSegs][kUsegTinyThreads];
   long long acc[kUsegRegSegs];
 #pragma unroll
   for (int g = 0; g < kUsegRegSegs; ++g) acc[g] = ident<OP, long long>();
-  constexpr int U = 8;
-  for (int64_t i0 = threadIdx.x; i0 < n; i0 += U * 1024) {
-    int64_t gv[U];
-    long long v[U];
+  const int64_t i0 = (int64_t)blockIdx.x * kUsegTinyRows + threadIdx.x;
+  int64_t gv[kUsegTinyU];
+  long long v[kUsegTinyU];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + u * 1024;
-      const bool ok = i < n;
-      gv[u] = ok ? (int64_t)ids[i] : -1;
-      v[u] = ok ? (long long)x[i] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int g = 0; g < kUsegRegSegs; ++g)
-        if (gv[u] == g) acc[g] = combine<OP, long long>(acc[g], v[u]);
+  for (int u = 0; u < kUsegTinyU; ++u) {
+    const int64_t i = i0 + u * kUsegTinyThreads;
+    const bool ok = i < n;
+    gv[u] = ok ? (int64_t)ids[i] : -1;
+    v[u] = ok ? (long long)x[i] : 0;
   }
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int g = 0; g < kUsegRegSegs; ++g) {
-    const long long t = wave_reduce<OP, long long>(acc[g]);
-    if (lane == 0) part[wave][g] = t;
-  }
+  for (int u = 0; u < kUsegTinyU; ++u)
+#pragma unroll
+    for (int g = 0; g < kUsegRegSegs; ++g)
+      if (gv[u] == g) acc[g] = combine<OP, long long>(acc[g], v[u]);
+#pragma unroll
+  for (int g = 0; g < kUsegRegSegs; ++g)
+    if (g < nseg) tab[g][threadIdx.x] = acc[g];
   __syncthreads();
-  if (threadIdx.x < nseg) {
-    const int g = threadIdx.x;
-    long long a = part[0][g];
-    for (int w = 1; w < 16; ++w) a = combine<OP, long long>(a, part[w][g]);
-    if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
-      if (a == ident<OP, long long>())
-        a = OP == (int)RedOp::MAX ? (long long)std::numeric_limits<T>::lowest() : (long long)std::numeric_limits<T>::max();
-    }
-    y[g] = T(a);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int g = wave; g < nseg; g += kUsegTinyThreads / 64) {
+    long long a = tab[g][lane];
+#pragma unroll
+    for (int q = 1; q < kUsegTinyThreads / 64; ++q) a = combine<OP, long long>(a, tab[g][lane + 64 * q]);
+    a = wave_reduce<OP, long long>(a);
+    if (lane == 0) part[(int64_t)blockIdx.x * nseg + g] = a;
   }
+}
+
+// one wave folds the B partial rows [B][nseg] in block order: the loads of
+// 8 rows are in flight together (a dependent load per row took ~6 us)
+template <typename T, int OP>
+__global__ __launch_bounds__(64) void useg_tiny_final(const long long* __restrict__ part, T* __restrict__ y, int64_t B,
+                                                      int nseg) {
+  const int g = threadIdx.x;
+  if (g >= nseg) return;
+  long long a = ident<OP, long long>();
+  constexpr int R = 8;
+  for (int64_t b0 = 0; b0 < B; b0 += R) {
+    long long t[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) t[r] = b0 + r < B ? part[(b0 + r) * nseg + g] : ident<OP, long long>();
+#pragma unroll
+    for (int r = 0; r < R; ++r) a = combine<OP, long long>(a, t[r]);
+  }
+  if constexpr (OP == (int)RedOp::MIN || OP == (int)RedOp::MAX) {
+    // TF: empty segments get the type's highest (min) / lowest (max) value
+    if (a == ident<OP, long long>())
+      a = OP == (int)RedOp::MAX ? (long long)std::numeric_limits<T>::lowest() : (long long)std::numeric_limits<T>::max();
+  }
+  y[g] = T(a);
 }
 
 template <typename T, typename I, int OP>
@@ -887,7 +926,13 @@ static void useg_typed(const void* x, const void* ids, void* y, int64_t n, int64
   using A = typename AccT<T>::type;
   if constexpr (std::is_integral<T>::value && OP != (int)RedOp::PROD) {
     if (inner == 1 && n <= kUsegSmallRows && nseg <= kUsegRegSegs) {
-      hipLaunchKernelGGL((useg_tiny_int<T, I, OP>), dim3(1), dim3(1024), 0, s, (const T*)x, (const I*)ids, (T*)y, n,
+      // partials: B x nseg 8-byte values, within the workspace of the
+      // LDS-private pass (B <= n / 1024 <= useg_blocks(n, nseg, 1))
+      const int64_t B = (n + kUsegTinyRows - 1) / kUsegTinyRows;
+      long long* part = static_cast<long long*>(ws);
+      hipLaunchKernelGGL((useg_tiny_int<T, I, OP>), dim3((unsigned)B), dim3(kUsegTinyThreads), 0, s, (const T*)x,
+                         (const I*)ids, part, n, (int)nseg);
+      hipLaunchKernelGGL((useg_tiny_final<T, OP>), dim3(1), dim3(64), 0, s, (const long long*)part, (T*)y, B,
                          (int)nseg);
       return;
     }

@@ -130,8 +130,9 @@ def test_unsorted_segment_sum_and_gather():
 @pytest.mark.parametrize("dtype", [np.int32, np.int64])
 @pytest.mark.parametrize("n", [1, 777, 25000, 262144])
 def test_small_int_segment_reduce_single_block(dtype, n, nseg):
-    """The one-block paths (inner == 1, integer data, n <= 256k: registers for
-    <= 16 segments, LDS atomics above):
+    """The small integer paths (inner == 1, integer data, n <= 256k: register
+    histograms in 1024-row blocks + a one-wave fold for <= 16 segments, one
+    block of LDS atomics above):
     negative and out-of-range ids are dropped, empty segments of Min/Max get
     the type's extreme value, Sum of int32 wraps like the slab path."""
     g = tf.Graph()
