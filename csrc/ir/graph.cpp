@@ -467,11 +467,18 @@ std::shared_ptr<Graph> Graph::with_values(const std::map<std::string, at::Tensor
     ht->bytes.assign(b, b + c.numel() * c.element_size());
     it->second.tensor = std::move(ht);
   }
-  auto g = std::make_shared<Graph>(std::move(d));
+  // same nodes, names and edges: copy the resolved structure instead of
+  // re-resolving every input by name; only the def pointers move
+  auto g = std::shared_ptr<Graph>(new Graph(*this, std::move(d)));
   std::lock_guard<std::mutex> lk(key_mu_);
   g->key_ = key_;
   g->params_ = params_;
   return g;
+}
+
+Graph::Graph(const Graph& base, GraphDef def) : def_(std::move(def)), nodes_(base.nodes_), by_name_(base.by_name_) {
+  TFA_CHECK(def_.nodes.size() == nodes_.size(), "graph copy: node count changed");
+  for (size_t i = 0; i < nodes_.size(); ++i) nodes_[i].def = &def_.nodes[i];
 }
 
 uint64_t Graph::structure_key() const {
@@ -594,6 +601,36 @@ Graph::Infos Graph::infer_impl(const std::vector<int>& order, const std::map<int
       d = d || (!infos[ni].empty() && !infos[ni][0].value && infos[ni][0].row == RowClass::ROW);
       dyn[ni] = d;
       continue;
+    }
+    if (base && !n.inputs.empty()) {
+      // redone, but every input that changed carries no value and kept its
+      // dtype / shape / row class (inputs that did not change are the base's):
+      // the node's infos are the base's (inference is a function of the input
+      // infos and the unchanged attributes; a node with a valueless input is
+      // never folded). A rebuilt K-Means graph re-infers only the few nodes
+      // its new centres fold into, not everything downstream of them.
+      bool same = base->at(ni).size() == static_cast<size_t>(n.num_outputs);
+      for (auto& r : n.inputs) {
+        if (!same) break;
+        if (!(*redo)[r.node]) continue;
+        if (r.index >= static_cast<int>(infos[r.node].size()) ||
+            r.index >= static_cast<int>((*base)[r.node].size())) {
+          same = false;
+          break;
+        }
+        const TensorInfo& a = infos[r.node][r.index];
+        const TensorInfo& b = (*base)[r.node][r.index];
+        same = !a.value && !b.value && !a.strings && !b.strings && a.dtype == b.dtype && a.shape == b.shape &&
+               a.row == b.row;
+      }
+      if (same) {
+        infos[ni] = (*base)[ni];
+        bool d = n.op == "Placeholder" || n.op == "PlaceholderV2";
+        if (const OpDef* od0 = reg.find(n.op)) d = d || od0->stateful;
+        for (auto& r : n.inputs) d = d || dyn[r.node];
+        dyn[ni] = d;
+        continue;
+      }
     }
     auto fit = feeds.find(ni);
     if (fit != feeds.end()) {

@@ -195,6 +195,10 @@ class Graph {
   std::shared_ptr<Graph> with_values(const std::map<std::string, at::Tensor>& values) const;
 
  private:
+  // a copy of `base` (same structure) over `def`, a copy of base's GraphDef
+  // with some constant payloads replaced (with_values)
+  Graph(const Graph& base, GraphDef def);
+
   GraphDef def_;
   std::vector<Node> nodes_;
   std::unordered_map<std::string, int> by_name_;
