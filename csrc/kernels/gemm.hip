@@ -548,15 +548,16 @@ struct F32Plan {
 // 128x128) and ties the headline 2.5Mx512x512; 256x96 (8x1) and 128x128 (2x4)
 // win some Inception convs. 256x192, a BK=32 256x128 and BK=32 128x64 /
 // 128x32 (one whole C=32 filter tap per k tile) never won.
-// 16-17 are 8-wave versions of the narrow conv tiles: 128x192 as 4x2 waves
-// (each 32x96, the wave tile of 64x192) and 256x64 as 8x1 (each 32x64): the
-// block's A and B tiles are shared by twice the waves (less global and LDS
-// traffic per FLOP) at the same occupancy.
-constexpr int kNumTiles = 18;
+// 16-18 are 8-wave versions of narrow conv tiles: 128x192 as 4x2 waves
+// (each 32x96, the wave tile of 64x192), 256x64 as 8x1 (each 32x64) and
+// 128x64 as 4x2 (each 32x32, the wave tile of 64x64): the block's A and B
+// tiles are shared by twice the waves (less global and LDS traffic per FLOP)
+// at the same wave tile. 256x160 as 8x1 never won (profiles/r4_tiles/).
+constexpr int kNumTiles = 19;
 constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
                                       {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128},
                                       {256, 64}, {256, 32}, {256, 96}, {256, 128}, {256, 96},
-                                      {128, 128}, {128, 192}, {256, 64}};
+                                      {128, 128}, {128, 192}, {256, 64}, {128, 64}};
 
 int64_t tile_blocks(int c, int64_t M, int64_t N, int64_t batch) {
   return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
@@ -656,7 +657,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 14: TFA_LAUNCH_TILE(256, 96, 8, 1); break;
     case 15: TFA_LAUNCH_TILE(128, 128, 2, 4); break;
     case 16: TFA_LAUNCH_TILE(128, 192, 4, 2); break;
-    default: TFA_LAUNCH_TILE(256, 64, 8, 1); break;
+    case 17: TFA_LAUNCH_TILE(256, 64, 8, 1); break;
+    default: TFA_LAUNCH_TILE(128, 64, 4, 2); break;
   }
 #undef TFA_LAUNCH_TILE
 #undef TFA_LAUNCH_TILE_BK
