@@ -239,6 +239,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              return l;
            })
       .def("run", &Program::run, py::call_guard<py::gil_scoped_release>())
+      .def("run_concurrent", &Program::run_concurrent, py::arg("inputs_list"), py::arg("max_streams") = 4,
+           py::call_guard<py::gil_scoped_release>(),
+           "independent runs over several input sets on one GPU, forked onto engine side streams and joined "
+           "back into the caller's stream")
       .def("run_chunked", &Program::run_chunked, py::arg("seg_inputs"), py::arg("seg_outputs"),
            py::arg("chunk_rows"), py::arg("device"), py::arg("depth") = 3, py::arg("wait") = true,
            py::call_guard<py::gil_scoped_release>())

@@ -1782,6 +1782,84 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
   return outs;
 }
 
+namespace {
+// engine side streams and fork/join events per device (created once, never
+// destroyed: runs may outlive static teardown)
+struct SideStreams {
+  std::mutex mu;
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> events;  // [0]: fork; [1]: previous caller; [2 + i]: join of stream i
+  hipStream_t last_caller = nullptr;
+};
+SideStreams& side_streams(int dev) {
+  static std::mutex m;
+  static std::map<int, SideStreams*> all;
+  std::lock_guard<std::mutex> lk(m);
+  auto& p = all[dev];
+  if (!p) p = new SideStreams();
+  return *p;
+}
+}  // namespace
+
+std::vector<std::vector<at::Tensor>> Program::run_concurrent(
+    const std::vector<std::vector<at::Tensor>>& inputs_list, int max_streams) {
+  std::vector<std::vector<at::Tensor>> outs;
+  if (inputs_list.empty()) return outs;
+  TFA_CHECK(!inputs_list[0].empty() && inputs_list[0][0].is_cuda(), "run_concurrent: device inputs expected");
+  const int dev = inputs_list[0][0].device().index();
+  for (auto& ins : inputs_list)
+    for (auto& t : ins)
+      TFA_CHECK(t.is_cuda() && t.device().index() == dev, "run_concurrent: all inputs on one device");
+  const int k = std::max(1, std::min<int>(max_streams, static_cast<int>(inputs_list.size())));
+  c10::hip::HIPGuard guard(dev);
+  const hipStream_t caller = c10::hip::getCurrentHIPStream(dev).stream();
+  SideStreams& ss = side_streams(dev);
+  std::lock_guard<std::mutex> lk(ss.mu);  // one fork/join at a time per device (events are shared)
+  while (static_cast<int>(ss.streams.size()) < k) {
+    hipStream_t st;
+    TFA_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess, "run_concurrent: hipStreamCreate");
+    ss.streams.push_back(st);
+  }
+  while (ss.events.size() < ss.streams.size() + 2) {
+    hipEvent_t e;
+    TFA_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "run_concurrent: hipEventCreate");
+    ss.events.push_back(e);
+  }
+  // Fork: every side stream waits for the caller's work so far. Outputs made
+  // on side stream i go back to ITS free list in the pool when the caller
+  // drops them; only these private streams allocate from those lists, and
+  // only after such a fork, so a reuse is ordered after every read the caller
+  // queued before dropping them -- no per-block stream records (an event per
+  // freed block cost more host time than the overlap saved). A call from a
+  // different caller stream also waits for the previous caller's work.
+  TFA_CHECK(hipEventRecord(ss.events[0], caller) == hipSuccess, "run_concurrent: hipEventRecord");
+  const bool other_caller = ss.last_caller && ss.last_caller != caller;
+  if (other_caller)
+    TFA_CHECK(hipEventRecord(ss.events[1], ss.last_caller) == hipSuccess, "run_concurrent: hipEventRecord");
+  for (int i = 0; i < k; ++i) {
+    TFA_CHECK(hipStreamWaitEvent(ss.streams[i], ss.events[0], 0) == hipSuccess, "run_concurrent: hipStreamWaitEvent");
+    if (other_caller)
+      TFA_CHECK(hipStreamWaitEvent(ss.streams[i], ss.events[1], 0) == hipSuccess, "run_concurrent: hipStreamWaitEvent");
+  }
+  ss.last_caller = caller;
+  outs.reserve(inputs_list.size());
+  for (size_t i = 0; i < inputs_list.size(); ++i) {
+    // partition i always runs on side stream i % k: its zero-copy replay
+    // instance keeps one stream across calls (no cross-stream drain)
+    const hipStream_t st = ss.streams[i % k];
+    c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromExternal(st, static_cast<c10::DeviceIndex>(dev)));
+    outs.push_back(run(inputs_list[i]));
+  }
+  // Join: the caller's stream waits for every side stream (its later
+  // allocations, which may reuse the inputs' blocks, and its reads of the
+  // outputs are ordered after the side-stream work)
+  for (int i = 0; i < k; ++i) {
+    TFA_CHECK(hipEventRecord(ss.events[2 + i], ss.streams[i]) == hipSuccess, "run_concurrent: hipEventRecord");
+    TFA_CHECK(hipStreamWaitEvent(caller, ss.events[2 + i], 0) == hipSuccess, "run_concurrent: hipStreamWaitEvent");
+  }
+  return outs;
+}
+
 std::vector<at::Tensor> Program::run(const std::vector<at::Tensor>& inputs) {
   TFA_CHECK(host_op_error_.empty(), host_op_error_);
   auto p = plan_for(inputs);

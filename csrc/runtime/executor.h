@@ -77,6 +77,15 @@ class Program {
   // Run on concrete inputs (all on one device: CPU or a GPU). Returns the fetches.
   std::vector<at::Tensor> run(const std::vector<at::Tensor>& inputs);
 
+  // Independent runs over several input sets on one GPU (the device-resident
+  // partitions of one map_blocks), forked onto up to `max_streams` engine side
+  // streams after the caller's stream and joined back into it: a partition
+  // whose chain of small kernels cannot fill the GPU runs beside the others.
+  // The fork/join is a few event records and waits on the host (no Python
+  // stream objects); outputs are ordered into the caller's stream.
+  std::vector<std::vector<at::Tensor>> run_concurrent(const std::vector<std::vector<at::Tensor>>& inputs_list,
+                                                      int max_streams = 4);
+
   // Pipelined host->device->host execution over row chunks of several segments.
   // seg_inputs[s][i]: pinned host tensor for feed i of segment s (leading dim = rows).
   // seg_outputs[s][j]: preallocated pinned host tensor for fetch j.

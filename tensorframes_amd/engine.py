@@ -355,7 +355,20 @@ def run_programs_concurrent(prog, inputs_list: List[List[torch.Tensor]], dev: to
     of a map_blocks) issued on up to 4 streams at once, so a GPU that one small
     partition cannot fill runs them side by side (K-Means: 4 partitions of
     25k rows, each a chain of small kernels). The results are ordered back
-    onto the caller's stream before they are returned."""
+    onto the caller's stream before they are returned. The fork/join runs in
+    C++ (Program::run_concurrent); the Python version below is the fallback
+    for program objects without it."""
+    if hasattr(prog, "run_concurrent"):
+        # native fork/join (Program::run_concurrent): engine side streams,
+        # events and pool-block bookkeeping in C++, GIL released
+        ins_list = [[t.contiguous() for t in ins] for ins in inputs_list]
+        if dev.index is None or dev.index == torch.cuda.current_device():
+            outs = [list(o) for o in prog.run_concurrent(ins_list)]
+        else:
+            with torch.cuda.device(dev):
+                outs = [list(o) for o in prog.run_concurrent(ins_list)]
+        metrics.add("concurrent_partition_runs", len(inputs_list))
+        return outs
     main = torch.cuda.current_stream(dev)
     pool = _side_streams.setdefault(dev.index, [])
     k = min(len(inputs_list), 4)
