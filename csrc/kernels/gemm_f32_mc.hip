@@ -1,0 +1,22 @@
+// f32 core tile kernels for m-contiguous A (transpose_a MatMuls): every tile of
+// gemm_f32_core.h instantiated for this A loader (one translation unit per
+// loader, so the builds run in parallel).
+#include "gemm_f32_core.h"
+
+namespace tfa {
+namespace k {
+namespace f32core {
+
+void launch_mcontig_b(const F32Plan& p, const GemmArgs& g, bool vec, hipStream_t s) {
+  if (vec) launch_cfg<A_MCONTIG, false, true>(p, g, ConvGeom{}, s);
+  else launch_cfg<A_MCONTIG, false, false>(p, g, ConvGeom{}, s);
+}
+
+void launch_mcontig_bt(const F32Plan& p, const GemmArgs& g, bool vec, hipStream_t s) {
+  if (vec) launch_cfg<A_MCONTIG, true, true>(p, g, ConvGeom{}, s);
+  else launch_cfg<A_MCONTIG, true, false>(p, g, ConvGeom{}, s);
+}
+
+}  // namespace f32core
+}  // namespace k
+}  // namespace tfa
