@@ -564,7 +564,9 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 15: TFA_LAUNCH_TILE(128, 128, 2, 4); break;
     case 16: TFA_LAUNCH_TILE(128, 192, 4, 2); break;
     case 17: TFA_LAUNCH_TILE(256, 64, 8, 1); break;
-    default: TFA_LAUNCH_TILE(128, 64, 4, 2); break;
+    case 18: TFA_LAUNCH_TILE(128, 64, 4, 2); break;
+    case 19: TFA_LAUNCH_TILE(128, 256, 4, 2); break;
+    default: TFA_LAUNCH_TILE(256, 256, 4, 2); break;
   }
 #undef TFA_LAUNCH_TILE
 #undef TFA_LAUNCH_TILE_BK

@@ -118,9 +118,10 @@ def test_every_f32_tile_gives_bitwise_identical_results():
     (Shapes sized so every forced tile stays single-pass: a split-K plan sums in
     another order, and the tuner never picks one.)"""
     rng = np.random.default_rng(9)
-    x = rng.uniform(-1, 1, (40000, 300)).astype(np.float32)
+    # >= 256 row tiles of the tallest (256-row) tiles: no forced tile goes split-K
+    x = rng.uniform(-1, 1, (70000, 300)).astype(np.float32)
     w = rng.uniform(-1, 1, (300, 256)).astype(np.float32)
-    img = rng.uniform(-1, 1, (96, 20, 20, 32)).astype(np.float32)
+    img = rng.uniform(-1, 1, (176, 20, 20, 32)).astype(np.float32)
     f = rng.uniform(-1, 1, (3, 3, 32, 192)).astype(np.float32)
     g = tf.Graph()
     with g.as_default():
