@@ -78,12 +78,14 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
 // 19-20 are 8-wave 128x256 (4x2 waves of 32x128) and 256x256 (4x2 waves of
 // 64x128, 1 block per CU): 4096^3 137.5 -> 140.9 TF, 8192^3 140.8 -> 142.2 TF,
 // 2.5M x 512 x 512 134.8 -> 135.6 TF; a 2x4 128x256 never beat them.
-constexpr int kNumTiles = 21;
+// 21 is 256x256 as 16 waves (4x4 waves of 64x64, 1024 threads, four waves
+// per SIMD in one block): 4096^3 141.2 TF, 8192^3 142.6 TF.
+constexpr int kNumTiles = 22;
 constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
                                       {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128},
                                       {256, 64}, {256, 32}, {256, 96}, {256, 128}, {256, 96},
                                       {128, 128}, {128, 192}, {256, 64}, {128, 64}, {128, 256},
-                                      {256, 256}};
+                                      {256, 256}, {256, 256}};
 
 int64_t tile_blocks(int c, int64_t M, int64_t N, int64_t batch) {
   return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;

@@ -117,7 +117,7 @@ __device__ __forceinline__ void out_col(const GemmArgs& g, float* Cb, int64_t co
 // block tile at a 64x64 / 64x96 wave tile, half the global traffic per FLOP of
 // a 4-wave 256x64 and half the accumulator registers of a 4-wave 256x128)
 template <int BM, int BN, int WM, int WN, int AL, bool TB, bool VEC, int BK>
-__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 8 ? 2 : (BM * BN > 128 * 192 ? 1 : 2)))
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 4 : (WM * WN == 8 ? 2 : (BM * BN > 128 * 192 ? 1 : 2))))
 void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_per_split, int flags) {
   constexpr int NT = 64 * WM * WN;
   // k-major LDS images. One written with scalar stores (a k-contiguous
@@ -129,7 +129,8 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
   constexpr int LDB = TB ? BN + 2 : BN + 4;
   const int vepi = flags & 1;  // bit 0: vector epilogue
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves, >= one 32x32 tile each");
+  static_assert((WM * WN == 4 || WM * WN == 8 || WM * WN == 16) && TM >= 1 && TN >= 1,
+                "4, 8 or 16 waves, >= one 32x32 tile each");
   constexpr int KQ = BK / 4;  // float4 pieces along k
   constexpr int APIECES = BM * BK / 4, BPIECES = BN * BK / 4;  // float4 pieces per tile
   constexpr int AP = (APIECES + NT - 1) / NT, BP = (BPIECES + NT - 1) / NT;
@@ -566,7 +567,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 17: TFA_LAUNCH_TILE(256, 64, 8, 1); break;
     case 18: TFA_LAUNCH_TILE(128, 64, 4, 2); break;
     case 19: TFA_LAUNCH_TILE(128, 256, 4, 2); break;
-    default: TFA_LAUNCH_TILE(256, 256, 4, 2); break;
+    case 20: TFA_LAUNCH_TILE(256, 256, 4, 2); break;
+    default: TFA_LAUNCH_TILE(256, 256, 4, 4); break;
   }
 #undef TFA_LAUNCH_TILE
 #undef TFA_LAUNCH_TILE_BK
