@@ -1,10 +1,13 @@
 // f32 MFMA GEMM + implicit-GEMM Conv2D for gfx950 (CDNA4).
 //
 // v_mfma_f32_32x32x2_f32 (exact f32: gfx950 has no xf32). One kernel
-// template over the block tile BMxBN (4 waves arranged WMxWN, each wave
+// template (gemm_f32_core.h, instantiated per A loader in gemm_f32_*.hip)
+// over the block tile BMxBN (4, 8 or 16 waves arranged WMxWN, each wave
 // owning (BM/WM)x(BN/WN) as 32x32 MFMA tiles) so the tile can follow the
-// problem: 128x128 for the big tall-skinny GEMMs, 128x64 / 64x64 / 128x32
-// for narrow conv layers, split-K for grids that cannot fill 256 CUs.
+// problem: 256x256 / 128x256 / 256x128 for big GEMMs, 128x192 / 64x64 /
+// 128x32 and friends for narrow conv layers, split-K for grids that cannot
+// fill 256 CUs. This file holds the tile table, the plans, the autotuner and
+// the entry points.
 //
 //  * k-major LDS images (As[k][m], Bs[k][n]): every MFMA operand read is 32
 //    consecutive floats per half-wave (conflict-free ds_read_b32);
