@@ -140,6 +140,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "tensorframes_amd native runtime (GraphDef executor + HIP/CDNA4 kernels)";
 
   py::register_exception<GraphError>(m, "GraphError", PyExc_ValueError);
+  py::register_exception<comm::CollectiveError>(m, "CollectiveError", PyExc_RuntimeError);
 
   py::class_<Graph, std::shared_ptr<Graph>>(m, "Graph")
       .def(py::init([](py::bytes b) { return Graph::from_bytes(std::string(b)); }))
@@ -741,8 +742,38 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::gil_scoped_release nogil;
           return std::make_shared<comm::RcclComm>(u, rank, size, device);
         }), py::arg("unique_id"), py::arg("rank"), py::arg("size"), py::arg("device"))
-        .def("abort", &comm::RcclComm::abort)
-        .def("async_error", &comm::RcclComm::async_error);
+        .def("abort", &comm::RcclComm::abort, GR())
+        .def("async_error", &comm::RcclComm::async_error)
+        .def("set_timeout", &comm::RcclComm::set_timeout, py::arg("seconds"), py::arg("exit_on_timeout") = true,
+             "seconds a collective may take (<= 0: unbounded); past it wait() raises CollectiveError, and past it "
+             "plus a grace period the watchdog thread aborts the communicator and exits the process "
+             "(exit_on_timeout) or marks it failed")
+        .def_property_readonly("timeout", &comm::RcclComm::timeout)
+        .def("wait", &comm::RcclComm::wait, GR(), "bounded wait for every collective issued so far")
+        .def("check", &comm::RcclComm::check, "raises CollectiveError if the communicator failed")
+        .def_property_readonly("failed", &comm::RcclComm::failed)
+        .def_property_readonly("inflight", &comm::RcclComm::inflight);
+    py::class_<comm::ShmComm, Comm, std::shared_ptr<comm::ShmComm>>(m, "ShmComm",
+        "host tensors of the ranks of one node through a POSIX shared-memory segment")
+        .def(py::init<const std::string&, int, int, int64_t, bool>(), py::arg("name"), py::arg("rank"),
+             py::arg("size"), py::arg("slot_bytes"), py::arg("create"), GR())
+        .def("unlink", &comm::ShmComm::unlink)
+        .def("set_timeout", &comm::ShmComm::set_timeout, py::arg("seconds"))
+        .def_property_readonly("slot_bytes", &comm::ShmComm::slot_bytes)
+        .def_property_readonly("attached", &comm::ShmComm::attached);
+    m.attr("EXIT_COLLECTIVE_TIMEOUT") = comm::kExitCollectiveTimeout;
+    m.def("device_stall", [](double seconds) {
+      k::device_stall(static_cast<uint64_t>(std::max(0.0, seconds) * 1e6),
+                      c10::hip::getCurrentHIPStream().stream());
+    }, py::arg("seconds"), "fault injection: a bounded (<= 60 s) spin kernel on the current stream");
+    m.def("can_access_peer", [](int a, int b) {
+      int ok = 0;
+      if (hipDeviceCanAccessPeer(&ok, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+      }
+      return ok != 0;
+    }, py::arg("device"), py::arg("peer"));
     m.def("rccl_unique_id", [] { return py::bytes(comm::rccl_unique_id()); });
     py::class_<comm::OneShotComm, std::shared_ptr<comm::OneShotComm>>(m, "OneShotComm",
         "single-hop all-reduce of payloads <= 64 KB through IPC-mapped peer buffers")
@@ -756,7 +787,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           o.all_reduce(t, comm::parse_op(op));
           return t;
         }, py::arg("tensor"), py::arg("op") = "Sum", GR())
-        .def("check", &comm::OneShotComm::check, GR());
+        .def("check", &comm::OneShotComm::check, GR())
+        .def("set_timeout", &comm::OneShotComm::set_timeout, py::arg("seconds"))
+        .def_property_readonly("alloc_kind", &comm::OneShotComm::alloc_kind)
+        .def_property_readonly("failed", &comm::OneShotComm::failed);
   }
   m.def("cat_rows", [](const std::vector<at::Tensor>& ts) {
     TFA_CHECK(!ts.empty(), "cat_rows: no tensors");

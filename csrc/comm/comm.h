@@ -14,9 +14,24 @@
 //   * OneShotComm — the small-message path: a single-hop all-reduce through
 //                  IPC-mapped peer buffers (kernels/oneshot.hip), exchanged
 //                  once; works for ranks that share a GPU too;
+//   * ShmComm    — host tensors of the ranks of ONE node through a POSIX
+//                  shared-memory segment (process-shared barrier + per-rank
+//                  slots): the data path of CPU-only multi-process jobs and
+//                  of the host-side control collectives of GPU jobs, in
+//                  place of gloo's TCP loopback;
 //   * FakeComm   — N in-process ranks (threads) over host memory: the CPU
 //                  test double that runs the same collective contract at
 //                  N = 2/4/8 without a GPU.
+//
+// Failure detection (the reference relied on Spark task failure
+// around RDD.reduce and the shuffle, DebugRowOps.scala:500, :524-525, :576):
+// every RcclComm collective records an event; wait() is a bounded wait on
+// them that raises CollectiveError past the timeout, and a watchdog thread
+// ends a process whose collective is still incomplete past the timeout plus a
+// grace period (the main thread is stuck somewhere it cannot raise: it calls
+// ncclCommAbort, prints the reason and exits with kExitCollectiveTimeout, so
+// the launcher tears the job down). OneShotComm's flag waits and ShmComm's
+// barriers are bounded by the same timeout.
 //
 // Collective contract (all kinds): every rank calls the same collectives in
 // the same order with tensors of the same dtype / shape (all_to_all_v: row
@@ -27,10 +42,15 @@
 #include <torch/extension.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../kernels/kernels.h"
@@ -39,6 +59,13 @@ namespace tfa {
 namespace comm {
 
 k::RedOp parse_op(const std::string& op);
+
+// a collective that timed out, or a communicator that failed asynchronously
+struct CollectiveError : std::runtime_error {
+  explicit CollectiveError(const std::string& m) : std::runtime_error(m) {}
+};
+
+constexpr int kExitCollectiveTimeout = 76;  // exit status of a rank ended by the watchdog
 
 class Comm {
  public:
@@ -120,15 +147,46 @@ class RcclComm : public Comm {
   void barrier() override;
   void abort();  // ncclCommAbort: unblocks a hung collective (timeout guard)
   std::string async_error();  // "" while healthy
+  // seconds a collective may take (<= 0: unbounded) and whether the watchdog
+  // ends the process when the main thread does not notice a stuck one
+  void set_timeout(double seconds, bool exit_on_timeout);
+  double timeout() const { return timeout_s_; }
+  // bounded wait for every collective issued so far; raises CollectiveError
+  // past the timeout (the comm is then failed: later calls raise too)
+  void wait();
+  // raises CollectiveError if the comm failed (timeout, async RCCL error)
+  void check();
+  bool failed() const { return failed_.load(); }
+  int64_t inflight() const;
 
  private:
+  void track(hipStream_t s);   // event after a collective, for wait() and the watchdog
+  void fail(const std::string& why);
+  void watchdog();
   void* comm_ = nullptr;  // ncclComm_t
   int rank_, size_, device_;
+  double timeout_s_ = 0;
+  bool exit_on_timeout_ = true;
+  struct Inflight {
+    hipEvent_t ev;
+    std::chrono::steady_clock::time_point t0;
+  };
+  mutable std::mutex wmu_;
+  std::condition_variable wcv_;
+  std::deque<Inflight> inflight_;
+  std::vector<hipEvent_t> free_events_;
+  std::atomic<bool> failed_{false}, stop_{false};
+  std::string fail_msg_;
+  std::thread wd_;
 };
 
 // ---------------------------------------------------------------- one-shot
 class OneShotComm {
  public:
+  // the buffer is allocated uncached (hipDeviceMallocUncached) so no GPU's L2
+  // holds lines a peer writes over xGMI; fine-grained, then plain hipMalloc
+  // are the fallbacks (alloc_kind() says which; the self-test in
+  // parallel/comm.py decides whether the path is used at all)
   OneShotComm(int rank, int size, int device);
   ~OneShotComm();
   std::string ipc_handle() const;                        // this rank's buffer, for the peers
@@ -137,18 +195,66 @@ class OneShotComm {
   static int64_t max_bytes() { return static_cast<int64_t>(k::kOneShotSlotBytes); }
   // in place, on the device's current stream
   void all_reduce(at::Tensor& t, k::RedOp op);
-  // throws if a flag wait timed out (reads the error word: synchronises)
+  // throws CollectiveError if a flag wait timed out (reads the error word:
+  // synchronises; the word is cleared, the comm stays failed)
   void check();
   int64_t calls() const { return calls_; }
+  void set_timeout(double seconds) { timeout_us_ = seconds > 0 ? static_cast<uint64_t>(seconds * 1e6) : 3600000000ull; }
+  const std::string& alloc_kind() const { return alloc_kind_; }
+  bool failed() const { return failed_; }
 
  private:
   int rank_, size_, device_;
+  uint64_t timeout_us_ = 600000000ull;
+  bool failed_ = false;
+  std::string alloc_kind_;
   void* own_ = nullptr;
   k::OneShotPeers peers_{};
   std::vector<void*> opened_;
   uint32_t epoch_ = 0;
   bool ready_ = false;
   int64_t calls_ = 0;
+};
+
+// ---------------------------------------------------------------- ShmComm
+// Layout of the segment: [control block][result slot][slot of rank 0]...[slot
+// of rank W-1]; control = a process-shared sense-reversing barrier and, per
+// rank, kMaxRanks int64 of metadata (all_to_all_v row counts). Every collective moves
+// its payload through the slots in rounds of at most `slot_bytes`.
+class ShmComm : public Comm {
+ public:
+  static constexpr int kMaxRanks = 64;
+  // rank 0 creates the segment (create = true), the others attach after it;
+  // unlink() once every rank is attached (the mapping stays valid)
+  ShmComm(const std::string& name, int rank, int size, int64_t slot_bytes, bool create);
+  ~ShmComm() override;
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  std::string kind() const override { return "shm"; }
+  void all_reduce(at::Tensor& t, k::RedOp op) override;
+  at::Tensor all_gather(const at::Tensor& t) override;
+  at::Tensor all_to_all_v(const at::Tensor& x, const std::vector<int64_t>& send_rows,
+                          const std::vector<int64_t>& recv_rows) override;
+  void broadcast(at::Tensor& t, int root) override;
+  void barrier() override;
+  void unlink();
+  void set_timeout(double seconds) { timeout_s_ = seconds; }
+  int64_t slot_bytes() const { return slot_; }
+  int attached() const;  // ranks that have mapped the segment so far
+
+ private:
+  struct Ctrl;
+  char* slot(int r) const;
+  char* result() const;
+  int64_t* meta(int r) const;
+  [[noreturn]] void fail_all(const std::string& why);
+  std::string name_;
+  int rank_, size_;
+  int64_t slot_;
+  size_t bytes_ = 0;
+  char* base_ = nullptr;
+  double timeout_s_ = 600;
+  bool linked_ = false;
 };
 
 }  // namespace comm

@@ -75,8 +75,13 @@ constexpr size_t kOneShotBufBytes = kOneShotErrOffset + 256;
 struct OneShotPeers {
   void* buf[kOneShotMaxRanks];  // every rank's buffer, mapped into this process ([rank] = own)
 };
+// timeout_us bounds every flag wait (a missing peer sets the error word)
 void oneshot_all_reduce(RedOp op, DType dt, const void* in, void* out, int64_t n, int rank, int world,
-                        const OneShotPeers& p, uint32_t epoch, hipStream_t s);
+                        const OneShotPeers& p, uint32_t epoch, uint64_t timeout_us, hipStream_t s);
+// fault injection: one wave that spins for `us` microseconds (at most 60 s) on
+// the device's realtime counter, then exits; work queued behind it on `s`
+// waits (a stalled peer / slow rank, for the collective timeout tests)
+void device_stall(uint64_t us, hipStream_t s);
 
 size_t unsorted_segment_workspace_bytes(RedOp op, DType dt, int64_t n, int64_t inner, int64_t nseg);
 void unsorted_segment_reduce(RedOp op, DType dt, DType idt, const void* x, const void* ids,

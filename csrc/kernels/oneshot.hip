@@ -13,7 +13,8 @@
 // them in rank order. Every rank folds the same values in the same order, so
 // all ranks hold bitwise the same result (deterministic, also for floats).
 //
-// Buffer of each rank (hipMalloc'ed by comm/comm.cpp OneShotComm, exported with
+// Buffer of each rank (allocated UNCACHED by comm/comm.cpp OneShotComm, so no
+// GPU's L2 keeps a copy of a line another GPU writes over xGMI; exported with
 // hipIpcGetMemHandle, opened by every peer):
 //   [slot 0 data: 64 KB][slot 1 data: 64 KB][flags: 2 slots x 8 ranks u32]
 // Call e uses slot e & 1 and writes epoch e into the flags. Reusing a slot two
@@ -22,8 +23,9 @@
 // in order) had finished reading. Every access to the shared buffers is a
 // system-scope atomic (sc0 sc1: coherent across XCD L2s and across GPUs, so it
 // does not depend on how an importing process maps the pages), and the flag
-// wait is bounded (10 s of s_memrealtime) so a missing peer ends in an error
-// word, never in a wave that spins forever.
+// wait is bounded (Config.collective_timeout_s of s_memrealtime, passed per
+// launch) so a missing peer ends in an error word, never in a wave that spins
+// forever.
 #include "hip_common.h"
 
 namespace tfa {
@@ -40,7 +42,7 @@ __device__ __forceinline__ T fold(T a, T b) {
 }
 
 constexpr int kThreads = 1024;
-constexpr uint64_t kSpinTicks = 10ull * 100000000ull;  // 10 s of the 100 MHz realtime counter
+constexpr uint64_t kTicksPerUs = 100;  // the realtime counter runs at 100 MHz
 
 // 8-byte granules: the shared buffers are touched with 64-bit system-scope
 // atomics (half the transactions of 4-byte ones for f32 / i32 payloads)
@@ -53,7 +55,7 @@ union Granule {
 template <typename T, int OP>
 __global__ __launch_bounds__(kThreads) void oneshot_kernel(const T* in, T* out, int64_t n,
                                                           int rank, int world, OneShotPeers p, uint32_t epoch,
-                                                          int slot) {
+                                                          int slot, uint64_t spin_ticks) {
   constexpr int E = 8 / sizeof(T);  // elements per granule
   const int tid = threadIdx.x;
   const int64_t ng = (n + E - 1) / E;
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(const T* in, T* out, 
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > spin_ticks) {
         int* err = reinterpret_cast<int*>(static_cast<char*>(p.buf[rank]) + kOneShotErrOffset);
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -113,14 +115,21 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(const T* in, T* out, 
   }
 }
 
+// fault injection (device_stall): spin, bounded, then exit
+__global__ __launch_bounds__(64) void stall_kernel(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 template <typename T>
 void launch_t(RedOp op, const void* in, void* out, int64_t n, int rank, int world, const OneShotPeers& p,
-              uint32_t epoch, hipStream_t s) {
+              uint32_t epoch, uint64_t ticks, hipStream_t s) {
   const int slot = static_cast<int>(epoch & 1u);
   const T* x = static_cast<const T*>(in);
   T* y = static_cast<T*>(out);
-#define TFA_OS(OP_) \
-  hipLaunchKernelGGL((oneshot_kernel<T, (int)OP_>), dim3(1), dim3(kThreads), 0, s, x, y, n, rank, world, p, epoch, slot)
+#define TFA_OS(OP_)                                                                                        \
+  hipLaunchKernelGGL((oneshot_kernel<T, (int)OP_>), dim3(1), dim3(kThreads), 0, s, x, y, n, rank, world, p, \
+                     epoch, slot, ticks)
   switch (op) {
     case RedOp::SUM: TFA_OS(RedOp::SUM); break;
     case RedOp::PROD: TFA_OS(RedOp::PROD); break;
@@ -134,19 +143,27 @@ void launch_t(RedOp op, const void* in, void* out, int64_t n, int rank, int worl
 }  // namespace
 
 void oneshot_all_reduce(RedOp op, DType dt, const void* in, void* out, int64_t n, int rank, int world,
-                        const OneShotPeers& p, uint32_t epoch, hipStream_t s) {
+                        const OneShotPeers& p, uint32_t epoch, uint64_t timeout_us, hipStream_t s) {
   TFA_CHECK(world >= 1 && world <= kOneShotMaxRanks && rank >= 0 && rank < world, "oneshot: bad rank/world");
   TFA_CHECK(n >= 0 && n * dtype_size(dt) <= static_cast<int64_t>(kOneShotSlotBytes), "oneshot: payload over ",
             kOneShotSlotBytes, " bytes");
   for (int r = 0; r < world; ++r) TFA_CHECK(p.buf[r] != nullptr, "oneshot: peer ", r, " not mapped");
+  // every wait is bounded: at least 1 ms, at most one hour
+  const uint64_t ticks = std::min<uint64_t>(std::max<uint64_t>(timeout_us, 1000), 3600ull * 1000000ull) * kTicksPerUs;
   switch (dt) {
-    case DType::F32: launch_t<float>(op, in, out, n, rank, world, p, epoch, s); break;
-    case DType::F64: launch_t<double>(op, in, out, n, rank, world, p, epoch, s); break;
-    case DType::I32: launch_t<int32_t>(op, in, out, n, rank, world, p, epoch, s); break;
-    case DType::I64: launch_t<int64_t>(op, in, out, n, rank, world, p, epoch, s); break;
+    case DType::F32: launch_t<float>(op, in, out, n, rank, world, p, epoch, ticks, s); break;
+    case DType::F64: launch_t<double>(op, in, out, n, rank, world, p, epoch, ticks, s); break;
+    case DType::I32: launch_t<int32_t>(op, in, out, n, rank, world, p, epoch, ticks, s); break;
+    case DType::I64: launch_t<int64_t>(op, in, out, n, rank, world, p, epoch, ticks, s); break;
     default: TFA_CHECK(false, "oneshot all-reduce: dtype ", dtype_name(dt), " not supported");
   }
   TFA_LAUNCH_CHECK("oneshot_all_reduce");
+}
+
+void device_stall(uint64_t us, hipStream_t s) {
+  const uint64_t ticks = std::min<uint64_t>(us, 60ull * 1000000ull) * kTicksPerUs;
+  hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, ticks);
+  TFA_LAUNCH_CHECK("device_stall");
 }
 
 }  // namespace k

@@ -241,7 +241,12 @@ at::Tensor dev_empty(at::IntArrayRef sizes, at::ScalarType dt, const at::Device&
       if (e != hipSuccess || !p) {
         (void)hipGetLastError();
         g_fallbacks++;
-        return at::empty(sizes, opts);  // out of device memory here: the framework allocator's turn
+        // out of device memory here: the framework allocator's turn. Drop our
+        // lock first: if it is out of memory too, c10 runs the OOM observer
+        // (dev_pool_install_oom_hook), which takes S.mu on this same thread,
+        // and then raises OutOfMemoryError instead of deadlocking.
+        lk.unlock();
+        return at::empty(sizes, opts);
       }
       g_device_mallocs++;
       b = new Block{p, dev.index(), stream, want, {}};

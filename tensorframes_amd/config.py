@@ -56,8 +56,20 @@ class Config:
     map_rows_batch_rows: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_BATCH", 64, int))
     # re-runs of a partition task after a runtime (non-validation) failure; 0 = fail fast
     task_retries: int = dataclasses.field(default_factory=lambda: _env("TFA_TASK_RETRIES", 0, int))
-    # timeout of one collective (RCCL/gloo); a stuck collective aborts the job
+    # timeout of one collective (RCCL, one-shot, shared memory, gloo): past it
+    # the waiting rank raises CollectiveError (parallel/comm.py)
     collective_timeout_s: float = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_TIMEOUT_S", 600.0, float))
+    # an RCCL collective still incomplete past the timeout plus a grace period,
+    # with no thread waiting on it, ends the process (status 76) after
+    # ncclCommAbort, so the launcher tears the job down; False: the
+    # communicator is only marked failed (the next collective raises)
+    collective_timeout_exit: bool = dataclasses.field(default_factory=lambda: _env("TFA_COLLECTIVE_TIMEOUT_EXIT", True, bool))
+    # host-tensor collectives of the ranks of one node through a shared-memory
+    # segment (csrc/comm ShmComm) instead of gloo: the data path of CPU-only
+    # jobs, the row-count / flag exchanges of GPU jobs
+    shm_collectives: bool = dataclasses.field(default_factory=lambda: _env("TFA_SHM_COLLECTIVES", True, bool))
+    # bytes per rank of the shared segment (payloads move in rounds of this size)
+    shm_slot_bytes: int = dataclasses.field(default_factory=lambda: _env("TFA_SHM_SLOT_BYTES", 8 << 20, int))
     # CPU executor: programs with fewer input elements run on one intra-op thread
     cpu_parallel_min_elems: int = dataclasses.field(default_factory=lambda: _env("TFA_CPU_PARALLEL_MIN_ELEMS", 4_000_000, int))
     # float32 MatMul / Conv2D compute mode on the GPU: "f32" (exact, default),

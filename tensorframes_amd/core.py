@@ -1217,6 +1217,7 @@ def _agree_shapes(local: Dict[str, Optional[torch.Tensor]], static: Dict[str, Op
     desc = desc.to(dev)
     dist.all_reduce_(desc, "Max")
     desc = desc.cpu()
+    _comm_check(dev)  # a one-shot result read on the host: its flag waits must have succeeded
     for i, n in enumerate(todo):
         _check(int(desc[i, 0]) == 1, "Cannot reduce an empty DataFrame")
         shp = tuple(int(d) for d in desc[i, 2:2 + int(desc[i, 1])])
@@ -1276,13 +1277,18 @@ def _combine_monoids(partials: Dict[str, List[torch.Tensor]], ops: Dict[str, str
     host = [f.to("cpu", non_blocking=True) if f.is_cuda else f for _, f in flags]
     if dev.type == "cuda":
         torch.cuda.current_stream(dev).synchronize()
-        from .parallel import comm as _comm
-        ec = _comm.get()
-        if ec is not None:
-            ec.check()  # a one-shot flag wait that timed out raises here
+        _comm_check(dev)  # a one-shot flag wait that timed out raises here
     for (op, _), h in zip(flags, host):
         _check(bool(_FLAG_ANY[op](h[0].item())), "Cannot reduce an empty DataFrame")
     return out
+
+
+def _comm_check(dev: torch.device) -> None:
+    """After a device collective's result was synchronised: raise
+    CollectiveError if the engine communicator saw a timeout or a failure."""
+    if dev.type == "cuda" and dist.is_distributed():
+        from .parallel import comm as _comm
+        _comm.check_built()
 
 
 def _gather_rank_values(local: Dict[str, Optional[torch.Tensor]], static: Dict[str, Optional[tuple]],
@@ -1297,6 +1303,7 @@ def _gather_rank_values(local: Dict[str, Optional[torch.Tensor]], static: Dict[s
     shapes = _agree_shapes(local, static, dev)
     has = any(v is not None for v in local.values())
     flags = dist.all_gather_tensor(torch.tensor([int(has)], dtype=torch.int64, device=dev)).reshape(-1).cpu()
+    _comm_check(dev)
     _check(int(flags.sum()) > 0, "Cannot reduce an empty DataFrame")
     out = {}
     for n in names:
@@ -1408,13 +1415,16 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
     def task(blocks):
         res = {}
         dense_of = {}
-        if len(blocks) > 1:
+        if len(blocks) > 1 and uniform is not None:
             # this rank's device-resident partitions are one block for the
             # graph: a concatenation per column replaces a run per partition
-            # plus a run over the stacked partials. Valid for ANY reducer graph
-            # under the reduce_blocks contract (the graph takes any lead dim
-            # and is associative over stacked partials: reference
-            # DebugRowOps.scala:503-526, :741-750)
+            # plus a run over the stacked partials. Only for graphs whose every
+            # fetch is a recognised monoid (Sum/Min/Max/Prod over axis 0), for
+            # which the result cannot depend on how rows are grouped; any
+            # other reducer (e.g. a mean) keeps the reference's per-partition
+            # reduce followed by the fold of the partials (DebugRowOps.scala:
+            # 512-525, :741-750), so its result does not depend on which
+            # partitions share a rank
             dense = [(pid, _dense_inputs(b, cols, "reduce_blocks")) for pid, b in sorted(blocks.items())
                      if b.nrows > 0]
             dense_of = dict(dense)
@@ -1755,11 +1765,22 @@ def _shuffle_blocks(send: List[List[Block]], names: List[str], tf_types: Dict[st
         off = 0
         for n, wb in zip(dense, widths):
             dtype, cell = kinds[n]
-            cols[n] = rec[:, off:off + wb].contiguous().view(dtype).reshape((rec.shape[0],) + tuple(cell))
+            # each field copied out into a buffer of its own (offset 0): a
+            # slice of a 0- or 1-row record block counts as contiguous, so
+            # .contiguous() would keep the field's byte offset and a wider
+            # dtype view of it would fail
+            fld = engine.device_empty((rec.shape[0], wb), torch.uint8, rec.device)
+            fld.copy_(rec[:, off:off + wb])
+            cols[n] = fld.view(dtype).reshape((rec.shape[0],) + tuple(cell))
             off += wb
     for j, n in enumerate(names):
         if kinds[n] is not None:
             continue
+        if frame_comm.is_bytes_field(schema[n]):
+            # strings / binary: lengths + bytes as tensors, no pickling
+            binary = isinstance(schema[n].dataType, BinaryType)
+            cols[n] = frame_comm.shuffle_strings([p.columns[n] if p is not None and p.nrows else None for p in per],
+                                                 recv_rows, binary)
         else:
             got = dist.all_to_all_objects([column_values(p.columns[n]) if p is not None and p.nrows else []
                                            for p in per])

@@ -4,9 +4,12 @@ The reference distributes work with Spark (mapPartitions tasks, Broadcast,
 RDD.reduce to the driver, a groupBy shuffle; reference:
 src/main/scala/org/tensorframes/impl/DebugRowOps.scala:376-391,500,524,576).
 Here every rank runs the same program (SPMD), owns partitions
-``p % world_size == rank`` and exchanges data with torch.distributed
-collectives: backend "nccl" (= RCCL over xGMI on MI355X) for device tensors,
-"gloo" for host objects and for CPU-only runs.
+``p % world_size == rank`` and exchanges data through the engine's own
+communicators (parallel/comm.py): device tensors over RCCL / the one-shot
+xGMI all-reduce, host tensors over a shared-memory segment when the ranks
+share a node. torch.distributed is the bootstrap (rendezvous; gloo carries
+the handful of host objects exchanged once) and the fallback
+(`Config.collective_backend = "torch"`, ranks on several nodes).
 """
 from __future__ import annotations
 
@@ -107,6 +110,9 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, force
     dist.init_process_group(**kwargs)
     _state["initialized_here"] = True
     _ensure_groups()
+    if is_distributed():
+        from . import comm
+        comm.init_host()  # collectively: every rank calls init
     return is_distributed()
 
 
@@ -195,7 +201,40 @@ def local_partitions(num_partitions: int) -> List[int]:
 
 def barrier():
     if is_distributed():
+        shm = _host_comm()
+        if shm is not None:
+            with _traced("shm_barrier"):
+                shm.barrier()
+            return
         dist.barrier(group=_state["cpu_group"])
+
+
+# -- bootstrap: torch.distributed's gloo group, never the engine communicators
+#    (used while those are being built, and for the few objects exchanged once)
+def all_reduce_bootstrap_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
+    if is_distributed():
+        _ensure_groups()
+        dist.all_reduce(t, op=_OPS[op], group=_state["cpu_group"])
+    return t
+
+
+def broadcast_bootstrap_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if is_distributed():
+        _ensure_groups()
+        dist.broadcast(t, src=src, group=_state["cpu_group"])
+    return t
+
+
+def barrier_bootstrap():
+    if is_distributed():
+        _ensure_groups()
+        dist.barrier(group=_state["cpu_group"])
+
+
+def _host_comm():
+    """The shared-memory host communicator (built by init), or None."""
+    from . import comm
+    return comm.host()
 
 
 _pending_events: List[tuple] = []  # (name, start, end) device events not yet read
@@ -302,9 +341,14 @@ def all_to_all_objects(per_dest: List[Any]) -> List[Any]:
     sizes = all_to_all_counts([len(b) for b in payload])
     send = torch.frombuffer(bytearray(b"".join(payload)), dtype=torch.uint8) if any(payload) else \
         torch.empty(0, dtype=torch.uint8)
-    recv = torch.empty(sum(sizes), dtype=torch.uint8)
-    with _traced("all_to_all_objects", _nbytes(send)):
-        dist.all_to_all_single(recv, send, sizes, [len(b) for b in payload], group=_state["cpu_group"])
+    shm = _host_comm()
+    if shm is not None:
+        with _traced("all_to_all_objects", _nbytes(send)):
+            recv = shm.all_to_all_v(send, [len(b) for b in payload], sizes)
+    else:
+        recv = torch.empty(sum(sizes), dtype=torch.uint8)
+        with _traced("all_to_all_objects", _nbytes(send)):
+            dist.all_to_all_single(recv, send, sizes, [len(b) for b in payload], group=_state["cpu_group"])
     out, off, raw = [], 0, recv.numpy().tobytes()
     for n in sizes:
         out.append(pickle.loads(raw[off:off + n]))  # payloads written by our own ranks
@@ -336,6 +380,25 @@ def gather_rows(x: torch.Tensor, rows_per_rank: List[int], root: Optional[int] =
     _ensure_groups()
     x = x.contiguous()
     rows = [int(r) for r in rows_per_rank]
+    shm = _host_comm()
+    if shm is not None:
+        # every block at its exact size through the shared segment: to root
+        # only (an all_to_all where only root receives), or to every rank
+        w, me = world_size(), rank()
+        with _traced("shm_gather_rows", _nbytes(x)):
+            if root is None:
+                got = shm.all_to_all_v(x.repeat((w,) + (1,) * (x.dim() - 1)) if w > 1 else x,
+                                       [rows[me]] * w, rows)
+            else:
+                send = [rows[me] if r == root else 0 for r in range(w)]
+                got = shm.all_to_all_v(x, send, rows if me == root else [0] * w)
+        if root is not None and me != root:
+            return None
+        out, off = [], 0
+        for r in rows:
+            out.append(got[off:off + r])
+            off += r
+        return out
     mx = max(rows) if rows else 0
     if mx * len(rows) * 4 > sum(rows) * 5:
         return _gather_rows_exact(x, rows, root)
@@ -391,16 +454,27 @@ def broadcast_tensor(t: Optional[torch.Tensor], shape: tuple, dtype: torch.dtype
         return t
     _ensure_groups()
     buf = t.contiguous() if rank() == src else torch.empty(shape, dtype=dtype)
+    shm = _host_comm()
+    if shm is not None:
+        with _traced("shm_broadcast", _nbytes(buf)):
+            shm.broadcast(buf, src)
+        return buf
     with _traced("broadcast", _nbytes(buf)):
         dist.broadcast(buf, src=src, group=_state["cpu_group"])
     return buf
 
 
 def all_reduce_host_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
-    """In-place all-reduce of a small host tensor over the gloo group."""
+    """In-place all-reduce of a host tensor: the shared-memory communicator
+    when the ranks share a node, else the gloo group."""
     if not is_distributed():
         return t
     _ensure_groups()
+    shm = _host_comm()
+    if shm is not None and t.is_contiguous():
+        with _traced("shm_all_reduce", _nbytes(t)):
+            shm.all_reduce(t, op)
+        return t
     dist.all_reduce(t, op=_OPS[op], group=_state["cpu_group"])
     return t
 
@@ -411,6 +485,11 @@ def all_to_all_counts(send_counts: List[int]) -> List[int]:
         return [int(send_counts[0])]
     _ensure_groups()
     t = torch.tensor([int(c) for c in send_counts], dtype=torch.int64)
+    shm = _host_comm()
+    if shm is not None:
+        with _traced("shm_all_gather", _nbytes(t)):
+            allc = shm.all_gather(t)  # [world, world]: row s = what rank s sends
+        return allc[:, rank()].tolist()
     out = torch.empty_like(t)
     dist.all_to_all_single(out, t, group=_state["cpu_group"])
     return out.tolist()
@@ -438,6 +517,9 @@ def all_to_all_tensors(chunks: List[torch.Tensor], recv_rows: List[int]) -> torc
             return ec.all_to_all_rows(x, [int(c.shape[0]) for c in chunks], recv_rows)
     if x.is_cuda and not gpu_collectives():
         return all_to_all_tensors([c.cpu() for c in chunks], recv_rows).to(x.device)
+    if not x.is_cuda and _host_comm() is not None:
+        with _traced("shm_all_to_all", _nbytes(x)):
+            return _host_comm().all_to_all_v(x, [int(c.shape[0]) for c in chunks], [int(r) for r in recv_rows])
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
     out = _empty((sum(recv_rows),) + tuple(x.shape[1:]), x.dtype, x.device)
     with _traced("all_to_all", _nbytes(x), x.device):
@@ -460,6 +542,9 @@ def all_to_all_rows(x: torch.Tensor, send_rows: List[int], recv_rows: List[int])
             return ec.all_to_all_rows(x, send_rows, recv_rows)
     if x.is_cuda and not gpu_collectives():
         return all_to_all_rows(x.cpu(), send_rows, recv_rows).to(x.device)
+    if not x.is_cuda and _host_comm() is not None:
+        with _traced("shm_all_to_all", _nbytes(x)):
+            return _host_comm().all_to_all_v(x, [int(r) for r in send_rows], [int(r) for r in recv_rows])
     group = _state["device_group"] if x.is_cuda else _state["cpu_group"]
     out = _empty((sum(recv_rows),) + tuple(x.shape[1:]), x.dtype, x.device)
     with _traced("all_to_all", _nbytes(x), x.device):
@@ -490,6 +575,10 @@ def all_reduce_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
             return ec.all_reduce_(t.contiguous() if not t.is_contiguous() else t, op)
     if t.is_cuda and not gpu_collectives():  # gloo rehearsal: stage through the host
         return t.copy_(all_reduce_(t.cpu(), op))
+    if not t.is_cuda and _host_comm() is not None and t.is_contiguous():
+        with _traced("shm_all_reduce", _nbytes(t)):
+            _host_comm().all_reduce(t, op)
+        return t
     group = _state["device_group"] if t.is_cuda else _state["cpu_group"]
     with _traced("all_reduce", _nbytes(t), t.device):
         dist.all_reduce(t, op=_OPS[op], group=group)
@@ -508,6 +597,9 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
             return ec.all_gather(t)
     if t.is_cuda and not gpu_collectives():
         return all_gather_tensor(t.cpu()).to(t.device)
+    if not t.is_cuda and _host_comm() is not None:
+        with _traced("shm_all_gather", _nbytes(t)):
+            return _host_comm().all_gather(t)
     if t.is_cuda:
         out = _empty((world_size(),) + tuple(t.shape), t.dtype, t.device)
         with _traced("all_gather", _nbytes(t), t.device):

@@ -99,6 +99,11 @@ def column_kinds(blocks: Sequence, names: Sequence[str], schema) -> Dict[str, Ki
     return out
 
 
+def _empty_strings(binary: bool):
+    from ..frame.block import StringColumn
+    return StringColumn.from_values([], binary)
+
+
 def partition_rows(local: Dict[int, int], nparts: int) -> List[int]:
     """Rows of every partition (agreed by one int64 all-reduce)."""
     counts = torch.zeros(max(nparts, 1), dtype=torch.int64)
@@ -118,6 +123,37 @@ def _host_cat(cols: List[Any], kind: Kind) -> torch.Tensor:
 def _is_string_field(field) -> bool:
     from ..frame.types import StringType
     return isinstance(field.dataType, StringType)
+
+
+def is_bytes_field(field) -> bool:
+    """String or binary schema field: shuffled as tensors (shuffle_strings)."""
+    from ..frame.types import BinaryType, StringType
+    return isinstance(field.dataType, (StringType, BinaryType))
+
+
+def shuffle_strings(per_dest: List[Any], recv_rows: List[int], binary: bool):
+    """String / binary column rows per destination rank -> the rows this rank
+    receives (source-rank order), as one StringColumn. Moves an int64 length
+    tensor and a uint8 byte tensor in two all_to_alls: no Python object per
+    row crosses a rank (reference counterpart: the groupBy / repartition
+    shuffle, DebugRowOps.scala:576)."""
+    from ..frame.block import StringColumn, concat_columns
+    from ..ops import groupby as G
+    cols = [G.as_string_column(c, binary).to(torch.device("cpu")) if c is not None and len(c)
+            else StringColumn.from_values([], binary) for c in per_dest]
+    cat = concat_columns(cols) if len(cols) > 1 else cols[0]
+    lens = cat.lengths().contiguous()
+    got_lens = dist.all_to_all_rows(lens, [len(c) for c in cols], [int(r) for r in recv_rows])
+    send_b = [int(c.data.numel()) for c in cols]
+    # what each source sends us, in bytes: the sums of its received lengths
+    recv_b, off = [], 0
+    for r in recv_rows:
+        recv_b.append(int(got_lens[off:off + int(r)].sum()) if int(r) else 0)
+        off += int(r)
+    got = dist.all_to_all_rows(cat.data.contiguous(), send_b, recv_b)
+    offs = torch.zeros(got_lens.shape[0] + 1, dtype=torch.int64)
+    torch.cumsum(got_lens, 0, out=offs[1:])
+    return StringColumn(offs, got, binary)
 
 
 def _gather_strings(local, owned, counts, rows_of_rank, root, w) -> Optional[Dict[int, List[str]]]:
@@ -333,6 +369,24 @@ def repartition_blocks(local: Dict[int, Any], names: Sequence[str], schema, npar
             for q in mine:
                 ps = [t for _, t in sorted(pieces[q], key=lambda x: x[0])]
                 cols_out[q][n] = engine.cat_rows(ps) if ps else torch.empty((0,) + kind[1], dtype=kind[0], device=dev)
+        elif is_bytes_field(schema[n]) and dist.is_distributed():
+            from ..frame.block import concat_columns
+            from ..frame.types import BinaryType
+            from ..ops import groupby as G
+            binary = isinstance(schema[n].dataType, BinaryType)
+            per_dest = []
+            for r in range(w):
+                ps = [G.as_string_column(local[p].columns[n], binary).slice(st, st + ln) for (_, p, st, ln) in send[r]]
+                per_dest.append(concat_columns(ps) if ps else None)
+            got = shuffle_strings(per_dest, recv_rows, binary)
+            pos, pieces = 0, {q: [] for q in mine}
+            for s_ in range(w):
+                for (q, p, st, ln) in recv[s_]:
+                    pieces[q].append((p, got.slice(pos, pos + ln)))
+                    pos += ln
+            for q in mine:
+                ps = [c for _, c in sorted(pieces[q], key=lambda x: x[0])]
+                cols_out[q][n] = concat_columns(ps) if ps else _empty_strings(binary)
         else:
             tfd = _schema_tf(schema[n])
             if tfd is None:

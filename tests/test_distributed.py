@@ -1,7 +1,14 @@
-"""Multi-process (SPMD) execution over torch.distributed / gloo on the CPU,
-world_size 2 and 3: partitions pinned to ranks, collect/count gathers,
-reduce_blocks / reduce_rows cross-rank combine (all-reduce for monoids,
-all-gather + one graph run otherwise), aggregate's key shuffle (all-to-all)."""
+"""Multi-process (SPMD) execution on the CPU at world size 2, 3, 4 and 8:
+partitions pinned to ranks, collect/count gathers, reduce_blocks /
+reduce_rows cross-rank combine (all-reduce for monoids, all-gather + one
+graph run otherwise), aggregate's key shuffle (all-to-all), repartition.
+
+The data path runs through the engine's own shared-memory communicator
+(csrc/comm ShmComm, parallel/comm.init_host): the collective counters must
+show its calls and no gloo tensor collective or pickled object exchange on
+the reduce / aggregate paths (gloo is only the bootstrap). World 2 also runs
+with the shared-memory path off (the gloo fallback). Reference cross-partition
+points: DebugRowOps.scala:500, :524-525, :576, :732-750."""
 import json
 import os
 import socket
@@ -22,11 +29,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir, device="cpu"):
+def _worker(rank, world, port, outdir, device="cpu", shm=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), OMP_NUM_THREADS="1",
+                      TFA_SHM_COLLECTIVES="1" if shm else "0")
     if device == "cpu":
         os.environ["TFA_DEVICE"] = "cpu"
+    torch.set_num_threads(1)
     sys.path.insert(0, REPO)
     import numpy as np
 
@@ -79,11 +88,24 @@ def _worker(rank, world, port, outdir, device="cpu"):
         one = tfs.create_dataframe([Row(c="a", x=float(i)) for i in range(20)], num_partitions=5)
         agg = tfs.aggregate(tf.reduce_min(xi, [0], name="x"), one.groupBy("c"))
         res["agg_one"] = [list(r) for r in agg.collect()]
+    # int32 keys + float64 values through the packed-record shuffle, with
+    # fewer groups than ranks (most ranks receive 0 or 1 rows), non-monoid
+    import numpy as _np
+    kk = _np.array([i % 2 for i in range(12)], dtype=_np.int32)
+    xx = _np.arange(12, dtype=_np.float64)
+    few = tfs.from_columns({"k": kk, "x": xx}, num_partitions=6)
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        agg = tfs.aggregate(tf.identity(tf.reduce_max(xi, [0]) * 2.0, name="x"), few.groupBy("k"))
+        res["agg_few"] = sorted([[int(r.k), float(r.x)] for r in agg.collect()])
     # reductions make no host-object (pickled gloo) exchange; ranks without
     # data contribute identities (1 partition: only rank 0 has rows), also
     # when the output shape is only known at run time (unanalysed [?,?] column)
     from tensorframes_amd.utils.logging import metrics as _m
-    ago0 = _m.snapshot().get("collective_all_gather_object", 0)
+    snap0 = _m.snapshot()
+    ago0 = snap0.get("collective_all_gather_object", 0)
+    gloo0 = {k: snap0.get(k, 0) for k in ("collective_all_reduce", "collective_all_gather", "collective_all_to_all",
+                                          "collective_all_to_all_objects")}
     one_part = tfs.create_dataframe([Row(x=float(i), v=[float(i), 1.0]) for i in range(7)], num_partitions=1)
     with tf.Graph().as_default():
         xi = tf.placeholder(tf.double, shape=[None], name="x_input")
@@ -94,7 +116,17 @@ def _worker(rank, world, port, outdir, device="cpu"):
     with tf.Graph().as_default():
         xi = tf.placeholder(tf.double, shape=[None], name="x_input")
         res["gen_one_part"] = tfs.reduce_blocks(tf.identity(tf.reduce_max(xi, [0]), name="x"), one_part.select("x"))
-    res["ago_delta"] = _m.snapshot().get("collective_all_gather_object", 0) - ago0
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        agg = tfs.aggregate(tf.reduce_sum(xi, [0], name="x"), df.select("key", "x").groupBy("key"))
+        res["agg2"] = sorted([list(r) for r in agg.collect()])
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, shape=[None], name="x_input")
+        agg = tfs.aggregate(tf.identity(tf.reduce_sum(xi * xi, [0]), name="x"), df.select("key", "x").groupBy("key"))
+        res["agg_gen_str"] = sorted([list(r) for r in agg.collect()])
+    snap1 = _m.snapshot()
+    res["ago_delta"] = snap1.get("collective_all_gather_object", 0) - ago0
+    res["gloo_delta"] = {k: snap1.get(k, 0) - v for k, v in gloo0.items()}
     res["repart"] = [r.x for r in df.repartition(4).select("x").collect()]
     # checkpoint: every rank writes its own partitions, reads them back
     ck = os.path.join(outdir, "ck")
@@ -120,10 +152,16 @@ def _worker(rank, world, port, outdir, device="cpu"):
     dist.shutdown()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_spmd_world(world, tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    _check_results(tmp_path, world, "cpu")
+    _check_results(tmp_path, world, "cpu", shm=True)
+
+
+def test_spmd_world_gloo_fallback(tmp_path):
+    """The same program with the shared-memory path off: host collectives over gloo."""
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), "cpu", False), nprocs=2, join=True)
+    _check_results(tmp_path, 2, "cpu", shm=False)
 
 
 @pytest.mark.gpu
@@ -136,13 +174,22 @@ def test_spmd_two_ranks_share_one_gpu(tmp_path):
     _check_results(tmp_path, 2, "cuda")
 
 
-def _check_results(tmp_path, world, device):
+def _check_results(tmp_path, world, device, shm=False):
     outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
     assert all(o["device"] == device for o in outs)
     for o in outs:  # collectives are counted (metrics) on every rank
-        reduces = sum(o["coll"].get(k, 0) for k in ("collective_all_reduce", "collective_oneshot_all_reduce"))
-        assert o["coll"].get("collective_all_to_all", 0) >= 1 and reduces >= 1
-        assert o["coll"]["collective_bytes"] > 0
+        c = o["coll"]
+        reduces = sum(c.get(k, 0) for k in ("collective_all_reduce", "collective_oneshot_all_reduce",
+                                             "collective_rccl_all_reduce", "collective_shm_all_reduce"))
+        a2a = sum(c.get(k, 0) for k in ("collective_all_to_all", "collective_rccl_all_to_all",
+                                         "collective_shm_all_to_all"))
+        assert a2a >= 1 and reduces >= 1
+        assert c["collective_bytes"] > 0
+        if shm:
+            # the engine's communicator carried the data: no gloo tensor
+            # collective and no pickled exchange on the reduce/aggregate paths
+            assert c.get("collective_shm_all_reduce", 0) >= 1 and c.get("collective_shm_all_to_all", 0) >= 1
+            assert all(v == 0 for v in o["gloo_delta"].values()), o["gloo_delta"]
     xs = [float(i) for i in range(20)]
     parts = sorted(p for o in outs for p in o["local_parts"])
     assert parts == [0, 1, 2, 3, 4]
@@ -158,6 +205,9 @@ def _check_results(tmp_path, world, device):
                                 for k in range(4)]
         assert o["agg_gen"] == [[k, sum(x * x for x in xs if int(x) % 4 == k)] for k in range(4)]
         assert o["agg_one"] == [["a", 0.0]]
+        assert o["agg2"] == want
+        assert o["agg_gen_str"] == sorted([[k, sum(x * x for x in xs if str(int(x) % 3) == k)] for k in ("0", "1", "2")])
+        assert o["agg_few"] == [[0, 20.0], [1, 22.0]]
         assert o["sum_one_part"] == 21.0 and o["vmin_one_part"] == [0.0, 1.0] and o["gen_one_part"] == 6.0
         assert o["ago_delta"] == 0
         assert o["repart"] == xs

@@ -153,9 +153,10 @@ def test_repartition_device_agreed_by_every_rank(tmp_path):
         assert res == {"x": "cpu", "y": "meta"}
 
 
-def _gather_worker(rank, world, port, outdir):
+def _gather_worker(rank, world, port, outdir, shm=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TFA_DEVICE="cpu", OMP_NUM_THREADS="1")
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TFA_DEVICE="cpu", OMP_NUM_THREADS="1",
+                      TFA_SHM_COLLECTIVES="1" if shm else "0")
     sys.path.insert(0, REPO)
     import torch
 
@@ -166,30 +167,36 @@ def _gather_worker(rank, world, port, outdir):
     res = {}
     for name, rows in (("skewed", [0, 7, 300]), ("balanced", [10, 11, 12])):
         x = torch.arange(rows[rank] * 2, dtype=torch.float64).reshape(rows[rank], 2) + 1000 * rank
-        before = metrics.snapshot().get("collective_gather_rows_exact", 0)
+        before = metrics.snapshot()
         everyone = dist.gather_rows(x, rows)
         at_root = dist.gather_rows(x, rows, root=2)
+        after = metrics.snapshot()
         res[name] = {
             "all": [p.tolist() for p in everyone],
             "root": None if at_root is None else [p.tolist() for p in at_root],
-            "exact": metrics.snapshot().get("collective_gather_rows_exact", 0) - before,
+            "exact": after.get("collective_gather_rows_exact", 0) - before.get("collective_gather_rows_exact", 0),
+            "shm": after.get("collective_shm_gather_rows", 0) - before.get("collective_shm_gather_rows", 0),
         }
     with open(os.path.join(outdir, f"g{rank}.json"), "w") as f:
         json.dump(res, f)
     dist.shutdown()
 
 
-def test_gather_rows_exact_sizes_for_skewed_ranks(tmp_path):
+@pytest.mark.parametrize("shm", [False, True])
+def test_gather_rows_exact_sizes_for_skewed_ranks(tmp_path, shm):
     """VERDICT r3 (weak 6): collect padded every rank to the largest row
     count. Skewed blocks now travel at their own sizes (p2p to the root, one
     broadcast per rank for all-gather); balanced ones keep the single padded
     collective. Both give every rank's exact block, in rank order."""
     world = 3
-    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path), shm), nprocs=world, join=True)
     out = [json.load(open(tmp_path / f"g{r}.json")) for r in range(world)]
     for name, rows in (("skewed", [0, 7, 300]), ("balanced", [10, 11, 12])):
         want = [[[float(2 * i + 1000 * r), float(2 * i + 1 + 1000 * r)] for i in range(rows[r])] for r in range(world)]
         for r in range(world):
             assert out[r][name]["all"] == want
             assert out[r][name]["root"] == (want if r == 2 else None)
-            assert (out[r][name]["exact"] > 0) == (name == "skewed")
+            if shm:  # the shared segment moves every block at its own size
+                assert out[r][name]["shm"] == 2 and out[r][name]["exact"] == 0
+            else:
+                assert (out[r][name]["exact"] > 0) == (name == "skewed")

@@ -7,7 +7,15 @@
   ranks (processes) sharing the one GPU: every dtype and op against numpy,
   payloads up to the 64 KB cap, enough calls to cycle both buffer slots.
 
-The N = 2/4/8 contract runs on FakeComm in tests/test_comm.py. Reference: the
+Failure detection: a collective queued behind a stalled stream
+(kernels device_stall, a bounded spin) makes RcclComm.wait() raise
+CollectiveError at the timeout instead of hanging; a process stuck in an
+unbounded synchronisation is ended by the watchdog with status 76. The
+one-shot path's start-up self-test runs at world 1 and with two ranks on the
+GPU, and a forced failure switches every rank to RCCL.
+
+The N = 2/4/8 contract runs on FakeComm in tests/test_comm.py and on the
+shared-memory communicator in tests/test_shm_comm.py. Reference: the
 partial combine and the groupBy shuffle of
 src/main/scala/org/tensorframes/impl/DebugRowOps.scala:500,524-525,576,732-750."""
 import os
@@ -83,8 +91,9 @@ def _oneshot_worker(rank, world, port, outdir):
     hs = [None] * world
     tdist.all_gather_object(hs, o.ipc_handle())
     o.open(hs)
+    from tensorframes_amd.parallel import comm as _comm
+    res = {"bad": [], "selftest": _comm._oneshot_self_test(o, rank, world, 0), "alloc": o.alloc_kind}
     rng = np.random.default_rng(1234)
-    res = {"bad": []}
     # the same sequence on both ranks: sizes up to the 64 KB cap, every dtype
     # and op, more calls than slots
     for it in range(24):
@@ -116,7 +125,8 @@ def test_oneshot_two_ranks_share_one_gpu(tmp_path):
     mp.spawn(_oneshot_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         res = json.load(open(tmp_path / f"os{r}.json"))
-        assert res["bad"] == [] and res["calls"] == 24, res
+        assert res["selftest"] is None, res  # the start-up self-test passes across processes
+        assert res["bad"] == [] and res["calls"] == 24 + 6, res
 
 
 def test_engine_comm_serves_reduce_blocks_under_rccl_group(monkeypatch):
@@ -146,3 +156,104 @@ def test_engine_comm_serves_reduce_blocks_under_rccl_group(monkeypatch):
     finally:
         dist.shutdown()
         config.force_collectives = old
+
+
+def test_oneshot_buffer_is_uncached():
+    """The flag/slot buffer must not be L2-cacheable (peers write it over xGMI)."""
+    _need_gpu()
+    from tensorframes_amd._native import _C
+    o = _C.OneShotComm(0, 1, 0)
+    assert o.alloc_kind in ("uncached", "fine-grained"), o.alloc_kind
+
+
+def _forced_world(monkeypatch):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+
+
+def test_oneshot_self_test_and_forced_fallback(monkeypatch):
+    """world 1 (RCCL group, force_collectives): the self-test enables the
+    one-shot path; TFA_ONESHOT_SELFTEST_FAIL=1 makes every rank use RCCL."""
+    _need_gpu()
+    from tensorframes_amd.config import config
+    from tensorframes_amd.parallel import comm, dist
+    from tensorframes_amd.utils.logging import metrics
+    _forced_world(monkeypatch)
+    old = config.force_collectives
+    try:
+        assert dist.init(backend="nccl", force=True)
+        ok0 = metrics.snapshot().get("oneshot_selftest_ok", 0)
+        ec = comm.get()
+        assert ec.kinds == ["oneshot", "rccl"]
+        assert metrics.snapshot().get("oneshot_selftest_ok", 0) == ok0 + 1
+        dist.shutdown()
+        monkeypatch.setenv("TFA_ONESHOT_SELFTEST_FAIL", "1")
+        monkeypatch.delenv("MASTER_PORT", raising=False)
+        assert dist.init(backend="nccl", force=True)
+        ec = comm.get()
+        assert ec.kinds == ["rccl"]
+        t = torch.ones(16, device="cuda")
+        ec.all_reduce_(t)  # small payload now on RCCL
+        ec.wait()
+        assert t.tolist() == [1.0] * 16
+    finally:
+        dist.shutdown()
+        config.force_collectives = old
+
+
+def test_rccl_wait_times_out_behind_a_stalled_stream():
+    """A collective that cannot complete (here: queued behind a 3 s stall
+    kernel) raises CollectiveError at the 0.5 s timeout, not at completion;
+    the communicator is then failed and refuses new collectives."""
+    _need_gpu()
+    import time
+
+    from tensorframes_amd._native import _C
+    c = _C.RcclComm(_C.rccl_unique_id(), 0, 1, 0)
+    c.set_timeout(0.5, False)
+    x = torch.ones(1 << 20, device="cuda")
+    torch.cuda.synchronize()
+    _C.device_stall(3.0)
+    c.all_reduce(x, "Sum")
+    t0 = time.time()
+    with pytest.raises(_C.CollectiveError, match="timed out"):
+        c.wait()
+    waited = time.time() - t0
+    assert waited < 2.0, waited
+    torch.cuda.synchronize()  # the stall ends; the queued collective completes
+    assert c.failed
+    with pytest.raises(_C.CollectiveError):
+        c.all_reduce(x, "Sum")
+    # a healthy communicator: wait() returns once the work is done
+    c2 = _C.RcclComm(_C.rccl_unique_id(), 0, 1, 0)
+    c2.set_timeout(5.0, False)
+    c2.all_reduce(x, "Sum")
+    c2.wait()
+    assert c2.inflight == 0 and not c2.failed
+
+
+def test_rccl_watchdog_ends_a_stuck_process(tmp_path):
+    """The main thread blocks in an unbounded synchronisation behind a stalled
+    collective: the watchdog aborts the communicator and exits with 76."""
+    _need_gpu()
+    import subprocess
+    import sys
+    import time
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, time, torch; sys.path.insert(0, %r)\n"
+        "from tensorframes_amd._native import _C\n"
+        "c = _C.RcclComm(_C.rccl_unique_id(), 0, 1, 0)\n"
+        "c.set_timeout(0.3, True)\n"
+        "x = torch.ones(1 << 20, device='cuda'); torch.cuda.synchronize()\n"
+        "print('T0', time.time(), flush=True)\n"
+        "_C.device_stall(12.0)\n"
+        "c.all_reduce(x, 'Sum')\n"
+        "torch.cuda.synchronize()\n"
+        "print('NOT REACHED')\n" % repo)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    end = time.time()
+    assert p.returncode == 76, (p.returncode, p.stderr[-2000:])
+    assert "NOT REACHED" not in p.stdout and "aborting the RCCL communicator" in p.stderr
+    t0 = float(p.stdout.split("T0")[1].split()[0])
+    assert end - t0 < 9.0, end - t0  # ended by the watchdog, not by the 12 s stall finishing
