@@ -277,6 +277,8 @@ void dev_record_stream(const at::Tensor& t, hipStream_t s) {
       return;
     }
   }
+  // an alias of a HIP graph's output buffer: the next replay waits for `s`
+  if (replay_alias_record_stream(p, s)) return;
   // not ours: the framework allocator tracks it
   c10::hip::HIPCachingAllocator::recordStream(
       t.storage().data_ptr(), c10::hip::getStreamFromExternal(s, t.device().index()));

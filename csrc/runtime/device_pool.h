@@ -21,6 +21,10 @@ at::Tensor dev_empty_like(const at::Tensor& t, hipStream_t stream);
 // `t` (any device tensor) is also used on `s`: its memory is not reused
 // before s's work queued so far has finished
 void dev_record_stream(const at::Tensor& t, hipStream_t s);
+// the executor's hook for memory it hands out that is neither the pool's nor
+// c10's to recycle (aliases of a HIP graph's output buffers): returns true
+// when `p` is such memory and the use on `s` was recorded (executor.cpp)
+bool replay_alias_record_stream(const void* p, hipStream_t s);
 // D2D copy of a contiguous tensor into fresh pool memory (hipMemcpyAsync)
 at::Tensor dev_clone(const at::Tensor& t, hipStream_t stream);
 // at::empty for op temporaries: device tensors come from the pool, ordered

@@ -18,6 +18,7 @@
 #include <unistd.h>
 #include <cstdlib>
 #include <set>
+#include <unordered_map>
 #include <sstream>
 
 #include "../ir/ops_common.h"
@@ -267,7 +268,13 @@ struct Program::Plan {
   // the caller has dropped every output of its last replay (storage use
   // counts back at their values right after the capture). While they are
   // held, a second, `cloning` instance replays and copies its outputs out.
-  struct PtrCap {
+  // Uses of the aliases on other streams: a consumer that queued work reading
+  // an alias on another stream and said so (engine.record_stream ->
+  // dev_record_stream -> replay_alias_record_stream) gets an event recorded
+  // there; the next replay waits for those events before it rewrites the
+  // buffers, so dropping the host reference early is safe (ReplayOrder only
+  // orders replays against each other).
+  struct PtrCap : AliasUseSink {
     bool cloning = false;
     std::unique_ptr<HipGraph> graph;
     std::vector<at::Tensor> static_out;
@@ -276,16 +283,33 @@ struct Program::Plan {
     hipStream_t stream = nullptr;
     int64_t last_use = 0;
     ReplayOrder order;
+    std::mutex use_mu;
+    std::vector<hipEvent_t> uses;   // events on consumer streams since the last replay
     bool outputs_free() const {
       for (size_t i = 0; i < static_out.size(); ++i)
         if (!input_alias[i] && static_out[i].storage().use_count() > base_uc[i]) return false;
       return true;
     }
-    ~PtrCap() {
-      order.drain();
-      graph.reset();
-      if (stream) (void)hipStreamDestroy(stream);
+    void record_use(hipStream_t s) override {
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(s);  // no event: make the use complete now instead
+        return;
+      }
+      (void)hipEventRecord(e, s);
+      std::lock_guard<std::mutex> lk(use_mu);
+      uses.push_back(e);
     }
+    void wait_uses(hipStream_t cur) {
+      std::lock_guard<std::mutex> lk(use_mu);
+      for (hipEvent_t e : uses) {
+        (void)hipStreamWaitEvent(cur, e, 0);
+        (void)hipEventDestroy(e);  // destroyed after the wait is enqueued: HIP keeps it until then
+      }
+      uses.clear();
+    }
+    ~PtrCap() override;
   };
   std::mutex ptr_mu;
   std::map<std::vector<const void*>, int> ptr_seen;  // pointer set -> runs seen (bounded)
@@ -294,6 +318,51 @@ struct Program::Plan {
   bool ptr_declined = false;
   int64_t ptr_eager_ns = 0, ptr_eager_n = 0, ptr_replay_ns = 0, ptr_replay_n = 0;
 };
+
+namespace {
+// storage base of every aliased replay output -> its capture
+std::mutex g_alias_mu;
+std::unordered_map<const void*, Program::AliasUseSink*>& alias_registry() {
+  static auto* m = new std::unordered_map<const void*, Program::AliasUseSink*>();
+  return *m;
+}
+void register_aliases(Program::AliasUseSink* sink, const std::vector<const void*>& ptrs) {
+  std::lock_guard<std::mutex> lk(g_alias_mu);
+  for (const void* q : ptrs) alias_registry()[q] = sink;
+}
+void unregister_aliases(Program::AliasUseSink* sink, const std::vector<const void*>& ptrs) {
+  std::lock_guard<std::mutex> lk(g_alias_mu);
+  for (const void* q : ptrs) {
+    auto it = alias_registry().find(q);
+    if (it != alias_registry().end() && it->second == sink) alias_registry().erase(it);
+  }
+}
+std::vector<const void*> alias_ptrs(const std::vector<at::Tensor>& outs, const std::vector<bool>& input_alias) {
+  std::vector<const void*> v;
+  for (size_t i = 0; i < outs.size(); ++i)
+    if (!input_alias[i]) v.push_back(outs[i].storage().data_ptr().get());
+  return v;
+}
+}  // namespace
+
+Program::Plan::PtrCap::~PtrCap() {
+  if (!cloning) unregister_aliases(this, alias_ptrs(static_out, input_alias));
+  for (hipEvent_t e : uses) {
+    (void)hipEventSynchronize(e);
+    (void)hipEventDestroy(e);
+  }
+  order.drain();
+  graph.reset();
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+bool replay_alias_record_stream(const void* p, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_alias_mu);
+  auto it = alias_registry().find(p);
+  if (it == alias_registry().end()) return false;
+  it->second->record_use(s);
+  return true;
+}
 
 Program::Program(std::shared_ptr<Graph> g, const std::vector<std::string>& fetches,
                  const std::vector<std::string>& feeds)
@@ -1748,6 +1817,7 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
     }
     stats_.graphs_captured++;
     use = pc.get();
+    if (!pc->cloning) register_aliases(pc.get(), alias_ptrs(pc->static_out, pc->input_alias));
     p.ptr_caps[key].push_back(std::move(pc));
     p.ptr_seen.erase(key);
   }
@@ -1759,6 +1829,7 @@ std::optional<std::vector<at::Tensor>> Program::run_ptr_graph(Plan& p, const std
     p.used_streams[dev].insert(cur);
   }
   use->order.before(cur);
+  use->wait_uses(cur);  // readers of the previous aliases on other streams
   use->graph->replay(cur);
   use->order.after(cur);
   std::vector<at::Tensor> outs;

@@ -127,6 +127,15 @@ class Program {
   std::string host_op_error_;  // set when a host-only op is reachable (analysis ok, running not)
   struct Step;
   struct Plan;
+ public:
+  // a captured replay whose output buffers are handed out as aliases: told
+  // about every other stream a consumer queued reads of an alias on
+  struct AliasUseSink {
+    virtual ~AliasUseSink() = default;
+    virtual void record_use(hipStream_t s) = 0;
+  };
+
+ private:
   std::shared_ptr<Plan> plan_for(const std::vector<at::Tensor>& inputs);
   std::shared_ptr<Plan> build_plan(const std::vector<at::Tensor>& inputs, bool force_gpu);
   std::vector<at::Tensor> execute(Plan& p, const std::vector<at::Tensor>& inputs, void* stream);
