@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "gemm_f32_core.h"
+#include "gemm_g2_core.h"
 #include "gemm_internal.h"
 #include "hip_common.h"
 
@@ -83,12 +84,32 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
 // 2.5M x 512 x 512 134.8 -> 135.6 TF; a 2x4 128x256 never beat them.
 // 21 is 256x256 as 16 waves (4x4 waves of 64x64, 1024 threads, four waves
 // per SIMD in one block): 4096^3 141.2 TF, 8192^3 142.6 TF.
-constexpr int kNumTiles = 22;
+// 22-27 are the g2 core (gemm_g2_core.h: one wave per SIMD, LDS-DMA staging,
+// k-permuted b128 fragments), kG2Tiles in order; used where its loaders apply
+// (k-contiguous A or the conv im2col with C % 4 == 0, 16-byte aligned rows).
+constexpr int kFirstG2 = 22;
+constexpr int kNumTiles = kFirstG2 + g2::kNumG2Tiles;
 constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {128, 32},
                                       {128, 96}, {128, 192}, {128, 160}, {64, 192}, {256, 128},
                                       {256, 64}, {256, 32}, {256, 96}, {256, 128}, {256, 96},
                                       {128, 128}, {128, 192}, {256, 64}, {128, 64}, {128, 256},
-                                      {256, 256}, {256, 256}};
+                                      {256, 256}, {256, 256},
+                                      // g2
+                                      {256, 256}, {256, 192}, {256, 128}, {256, 64}, {128, 128}, {128, 64}};
+static_assert(g2::kG2Tiles[0][0] == 256 && g2::kG2Tiles[0][1] == 256 && g2::kG2Tiles[5][1] == 64,
+              "kTiles' g2 rows mirror kG2Tiles");
+
+// the g2 core's loaders: k-contiguous A (or the vec conv loader), 16-byte
+// aligned operand rows, whole 4-column quads of B [K][N]
+bool g2_ok(const GemmArgs& g, int al, bool vec) {
+  static const bool off = [] {
+    const char* e = std::getenv("TFA_GEMM_G2");
+    return e && std::atoi(e) == 0;
+  }();
+  if (off || !vec || (al != A_KCONTIG && al != A_CONV)) return false;
+  if (!g.tb && g.N % 4 != 0) return false;
+  return g.K % 4 == 0;
+}
 
 int64_t tile_blocks(int c, int64_t M, int64_t N, int64_t batch) {
   return ((M + kTiles[c][0] - 1) / kTiles[c][0]) * ((N + kTiles[c][1] - 1) / kTiles[c][1]) * batch;
@@ -120,7 +141,7 @@ std::atomic<int>& forced_tile() {
 int tile_env() { return forced_tile().load(); }
 
 // Heuristic plan (also the fallback of the autotuner and what sizes the split-K workspace)
-F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
+F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch, bool use_forced = true) {
   // narrow N picks a narrow tile (a 128-wide tile on N=32 wastes 3/4 of the MFMAs)
   int cfg = N <= 32 ? 4 : (N <= 64 ? 1 : 0);
   // big GEMMs: 256x64 with the 4 waves stacked along M (each 64x64, B fragments shared);
@@ -131,11 +152,19 @@ F32Plan plan_f32(int64_t M, int64_t N, int64_t K, int64_t batch) {
     if (cfg == 0) cfg = N > 96 ? 2 : 3;
     else if (cfg == 1) cfg = 3;
   }
-  if (tile_env() >= 0) cfg = tile_env();  // tuning override
+  if (use_forced && tile_env() >= 0) cfg = tile_env();  // tuning override
   return plan_for(cfg, M, N, K, batch);
 }
 
 void launch_plan(const F32Plan& p, const GemmArgs& g, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
+  if (p.cfg >= kFirstG2) {
+    TFA_CHECK(g2_ok(g, al, vec), "gemm: g2 tile on an operand layout it does not load");
+    F32Plan q = p;
+    q.cfg -= kFirstG2;
+    if (al == A_CONV) g2::launch_conv(q, g, cg, s);
+    else g2::launch_kc(q, g, s);
+    return;
+  }
   if (al == A_CONV) launch_conv(p, g, vec, cg, s);
   else if (al == A_KCONTIG && !g.tb) launch_kcontig_b(p, g, vec, s);
   else if (al == A_KCONTIG) launch_kcontig_bt(p, g, vec, s);
@@ -205,6 +234,7 @@ F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, co
     for (int c = 0; c < kNumTiles; ++c) {
       const F32Plan q = plan_for(c, g.M, g.N, g.K, g.batch);
       if (q.splits != 1) continue;
+      if (c >= kFirstG2 && !g2_ok(g, al, vec)) continue;
       if (c != heur.cfg && kTiles[c][1] >= 2 * g.N && kTiles[c][1] > 32) continue;  // mostly-padding tile
       if (round == 0) launch_plan(q, g, al, vec, cg, s);  // warm
       (void)hipEventRecord(e0, s);
@@ -238,6 +268,8 @@ F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, co
 
 void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
   F32Plan p = plan_f32(g0.M, g0.N, g0.K, g0.batch);
+  if (p.cfg >= kFirstG2 && !g2_ok(g0, al, vec))  // a forced g2 tile on a layout it does not load
+    p = plan_f32(g0.M, g0.N, g0.K, g0.batch, false);
   if (p.splits == 1 && autotune_on()) p = tuned_plan(p, g0, al, vec, cg, s);
   GemmArgs g = g0;
   if (p.splits > 1) {

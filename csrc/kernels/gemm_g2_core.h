@@ -1,0 +1,420 @@
+// The "g2" f32 MFMA core: one wave per SIMD, LDS-DMA staging (gfx950).
+//
+// The round-4 core (gemm_f32_core.h) stages tiles through registers and
+// ds_write, reads one k-step of fragments per ds_read_b32, and keeps 2-4
+// waves per SIMD; its MFMA pipe sat ~13 % idle on the big shapes. This core
+// is the structure measured in scripts/g2_lab.hip (4096^3 144 TF, 8192^3 145
+// TF, 2.56M x 512 x 512 135 TF against 139.7 / 142.5 / 131.9 for the round-4
+// core on the same box):
+//
+//   * a block of 4 waves (one per SIMD) over BM x BN, each wave a
+//     (BM/WM) x (BN/WN) tile of 32x32 accumulators: up to 256 accumulator
+//     registers per lane, which the compiler keeps in AGPRs;
+//   * operands go global -> LDS with global_load_lds_dwordx4 (no VGPR
+//     staging, no ds_write). The DMA image of an instruction is lane-linear,
+//     so the layout is chosen through the per-lane SOURCE addresses:
+//       - k-contiguous operands (A [M][K], conv im2col rows, B^T [N][K]):
+//         one instruction = 16 rows x 64 B (whole row segments: coalesced),
+//         image [row][4 k-quad slots] with slot c holding k quad
+//         c ^ ((row >> 2) & 3), which makes the fragment reads conflict-free;
+//       - row-contiguous B ([K][N] weights): image [k][n], one instruction =
+//         256 consecutive floats of it;
+//   * fragments: a lane reads its row's k quad with one ds_read_b128 and
+//     feeds it to 2 MFMA k-steps (a [k][n] image: one ds_read_b32 per step),
+//     pairing k = 2t / 2t+1 across the wave halves exactly as the round-4
+//     core does, so every tile of both cores gives bit-identical results;
+//   * a ring of STAGES LDS stages of BK = 16 with one stage in flight beyond
+//     the next: counted vmcnt (never 0 in the steady loop), one raw s_barrier
+//     per stage; the next fragments (and the next stage's first ones) are
+//     read in the shadow of the current MFMAs, and the stage's LDS-DMA
+//     instructions are spread between the first MFMAs (sched_group_barrier:
+//     each costs ~60 issue cycles when issued back to back);
+//   * out-of-range rows, padding taps and the K tail read a 16-byte zero page
+//     (the DMA source is per lane), so interior and edge blocks run one path;
+//   * epilogue as the round-4 core: bias + none/ReLU/ReLU6 through a
+//     wave-private LDS tile and float4 stores, the sibling-conv segments, the
+//     heavy (transcendental / chained) epilogue, split-K partial slabs.
+#pragma once
+
+#include "gemm_f32_core.h"
+
+namespace tfa {
+namespace k {
+namespace g2 {
+
+using f32core::A_CONV;
+using f32core::A_KCONTIG;
+using f32core::ConvGeom;
+using f32core::F32Plan;
+
+enum BLoad { B_RC = 0, B_KC = 1 };  // B [K][N] (row-contiguous) or B^T [N][K]
+
+// the launcher translation units (cfg indexes kG2Tiles): k-contiguous A with
+// B [K][N] or B^T [N][K] (g.tb), and the implicit-GEMM conv (filter [K][N])
+void launch_kc(const F32Plan& p, const GemmArgs& g, hipStream_t s);
+void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s);
+
+// {BM, BN, WM, WN, STAGES}
+constexpr int kNumG2Tiles = 6;
+constexpr int kG2Tiles[kNumG2Tiles][5] = {
+    {256, 256, 2, 2, 4}, {256, 192, 2, 2, 4}, {256, 128, 2, 2, 4},
+    {256, 64, 4, 1, 5},  {128, 128, 2, 2, 5}, {128, 64, 2, 2, 5}};
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// global -> LDS, 16 bytes per lane: lane i lands at lds + 16 * i
+__device__ __forceinline__ void glds16(const void* gp, void* lds) {
+  __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt at their maxima; gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, int AL, int BL>
+__global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
+                                                           int64_t k_per_split, int flags) {
+  constexpr int NW = WM * WN, NT = 64 * NW, BK = 16, KQ = BK / 4;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4, STAGE = A_BYTES + B_BYTES;
+  constexpr int AI = BM / 16 / NW;  // A: 16 rows per LDS-DMA instruction
+  constexpr int BI = BN / 16 / NW;  // B: 16 rows ([N][K]) or 256 floats ([K][N]) per instruction
+  constexpr int G = AI + BI;         // LDS-DMA instructions per wave per stage
+  constexpr int kEpi = NW * 32 * 32 * 4;
+  static_assert(NW == 4 && TM >= 1 && TN >= 1 && AI >= 1 && BI >= 1 && BM % (16 * NW) == 0 && BN % (16 * NW) == 0,
+                "4 waves, >= one 32x32 tile each, whole DMA instructions per wave");
+  static_assert(STAGES >= 3 && STAGES * STAGE <= 160 * 1024 && STAGES * STAGE >= kEpi, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int nwg = tiles_m * tiles_n;
+  const int wg = f32core::xcd_remap(blockIdx.x, nwg);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * BN;
+  const int64_t bz = blockIdx.y;
+  const float* A = static_cast<const float*>(g.A) + bz * g.strideA;
+  const float* B = static_cast<const float*>(g.B) + bz * g.strideB;
+  const int64_t M = g.M, N = g.N, K = g.K;
+  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = min(K, kbeg + k_per_split);
+  const float* zero = f32core::kZeroPage;
+
+  // ---- A pieces: instruction q = wave*AI + i covers rows 16q .. 16q+15,
+  // lane -> row 16q + lane/4, k quad koff/4 of the stage (swizzled slot).
+  // Every source choice below is a select on bitwise-combined conditions:
+  // a branch here makes the compiler drain the DMA queue (vmcnt(0)) at the
+  // join, which serialises the ring.
+  const int koff = 4 * ((lane & 3) ^ ((lane >> 4) & 3));
+  const float* ap[AI];  // k-contiguous: this stage's 16-byte piece of the row; conv: the image base
+  bool aok[AI];         // row in range
+  int cih[AI], ciw[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int64_t m = m0 + (wave * AI + i) * 16 + lane / 4;
+    aok[i] = m < M;
+    const int64_t mc = aok[i] ? m : 0;
+    if constexpr (AL == A_KCONTIG) {
+      ap[i] = A + mc * g.lda + kbeg + koff;
+      cih[i] = ciw[i] = 0;
+    } else {
+      int64_t ow, oh, n;
+      if (cg.fast) {
+        const uint32_t m32 = (uint32_t)mc, t = fdiv(m32, cg.fOW), q = fdiv(t, cg.fOH);
+        ow = m32 - t * (uint32_t)cg.OW;
+        oh = t - q * (uint32_t)cg.OH;
+        n = q;
+      } else {
+        ow = mc % cg.OW;
+        const int64_t t = mc / cg.OW;
+        oh = t % cg.OH;
+        n = t / cg.OH;
+      }
+      ap[i] = A + n * (int64_t)cg.H * cg.W * cg.C;
+      cih[i] = (int)(oh * cg.sh - cg.pt);
+      ciw[i] = (int)(ow * cg.sw - cg.pl);
+    }
+  }
+  // conv: this lane's k -> (kh, kw, c), advanced by BK per stage
+  int kc = 0, kkw = 0, kkh = 0;
+  if constexpr (AL == A_CONV) {
+    const int k = (int)(kbeg + koff);
+    kc = k % cg.C;
+    const int t = k / cg.C;
+    kkw = t % cg.KW;
+    kkh = t / cg.KW;
+  }
+  // ---- B pieces: running source pointers (advanced by one stage per issue)
+  const float* bp[BI];
+  bool bok[BI];
+  int bk_[BI];  // the piece's k within the stage
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int q = wave * BI + i;
+    if constexpr (BL == B_KC) {
+      const int64_t n = n0 + q * 16 + lane / 4;
+      bok[i] = n < N;
+      bp[i] = B + (bok[i] ? n : 0) * g.ldb + kbeg + koff;
+      bk_[i] = koff;
+    } else {
+      const int e = q * 256 + 4 * lane;
+      const int kb = e / BN, nb = e % BN;
+      bok[i] = n0 + nb < N;
+      bp[i] = B + (kbeg + kb) * g.ldb + (bok[i] ? n0 + nb : 0);
+      bk_[i] = kb;
+    }
+  }
+  const int64_t bstep = BL == B_KC ? BK : (int64_t)BK * g.ldb;  // elements per stage
+  int64_t kpos = kbeg;  // k0 of the next stage to issue
+
+  // issue the LDS-DMA of the next stage into ring slot `slot`. Every source
+  // choice is a select on bitwise-combined conditions and the pointers only
+  // ever advance by constants: a branch (or a spill reload) here makes the
+  // compiler drain the DMA queue (vmcnt(0)) at the join, serialising the ring.
+  auto issue = [&](int slot) __attribute__((always_inline)) {
+    char* base = smem + slot * STAGE;
+    const bool kok = kpos + koff < kend;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const float* src;
+      if constexpr (AL == A_KCONTIG) {
+        src = (aok[i] & kok) ? ap[i] : zero;
+        ap[i] += BK;
+      } else {
+        const int ih = cih[i] + kkh * cg.dh, iw = ciw[i] + kkw * cg.dw;
+        const bool ok = aok[i] & kok & (ih >= 0) & (ih < cg.H) & (iw >= 0) & (iw < cg.W);
+        src = ok ? ap[i] + ((ih * cg.W + iw) * cg.C + kc) : zero;
+      }
+      glds16(src, base + (wave * AI + i) * 1024);
+    }
+    if constexpr (AL == A_CONV) {
+      // advance (kc, kkw, kkh) by BK; C >= 4, so at most BK / 4 carries: a
+      // fixed, select-only sequence (no data-dependent loop)
+      kc += BK;
+#pragma unroll
+      for (int r = 0; r < BK / 4; ++r) {
+        const bool carry = kc >= cg.C;
+        kc = carry ? kc - cg.C : kc;
+        const int w1 = kkw + (carry ? 1 : 0);
+        const bool wrap = w1 == cg.KW;
+        kkw = wrap ? 0 : w1;
+        kkh = kkh + (wrap ? 1 : 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const bool ok = bok[i] & (kpos + bk_[i] < kend);
+      glds16(ok ? bp[i] : zero, base + A_BYTES + (wave * BI + i) * 1024);
+      bp[i] += bstep;
+    }
+    kpos += BK;
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){};
+
+  // Fragments, in the round-4 core's summation order: MFMA k-step t pairs k
+  // = 2t (lanes 0-31) with k = 2t+1 (lanes 32-63), steps in increasing k, so
+  // every tile of either core gives bit-identical results (the autotuner's
+  // pick never changes a result). One b128 read of a row's k quad serves two
+  // steps: half 0 takes components 0 / 2, half 1 components 1 / 3 (one
+  // v_cndmask per operand); a [k][n] image is read per step (ds_read_b32).
+  struct Frag {
+    float a[TM][2], b[TN][2];
+  };
+  const int slot_sw = (r32 >> 2) & 3;  // the rows a lane reads differ by multiples of 32: one swizzle
+  auto read = [&](int kt, int q, Frag& f) __attribute__((always_inline)) {
+    const char* st = smem + (kt % STAGES) * STAGE;
+    const int slot = q ^ slot_sw;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(st + (wm * (BM / WM) + i * 32 + r32) * 64 + slot * 16);
+      f.a[i][0] = h ? v[1] : v[0];
+      f.a[i][1] = h ? v[3] : v[2];
+    }
+#pragma unroll
+    for (int jn = 0; jn < TN; ++jn) {
+      const int n = wn * (BN / WN) + jn * 32 + r32;
+      if constexpr (BL == B_KC) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(st + A_BYTES + n * 64 + slot * 16);
+        f.b[jn][0] = h ? v[1] : v[0];
+        f.b[jn][1] = h ? v[3] : v[2];
+      } else {
+        const float* bs = reinterpret_cast<const float*>(st + A_BYTES) + (4 * q + h) * BN + n;
+        f.b[jn][0] = bs[0];
+        f.b[jn][1] = bs[2 * BN];
+      }
+    }
+  };
+  auto mma = [&](const Frag& f) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < TN; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][s], f.b[jn][s], acc[i][jn], 0, 0, 0);
+  };
+  // MFMAs per k quad, fragment read instructions per k quad
+  constexpr int NM = 2 * TM * TN, RD = TM + (BL == B_KC ? TN : 2 * TN);
+
+  const int KT = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+  // prologue: stages 0 .. S-2 (a stage past KT reads only zero pages)
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) issue(s);
+  wait_vm<G * (STAGES - 2)>();  // stage 0 landed
+  __builtin_amdgcn_s_barrier();
+  Frag cur, nxt;
+  if (KT > 0) read(0, 0, cur);
+  // one stage: stage kt+1 retired for every wave (counted wait + barrier),
+  // which also frees the slot of stage kt-1 for the DMA of stage kt+S-1;
+  // then KQ k quads of MFMAs, each with the next quad's reads (the next
+  // stage's first quad after the last) in its shadow
+  auto stage = [&](int kt, auto do_issue) __attribute__((always_inline)) {
+    constexpr bool ISSUE = decltype(do_issue)::value;
+    if (kt + STAGES - 2 < KT) wait_vm<G * (STAGES - 3)>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {
+      if (j + 1 < KQ) read(kt, j + 1, nxt);
+      else if (kt + 1 < KT) read(kt + 1, 0, nxt);
+      if (ISSUE && j == 0) issue((kt + STAGES - 1) % STAGES);
+      mma(cur);
+      // spread the stage's DMA (first pair only) and the next pair's reads
+      // between the MFMAs: MFMA, load, MFMA, load, ... then the rest
+      static_for<NM>([&](auto qc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        __builtin_amdgcn_sched_group_barrier(f32core::kSchedMfma, 1, 0);
+        if constexpr (ISSUE) {
+          if (j == 0 && q < G) __builtin_amdgcn_sched_group_barrier(f32core::kSchedVmemRead, 1, 0);
+          else if (j == 0 && q < G + RD) __builtin_amdgcn_sched_group_barrier(f32core::kSchedDsRead, 1, 0);
+          else if (j != 0 && q < RD) __builtin_amdgcn_sched_group_barrier(f32core::kSchedDsRead, 1, 0);
+        } else {
+          if (q < RD) __builtin_amdgcn_sched_group_barrier(f32core::kSchedDsRead, 1, 0);
+        }
+      });
+      cur = nxt;
+    }
+  };
+  int kt = 0;
+  for (; kt + STAGES - 1 < KT; ++kt) stage(kt, std::true_type{});
+  for (; kt < KT; ++kt) stage(kt, std::false_type{});
+  __syncthreads();  // every wave is done with the ring: its LDS becomes the epilogue staging
+
+  // ---- epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  const int vepi = flags & 1;
+  float* ws = static_cast<float*>(g.workspace);
+  const float* bias = static_cast<const float*>(g.bias);
+  const bool heavy = !ws && !(g.act <= ACT_RELU6 && g.epi.n == 0);
+  float* Cb = static_cast<float*>(g.C) + bz * g.strideC;
+  if (vepi) {
+    float* stg = reinterpret_cast<float*>(smem) + wave * 1024;
+    static_for<TN>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      static_for<TM>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        const f32x16 v = acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) stg[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + r32] = v[r];
+        const int64_t col = n0 + wn * (BN / WN) + j * 32 + 4 * (lane & 7);
+        if (col < N) {
+          float* cbase;
+          int64_t cld;
+          int cact;
+          f32core::out_col(g, Cb, col, cbase, cld, cact);
+          float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (bias) bv = make_float4(bias[col], bias[col + 1], bias[col + 2], bias[col + 3]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rr = 8 * q + (lane >> 3);
+            const int64_t row = m0 + wm * (BM / WM) + i * 32 + rr;
+            float4 o = *reinterpret_cast<const float4*>(&stg[rr * 32 + 4 * (lane & 7)]);
+            o.x = act_fast(o.x + bv.x, cact);
+            o.y = act_fast(o.y + bv.y, cact);
+            o.z = act_fast(o.z + bv.z, cact);
+            o.w = act_fast(o.w + bv.w, cact);
+            if (row < M) *reinterpret_cast<float4*>(cbase + row * cld) = o;
+          }
+        }
+      });
+    });
+    return;
+  }
+  static_for<TN>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    const int64_t col = n0 + wn * (BN / WN) + j * 32 + r32;
+    if (col >= N) return;
+    const float bv = (!ws && bias) ? bias[col] : 0.f;
+    float* cbase;
+    int64_t cld;
+    int cact;
+    f32core::out_col(g, Cb, col, cbase, cld, cact);
+    if (heavy) cact = ACT_NONE;
+    static_for<TM>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      const f32x16 v = acc[i][j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= M) continue;
+        if (ws)  // split-K partial slab [split][batch][M][N]
+          ws[(((int64_t)blockIdx.z * gridDim.y + bz) * M + row) * N + col] = v[r];
+        else
+          cbase[row * cld] = act_fast(v[r] + bv, cact);
+      }
+    });
+  });
+  if (heavy) {
+#pragma nounroll
+    for (int e = 0; e < TN * TM * 16; ++e) {
+      const int j = e / (TM * 16), i = (e / 16) % TM, r = e % 16;
+      const int64_t col = n0 + wn * (BN / WN) + j * 32 + r32;
+      const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (col >= N || row >= M) continue;
+      float* cbase;
+      int64_t cld;
+      int cact;
+      f32core::out_col(g, Cb, col, cbase, cld, cact);
+      float* p = cbase + row * cld;
+      *p = epi_apply(g.epi, act_apply(*p, cact), row, col, N, bz * M * N);
+    }
+  }
+}
+
+template <int AL, int BL>
+void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s) {
+  const int vepi = p.splits == 1 ? f32core::vector_epilogue(g) : 0;
+  const int bm = kG2Tiles[p.cfg][0], bn = kG2Tiles[p.cfg][1];
+  const int64_t tm = (g.M + bm - 1) / bm, tn = (g.N + bn - 1) / bn;
+  TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
+  TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");
+  dim3 grid((unsigned)(tm * tn), (unsigned)g.batch, (unsigned)p.splits);
+#define TFA_G2(BM_, BN_, WM_, WN_, S_)                                                                          \
+  hipLaunchKernelGGL((g2_tile<BM_, BN_, WM_, WN_, S_, AL, BL>), grid, dim3(64 * WM_ * WN_), 0, s, g, (int)tm, \
+                     (int)tn, cg, p.k_per_split, vepi)
+  switch (p.cfg) {
+    case 0: TFA_G2(256, 256, 2, 2, 4); break;
+    case 1: TFA_G2(256, 192, 2, 2, 4); break;
+    case 2: TFA_G2(256, 128, 2, 2, 4); break;
+    case 3: TFA_G2(256, 64, 4, 1, 5); break;
+    case 4: TFA_G2(128, 128, 2, 2, 5); break;
+    default: TFA_G2(128, 64, 2, 2, 5); break;
+  }
+#undef TFA_G2
+}
+
+}  // namespace
+}  // namespace g2
+}  // namespace k
+}  // namespace tfa
