@@ -545,6 +545,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     c10::hip::HIPGuard guard(rec.device().index());
     k::unpack_rows(pc, rec.contiguous().data_ptr(), n, R, c10::hip::getCurrentHIPStream(rec.device().index()).stream());
   }, "records [n, R] -> the preallocated device columns (same layout as pack_rows)");
+  m.def("ragged_image_prep", [](const at::Tensor& data, const at::Tensor& offs, const at::Tensor& hw, int C, int OH,
+                                 int OW, int mode, int oy, int ox, int h, int w,
+                                 const std::vector<std::pair<int, std::vector<float>>>& ops) {
+    // the batched map_rows image pre-stage (kernels/image.hip ragged_prep_kernel)
+    TFA_CHECK(data.is_cuda() && data.scalar_type() == at::kByte && data.dim() == 1 && data.is_contiguous(),
+              "ragged_image_prep: data must be a contiguous uint8 device buffer");
+    const int64_t n = offs.numel();
+    TFA_CHECK(offs.is_cuda() && offs.scalar_type() == at::kLong && offs.is_contiguous() && hw.is_cuda() &&
+                  hw.scalar_type() == at::kInt && hw.is_contiguous() && hw.numel() == 2 * n,
+              "ragged_image_prep: offsets int64 [n] and hw int32 [n, 2] device tensors expected");
+    TFA_CHECK(ops.size() <= 4, "ragged_image_prep: at most 4 elementwise steps");
+    k::RaggedPrepArgs a;
+    a.n = n; a.C = C; a.OH = OH; a.OW = OW; a.mode = mode; a.oy = oy; a.ox = ox; a.h = h; a.w = w;
+    a.nops = static_cast<int>(ops.size());
+    for (size_t q = 0; q < ops.size(); ++q) {
+      TFA_CHECK(ops[q].first >= 0 && ops[q].first <= 2, "ragged_image_prep: step kind must be 0 add, 1 sub, 2 mul");
+      const auto& v = ops[q].second;
+      TFA_CHECK(v.size() == 1 || static_cast<int>(v.size()) == C, "ragged_image_prep: step constant of ", v.size(),
+                " values for ", C, " channels");
+      a.op_kind[q] = ops[q].first;
+      a.op_chan[q] = v.size() > 1;
+      for (size_t c = 0; c < v.size(); ++c) a.op_val[q][c] = v[c];
+    }
+    c10::hip::HIPGuard guard(data.device().index());
+    at::Tensor y = pool_empty({n, h, w, C}, data.options().dtype(at::kFloat));
+    a.x = data.data_ptr<uint8_t>();
+    a.offs = offs.data_ptr<int64_t>();
+    a.hw = hw.data_ptr<int32_t>();
+    a.y = y.data_ptr<float>();
+    k::ragged_image_prep(a, c10::hip::getCurrentHIPStream(data.device().index()).stream());
+    return y;
+  }, py::arg("data"), py::arg("offsets"), py::arg("hw"), py::arg("channels"), py::arg("resize_h"),
+        py::arg("resize_w"), py::arg("mode"), py::arg("crop_y"), py::arg("crop_x"), py::arg("crop_h"),
+        py::arg("crop_w"), py::arg("ops"),
+        "n ragged uint8 HWC images -> f32 [n, crop_h, crop_w, C]: bilinear resize, crop, elementwise steps");
   m.def("gather_rows", [](const at::Tensor& x0, const at::Tensor& idx) {
     TFA_CHECK(x0.is_cuda() && idx.is_cuda() && idx.scalar_type() == at::kLong, "gather_rows: device tensors");
     c10::hip::HIPGuard guard(x0.device().index());

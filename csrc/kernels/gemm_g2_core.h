@@ -27,8 +27,8 @@
 //     the next: counted vmcnt (never 0 in the steady loop), one raw s_barrier
 //     per stage; the next fragments (and the next stage's first ones) are
 //     read in the shadow of the current MFMAs, and the stage's LDS-DMA
-//     instructions are spread between the first MFMAs (sched_group_barrier:
-//     each costs ~60 issue cycles when issued back to back);
+//     instructions are spread over its k quads and between the MFMAs
+//     (sched_group_barrier: each costs ~60 issue cycles back to back);
 //   * out-of-range rows, padding taps and the K tail read a 16-byte zero page
 //     (the DMA source is per lane), so interior and edge blocks run one path;
 //   * epilogue as the round-4 core: bias + none/ReLU/ReLU6 through a
@@ -174,15 +174,16 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
   const int64_t bstep = BL == B_KC ? BK : (int64_t)BK * g.ldb;  // elements per stage
   int64_t kpos = kbeg;  // k0 of the next stage to issue
 
-  // issue the LDS-DMA of the next stage into ring slot `slot`. Every source
+  // The LDS-DMA of one stage, piece by piece (A pieces 0..AI-1, then B
+  // pieces), so the main loop can place each between two MFMAs. Every source
   // choice is a select on bitwise-combined conditions and the pointers only
   // ever advance by constants: a branch (or a spill reload) here makes the
   // compiler drain the DMA queue (vmcnt(0)) at the join, serialising the ring.
-  auto issue = [&](int slot) __attribute__((always_inline)) {
+  auto issue_piece = [&](int slot, int p) __attribute__((always_inline)) {
     char* base = smem + slot * STAGE;
     const bool kok = kpos + koff < kend;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
+    if (p < AI) {
+      const int i = p;
       const float* src;
       if constexpr (AL == A_KCONTIG) {
         src = (aok[i] & kok) ? ap[i] : zero;
@@ -193,28 +194,31 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
         src = ok ? ap[i] + ((ih * cg.W + iw) * cg.C + kc) : zero;
       }
       glds16(src, base + (wave * AI + i) * 1024);
-    }
-    if constexpr (AL == A_CONV) {
-      // advance (kc, kkw, kkh) by BK; C >= 4, so at most BK / 4 carries: a
-      // fixed, select-only sequence (no data-dependent loop)
-      kc += BK;
+      if (AL == A_CONV && i == AI - 1) {
+        // advance (kc, kkw, kkh) by BK; C >= 4, so at most BK / 4 carries:
+        // a fixed, select-only sequence (no data-dependent loop)
+        kc += BK;
 #pragma unroll
-      for (int r = 0; r < BK / 4; ++r) {
-        const bool carry = kc >= cg.C;
-        kc = carry ? kc - cg.C : kc;
-        const int w1 = kkw + (carry ? 1 : 0);
-        const bool wrap = w1 == cg.KW;
-        kkw = wrap ? 0 : w1;
-        kkh = kkh + (wrap ? 1 : 0);
+        for (int r = 0; r < BK / 4; ++r) {
+          const bool carry = kc >= cg.C;
+          kc = carry ? kc - cg.C : kc;
+          const int w1 = kkw + (carry ? 1 : 0);
+          const bool wrap = w1 == cg.KW;
+          kkw = wrap ? 0 : w1;
+          kkh = kkh + (wrap ? 1 : 0);
+        }
       }
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
+    } else {
+      const int i = p - AI;
       const bool ok = bok[i] & (kpos + bk_[i] < kend);
       glds16(ok ? bp[i] : zero, base + A_BYTES + (wave * BI + i) * 1024);
       bp[i] += bstep;
+      if (i == BI - 1) kpos += BK;
     }
-    kpos += BK;
+  };
+  auto issue = [&](int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < G; ++p) issue_piece(slot, p);
   };
 
   f32x16 acc[TM][TN];
@@ -229,26 +233,26 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
   // pick never changes a result). One b128 read of a row's k quad serves two
   // steps: half 0 takes components 0 / 2, half 1 components 1 / 3 (one
   // v_cndmask per operand); a [k][n] image is read per step (ds_read_b32).
+  // b128 quads are kept whole until their MFMAs: selecting a lane's two
+  // components right after the read would make the wave wait for it there
   struct Frag {
-    float a[TM][2], b[TN][2];
+    f32x4 a[TM];
+    f32x4 bq[BL == B_KC ? TN : 1];  // B^T quads
+    float b[TN][2];                 // B [K][N]: the two k of the lane's half
   };
   const int slot_sw = (r32 >> 2) & 3;  // the rows a lane reads differ by multiples of 32: one swizzle
-  auto read = [&](int kt, int q, Frag& f) __attribute__((always_inline)) {
+  // fragment r of k quad q of stage kt: r < TM an A fragment, else B fragment r - TM
+  auto read_frag = [&](int kt, int q, int r, Frag& f) __attribute__((always_inline)) {
     const char* st = smem + (kt % STAGES) * STAGE;
     const int slot = q ^ slot_sw;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(st + (wm * (BM / WM) + i * 32 + r32) * 64 + slot * 16);
-      f.a[i][0] = h ? v[1] : v[0];
-      f.a[i][1] = h ? v[3] : v[2];
-    }
-#pragma unroll
-    for (int jn = 0; jn < TN; ++jn) {
+    if (r < TM) {
+      const int i = r;
+      f.a[i] = *reinterpret_cast<const f32x4*>(st + (wm * (BM / WM) + i * 32 + r32) * 64 + slot * 16);
+    } else {
+      const int jn = r - TM;
       const int n = wn * (BN / WN) + jn * 32 + r32;
       if constexpr (BL == B_KC) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(st + A_BYTES + n * 64 + slot * 16);
-        f.b[jn][0] = h ? v[1] : v[0];
-        f.b[jn][1] = h ? v[3] : v[2];
+        f.bq[jn] = *reinterpret_cast<const f32x4*>(st + A_BYTES + n * 64 + slot * 16);
       } else {
         const float* bs = reinterpret_cast<const float*>(st + A_BYTES) + (4 * q + h) * BN + n;
         f.b[jn][0] = bs[0];
@@ -256,17 +260,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
       }
     }
   };
-  auto mma = [&](const Frag& f) __attribute__((always_inline)) {
+  auto read = [&](int kt, int q, Frag& f) __attribute__((always_inline)) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int jn = 0; jn < TN; ++jn)
-          acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][s], f.b[jn][s], acc[i][jn], 0, 0, 0);
+    for (int r = 0; r < TM + TN; ++r) read_frag(kt, q, r, f);
   };
-  // MFMAs per k quad, fragment read instructions per k quad
-  constexpr int NM = 2 * TM * TN, RD = TM + (BL == B_KC ? TN : 2 * TN);
+  constexpr int NM = 2 * TM * TN;  // MFMAs per k quad
+  constexpr int NR = TM + TN;      // fragment reads per k quad
 
   const int KT = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
   // prologue: stages 0 .. S-2 (a stage past KT reads only zero pages)
@@ -275,37 +274,56 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
   wait_vm<G * (STAGES - 2)>();  // stage 0 landed
   __builtin_amdgcn_s_barrier();
   Frag cur, nxt;
-  if (KT > 0) read(0, 0, cur);
-  // one stage: stage kt+1 retired for every wave (counted wait + barrier),
+  read(0, 0, cur);
+  // One stage: stage kt+1 retired for every wave (counted wait + barrier),
   // which also frees the slot of stage kt-1 for the DMA of stage kt+S-1;
-  // then KQ k quads of MFMAs, each with the next quad's reads (the next
-  // stage's first quad after the last) in its shadow
+  // then KQ k quads of NM MFMAs, each with the next quad's fragment reads
+  // (the next stage's first quad after the last) in its shadow. The stage's
+  // G DMA pieces are spread over the quads (each costs ~60 issue cycles when
+  // issued back to back) and, inside a quad, alternate with the MFMAs
+  // (sched_group_barrier), as do the fragment reads. A stage past KT reads a
+  // slot with no live data: those values feed no MFMA.
   auto stage = [&](int kt, auto do_issue) __attribute__((always_inline)) {
     constexpr bool ISSUE = decltype(do_issue)::value;
     if (kt + STAGES - 2 < KT) wait_vm<G * (STAGES - 3)>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
+    const int slot_next = (kt + STAGES - 1) % STAGES;
+    static_for<KQ>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      // DMA pieces [p0, p1) go with quad j
+      constexpr int p0 = ISSUE ? (G * j) / KQ : 0, p1 = ISSUE ? (G * (j + 1)) / KQ : 0;
+      constexpr int NP = p1 - p0;
+      if constexpr (j + 1 < KQ) read(kt, j + 1, nxt);
+      else read(kt + 1, 0, nxt);
+      static_for<NP>([&](auto pc) __attribute__((always_inline)) {
+        issue_piece(slot_next, p0 + decltype(pc)::value);
+      });
 #pragma unroll
-    for (int j = 0; j < KQ; ++j) {
-      if (j + 1 < KQ) read(kt, j + 1, nxt);
-      else if (kt + 1 < KT) read(kt + 1, 0, nxt);
-      if (ISSUE && j == 0) issue((kt + STAGES - 1) % STAGES);
-      mma(cur);
-      // spread the stage's DMA (first pair only) and the next pair's reads
-      // between the MFMAs: MFMA, load, MFMA, load, ... then the rest
-      static_for<NM>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        __builtin_amdgcn_sched_group_barrier(f32core::kSchedMfma, 1, 0);
-        if constexpr (ISSUE) {
-          if (j == 0 && q < G) __builtin_amdgcn_sched_group_barrier(f32core::kSchedVmemRead, 1, 0);
-          else if (j == 0 && q < G + RD) __builtin_amdgcn_sched_group_barrier(f32core::kSchedDsRead, 1, 0);
-          else if (j != 0 && q < RD) __builtin_amdgcn_sched_group_barrier(f32core::kSchedDsRead, 1, 0);
-        } else {
-          if (q < RD) __builtin_amdgcn_sched_group_barrier(f32core::kSchedDsRead, 1, 0);
+      for (int sk = 0; sk < 2; ++sk) {
+        float av[TM], bv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) av[i] = h ? cur.a[i][2 * sk + 1] : cur.a[i][2 * sk];
+#pragma unroll
+        for (int jn = 0; jn < TN; ++jn) {
+          if constexpr (BL == B_KC) bv[jn] = h ? cur.bq[jn][2 * sk + 1] : cur.bq[jn][2 * sk];
+          else bv[jn] = cur.b[jn][sk];
         }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int jn = 0; jn < TN; ++jn)
+            acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[jn], acc[i][jn], 0, 0, 0);
+      }
+      // MFMA, DMA piece, MFMA, DMA piece, ..., then MFMA, read, MFMA, read, ...
+      static_for<NM>([&](auto xc) __attribute__((always_inline)) {
+        constexpr int x = decltype(xc)::value;
+        __builtin_amdgcn_sched_group_barrier(f32core::kSchedMfma, 1, 0);
+        if constexpr (x < NP) __builtin_amdgcn_sched_group_barrier(f32core::kSchedVmemRead, 1, 0);
+        else if constexpr (x < NP + NR) __builtin_amdgcn_sched_group_barrier(f32core::kSchedDsRead, 1, 0);
       });
       cur = nxt;
-    }
+    });
   };
   int kt = 0;
   for (; kt + STAGES - 1 < KT; ++kt) stage(kt, std::true_type{});

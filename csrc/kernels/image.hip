@@ -1,6 +1,11 @@
 // Image resize kernels (NHWC) for the image-scoring preprocessing graphs
 // (TF ResizeBilinear / ResizeNearestNeighbor semantics, incl. align_corners
-// and half_pixel_centers).
+// and half_pixel_centers), and the batched ragged pre-stage of the reference's
+// JPEG scoring graph (read_image.py:35-75: decode -> cast -> resize -> central
+// crop -> mean subtraction, one image per row): every decoded image of a
+// map_rows chunk in ONE ragged uint8 buffer, one kernel producing the
+// [rows, h, w, C] float batch the CNN reads (instead of a short program per
+// row).
 //
 // One thread per output pixel x 4 channels: the 2 (nearest: 1) source rows
 // are read as contiguous channel runs, so loads coalesce along C.
@@ -15,6 +20,14 @@ namespace {
 
 __device__ __forceinline__ float src_coord(int64_t dst, float scale, int mode) {
   return mode == 2 ? ((float)dst + 0.5f) * scale - 0.5f : (float)dst * scale;
+}
+
+// the bilinear blend shared by both resize paths (one expression: one rounding
+// / contraction pattern for both)
+__device__ __forceinline__ float bilerp(float tl, float tr, float bl, float br, float lx, float ly) {
+  const float top = tl + (tr - tl) * lx;
+  const float bot = bl + (br - bl) * lx;
+  return top + (bot - top) * ly;
 }
 
 template <typename T>
@@ -37,9 +50,45 @@ __global__ __launch_bounds__(256) void resize_bilinear_kernel(ResizeArgs a, int6
     const T* base = x + nn * a.H * a.W * a.C + c;
     const float tl = (float)base[(y0 * a.W + x0) * a.C], tr = (float)base[(y0 * a.W + x1) * a.C];
     const float bl = (float)base[(y1 * a.W + x0) * a.C], br = (float)base[(y1 * a.W + x1) * a.C];
-    const float top = tl + (tr - tl) * lx;
-    const float bot = bl + (br - bl) * lx;
-    y[i] = top + (bot - top) * ly;
+    y[i] = bilerp(tl, tr, bl, br, lx, ly);
+  }
+}
+
+// one output element (image n, crop row yy, col xx, channel c) of the
+// batched pre-stage: the bilinear sample of the resized image at
+// (oy + yy, ox + xx), computed exactly as resize_bilinear_kernel does on the
+// cast image (so a batch equals the per-row program bit for bit), then the
+// elementwise steps in graph order
+__global__ __launch_bounds__(256) void ragged_prep_kernel(RaggedPrepArgs a, int64_t total) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c = (int)(i % a.C);
+    int64_t t = i / a.C;
+    const int xx = (int)(t % a.w);
+    t /= a.w;
+    const int yy = (int)(t % a.h);
+    const int64_t nn = t / a.h;
+    const int64_t H = a.hw[2 * nn], W = a.hw[2 * nn + 1];
+    const float sh = (a.mode == 1 && a.OH > 1) ? float(H - 1) / float(a.OH - 1) : float(H) / float(a.OH);
+    const float sw = (a.mode == 1 && a.OW > 1) ? float(W - 1) / float(a.OW - 1) : float(W) / float(a.OW);
+    const float iy = src_coord(a.oy + yy, sh, a.mode), ix = src_coord(a.ox + xx, sw, a.mode);
+    const float fy = floorf(iy), fx = floorf(ix);
+    const int64_t y0 = max((int64_t)fy, (int64_t)0), y1 = min((int64_t)ceilf(iy), H - 1);
+    const int64_t x0 = max((int64_t)fx, (int64_t)0), x1 = min((int64_t)ceilf(ix), W - 1);
+    const float ly = iy - fy, lx = ix - fx;
+    const uint8_t* base = a.x + a.offs[nn] + c;
+    const float tl = (float)base[(y0 * W + x0) * a.C], tr = (float)base[(y0 * W + x1) * a.C];
+    const float bl = (float)base[(y1 * W + x0) * a.C], br = (float)base[(y1 * W + x1) * a.C];
+    float v = bilerp(tl, tr, bl, br, lx, ly);
+    for (int q = 0; q < a.nops; ++q) {
+      const float k = a.op_val[q][a.op_chan[q] ? c : 0];
+      switch (a.op_kind[q]) {
+        case 0: v = v + k; break;
+        case 1: v = v - k; break;
+        default: v = v * k; break;
+      }
+    }
+    a.y[i] = v;
   }
 }
 
@@ -88,6 +137,15 @@ void resize_bilinear(DType dt, const ResizeArgs& a, hipStream_t s) {
     default: TFA_CHECK(false, "resize_bilinear: dtype ", dtype_name(dt), " not supported");
   }
   TFA_LAUNCH_CHECK("resize_bilinear");
+}
+
+void ragged_image_prep(const RaggedPrepArgs& a, hipStream_t s) {
+  const int64_t total = a.n * a.h * a.w * a.C;
+  if (total <= 0) return;
+  TFA_CHECK(a.C >= 1 && a.C <= 4 && a.nops >= 0 && a.nops <= 4 && a.OH > 0 && a.OW > 0, "ragged_image_prep: bad args");
+  TFA_CHECK(a.oy >= 0 && a.ox >= 0 && a.oy + a.h <= a.OH && a.ox + a.w <= a.OW, "ragged_image_prep: crop outside");
+  hipLaunchKernelGGL(ragged_prep_kernel, dim3(ew_grid(total)), dim3(256), 0, s, a, total);
+  TFA_LAUNCH_CHECK("ragged_image_prep");
 }
 
 void resize_nearest(int64_t elem_size, const ResizeArgs& a, hipStream_t s) {

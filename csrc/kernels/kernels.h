@@ -255,6 +255,23 @@ struct ResizeArgs {
 };
 void resize_bilinear(DType dt, const ResizeArgs& a, hipStream_t s);  // output f32
 void resize_nearest(int64_t elem_size, const ResizeArgs& a, hipStream_t s);
+// batched ragged image pre-stage: n uint8 HWC images of their own sizes (byte
+// offsets offs[n], (H, W) pairs hw[2n]) -> f32 [n, h, w, C]: bilinear resize
+// to OH x OW (mode 0 default, 1 align_corners, 2 half_pixel_centers), crop at
+// (oy, ox), then up to 4 elementwise steps (0 add, 1 sub, 2 mul; a scalar or
+// per-channel constant)
+struct RaggedPrepArgs {
+  int64_t n = 0;
+  int C = 3, OH = 0, OW = 0, oy = 0, ox = 0, h = 0, w = 0, mode = 0;
+  int nops = 0;
+  int op_kind[4] = {0, 0, 0, 0}, op_chan[4] = {0, 0, 0, 0};
+  float op_val[4][4] = {};
+  const uint8_t* x = nullptr;
+  const int64_t* offs = nullptr;
+  const int32_t* hw = nullptr;
+  float* y = nullptr;
+};
+void ragged_image_prep(const RaggedPrepArgs& a, hipStream_t s);
 // ------------------------------------------------------------ wider op set (extra.hip)
 // Pad / PadV2 (mode 0, constant = cbits reinterpreted as the element) and
 // MirrorPad (mode 1 REFLECT, 2 SYMMETRIC); in_strides in elements

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("kind", choices=["gemm", "conv"])
     ap.add_argument("dims", nargs="+")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tb", action="store_true", help="gemm: B given as [N][K] (transpose_b)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
@@ -31,7 +32,9 @@ def main():
         m, n, k = map(int, a.dims)
         with g.as_default():
             x = tf.placeholder(tf.float32, [None, k], name="x")
-            tf.identity(tf.matmul(x, tf.constant(rng.standard_normal((k, n)).astype(np.float32))), name="y")
+            wshape = (n, k) if a.tb else (k, n)
+            tf.identity(tf.matmul(x, tf.constant(rng.standard_normal(wshape).astype(np.float32)), transpose_b=a.tb),
+                        name="y")
         xin = torch.randn((m, k), device=dev)
         fl = 2.0 * m * n * k
     else:
@@ -61,7 +64,7 @@ def main():
     ev[1].record()
     torch.cuda.synchronize()
     ms = ev[0].elapsed_time(ev[1]) / a.iters
-    print(json.dumps({"kind": a.kind, "dims": a.dims, "tile": os.environ.get("TFA_GEMM_TILE"), "ms": ms,
+    print(json.dumps({"kind": a.kind + ("_tb" if a.tb else ""), "dims": a.dims, "tile": os.environ.get("TFA_GEMM_TILE"), "ms": ms,
                       "tflops": fl / ms / 1e9}), flush=True)
 
 

@@ -18,11 +18,12 @@ step() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop after $name rc=$rc"; exit $rc; fi
 }
 step g2_tests 400 python -u -m pytest tests/test_gpu_g2.py tests/test_gpu_precision.py -x -q --timeout 300 --timeout-method thread
-for t in ${TILES:-20 21 22 23 24}; do
+for t in ${TILES:-21 22 24}; do
   TFA_GEMM_TILE=$t step "ab_4096_t$t" 120 python scripts/gemm_one.py gemm 4096 4096 4096 --iters 30
+  TFA_GEMM_TILE=$t step "ab_4096tb_t$t" 120 python scripts/gemm_one.py gemm 4096 4096 4096 --iters 30 --tb
   TFA_GEMM_TILE=$t step "ab_8192_t$t" 120 python scripts/gemm_one.py gemm 8192 8192 8192 --iters 10
 done
-for t in 13 20 22 23; do
+for t in 13 22 24; do
   TFA_GEMM_TILE=$t step "ab_head_t$t" 120 python scripts/gemm_one.py gemm 2500000 512 512 --iters 20
 done
 for t in 8 16 23 24; do

@@ -54,6 +54,10 @@ class Config:
     map_rows_vectorize: bool = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_VECTORIZE", True, bool))
     # map_rows batch-of-one cut: rows whose cut tensors are concatenated into one batched run
     map_rows_batch_rows: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_BATCH", 64, int))
+    # map_rows image scoring: the per-row decode -> resize -> crop -> normalise
+    # part of a chunk runs as ONE ragged-batch kernel (core._ImagePrep)
+    map_rows_batched_prestage: bool = dataclasses.field(
+        default_factory=lambda: _env("TFA_MAP_ROWS_BATCHED_PRESTAGE", True, bool))
     # re-runs of a partition task after a runtime (non-validation) failure; 0 = fail fast
     task_retries: int = dataclasses.field(default_factory=lambda: _env("TFA_TASK_RETRIES", 0, int))
     # timeout of one collective (RCCL, one-shot, shared memory, gloo): past it

@@ -630,6 +630,146 @@ def _host_contents(spec: GraphSpec, host) -> List[str]:
     return [g.node_inputs(hf.node)[0].split(":")[0] for hf in host]
 
 
+class _ImagePrep:
+    """The per-row part of the reference's JPEG scoring graph, recognised and
+    run for a whole chunk of rows at once (reference
+    src/main/python/tensorframes_snippets/read_image.py:35-75): decoded uint8
+    image -> Cast float -> ResizeBilinear (const size) -> Slice (central crop)
+    -> up to 4 Add / Sub / Mul by a constant -> ExpandDims(0), the row's cut
+    tensor. The decoded images of a chunk (each its own H x W) are packed into
+    one page-locked buffer, copied in one DMA, and ONE kernel
+    (kernels/image.hip ragged_prep_kernel) writes the [rows, h, w, C] batch
+    the CNN reads, with the same arithmetic as the per-row ops (bit-identical
+    results)."""
+
+    def __init__(self, C, OH, OW, mode, oy, ox, h, w, ops):
+        self.C, self.OH, self.OW, self.mode = C, OH, OW, mode
+        self.oy, self.ox, self.h, self.w, self.ops = oy, ox, h, w, ops
+        self._inflight: List[tuple] = []  # (event, pinned buffer) of copies not yet known done
+
+    def run(self, imgs, dev) -> torch.Tensor:
+        arrs = [np.asarray(t) for t in imgs]
+        for a in arrs:
+            _check(a.ndim == 3 and a.shape[2] == self.C and a.dtype == np.uint8,
+                   f"image pre-stage: decoded image of shape {a.shape} / {a.dtype}, [H, W, {self.C}] uint8 expected")
+        sizes = np.array([a.size for a in arrs], dtype=np.int64)
+        offs = np.zeros(len(arrs), dtype=np.int64)
+        np.cumsum(sizes[:-1], out=offs[1:])
+        hw = np.array([[a.shape[0], a.shape[1]] for a in arrs], dtype=np.int32)
+        total = int(sizes.sum())
+        # meta (offsets, sizes) and pixels in one page-locked buffer, one DMA
+        mbytes = offs.nbytes + hw.nbytes
+        buf = _C.empty_pinned([mbytes + total], torch.uint8)
+        hb = buf.numpy()
+        hb[:offs.nbytes] = offs.view(np.uint8)
+        hb[offs.nbytes:mbytes] = hw.reshape(-1).view(np.uint8)
+        np.concatenate([a.reshape(-1) for a in arrs], out=hb[mbytes:])
+        d = engine.device_empty(mbytes + total, torch.uint8, dev)
+        d.copy_(buf, non_blocking=True)
+        # the pinned buffer returns to its pool only once its DMA has run
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self._inflight = [(e, b) for e, b in self._inflight if not e.query()] + [(ev, buf)]
+        doffs = d[:offs.nbytes].view(torch.int64)
+        dhw = d[offs.nbytes:mbytes].view(torch.int32)
+        return _C.ragged_image_prep(d[mbytes:], doffs, dhw, self.C, self.OH, self.OW, self.mode, self.oy, self.ox,
+                                    self.h, self.w, self.ops)
+
+
+def _match_image_prep(graph_bytes: bytes, row_feeds: List[str], cut: str) -> Optional[_ImagePrep]:
+    """The chain feed -> cut as an _ImagePrep, or None when it is anything else."""
+    if len(row_feeds) != 1:
+        return None
+    try:
+        light = P.parse_graphdef(_C.light_graphdef(graph_bytes, 4096))
+    except Exception:  # noqa: BLE001 - not recognisable: the per-row path stays
+        return None
+    by_name = {nd.name: nd for nd in light.node}
+    consumers: Dict[str, List[str]] = {}
+    for nd in light.node:
+        for i in nd.input:
+            consumers.setdefault(i.split(":")[0].lstrip("^"), []).append(nd.name)
+
+    def const(name):
+        nd = by_name.get(name.split(":")[0])
+        if nd is None or nd.op != "Const" or "value" not in nd.attr:
+            return None
+        try:
+            return nd.attr["value"].value.to_numpy()
+        except Exception:  # noqa: BLE001
+            return None
+
+    def attr_b(nd, k):
+        a = nd.attr.get(k)
+        return bool(a.value) if a is not None else False
+
+    cur = row_feeds[0].split(":")[0]
+    size = crop = None
+    mode, C, ops, saw_cast = 0, None, [], False
+    while cur != cut:
+        nxt = consumers.get(cur, [])
+        if len(nxt) != 1:
+            return None
+        nd = by_name[nxt[0]]
+        ins = [i.split(":")[0] for i in nd.input if not i.startswith("^")]
+        if not ins or ins[0] != cur and nd.op not in ("Add", "AddV2", "Sub", "Mul"):
+            return None
+        if nd.op == "Cast":
+            if saw_cast or nd.attr.get("DstT") is None or nd.attr["DstT"].value != D.DT_FLOAT:
+                return None
+            saw_cast = True
+        elif nd.op == "ExpandDims":
+            dim = const(nd.input[1])
+            if dim is None or int(np.asarray(dim).reshape(-1)[0]) != 0:
+                return None
+        elif nd.op == "Squeeze":
+            a = nd.attr.get("squeeze_dims")
+            if a is None or list(a.value.get("i", [])) not in ([0],):
+                return None
+        elif nd.op == "ResizeBilinear":
+            if not saw_cast or size is not None or crop is not None:
+                return None
+            sz = const(nd.input[1])
+            if sz is None or np.asarray(sz).size != 2:
+                return None
+            size = [int(v) for v in np.asarray(sz).reshape(-1)]
+            align, half = attr_b(nd, "align_corners"), attr_b(nd, "half_pixel_centers")
+            mode = 1 if align else (2 if half else 0)
+        elif nd.op == "Slice":
+            b, sz = const(nd.input[1]), const(nd.input[2])
+            if size is None or crop is not None or ops or b is None or sz is None:
+                return None
+            b, sz = [int(v) for v in np.asarray(b).reshape(-1)], [int(v) for v in np.asarray(sz).reshape(-1)]
+            if len(b) != 3 or len(sz) != 3 or b[2] != 0 or sz[0] < 0 or sz[1] < 0:
+                return None
+            crop = (b[0], b[1], sz[0], sz[1])
+            if sz[2] >= 0:
+                C = sz[2]
+        elif nd.op in ("Add", "AddV2", "Sub", "Mul"):
+            other = [i for i in ins if i != cur]
+            if len(ins) != 2 or len(other) != 1 or (nd.op == "Sub" and ins[0] != cur):
+                return None
+            v = const(other[0])
+            if v is None or crop is None or len(ops) == 4 or np.asarray(v).dtype != np.float32:
+                return None
+            v = np.asarray(v, dtype=np.float32).reshape(-1)
+            if v.size > 4:
+                return None
+            ops.append((0 if nd.op in ("Add", "AddV2") else 1 if nd.op == "Sub" else 2, [float(x) for x in v]))
+        else:
+            return None
+        cur = nd.name
+    if size is None or crop is None:
+        return None
+    C = C or max([len(v) for _, v in ops] + [3])
+    if any(len(v) not in (1, C) for _, v in ops):
+        return None
+    oy, ox, h, w = crop
+    if oy + h > size[0] or ox + w > size[1]:
+        return None
+    return _ImagePrep(C, size[0], size[1], mode, oy, ox, h, w, ops)
+
+
 class _BatchCut:
     """map_rows fast path for per-row graphs that build a batch of one
     (`expand_dims(preprocessed_image, 0)` -> CNN, the reference's read_image
@@ -648,6 +788,7 @@ class _BatchCut:
         self.graph_bytes, self.fetch_refs, self.row_feeds = graph_bytes, list(fetch_refs), list(row_feeds)
         self.cut = None
         self.modes: List[str] = []
+        self.image_prep: Optional[_ImagePrep] = None
         self._side: Dict[int, Any] = {}
         try:
             self._find()
@@ -777,6 +918,7 @@ class _BatchCut:
         self.modes = modes
         self.pre = engine.program(self.graph_bytes, [node + ":0"], self.row_feeds)
         self.post = prog
+        self.image_prep = _match_image_prep(self.graph_bytes, self.row_feeds, node)
         return True
 
     def run(self, nrows: int, row_inputs, dev, per_out) -> None:
@@ -792,10 +934,23 @@ class _BatchCut:
             if side is None:
                 side = self._side[dev.index] = torch.cuda.Stream(dev)
         step = max(1, int(config.map_rows_batch_rows))
+        prep = self.image_prep if (dev.type == "cuda" and config.map_rows_batched_prestage) else None
         for a in range(0, nrows, step):
             rows = range(a, min(nrows, a + step))
             cut = []
-            for i in rows:
+            if prep is not None:
+                # the whole chunk's pre-stage in one kernel: every decoded
+                # image in ONE pinned ragged buffer, one copy, one launch
+                t0 = time.perf_counter()
+                imgs = [row_inputs(i)[0] for i in rows]
+                t1 = time.perf_counter()
+                with torch.cuda.stream(side):
+                    cut = [prep.run(imgs, dev)]
+                engine.record_stream(cut[0], main)
+                t_in += t1 - t0
+                t_pre += time.perf_counter() - t1
+                metrics.add("map_rows_batched_prestage_rows", len(imgs))
+            for i in (rows if prep is None else ()):
                 t0 = time.perf_counter()
                 feeds = row_inputs(i)
                 t1 = time.perf_counter()

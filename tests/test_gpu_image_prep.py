@@ -1,0 +1,83 @@
+"""The batched image pre-stage of map_rows image scoring (core._ImagePrep,
+kernels/image.hip ragged_prep_kernel): the reference's JPEG scoring graph
+(src/main/python/tensorframes_snippets/read_image.py:35-75, one image per row)
+run with the per-row pre-program and with the ragged-batch kernel must give
+bit-identical top-k values and indices; the kernel alone against the per-image
+CPU-oracle ops (Cast -> ResizeBilinear -> Slice -> Sub) on images of mixed
+sizes and every resize mode."""
+import io
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import tensorframes_amd as tfs  # noqa: E402
+from tensorframes_amd import Row, engine, tf  # noqa: E402
+from tensorframes_amd._native import _C  # noqa: E402
+from tensorframes_amd.models import cnn  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def _jpegs(n, rng):
+    from PIL import Image
+    out = []
+    for _ in range(n):
+        h, w = rng.integers(60, 160, 2)
+        buf = io.BytesIO()
+        Image.fromarray(rng.integers(0, 255, (h, w, 3), dtype=np.uint8)).save(buf, format="JPEG", quality=90)
+        out.append(bytearray(buf.getvalue()))
+    return out
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_ragged_kernel_matches_per_image_ops(mode):
+    rng = np.random.default_rng(mode)
+    imgs = [rng.integers(0, 255, (int(h), int(w), 3), dtype=np.uint8) for h, w in rng.integers(20, 90, (7, 2))]
+    OH, OW, oy, ox, h, w = 48, 40, 4, 3, 40, 33
+    mean = [10.5, -3.25, 100.0]
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.uint8, [None, None, 3], name="x")
+        y = tf.cast(x, tf.float32)
+        y = tf.image.resize_bilinear(tf.expand_dims(y, 0), [OH, OW], align_corners=mode == 1,
+                                     half_pixel_centers=mode == 2)
+        y = tf.slice(tf.squeeze(y, [0]), [oy, ox, 0], [h, w, -1])
+        tf.multiply(tf.subtract(y, tf.constant(np.array(mean, np.float32))), 0.5, name="out")
+    prog = engine.program(g.serialize(), ["out"], ["x"])
+    want = [engine.run_program(prog, [torch.from_numpy(a)], DEV)[0].cpu() for a in imgs]
+    sizes = np.array([a.size for a in imgs])
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)).to(DEV)
+    hw = torch.tensor([[a.shape[0], a.shape[1]] for a in imgs], dtype=torch.int32, device=DEV)
+    data = torch.from_numpy(np.concatenate([a.reshape(-1) for a in imgs])).to(DEV)
+    got = _C.ragged_image_prep(data, offs, hw, 3, OH, OW, mode, oy, ox, h, w, [(1, mean), (2, [0.5])]).cpu()
+    assert got.shape == (len(imgs), h, w, 3)
+    for i, wnt in enumerate(want):
+        assert torch.equal(got[i], wnt), f"image {i}: max diff {(got[i] - wnt).abs().max().item()}"
+
+
+def test_batched_prestage_equals_per_row_scoring():
+    rng = np.random.default_rng(5)
+    jpgs = _jpegs(70, rng)
+    df = tfs.create_dataframe([Row(uri=f"img{i}", image_data=b) for i, b in enumerate(jpgs)], num_partitions=1)
+    g = cnn.jpeg_scoring_graph("vgg16", contents=bytes(jpgs[0]), width=0.125)
+    res = {}
+    for on in (False, True):
+        tfs.set_config(map_rows_batched_prestage=on)
+        tfs.metrics.reset()
+        with g.as_default():
+            pred = tfs.map_rows(["index", "value"], df, feed_dict={"DecodeJpeg/contents": "image_data"})
+            rows = pred.select("uri", "index", "value").collect()
+        res[on] = rows
+        batched = tfs.metrics.snapshot().get("map_rows_batched_prestage_rows", 0)
+        assert (batched == len(jpgs)) == on
+    tfs.set_config(map_rows_batched_prestage=True)
+    for a, b in zip(res[False], res[True]):
+        assert a.uri == b.uri
+        assert list(a["index"]) == list(b["index"])
+        assert np.array_equal(np.asarray(a["value"]), np.asarray(b["value"]))
