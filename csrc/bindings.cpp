@@ -13,6 +13,7 @@
 #include "runtime/device_pool.h"
 #include "runtime/executor.h"
 #include "runtime/jit.h"
+#include "runtime/jpeg_decode.h"
 
 namespace py = pybind11;
 using namespace tfa;
@@ -414,6 +415,95 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, py::arg("offsets"), py::arg("data"), py::arg("words"),
         "string keys -> [words + 1, n] int64: big-endian 8-byte words (sign-flipped) + byte length; signed order "
         "of the columns = lexicographic order of the strings");
+  m.def("string_key_hash", [](const at::Tensor& offsets, const at::Tensor& data) {
+    TFA_CHECK(offsets.scalar_type() == at::kLong && offsets.dim() == 1 && offsets.size(0) >= 1,
+              "string_key_hash: offsets must be int64[n+1]");
+    TFA_CHECK(data.scalar_type() == at::kByte && data.dim() == 1, "string_key_hash: data must be uint8[bytes]");
+    TFA_CHECK(offsets.device() == data.device(), "string_key_hash: offsets and data on different devices");
+    const int64_t n = offsets.size(0) - 1;
+    at::Tensor oc = offsets.contiguous(), dc = data.contiguous();
+    if (!oc.is_cuda()) {
+      at::Tensor out = at::empty({2, n}, oc.options());
+      const int64_t* o = oc.data_ptr<int64_t>();
+      const uint8_t* d = dc.data_ptr<uint8_t>();
+      int64_t* y = out.data_ptr<int64_t>();
+      for (int64_t i = 0; i < n; ++i) {
+        const int64_t a = o[i], len = o[i + 1] - a;
+        uint64_t v = 0;
+        for (int b = 0; b < 8; ++b) v |= static_cast<uint64_t>(b < len ? d[a + b] : 0) << (56 - 8 * b);
+        y[i] = static_cast<int64_t>(v ^ 0x8000000000000000ull);
+        y[n + i] = len > 8 ? static_cast<int64_t>(k::string_key_hash_host(d + a, len) + 9) : len;
+      }
+      return out;
+    }
+    c10::hip::HIPGuard guard(oc.device().index());
+    at::Tensor out = pool_empty({2, n}, oc.options());
+    k::string_key_hash(oc.data_ptr<int64_t>(), dc.data_ptr<uint8_t>(), n, out.data_ptr<int64_t>(),
+                   c10::hip::getCurrentHIPStream(oc.device().index()).stream());
+    return out;
+  }, py::arg("offsets"), py::arg("data"),
+        "bounded-width string keys -> [2, n] int64: sign-flipped big-endian word 0, tag = length for keys of "
+        "<= 8 bytes, else 9 + a 62-bit hash of the whole key");
+  m.def("string_verify", [](const at::Tensor& offsets, const at::Tensor& data, const at::Tensor& ids,
+                            const at::Tensor& rep) {
+    TFA_CHECK(offsets.scalar_type() == at::kLong && ids.scalar_type() == at::kLong && rep.scalar_type() == at::kLong,
+              "string_verify: int64 offsets / ids / representatives");
+    const int64_t n = offsets.size(0) - 1;
+    TFA_CHECK(ids.dim() == 1 && ids.size(0) == n, "string_verify: one id per string");
+    TFA_CHECK(offsets.device() == data.device() && ids.device() == data.device() && rep.device() == data.device(),
+              "string_verify: tensors on different devices");
+    at::Tensor oc = offsets.contiguous(), dc = data.contiguous(), ic = ids.contiguous(), rc = rep.contiguous();
+    if (!oc.is_cuda()) {
+      const int64_t* o = oc.data_ptr<int64_t>();
+      const uint8_t* d = dc.data_ptr<uint8_t>();
+      const int64_t* id = ic.data_ptr<int64_t>();
+      const int64_t* r = rc.data_ptr<int64_t>();
+      for (int64_t i = 0; i < n; ++i) {
+        const int64_t a = o[i], len = o[i + 1] - a, q = r[id[i]];
+        if (len <= 8 || q == i) continue;
+        if (o[q + 1] - o[q] != len || std::memcmp(d + a, d + o[q], len) != 0) return false;
+      }
+      return true;
+    }
+    c10::hip::HIPGuard guard(oc.device().index());
+    hipStream_t st = c10::hip::getCurrentHIPStream(oc.device().index()).stream();
+    at::Tensor flag = pool_empty({1}, oc.options().dtype(at::kInt));
+    TFA_CHECK(hipMemsetAsync(flag.data_ptr(), 0, sizeof(int), st) == hipSuccess, "string_verify: memset failed");
+    k::string_verify(oc.data_ptr<int64_t>(), dc.data_ptr<uint8_t>(), ic.data_ptr<int64_t>(), rc.data_ptr<int64_t>(), n,
+                     flag.data_ptr<int>(), st);
+    return flag.item<int>() == 0;
+  }, "True when every string equals its group representative's (no hash collision)");
+  m.def("gather_strings", [](const at::Tensor& offsets, const at::Tensor& data, const at::Tensor& idx) {
+    // rows idx of a device string column -> (host offsets [n+1], device bytes)
+    TFA_CHECK(offsets.is_cuda() && data.is_cuda() && idx.is_cuda() && offsets.scalar_type() == at::kLong &&
+                  idx.scalar_type() == at::kLong && data.scalar_type() == at::kByte,
+              "gather_strings: device int64 offsets / idx and uint8 data expected");
+    c10::hip::HIPGuard guard(data.device().index());
+    hipStream_t st = c10::hip::getCurrentHIPStream(data.device().index()).stream();
+    at::Tensor oc = offsets.contiguous(), ic = idx.contiguous(), dc = data.contiguous();
+    const int64_t n = ic.numel();
+    at::Tensor lens = pool_empty({std::max<int64_t>(n, 1)}, oc.options());
+    k::string_lens(oc.data_ptr<int64_t>(), ic.data_ptr<int64_t>(), n, lens.data_ptr<int64_t>(), st);
+    at::Tensor new_offs = at::empty({n + 1}, at::TensorOptions().dtype(at::kLong));
+    int64_t* no = new_offs.data_ptr<int64_t>();
+    no[0] = 0;
+    if (n) {
+      std::vector<int64_t> lh(n);
+      TFA_CHECK(hipMemcpyAsync(lh.data(), lens.data_ptr(), n * sizeof(int64_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess, "gather_strings: length copy failed");
+      for (int64_t g = 0; g < n; ++g) no[g + 1] = no[g] + lh[g];
+    }
+    at::Tensor out = pool_empty({std::max<int64_t>(no[n], 1)}, dc.options());
+    if (n) {
+      at::Tensor dno = pool_empty({n + 1}, oc.options());
+      TFA_CHECK(hipMemcpyAsync(dno.data_ptr(), no, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st) == hipSuccess,
+                "gather_strings: offset copy failed");
+      k::gather_bytes(dc.data_ptr<uint8_t>(), oc.data_ptr<int64_t>(), ic.data_ptr<int64_t>(), dno.data_ptr<int64_t>(), n,
+                      out.data_ptr<uint8_t>(), st);
+      TFA_CHECK(hipStreamSynchronize(st) == hipSuccess, "gather_strings: gather failed");  // `no` is pageable
+    }
+    return py::make_tuple(new_offs, out.narrow(0, 0, no[n]));
+  }, "rows idx of a device string column -> (host int64 offsets [n+1], device uint8 bytes)");
   m.def("key_dest", [](const std::vector<at::Tensor>& keys, int64_t world) {
     TFA_CHECK(!keys.empty() && keys[0].is_cuda(), "key_dest: device key columns expected");
     c10::hip::HIPGuard guard(keys[0].device().index());
@@ -545,6 +635,60 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     c10::hip::HIPGuard guard(rec.device().index());
     k::unpack_rows(pc, rec.contiguous().data_ptr(), n, R, c10::hip::getCurrentHIPStream(rec.device().index()).stream());
   }, "records [n, R] -> the preallocated device columns (same layout as pack_rows)");
+  // native JPEG decode into one ragged (pinned) buffer (runtime/jpeg_decode.cpp)
+  struct PyJpegBatch {
+    std::vector<py::buffer_info> views;  // keep the cells' buffers exported while decoding
+    std::unique_ptr<tfa::JpegBatch> job;
+    ~PyJpegBatch() { job.reset(); }  // waits for the tasks before the views go
+  };
+  py::class_<PyJpegBatch>(m, "JpegBatch")
+      .def(py::init([](const py::list& cells, int channels, int threads, bool pinned) {
+             TFA_CHECK(channels == 1 || channels == 3, "JpegBatch: channels must be 1 or 3");
+             auto b = std::make_unique<PyJpegBatch>();
+             std::vector<std::pair<const uint8_t*, size_t>> ptrs;
+             b->views.reserve(cells.size());
+             for (auto c : cells) {
+               b->views.push_back(py::reinterpret_borrow<py::buffer>(c).request());
+               const auto& v = b->views.back();
+               ptrs.emplace_back(static_cast<const uint8_t*>(v.ptr), static_cast<size_t>(v.size * v.itemsize));
+             }
+             b->job = std::make_unique<tfa::JpegBatch>(std::move(ptrs), channels, threads, pinned);
+             return b;
+           }),
+           py::arg("cells"), py::arg("channels"), py::arg("threads"), py::arg("pinned") = true)
+      .def_property_readonly("header_ok", [](const PyJpegBatch& b) { return b.job->header_ok(); })
+      .def_property_readonly("bad_header", [](const PyJpegBatch& b) { return b.job->bad_header(); })
+      .def("wait", [](PyJpegBatch& b) {
+        py::gil_scoped_release nogil;
+        return b.job->wait();
+      }, "block until every image is decoded; returns the indices that failed")
+      .def_property_readonly("buffer", [](const PyJpegBatch& b) { return b.job->buffer(); })
+      .def_property_readonly("meta_bytes", [](const PyJpegBatch& b) { return b.job->meta_bytes(); })
+      .def_property_readonly("offsets_bytes", [](const PyJpegBatch& b) { return b.job->offsets_bytes(); })
+      .def("shape", [](const PyJpegBatch& b, int64_t i) { return b.job->shape(i); })
+      .def("pixel_offset", [](const PyJpegBatch& b, int64_t i) { return b.job->pixel_offset(i); });
+  m.def("jpeg_native_available", [] {
+    std::string why;
+    bool ok = tfa::jpeg_native_available(&why);
+    return py::make_tuple(ok, why);
+  });
+  m.def("jpeg_decode", [](const py::buffer& data, int channels) {
+    auto v = data.request();
+    tfa::JpegHeader h;
+    const auto* p = static_cast<const uint8_t*>(v.ptr);
+    size_t n = static_cast<size_t>(v.size * v.itemsize);
+    TFA_CHECK(tfa::jpeg_parse_header(p, n, &h), "jpeg_decode: not a supported JPEG");
+    at::Tensor out = at::empty({h.height, h.width, channels}, at::kByte);
+    std::string err;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = tfa::jpeg_decode_into(p, n, channels, out.data_ptr<uint8_t>(), out.numel(), &err);
+    }
+    TFA_CHECK(ok, "jpeg_decode: ", err);
+    return out;
+  }, py::arg("data"), py::arg("channels") = 3, "decode one JPEG on the calling thread (tests, tools)");
+  m.def("decode_pool_threads", &tfa::decode_pool_threads);
   m.def("ragged_image_prep", [](const at::Tensor& data, const at::Tensor& offs, const at::Tensor& hw, int C, int OH,
                                  int OW, int mode, int oy, int ox, int h, int w,
                                  const std::vector<std::pair<int, std::vector<float>>>& ops) {

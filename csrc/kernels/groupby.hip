@@ -648,6 +648,111 @@ void string_words(const int64_t* offs, const uint8_t* data, int64_t n, int W, in
   TFA_LAUNCH_CHECK("string_words");
 }
 
+// ---- bounded-width string keys: (word 0, tag) per row, 2 words whatever
+// the longest key. tag = length for keys of <= 8 bytes (exact: word 0 holds
+// all their bytes), 9 + a 62-bit hash of all the bytes (and the length) for
+// longer ones, so a long key sorts after the short key that is its 8-byte
+// prefix. Groups are verified against one representative row each
+// (string_verify); only prefix ties among long keys need an exact re-order
+// (ops/groupby.py).
+__host__ __device__ inline uint64_t skey_hash(const uint8_t* p, int64_t len) {
+  uint64_t h = 0x243F6A8885A308D3ull ^ (static_cast<uint64_t>(len) * 0x9E3779B97F4A7C15ull);
+  for (int64_t j = 0; j < len; j += 8) {
+    uint64_t k = 0;
+    const int64_t m = len - j < 8 ? len - j : 8;
+    for (int64_t b = 0; b < m; ++b) k |= static_cast<uint64_t>(p[j + b]) << (8 * b);
+    h ^= k * 0xBF58476D1CE4E5B9ull;
+    h = ((h << 27) | (h >> 37)) * 0x94D049BB133111EBull + 0x2545F4914F6CDD1Dull;
+  }
+  h ^= h >> 33;
+  h *= 0xFF51AFD7ED558CCDull;
+  h ^= h >> 33;
+  h *= 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 33;
+  return (h >> 2) + 1;
+}
+
+__global__ __launch_bounds__(kT) void string_key_hash_kernel(const int64_t* __restrict__ offs,
+                                                             const uint8_t* __restrict__ data, int64_t n,
+                                                             int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = offs[i], len = offs[i + 1] - a;
+    uint64_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v |= static_cast<uint64_t>(b < len ? data[a + b] : 0) << (56 - 8 * b);
+    out[i] = static_cast<int64_t>(v ^ 0x8000000000000000ull);
+    out[n + i] = len > 8 ? static_cast<int64_t>(skey_hash(data + a, len) + 9) : len;
+  }
+}
+
+// flag <- 1 when a row's bytes differ from its group representative's (a
+// hash collision); rows of <= 8 bytes are exact by construction
+__global__ __launch_bounds__(kT) void string_verify_kernel(const int64_t* __restrict__ offs,
+                                                           const uint8_t* __restrict__ data,
+                                                           const int64_t* __restrict__ ids,
+                                                           const int64_t* __restrict__ rep, int64_t n,
+                                                           int* __restrict__ flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = offs[i], len = offs[i + 1] - a;
+    if (len <= 8) continue;
+    const int64_t r = rep[ids[i]];
+    if (r == i) continue;
+    const int64_t ra = offs[r];
+    bool diff = offs[r + 1] - ra != len;
+    for (int64_t j = 8; j < len && !diff; ++j) diff = data[a + j] != data[ra + j];
+    if (diff) flag[0] = 1;
+  }
+}
+
+void string_key_hash(const int64_t* offs, const uint8_t* data, int64_t n, int64_t* out, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(string_key_hash_kernel, dim3(ew_grid(n)), dim3(kT), 0, s, offs, data, n, out);
+  TFA_LAUNCH_CHECK("string_key_hash");
+}
+
+void string_verify(const int64_t* offs, const uint8_t* data, const int64_t* ids, const int64_t* rep, int64_t n,
+                   int* flag, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(string_verify_kernel, dim3(ew_grid(n)), dim3(kT), 0, s, offs, data, ids, rep, n, flag);
+  TFA_LAUNCH_CHECK("string_verify");
+}
+
+uint64_t string_key_hash_host(const uint8_t* p, int64_t len) { return skey_hash(p, len); }
+
+// rows idx of a string column: one block per output string (block-stride)
+__global__ __launch_bounds__(kT) void gather_bytes_kernel(const uint8_t* __restrict__ data,
+                                                          const int64_t* __restrict__ offs,
+                                                          const int64_t* __restrict__ idx,
+                                                          const int64_t* __restrict__ new_offs, int64_t n,
+                                                          uint8_t* __restrict__ out) {
+  for (int64_t g = blockIdx.x; g < n; g += gridDim.x) {
+    const int64_t a = offs[idx[g]], len = offs[idx[g] + 1] - a, o = new_offs[g];
+    for (int64_t j = threadIdx.x; j < len; j += blockDim.x) out[o + j] = data[a + j];
+  }
+}
+
+__global__ __launch_bounds__(kT) void string_lens_kernel(const int64_t* __restrict__ offs,
+                                                         const int64_t* __restrict__ idx, int64_t n,
+                                                         int64_t* __restrict__ lens) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x)
+    lens[g] = offs[idx[g] + 1] - offs[idx[g]];
+}
+
+void string_lens(const int64_t* offs, const int64_t* idx, int64_t n, int64_t* lens, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(string_lens_kernel, dim3(ew_grid(n)), dim3(kT), 0, s, offs, idx, n, lens);
+  TFA_LAUNCH_CHECK("string_lens");
+}
+
+void gather_bytes(const uint8_t* data, const int64_t* offs, const int64_t* idx, const int64_t* new_offs, int64_t n,
+                  uint8_t* out, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(gather_bytes_kernel, dim3(static_cast<int>(std::min<int64_t>(n, 65536))), dim3(kT), 0, s, data,
+                     offs, idx, new_offs, n, out);
+  TFA_LAUNCH_CHECK("gather_bytes");
+}
+
+
 void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s) {
   if (n == 0) return;
   TFA_CHECK(world >= 1, "hash_mod: world must be >= 1");

@@ -103,6 +103,18 @@ void key_hash(DType dt, const void* keys, int64_t n, uint64_t* h, bool accumulat
 void hash_mod(const uint64_t* h, int64_t n, int64_t world, int64_t* dest, hipStream_t s);
 // string keys as W big-endian words (sign-flipped) + length, column-major [W+1][n]
 void string_words(const int64_t* offs, const uint8_t* data, int64_t n, int W, int64_t* out, hipStream_t s);
+// bounded-width string keys: [2][n] int64 = (sign-flipped big-endian word 0,
+// tag = length for keys <= 8 bytes, else 9 + 62-bit hash); string_verify sets
+// flag[0] when a row's bytes differ from its group representative's
+void string_key_hash(const int64_t* offs, const uint8_t* data, int64_t n, int64_t* out, hipStream_t s);
+void string_verify(const int64_t* offs, const uint8_t* data, const int64_t* ids, const int64_t* rep, int64_t n,
+                   int* flag, hipStream_t s);
+uint64_t string_key_hash_host(const uint8_t* p, int64_t len);  // the same hash on the host
+// rows idx of a string column: lens[g] = length of row idx[g]; gather_bytes
+// copies them to out at new_offs (the exclusive scan of lens)
+void string_lens(const int64_t* offs, const int64_t* idx, int64_t n, int64_t* lens, hipStream_t s);
+void gather_bytes(const uint8_t* data, const int64_t* offs, const int64_t* idx, const int64_t* new_offs, int64_t n,
+                  uint8_t* out, hipStream_t s);
 // ids [n] in [0, nseg) -> rows ordered by segment (stable) perm [n] and CSR
 // offsets [nseg + 1]; out-of-range ids are dropped
 size_t segment_csr_workspace_bytes(int64_t n, int64_t nseg);

@@ -1,6 +1,5 @@
 #!/bin/bash
-# round 5: batched image pre-stage + native JPEG decode (tests + read_image example),
-# the string-key GPU tests (bounded key width)
+# round 5: where the steady-state image-scoring time goes (host profile, GPU kernel stats)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/r5
@@ -10,13 +9,13 @@ step() {
   echo "== $name ($(date +%T))"
   timeout -k 10 "$secs" "$@" > "gpurun_out/r5/$name.log" 2>&1
   local rc=$?
-  tail -n 4 "gpurun_out/r5/$name.log"
+  tail -n 3 "gpurun_out/r5/$name.log"
   if grep -qiE "memory access fault|illegal address|HSA_STATUS_ERROR|core dumped" "gpurun_out/r5/$name.log"; then
     echo "GPU fault in $name"; exit 99
   fi
   if [ $rc -ne 0 ]; then echo "stop after $name rc=$rc"; exit $rc; fi
 }
-step img_tests 300 python -u -m pytest tests/test_gpu_image_prep.py tests/test_jpeg_native.py tests/test_gpu_string_keys.py -x -v -s --timeout 200 --timeout-method thread
-step read_image 400 python examples/read_image.py --images 4096
-TFA_PRECISION=bf16x3 step read_image_bf16x3 400 python examples/read_image.py --images 4096
+step img_cprofile 400 python -m cProfile -o gpurun_out/r5/img.prof examples/read_image.py --images 4096
+export TMPDIR=/tmp
+step img_rocprof 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5/prof_img -o img -- python3 examples/read_image.py --images 4096
 exit 0

@@ -58,6 +58,15 @@ class Config:
     # part of a chunk runs as ONE ragged-batch kernel (core._ImagePrep)
     map_rows_batched_prestage: bool = dataclasses.field(
         default_factory=lambda: _env("TFA_MAP_ROWS_BATCHED_PRESTAGE", True, bool))
+    # ... with its JPEG cells decoded by the native libjpeg thread pool straight
+    # into the chunk's pinned buffer (runtime/jpeg_decode.cpp), no GIL held
+    native_jpeg_decode: bool = dataclasses.field(default_factory=lambda: _env("TFA_NATIVE_JPEG", True, bool))
+    # groupBy string keys longer than 8 bytes: 2 words per row (word 0, 62-bit
+    # hash) verified per group, instead of one word per 8 bytes of the
+    # longest key + length (ops/groupby.string_key_hashed)
+    string_key_hash: bool = dataclasses.field(default_factory=lambda: _env("TFA_STRING_KEY_HASH", True, bool))
+    # threads of the native decode pool (0: min(16, CPUs available))
+    decode_threads: int = dataclasses.field(default_factory=lambda: _env("TFA_DECODE_THREADS", 0, int))
     # re-runs of a partition task after a runtime (non-validation) failure; 0 = fail fast
     task_retries: int = dataclasses.field(default_factory=lambda: _env("TFA_TASK_RETRIES", 0, int))
     # timeout of one collective (RCCL, one-shot, shared memory, gloo): past it

@@ -25,7 +25,7 @@ import torch
 from . import engine
 from ._native import _C
 from .config import config
-from .frame.block import (Block, ObjectColumn, RaggedColumn, build_column, column_tf_dtype,
+from .frame.block import (Block, ObjectColumn, RaggedColumn, StringColumn, build_column, column_tf_dtype,
                           column_values, concat_blocks, is_dense)
 from .frame.column_info import ColumnInformation, SparkTFColInfo, explain_schema
 from .frame.dataframe import DataFrame, GroupedData, _Derived, _Materialized, _sort_key
@@ -581,11 +581,17 @@ def map_rows(fetches, dframe: DataFrame, feed_dict: Optional[Dict[str, str]] = N
                 if bcut is not None and b.nrows >= 2 and any(d is None for d in done):
                     todo = [i for i in range(b.nrows) if done[i] is None]
                     sub = [[None] * len(todo) for _ in outputs]
-                    bcut.run(len(todo), lambda k: [cv[todo[k]] for cv in cell_views] +
-                             [hv[todo[k]] for hv in host_views], dev, sub)
-                    for j in range(len(outputs)):
-                        for k, i in enumerate(todo):
-                            per_out[j][i] = sub[j][k]
+                    raw = None
+                    if not cell_views and len(host_views) == 1 and isinstance(host_views[0], _LazyDecoded):
+                        raw = (host[0], [host_views[0].cells[i] for i in todo])
+                    whole = bcut.run(len(todo), lambda k: [cv[todo[k]] for cv in cell_views] +
+                                     [hv[todo[k]] for hv in host_views], dev, sub, raw=raw)
+                    if whole is not None and len(todo) == b.nrows:
+                        per_out = whole  # the chunks' batched outputs, concatenated once
+                    else:
+                        for j in range(len(outputs)):
+                            for k, i in enumerate(todo):
+                                per_out[j][i] = sub[j][k]
                     done = [True] * b.nrows
                 for i in range(b.nrows):
                     if done[i] is not None:
@@ -664,14 +670,19 @@ class _ImagePrep:
         hb[:offs.nbytes] = offs.view(np.uint8)
         hb[offs.nbytes:mbytes] = hw.reshape(-1).view(np.uint8)
         np.concatenate([a.reshape(-1) for a in arrs], out=hb[mbytes:])
-        d = engine.device_empty(mbytes + total, torch.uint8, dev)
+        return self.run_packed(buf, offs.nbytes, mbytes, dev)
+
+    def run_packed(self, buf: torch.Tensor, offs_nbytes: int, mbytes: int, dev) -> torch.Tensor:
+        """`buf` = [int64 offsets | int32 hw pairs | pixels] in pinned memory
+        (the layout _C.JpegBatch decodes into)."""
+        d = engine.device_empty(buf.numel(), torch.uint8, dev)
         d.copy_(buf, non_blocking=True)
         # the pinned buffer returns to its pool only once its DMA has run
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
         self._inflight = [(e, b) for e, b in self._inflight if not e.query()] + [(ev, buf)]
-        doffs = d[:offs.nbytes].view(torch.int64)
-        dhw = d[offs.nbytes:mbytes].view(torch.int32)
+        doffs = d[:offs_nbytes].view(torch.int64)
+        dhw = d[offs_nbytes:mbytes].view(torch.int32)
         return _C.ragged_image_prep(d[mbytes:], doffs, dhw, self.C, self.OH, self.OW, self.mode, self.oy, self.ox,
                                     self.h, self.w, self.ops)
 
@@ -921,8 +932,12 @@ class _BatchCut:
         self.image_prep = _match_image_prep(self.graph_bytes, self.row_feeds, node)
         return True
 
-    def run(self, nrows: int, row_inputs, dev, per_out) -> None:
-        """row_inputs(i) -> the per-row feed tensors; fills per_out[j][i]."""
+    def run(self, nrows: int, row_inputs, dev, per_out, raw=None) -> Optional[List[torch.Tensor]]:
+        """row_inputs(i) -> the per-row feed tensors; fills per_out[j][i] and
+        returns each output column as one [nrows, ...] tensor.
+        raw: (host feed, its undecoded cells in row order) when the one row
+        feed is an image decoder's output: the batched pre-stage then decodes
+        each chunk natively (_C.JpegBatch) while the previous chunk runs."""
         t_in = t_pre = t_post = 0.0
         # The per-row part runs on a side stream: its (pageable) input copies
         # would otherwise queue behind the previous chunk's model on the
@@ -935,10 +950,27 @@ class _BatchCut:
                 side = self._side[dev.index] = torch.cuda.Stream(dev)
         step = max(1, int(config.map_rows_batch_rows))
         prep = self.image_prep if (dev.type == "cuda" and config.map_rows_batched_prestage) else None
+        native = _native_jpeg(prep, raw)
+        nxt = native(0, step) if native is not None else None
+        chunks: List[List[torch.Tensor]] = [[] for _ in self.modes]
         for a in range(0, nrows, step):
             rows = range(a, min(nrows, a + step))
             cut = []
-            if prep is not None:
+            job = nxt
+            if native is not None and a + step < nrows:
+                nxt = native(a + step, step)  # decodes while this chunk runs
+            if job is not None:
+                t0 = time.perf_counter()
+                _finish_jpeg_batch(job, raw[0], raw[1][a:a + step])
+                t1 = time.perf_counter()
+                with torch.cuda.stream(side):
+                    cut = [prep.run_packed(job.buffer, job.offsets_bytes, job.meta_bytes, dev)]
+                engine.record_stream(cut[0], main)
+                t_in += t1 - t0
+                t_pre += time.perf_counter() - t1
+                metrics.add("map_rows_batched_prestage_rows", len(rows))
+                metrics.add("map_rows_native_decode_rows", len(rows))
+            elif prep is not None:
                 # the whole chunk's pre-stage in one kernel: every decoded
                 # image in ONE pinned ragged buffer, one copy, one launch
                 t0 = time.perf_counter()
@@ -975,6 +1007,7 @@ class _BatchCut:
                 main.wait_stream(side)
             outs = engine.run_program(self.post, [engine.cat_rows(cut)], dev)
             for j, (o, mode) in enumerate(zip(outs, self.modes)):
+                chunks[j].append(o)
                 for k, i in enumerate(rows):
                     per_out[j][i] = o[k] if mode == "index" else o[k:k + 1]
             t_post += time.perf_counter() - t0
@@ -983,6 +1016,50 @@ class _BatchCut:
         metrics.add("map_rows_batch_cut_inputs_ms", t_in * 1e3)
         metrics.add("map_rows_batch_cut_pre_ms", t_pre * 1e3)
         metrics.add("map_rows_batch_cut_post_ms", t_post * 1e3)
+        # each output column as ONE tensor: the chunks' [rows, ...] outputs
+        # concatenated (one copy kernel), not re-stacked row by row
+        if not nrows or any(not c for c in chunks):
+            return None
+        cols = [engine.cat_rows(c) if len(c) > 1 else c[0] for c in chunks]
+        return [c if mode == "index" else c.unsqueeze(1) for c, mode in zip(cols, self.modes)]
+
+
+def _native_jpeg(prep, raw):
+    """start(a, n) -> a _C.JpegBatch decoding raw cells [a, a+n) (None when a
+    cell is not a JPEG the native decoder takes), or None when the native
+    decode does not apply at all."""
+    if prep is None or raw is None or not config.native_jpeg_decode or prep.C not in (1, 3):
+        return None
+    hf, cells = raw
+    if hf.op not in ("DecodeJpeg", "DecodeImage") or hf.channels != prep.C or not _C.jpeg_native_available()[0]:
+        return None
+    threads = config.decode_threads or min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                                           else (os.cpu_count() or 1))
+
+    def start(a, n):
+        chunk = cells[a:a + n]
+        if not all(isinstance(c, (bytes, bytearray)) for c in chunk):
+            return None
+        job = _C.JpegBatch(list(chunk), prep.C, threads, True)
+        return job if job.header_ok else None
+    return start
+
+
+def _finish_jpeg_batch(job, hf, cells) -> None:
+    """Wait for a JpegBatch; images it could not decode (libjpeg warnings,
+    e.g. truncated data) go through the Python decoder, with its errors."""
+    failed = job.wait()
+    if not failed:
+        return
+    hb = job.buffer.numpy()
+    base = job.meta_bytes
+    for i in failed:
+        arr = hf.decode(cells[i])
+        shp = tuple(job.shape(i))
+        _check(arr.shape == shp, f"image decode: {arr.shape} from the Python decoder, header said {shp}")
+        o = base + job.pixel_offset(i)
+        hb[o:o + arr.size] = arr.reshape(-1)
+    metrics.add("map_rows_native_decode_fallback_rows", len(failed))
 
 
 _LIFT_CACHE: Dict[tuple, tuple] = {}  # (graph, fetches, feeds, cell ranks) -> (lifted bytes, program)
@@ -1199,25 +1276,40 @@ class _RowVectorizer:
 
 class _LazyDecoded:
     """Per-row decoded images of one block, decoded on a small thread pool
-    (PIL releases the GIL while decoding) ahead of the row loop."""
+    (PIL releases the GIL while decoding) ahead of the row loop. The pool
+    starts on the first row access: the batched image pre-stage decodes the
+    raw `cells` natively instead and never touches it."""
 
     def __init__(self, hf, cells):
+        self.hf, self.cells = hf, cells
+        self._pool = None
+        self._first = None
+        self._futs: list = []
+
+    def _start(self):
         from concurrent.futures import ThreadPoolExecutor
         # 4 by default: the decoders' Python parts hold the GIL and slow the row
         # loop that feeds the GPU (JPEG -> VGG-16 on MI355X: 1/2/4/8/16 threads ->
         # 1388/2097/2303/1800/1743 img/s, profiles/r1_read_image/)
-        workers = int(os.environ.get("TFA_DECODE_THREADS", "0")) or min(4, os.cpu_count() or 1)
+        workers = config.decode_threads or min(4, os.cpu_count() or 1)
         self._pool = ThreadPoolExecutor(max_workers=workers)
-        self._futs = [self._pool.submit(hf.decode, c) for c in cells]
+        self._futs = [self._pool.submit(self.hf.decode, c) for c in self.cells]
 
     def __getitem__(self, i):
+        if self._pool is None:
+            if i == 0:  # device choice peeks at row 0 (_rows_device): no pool yet
+                if self._first is None:
+                    self._first = torch.from_numpy(self.hf.decode(self.cells[0]))
+                return self._first
+            self._start()
         return torch.from_numpy(self._futs[i].result())
 
     def __len__(self):
-        return len(self._futs)
+        return len(self.cells)
 
     def __del__(self):
-        self._pool.shutdown(wait=False, cancel_futures=True)
+        if self._pool is not None:
+            self._pool.shutdown(wait=False, cancel_futures=True)
 
 
 def _decoded_cells(hf, b: Block):
@@ -1978,14 +2070,15 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         on_device = any(b.columns[n].is_cuda for b in blocks.values() if b.nrows for n in out_names) or \
             dev.type == "cuda"
         parts = [b for _, b in sorted(blocks.items()) if b.nrows]
-        K: List[torch.Tensor] = expand_keys(parts, dev)
+        K, hashed = expand_keys(parts, dev)
+        ustr = empty_ustr(hashed)
         V: Dict[str, Optional[torch.Tensor]] = {n: None for n in out_names}
         if parts:
             # this rank's keys are factorised ONCE over all its partitions
             # (one id space), so every partition reduces straight into its
             # row of a [P, groups, ...] buffer and the partitions combine by an
             # elementwise fold: no second factorisation on a single rank
-            ids, K, ng = G.group_ids(K)
+            ids, K, ng, ustr = G.group_keys(K, hashed)
             bounds = np.cumsum([0] + [b.nrows for b in parts])
             for n in out_names:
                 vals = [b.columns[n].to(dev).contiguous() for b in parts]
@@ -2004,7 +2097,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             out_cols: Dict[str, Any] = dict(V)
             if not on_device or not keep_on_device:
                 out_cols = {k: v.cpu() for k, v in out_cols.items()}
-            out_cols.update(collapse_keys(K, on_device and keep_on_device))
+            out_cols.update(collapse_keys(K, on_device and keep_on_device, ustr))
             metrics.add("aggregate_device_groupby" if dev.type == "cuda" else "aggregate_host_groupby")
             return {0: Block(ngk, {c: out_cols[c] for c in all_cols})}
         if dist.is_distributed():
@@ -2016,17 +2109,19 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                 if V[n] is None:
                     V[n] = engine.device_empty((0,) + tuple(cells[n]), D.torch_dtype(summary[n].tf_dtype), dev)
             nk = len(K)  # expanded key columns (string keys: words + length)
-            recv = G.route(K, [V[n] for n in out_names])
+            pos = sorted(hashed)
+            recv, rstr = G.route(K, [V[n] for n in out_names], strings=[ustr[p] for p in pos])
             K, V = recv[:nk], dict(zip(out_names, recv[nk:]))
+            hashed = dict(zip(pos, rstr))
         if K[0].shape[0] == 0:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, dist.world_size()))}
-        ids, uniq, ng = G.group_ids(K)
+        ids, uniq, ng, ustr = G.group_keys(K, hashed)
         out_cols: Dict[str, Any] = {}
         for n in out_names:
             out_cols[n] = _C.unsorted_segment_reduce(monoid[n], V[n].contiguous(), ids, ng)
         if not on_device or not keep_on_device:
             out_cols = {k: v.cpu() for k, v in out_cols.items()}
-        out_cols.update(collapse_keys(uniq, on_device and keep_on_device))
+        out_cols.update(collapse_keys(uniq, on_device and keep_on_device, ustr))
         metrics.add("aggregate_device_groupby" if dev.type == "cuda" else "aggregate_host_groupby")
         return {dist.rank(): Block(ng, {c: out_cols[c] for c in all_cols})}
 
@@ -2049,18 +2144,26 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
     numeric_keys = device_keys_ok
     key_width: Dict[str, int] = {}
 
-    def expand_keys(parts: List[Block], dev) -> List[torch.Tensor]:
-        """The key columns of these partitions as int64/numeric device columns
-        (string keys: W words + length each). Collective for string keys: the
-        word count is agreed by a Max all-reduce, every rank calls this."""
+    exact_string_keys = [not config.string_key_hash]  # set after a (62-bit) hash collision
+
+    def expand_keys(parts: List[Block], dev) -> Tuple[List[torch.Tensor], Dict[int, Any]]:
+        """The key columns of these partitions as int64/numeric device columns,
+        and {position of a hashed string key's word 0: its row strings}.
+        String columns whose keys all fit 8 bytes (agreed by a Max all-reduce:
+        every rank calls this) are packed exactly (word + length); longer
+        ones become 2 words per row whatever the longest key (word 0, tag =
+        length or 9 + 62-bit hash; ops/groupby.string_key_hashed), verified
+        per group by group_keys."""
         from .ops import groupby as G
         out: List[torch.Tensor] = []
+        hashed: Dict[int, Any] = {}
         strs = {k: [G.as_string_column(b.columns[k], key_kinds[k] == "bin") for b in parts]
                 for k in keys if key_kinds[k] != "num"}
         if strs:
             widths = torch.tensor([G.string_width(strs[k]) for k in strs], dtype=torch.int64)
             dist.all_reduce_host_(widths, "Max")
-            key_width.update({k: int(w) for k, w in zip(strs, widths.tolist())})
+            key_width.update({k: (int(w) if int(w) <= 1 or exact_string_keys[0] else 0)
+                              for k, w in zip(strs, widths.tolist())})
         for k in keys:
             if key_kinds[k] == "num":
                 kdt = D.torch_dtype(tf_types[k])
@@ -2068,14 +2171,22 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                            else engine.device_empty(0, kdt, dev))
                 continue
             w = key_width[k]
+            if w == 0:
+                rows = G.concat_strings([c.to(dev) for c in strs[k]]) if strs[k] else \
+                    StringColumn.from_values([], key_kinds[k] == "bin")
+                hashed[len(out)] = rows
+                out.extend(G.string_key_hashed(rows, dev) if len(rows) else
+                           [engine.device_empty(0, torch.int64, dev) for _ in range(2)])
+                continue
             cols = [G.string_key_words(c, w, dev) for c in strs[k]]
             for j in range(w + 1):
                 out.append(engine.cat_rows([c[j] for c in cols]) if cols
                            else engine.device_empty(0, torch.int64, dev))
-        metrics.add("aggregate_string_key_words", sum(key_width.get(k, 0) for k in keys))
-        return out
+        # key words per row (exact: W words + length; hashed: word 0 + tag)
+        metrics.add("aggregate_string_key_words", sum((key_width.get(k, 0) or 1) + 1 for k in strs))
+        return out, hashed
 
-    def collapse_keys(cols: List[torch.Tensor], keep: bool) -> Dict[str, Any]:
+    def collapse_keys(cols: List[torch.Tensor], keep: bool, ustr: Dict[int, Any]) -> Dict[str, Any]:
         """Expanded group key columns -> the output key columns."""
         from .ops import groupby as G
         out, j = {}, 0
@@ -2083,11 +2194,18 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
             if key_kinds[k] == "num":
                 out[k] = cols[j] if keep else cols[j].cpu()
                 j += 1
+            elif key_width[k] == 0:
+                out[k] = ustr[j]
+                j += 2
             else:
                 w = key_width[k]
                 out[k] = G.words_to_strings(cols[j:j + w + 1], key_kinds[k] == "bin")
                 j += w + 1
         return out
+
+    def empty_ustr(hashed):
+        return {p: StringColumn.from_values([], sc.binary) for p, sc in hashed.items()}
+
     # static cell shapes of the reduced columns (from the schema), for ranks without rows
     agg_static = {}
     for n in out_names:
@@ -2154,7 +2272,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         from .ops import groupby as G
         dev = engine.compute_device()
         parts = [b for _, b in sorted(blocks.items()) if b.nrows]
-        K = expand_keys(parts, dev)
+        K, hashed = expand_keys(parts, dev)
         if parts:
             V = [engine.cat_rows([b.columns[n].to(dev).contiguous() for b in parts]) for n in out_names]
         else:
@@ -2163,11 +2281,13 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
                  for n in out_names]
         if dist.is_distributed():
             nk = len(K)
-            recv = G.route(K, V)
+            pos = sorted(hashed)
+            recv, rstr = G.route(K, V, strings=[hashed[p] for p in pos])
             K, V = recv[:nk], recv[nk:]
+            hashed = dict(zip(pos, rstr))
         if K[0].shape[0] == 0:
             return {p: Block(0, _empty_agg_cols(df, keys, out_names)) for p in dist.local_partitions(max(1, dist.world_size()))}
-        ids, uniq, ng = G.group_ids(K)
+        ids, uniq, ng, ustr = G.group_keys(K, hashed)
         perm, offsets = _C.segment_csr(ids, ng)
         off_h = offsets.cpu().numpy()
         counts = np.diff(off_h)
@@ -2204,7 +2324,7 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         out_cols: Dict[str, Any] = dict(out)
         if not keep_on_device:
             out_cols = {k: v.cpu() for k, v in out_cols.items()}
-        out_cols.update(collapse_keys(uniq, keep_on_device))
+        out_cols.update(collapse_keys(uniq, keep_on_device, ustr))
         return {dist.rank(): Block(ng, {c: out_cols[c] for c in all_cols})}
 
     # static cell shapes of the input columns, for ranks without rows
@@ -2293,7 +2413,21 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         o = summary[n]
         shape = (o.shape if o.shape is not None else Shape()).prepend(UNKNOWN)
         out_fields.append(ColumnInformation.struct_field(n, o.tf_dtype, shape))
-    return DataFrame(StructType(out_fields), _Derived(df, compute, streamable=False), max(1, dist.world_size()))
+    def compute_keys_checked(blocks):
+        from .ops import groupby as G
+        try:
+            return compute(blocks)
+        except G.StringKeyCollision as e:
+            # 2^-62 per pair of distinct long keys: a rank alone cannot redo a
+            # collective aggregation, so only a single process falls back
+            if dist.is_distributed():
+                raise TensorFramesError(f"aggregate: {e}; rerun with TFA_STRING_KEY_HASH=0") from e
+            metrics.add("aggregate_string_key_collisions")
+            exact_string_keys[0] = True
+            return compute(blocks)
+
+    return DataFrame(StructType(out_fields), _Derived(df, compute_keys_checked, streamable=False),
+                     max(1, dist.world_size()))
 
 
 def _tf_of_field(f: StructField) -> Optional[int]:

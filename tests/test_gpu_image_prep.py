@@ -61,23 +61,44 @@ def test_ragged_kernel_matches_per_image_ops(mode):
         assert torch.equal(got[i], wnt), f"image {i}: max diff {(got[i] - wnt).abs().max().item()}"
 
 
-def test_batched_prestage_equals_per_row_scoring():
+@pytest.mark.parametrize("native", [False, True])
+def test_batched_prestage_equals_per_row_scoring(native):
     rng = np.random.default_rng(5)
     jpgs = _jpegs(70, rng)
+    # a grayscale file among the RGB ones (DecodeJpeg channels=3 replicates it)
+    buf = io.BytesIO()
+    from PIL import Image
+    Image.fromarray(rng.integers(0, 255, (90, 120), dtype=np.uint8)).save(buf, format="JPEG")
+    jpgs[17] = bytearray(buf.getvalue())
     df = tfs.create_dataframe([Row(uri=f"img{i}", image_data=b) for i, b in enumerate(jpgs)], num_partitions=1)
     g = cnn.jpeg_scoring_graph("vgg16", contents=bytes(jpgs[0]), width=0.125)
     res = {}
-    for on in (False, True):
-        tfs.set_config(map_rows_batched_prestage=on)
-        tfs.metrics.reset()
-        with g.as_default():
-            pred = tfs.map_rows(["index", "value"], df, feed_dict={"DecodeJpeg/contents": "image_data"})
-            rows = pred.select("uri", "index", "value").collect()
-        res[on] = rows
-        batched = tfs.metrics.snapshot().get("map_rows_batched_prestage_rows", 0)
-        assert (batched == len(jpgs)) == on
-    tfs.set_config(map_rows_batched_prestage=True)
+    try:
+        for on in (False, True):
+            tfs.set_config(map_rows_batched_prestage=on, native_jpeg_decode=native)
+            tfs.metrics.reset()
+            with g.as_default():
+                pred = tfs.map_rows(["index", "value"], df, feed_dict={"DecodeJpeg/contents": "image_data"})
+                rows = pred.select("uri", "index", "value").collect()
+            res[on] = rows
+            m = tfs.metrics.snapshot()
+            assert (m.get("map_rows_batched_prestage_rows", 0) == len(jpgs)) == on
+            assert (m.get("map_rows_native_decode_rows", 0) == len(jpgs)) == (on and native)
+    finally:
+        tfs.set_config(map_rows_batched_prestage=True, native_jpeg_decode=True)
     for a, b in zip(res[False], res[True]):
         assert a.uri == b.uri
         assert list(a["index"]) == list(b["index"])
         assert np.array_equal(np.asarray(a["value"]), np.asarray(b["value"]))
+
+
+def test_native_decode_falls_back_for_truncated_files():
+    """A truncated JPEG in a chunk: the native decoder reports it, the Python
+    decoder then raises its own error, as on the per-row path."""
+    rng = np.random.default_rng(9)
+    jpgs = _jpegs(8, rng)
+    jpgs[3] = jpgs[3][:len(jpgs[3]) // 2]
+    df = tfs.create_dataframe([Row(image_data=b) for b in jpgs], num_partitions=1)
+    g = cnn.jpeg_scoring_graph("vgg16", contents=bytes(jpgs[0]), width=0.125)
+    with g.as_default(), pytest.raises(Exception, match="(?i)truncated"):
+        tfs.map_rows(["index", "value"], df, feed_dict={"DecodeJpeg/contents": "image_data"}).collect()

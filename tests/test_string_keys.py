@@ -136,3 +136,70 @@ def test_string_keys_shuffle_without_pickling(world, tmp_path):
         got = dict(zip(res["keys"], res["x"]))
         assert set(got) == set(want.index)
         np.testing.assert_allclose([got[k] for k in want.index], want.to_numpy(), rtol=1e-9)
+
+
+def test_long_keys_bounded_width_exact_order():
+    """Keys longer than 8 bytes group on (word 0, tag = 9 + 62-bit hash): 2
+    words per row however long the longest key (one 4 KB key here), exact
+    against pandas, in lexicographic order even among long keys that share
+    their first 8 bytes (those sort by hash until re-ordered)."""
+    from tensorframes_amd.utils.logging import metrics
+    rng = np.random.default_rng(3)
+    pool = ["shared__" + "z" * int(n) + str(i) for i, n in enumerate(rng.integers(0, 30, 60))]
+    pool += ["shared__", "shared_", "shared__a", "s", "", "x" * 4096, "x" * 4095 + "y", "é" * 9]
+    keys = np.array(pool, dtype=object)[rng.integers(0, len(pool), 30000)]
+    x = rng.standard_normal(30000)
+    df = tfs.from_columns({"k": keys.astype(str), "x": x}, num_partitions=3)
+    metrics.reset()
+    rows = _agg(df, "k")
+    assert metrics.snapshot().get("aggregate_string_key_words") == 2  # word 0 + tag
+    want = pd.Series(x).groupby(keys.astype(str)).sum()
+    got_keys = [r.k for r in rows]
+    assert got_keys == sorted(want.index.tolist(), key=lambda s: s.encode())
+    np.testing.assert_allclose([r.x for r in rows], want[got_keys].to_numpy(), rtol=1e-10)
+
+
+def test_long_string_and_int_keys_order():
+    rng = np.random.default_rng(4)
+    s = np.array(["prefix__" + "q" * int(n) for n in range(12)] + ["prefix__b" * 3])[rng.integers(0, 13, 8000)]
+    i = rng.integers(0, 3, 8000).astype(np.int64)
+    x = rng.standard_normal(8000)
+    df = tfs.from_columns({"s": s, "i": i, "x": x}, num_partitions=2)
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.double, [None], name="x_input")
+        rows = tfs.aggregate(tf.reduce_sum(xi, [0], name="x"), df.groupBy("s", "i")).collect()
+    want = pd.DataFrame({"s": s, "i": i, "x": x}).groupby(["s", "i"])["x"].sum()
+    assert [(r.s, r.i) for r in rows] == sorted(want.index, key=lambda t: (t[0].encode(), t[1]))
+    got = {(r.s, r.i): r.x for r in rows}
+    np.testing.assert_allclose([got[t] for t in want.index], want.to_numpy(), rtol=1e-10)
+
+
+def test_hash_collision_is_detected_and_falls_back(monkeypatch):
+    """A (forced) hash collision: every long key gets the same hash. The
+    per-group verification catches it and the aggregation reruns on exact
+    words; the result is still exact."""
+    from tensorframes_amd.utils.logging import metrics
+    real = G.string_key_hashed
+
+    def colliding(col, dev):
+        w0, t = real(col, dev)
+        return [w0, torch.where(t >= G.HASH_TAG_MIN, torch.full_like(t, G.HASH_TAG_MIN), t)]
+    monkeypatch.setattr(G, "string_key_hashed", colliding)
+    keys = np.array(["collide_" + "a" * 20, "collide_" + "b" * 20, "short"])[np.arange(300) % 3]
+    x = np.arange(300, dtype=np.float64)
+    df = tfs.from_columns({"k": keys, "x": x})
+    metrics.reset()
+    rows = _agg(df, "k")
+    assert metrics.snapshot().get("aggregate_string_key_collisions") == 1
+    want = pd.Series(x).groupby(keys).sum()
+    assert [r.k for r in rows] == list(want.index)
+    np.testing.assert_allclose([r.x for r in rows], want.to_numpy())
+
+
+def test_group_keys_verification_direct():
+    col = StringColumn.from_values(["same_pre_" + "1" * 10, "same_pre_" + "2" * 10])
+    w0, t = G.string_key_hashed(col, torch.device("cpu"))
+    with pytest.raises(G.StringKeyCollision):
+        G.group_keys([w0, torch.full_like(t, G.HASH_TAG_MIN)], {0: col})
+    ids, uniq, ng, ustr = G.group_keys([w0, t], {0: col})
+    assert ng == 2 and ustr[0].values == sorted(col.values)
