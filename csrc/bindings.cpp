@@ -1080,6 +1080,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return pool_empty(sizes, at::TensorOptions().dtype(dt).device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
   }, py::arg("sizes"), py::arg("dtype"), py::arg("device"),
         "uninitialised device tensor from the engine pool, ordered on the device's current stream");
+  m.def("device_zeros", [](const std::vector<int64_t>& sizes, at::ScalarType dt, int device) {
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+    return pool_zeros(sizes, at::TensorOptions().dtype(dt).device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
+  }, py::arg("sizes"), py::arg("dtype"), py::arg("device"), "zeroed (hipMemsetAsync) device tensor from the engine pool");
+  m.def("fill_", [](at::Tensor& t, double value) {
+    TFA_CHECK(t.is_cuda() && t.is_contiguous(), "fill_: contiguous device tensor expected");
+    c10::hip::HIPGuard guard(t.device().index());
+    k::fill(from_scalar_type(t.scalar_type()), t.data_ptr(), t.numel(), value,
+            c10::hip::getCurrentHIPStream(t.device().index()).stream());
+    return t;
+  }, py::arg("tensor"), py::arg("value"), "fill a device tensor in place (kernels/elementwise fill)");
   m.def("record_stream", [](const at::Tensor& t, uint64_t stream) {
     TFA_CHECK(t.is_cuda(), "record_stream: device tensor expected");
     dev_record_stream(t, reinterpret_cast<hipStream_t>(stream));

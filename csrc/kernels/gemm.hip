@@ -108,6 +108,9 @@ bool g2_ok(const GemmArgs& g, int al, bool vec) {
   }();
   if (off || !vec || (al != A_KCONTIG && al != A_CONV)) return false;
   if (!g.tb && g.N % 4 != 0) return false;
+  // per-lane source offsets are 32-bit bytes within a 256-row block
+  constexpr int64_t kMaxLd = (int64_t(1) << 32) / (256 * 4) - 64;
+  if ((al == A_KCONTIG && g.lda > kMaxLd) || g.ldb > kMaxLd) return false;
   return g.K % 4 == 0;
 }
 

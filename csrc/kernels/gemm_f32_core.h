@@ -131,6 +131,7 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert((WM * WN == 4 || WM * WN == 8 || WM * WN == 16) && TM >= 1 && TN >= 1,
                 "4, 8 or 16 waves, >= one 32x32 tile each");
+  static_assert(BK % 8 == 0, "k is read in octets (k-step t: k = 8(t/4) + t%4 + 4 * half)");
   constexpr int KQ = BK / 4;  // float4 pieces along k
   constexpr int APIECES = BM * BK / 4, BPIECES = BN * BK / 4;  // float4 pieces per tile
   constexpr int AP = (APIECES + NT - 1) / NT, BP = (BPIECES + NT - 1) / NT;
@@ -381,8 +382,11 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
     auto tile = [&](int64_t knext, auto more) {
       constexpr bool NEXT = decltype(more)::value;
       float a[2][TM], b[2][TN];
-      auto rd = [&](int buf, int kk) {
-        const int kr = kk + (lane >> 5);
+      // k-step t pairs k = 8(t/4) + t%4 (lanes 0-31) with the same k + 4
+      // (lanes 32-63): the order of the g2 core's quad fragments
+      // (gemm_g2_core.h), so every f32 tile sums identically
+      auto rd = [&](int buf, int t) {
+        const int kr = 8 * (t >> 2) + (t & 3) + 4 * (lane >> 5);
 #pragma unroll
         for (int i = 0; i < TM; ++i) a[buf][i] = As[cur][kr][wm * (BM / WM) + i * 32 + (lane & 31)];
 #pragma unroll
@@ -393,7 +397,7 @@ void gemm_f32_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg, int64_t k_
       if constexpr (NEXT) load(knext, chk);
 #pragma unroll
       for (int kk = 0; kk < S; ++kk) {
-        if (kk + 1 < S) rd((kk + 1) & 1, 2 * (kk + 1));
+        if (kk + 1 < S) rd((kk + 1) & 1, kk + 1);
         if (NEXT && kk == S - 1) store(cur ^ 1);
 #pragma unroll
         for (int i = 0; i < TM; ++i)

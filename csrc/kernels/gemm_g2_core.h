@@ -20,9 +20,10 @@
 //       - row-contiguous B ([K][N] weights): image [k][n], one instruction =
 //         256 consecutive floats of it;
 //   * fragments: a lane reads its row's k quad with one ds_read_b128 and
-//     feeds it to 2 MFMA k-steps (a [k][n] image: one ds_read_b32 per step),
-//     pairing k = 2t / 2t+1 across the wave halves exactly as the round-4
-//     core does, so every tile of both cores gives bit-identical results;
+//     feeds it to 4 MFMA k-steps (a [k][n] image: one ds_read_b32 per step);
+//     the two wave halves carry the two quads of a k-octet (k = 8j + s and
+//     8j + 4 + s in step s), the order the round-4 core reads k in too, so
+//     every tile of both cores gives bit-identical results;
 //   * a ring of STAGES LDS stages of BK = 16 with one stage in flight beyond
 //     the next: counted vmcnt (never 0 in the steady loop), one raw s_barrier
 //     per stage; the next fragments (and the next stage's first ones) are
@@ -54,11 +55,14 @@ enum BLoad { B_RC = 0, B_KC = 1 };  // B [K][N] (row-contiguous) or B^T [N][K]
 void launch_kc(const F32Plan& p, const GemmArgs& g, hipStream_t s);
 void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s);
 
-// {BM, BN, WM, WN, STAGES}
+// {BM, BN, WM, WN, STAGES, OCC}: OCC blocks per CU. The big tiles hold 192-256
+// accumulators per lane and one block per CU; the smaller ones are sized
+// (<= 256 registers, <= 80 KB of LDS) for two, so one block's prologue and
+// epilogue overlap the other's main loop (K = 512 GEMMs, the convs)
 constexpr int kNumG2Tiles = 6;
-constexpr int kG2Tiles[kNumG2Tiles][5] = {
-    {256, 256, 2, 2, 4}, {256, 192, 2, 2, 4}, {256, 128, 2, 2, 4},
-    {256, 64, 4, 1, 5},  {128, 128, 2, 2, 5}, {128, 64, 2, 2, 5}};
+constexpr int kG2Tiles[kNumG2Tiles][6] = {
+    {256, 256, 2, 2, 4, 1}, {256, 192, 2, 2, 4, 1}, {256, 128, 2, 2, 3, 2},
+    {256, 64, 4, 1, 4, 2},  {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2}};
 
 namespace {
 
@@ -77,9 +81,9 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int AL, int BL>
-__global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
-                                                           int64_t k_per_split, int flags) {
+template <int BM, int BN, int WM, int WN, int STAGES, int OCC, int AL, int BL>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void g2_tile(GemmArgs g, int tiles_m, int tiles_n, ConvGeom cg,
+                                                             int64_t k_per_split, int flags) {
   constexpr int NW = WM * WN, NT = 64 * NW, BK = 16, KQ = BK / 4;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4, STAGE = A_BYTES + B_BYTES;
@@ -89,10 +93,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
   constexpr int kEpi = NW * 32 * 32 * 4;
   static_assert(NW == 4 && TM >= 1 && TN >= 1 && AI >= 1 && BI >= 1 && BM % (16 * NW) == 0 && BN % (16 * NW) == 0,
                 "4 waves, >= one 32x32 tile each, whole DMA instructions per wave");
-  static_assert(STAGES >= 3 && STAGES * STAGE <= 160 * 1024 && STAGES * STAGE >= kEpi, "LDS budget");
+  static_assert(STAGES >= 3 && STAGES * STAGE <= 160 * 1024 / OCC && STAGES * STAGE >= kEpi, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // wave index in an SGPR: every LDS-DMA destination (M0) and stage base is
+  // then scalar arithmetic, not a VGPR sum + v_readfirstlane per piece
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int wm = wave / WN, wn = wave % WN;
   const int h = lane >> 5, r32 = lane & 31;
   const int nwg = tiles_m * tiles_n;
@@ -107,23 +113,32 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
   const int64_t kend = min(K, kbeg + k_per_split);
   const float* zero = f32core::kZeroPage;
 
-  // ---- A pieces: instruction q = wave*AI + i covers rows 16q .. 16q+15,
-  // lane -> row 16q + lane/4, k quad koff/4 of the stage (swizzled slot).
-  // Every source choice below is a select on bitwise-combined conditions:
-  // a branch here makes the compiler drain the DMA queue (vmcnt(0)) at the
-  // join, which serialises the ring.
+  // ---- operand sources. k-contiguous A, and B either way: a block-uniform
+  // stage base (SGPRs, advanced by one stage per issue) plus a per-lane
+  // 32-bit byte offset fixed for the whole loop (global_load_lds saddr +
+  // voffset), so an unchecked piece costs no VALU at all. Checked pieces
+  // (edge blocks, the K tail) select the 16-byte zero page per lane. Every
+  // choice is a select: a branch here makes the compiler drain the DMA
+  // queue (vmcnt(0)) at the join, which serialises the ring.
+  // A instruction q = wave*AI + i covers rows 16q .. 16q+15, lane -> row
+  // 16q + lane/4, k quad koff/4 of the stage (swizzled slot).
   const int koff = 4 * ((lane & 3) ^ ((lane >> 4) & 3));
-  const float* ap[AI];  // k-contiguous: this stage's 16-byte piece of the row; conv: the image base
+  const char* abase = reinterpret_cast<const char*>(AL == A_KCONTIG ? A + m0 * g.lda + kbeg : A);
+  uint32_t aoff[AI];    // k-contiguous: byte offset of the lane's row piece from abase
+  const float* ap[AI];  // conv: the lane's image base
   bool aok[AI];         // row in range
   int cih[AI], ciw[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    const int64_t m = m0 + (wave * AI + i) * 16 + lane / 4;
+    const int r = (wave * AI + i) * 16 + lane / 4;
+    const int64_t m = m0 + r;
     aok[i] = m < M;
     const int64_t mc = aok[i] ? m : 0;
+    aoff[i] = 0;
+    ap[i] = A;
+    cih[i] = ciw[i] = 0;
     if constexpr (AL == A_KCONTIG) {
-      ap[i] = A + mc * g.lda + kbeg + koff;
-      cih[i] = ciw[i] = 0;
+      aoff[i] = (uint32_t)(((int64_t)r * g.lda + koff) * 4);
     } else {
       int64_t ow, oh, n;
       if (cg.fast) {
@@ -151,43 +166,43 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
     kkw = t % cg.KW;
     kkh = t / cg.KW;
   }
-  // ---- B pieces: running source pointers (advanced by one stage per issue)
-  const float* bp[BI];
+  const char* bbase = reinterpret_cast<const char*>(BL == B_KC ? B + n0 * g.ldb + kbeg : B + kbeg * g.ldb + n0);
+  uint32_t boff[BI];
   bool bok[BI];
   int bk_[BI];  // the piece's k within the stage
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     const int q = wave * BI + i;
     if constexpr (BL == B_KC) {
-      const int64_t n = n0 + q * 16 + lane / 4;
-      bok[i] = n < N;
-      bp[i] = B + (bok[i] ? n : 0) * g.ldb + kbeg + koff;
+      const int r = q * 16 + lane / 4;
+      bok[i] = n0 + r < N;
+      boff[i] = (uint32_t)(((int64_t)r * g.ldb + koff) * 4);
       bk_[i] = koff;
     } else {
       const int e = q * 256 + 4 * lane;
       const int kb = e / BN, nb = e % BN;
       bok[i] = n0 + nb < N;
-      bp[i] = B + (kbeg + kb) * g.ldb + (bok[i] ? n0 + nb : 0);
+      boff[i] = (uint32_t)(((int64_t)kb * g.ldb + nb) * 4);
       bk_[i] = kb;
     }
   }
-  const int64_t bstep = BL == B_KC ? BK : (int64_t)BK * g.ldb;  // elements per stage
+  constexpr int64_t astep = BK * 4;                                                  // bytes per stage
+  const int64_t bstep = BL == B_KC ? (int64_t)BK * 4 : (int64_t)BK * g.ldb * 4;
   int64_t kpos = kbeg;  // k0 of the next stage to issue
 
   // The LDS-DMA of one stage, piece by piece (A pieces 0..AI-1, then B
-  // pieces), so the main loop can place each between two MFMAs. Every source
-  // choice is a select on bitwise-combined conditions and the pointers only
-  // ever advance by constants: a branch (or a spill reload) here makes the
-  // compiler drain the DMA queue (vmcnt(0)) at the join, serialising the ring.
-  auto issue_piece = [&](int slot, int p) __attribute__((always_inline)) {
+  // pieces), so the main loop can place each between two MFMAs. CHECK: the
+  // block's rows / columns or the stage's k may fall outside the operands.
+  auto issue_piece = [&](int slot, int p, auto chk) __attribute__((always_inline)) {
+    constexpr bool CHECK = decltype(chk)::value;
     char* base = smem + slot * STAGE;
-    const bool kok = kpos + koff < kend;
+    const bool kok = !CHECK || kpos + koff < kend;
     if (p < AI) {
       const int i = p;
       const float* src;
       if constexpr (AL == A_KCONTIG) {
-        src = (aok[i] & kok) ? ap[i] : zero;
-        ap[i] += BK;
+        src = reinterpret_cast<const float*>(abase + aoff[i]);
+        if constexpr (CHECK) src = (aok[i] & kok) ? src : zero;
       } else {
         const int ih = cih[i] + kkh * cg.dh, iw = ciw[i] + kkw * cg.dw;
         const bool ok = aok[i] & kok & (ih >= 0) & (ih < cg.H) & (iw >= 0) & (iw < cg.W);
@@ -210,15 +225,19 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
       }
     } else {
       const int i = p - AI;
-      const bool ok = bok[i] & (kpos + bk_[i] < kend);
-      glds16(ok ? bp[i] : zero, base + A_BYTES + (wave * BI + i) * 1024);
-      bp[i] += bstep;
-      if (i == BI - 1) kpos += BK;
+      const float* src = reinterpret_cast<const float*>(bbase + boff[i]);
+      if constexpr (CHECK) src = (bok[i] & (kpos + bk_[i] < kend)) ? src : zero;
+      glds16(src, base + A_BYTES + (wave * BI + i) * 1024);
+      if (i == BI - 1) {
+        kpos += BK;
+        abase += astep;
+        bbase += bstep;
+      }
     }
   };
   auto issue = [&](int slot) __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p < G; ++p) issue_piece(slot, p);
+    for (int p = 0; p < G; ++p) issue_piece(slot, p, std::true_type{});
   };
 
   f32x16 acc[TM][TN];
@@ -227,23 +246,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){};
 
-  // Fragments, in the round-4 core's summation order: MFMA k-step t pairs k
-  // = 2t (lanes 0-31) with k = 2t+1 (lanes 32-63), steps in increasing k, so
-  // every tile of either core gives bit-identical results (the autotuner's
-  // pick never changes a result). One b128 read of a row's k quad serves two
-  // steps: half 0 takes components 0 / 2, half 1 components 1 / 3 (one
-  // v_cndmask per operand); a [k][n] image is read per step (ds_read_b32).
-  // b128 quads are kept whole until their MFMAs: selecting a lane's two
-  // components right after the read would make the wave wait for it there
+  // Fragments. MFMA k-step s of k-quad pair j takes k = 8j + s from lanes
+  // 0-31 and k = 8j + 4 + s from lanes 32-63, steps in increasing (j, s): a
+  // lane reads ITS row's k quad 2j + h once (ds_read_b128) and feeds its 4
+  // components to 4 steps, no per-step select. The round-4 core
+  // (gemm_f32_core.h) reads k in the same order, so every f32 tile gives
+  // bit-identical results (the autotuner's pick never changes a result).
+  // A [k][n] image (B row-contiguous) is read per step (ds_read_b32).
   struct Frag {
     f32x4 a[TM];
-    f32x4 bq[BL == B_KC ? TN : 1];  // B^T quads
-    float b[TN][2];                 // B [K][N]: the two k of the lane's half
+    f32x4 b[TN];
   };
   const int slot_sw = (r32 >> 2) & 3;  // the rows a lane reads differ by multiples of 32: one swizzle
-  // fragment r of k quad q of stage kt: r < TM an A fragment, else B fragment r - TM
-  auto read_frag = [&](int kt, int q, int r, Frag& f) __attribute__((always_inline)) {
+  // fragment r of k-quad pair j of stage kt: r < TM an A fragment, else B fragment r - TM
+  auto read_frag = [&](int kt, int j, int r, Frag& f) __attribute__((always_inline)) {
     const char* st = smem + (kt % STAGES) * STAGE;
+    const int q = 2 * j + h;
     const int slot = q ^ slot_sw;
     if (r < TM) {
       const int i = r;
@@ -252,20 +270,21 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
       const int jn = r - TM;
       const int n = wn * (BN / WN) + jn * 32 + r32;
       if constexpr (BL == B_KC) {
-        f.bq[jn] = *reinterpret_cast<const f32x4*>(st + A_BYTES + n * 64 + slot * 16);
+        f.b[jn] = *reinterpret_cast<const f32x4*>(st + A_BYTES + n * 64 + slot * 16);
       } else {
-        const float* bs = reinterpret_cast<const float*>(st + A_BYTES) + (4 * q + h) * BN + n;
-        f.b[jn][0] = bs[0];
-        f.b[jn][1] = bs[2 * BN];
+        const float* bs = reinterpret_cast<const float*>(st + A_BYTES) + 4 * q * BN + n;
+        f.b[jn] = (f32x4){bs[0], bs[BN], bs[2 * BN], bs[3 * BN]};
       }
     }
   };
-  auto read = [&](int kt, int q, Frag& f) __attribute__((always_inline)) {
+  auto read = [&](int kt, int j, Frag& f) __attribute__((always_inline)) {
 #pragma unroll
-    for (int r = 0; r < TM + TN; ++r) read_frag(kt, q, r, f);
+    for (int r = 0; r < TM + TN; ++r) read_frag(kt, j, r, f);
   };
-  constexpr int NM = 2 * TM * TN;  // MFMAs per k quad
-  constexpr int NR = TM + TN;      // fragment reads per k quad
+  constexpr int KP = KQ / 2;                            // k-quad pairs per stage
+  constexpr int NM = 4 * TM * TN;                       // MFMAs per pair
+  constexpr int NR = TM + TN * (BL == B_KC ? 1 : 4);    // LDS read instructions per pair
+  static_assert(KQ % 2 == 0, "whole k-quad pairs per stage");
 
   const int KT = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
   // prologue: stages 0 .. S-2 (a stage past KT reads only zero pages)
@@ -277,44 +296,38 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
   read(0, 0, cur);
   // One stage: stage kt+1 retired for every wave (counted wait + barrier),
   // which also frees the slot of stage kt-1 for the DMA of stage kt+S-1;
-  // then KQ k quads of NM MFMAs, each with the next quad's fragment reads
-  // (the next stage's first quad after the last) in its shadow. The stage's
-  // G DMA pieces are spread over the quads (each costs ~60 issue cycles when
-  // issued back to back) and, inside a quad, alternate with the MFMAs
+  // then KP pairs of NM MFMAs, each with the next pair's fragment reads (the
+  // next stage's first pair after the last) in its shadow. The stage's G DMA
+  // pieces are spread over the pairs (each costs ~60 issue cycles when
+  // issued back to back) and, inside a pair, alternate with the MFMAs
   // (sched_group_barrier), as do the fragment reads. A stage past KT reads a
   // slot with no live data: those values feed no MFMA.
-  auto stage = [&](int kt, auto do_issue) __attribute__((always_inline)) {
+  auto stage = [&](int kt, auto do_issue, auto do_check) __attribute__((always_inline)) {
     constexpr bool ISSUE = decltype(do_issue)::value;
-    if (kt + STAGES - 2 < KT) wait_vm<G * (STAGES - 3)>();
+    // a stage that issues stage kt+S-1 < KT has stage kt+S-2 in flight too
+    if (ISSUE || kt + STAGES - 2 < KT) wait_vm<G * (STAGES - 3)>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     const int slot_next = (kt + STAGES - 1) % STAGES;
-    static_for<KQ>([&](auto jc) __attribute__((always_inline)) {
+    static_for<KP>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      // DMA pieces [p0, p1) go with quad j
-      constexpr int p0 = ISSUE ? (G * j) / KQ : 0, p1 = ISSUE ? (G * (j + 1)) / KQ : 0;
+      // the stage's DMA pieces all go with pair 0 (measured: spreading them
+      // over the pairs leaves the last pair's pieces clustered at the loop
+      // end, where no MFMA hides them)
+      constexpr int p0 = 0, p1 = (ISSUE && j == 0) ? G : 0;
       constexpr int NP = p1 - p0;
-      if constexpr (j + 1 < KQ) read(kt, j + 1, nxt);
+      if constexpr (j + 1 < KP) read(kt, j + 1, nxt);
       else read(kt + 1, 0, nxt);
       static_for<NP>([&](auto pc) __attribute__((always_inline)) {
-        issue_piece(slot_next, p0 + decltype(pc)::value);
+        issue_piece(slot_next, p0 + decltype(pc)::value, do_check);
       });
 #pragma unroll
-      for (int sk = 0; sk < 2; ++sk) {
-        float av[TM], bv[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) av[i] = h ? cur.a[i][2 * sk + 1] : cur.a[i][2 * sk];
-#pragma unroll
-        for (int jn = 0; jn < TN; ++jn) {
-          if constexpr (BL == B_KC) bv[jn] = h ? cur.bq[jn][2 * sk + 1] : cur.bq[jn][2 * sk];
-          else bv[jn] = cur.b[jn][sk];
-        }
+      for (int sk = 0; sk < 4; ++sk)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int jn = 0; jn < TN; ++jn)
-            acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[jn], acc[i][jn], 0, 0, 0);
-      }
+            acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[i][sk], cur.b[jn][sk], acc[i][jn], 0, 0, 0);
       // MFMA, DMA piece, MFMA, DMA piece, ..., then MFMA, read, MFMA, read, ...
       static_for<NM>([&](auto xc) __attribute__((always_inline)) {
         constexpr int x = decltype(xc)::value;
@@ -325,9 +338,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void g2_tile(GemmArgs g, int tiles
       cur = nxt;
     });
   };
+  // stages whose DMA stays inside the operands (interior block, a stage
+  // entirely inside [kbeg, kend)) issue unchecked; the rest select per lane
   int kt = 0;
-  for (; kt + STAGES - 1 < KT; ++kt) stage(kt, std::true_type{});
-  for (; kt < KT; ++kt) stage(kt, std::false_type{});
+  const int KTF = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+  if (m0 + BM <= M && n0 + BN <= N)
+    for (; kt + STAGES - 1 < KTF; ++kt) stage(kt, std::true_type{}, std::false_type{});
+  for (; kt + STAGES - 1 < KT; ++kt) stage(kt, std::true_type{}, std::true_type{});
+  for (; kt < KT; ++kt) stage(kt, std::false_type{}, std::true_type{});
   __syncthreads();  // every wave is done with the ring: its LDS becomes the epilogue staging
 
   // ---- epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -418,16 +436,18 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
   TFA_CHECK(tm * tn < (int64_t(1) << 31), "gemm: grid too large");
   TFA_CHECK(g.batch <= 65535 && p.splits <= 65535, "gemm: batch/splits too large");
   dim3 grid((unsigned)(tm * tn), (unsigned)g.batch, (unsigned)p.splits);
-#define TFA_G2(BM_, BN_, WM_, WN_, S_)                                                                          \
-  hipLaunchKernelGGL((g2_tile<BM_, BN_, WM_, WN_, S_, AL, BL>), grid, dim3(64 * WM_ * WN_), 0, s, g, (int)tm, \
-                     (int)tn, cg, p.k_per_split, vepi)
+#define TFA_G2(C_)                                                                                             \
+  hipLaunchKernelGGL((g2_tile<kG2Tiles[C_][0], kG2Tiles[C_][1], kG2Tiles[C_][2], kG2Tiles[C_][3], kG2Tiles[C_][4], \
+                              kG2Tiles[C_][5], AL, BL>),                                                         \
+                     grid, dim3(64 * kG2Tiles[C_][2] * kG2Tiles[C_][3]), 0, s, g, (int)tm, (int)tn, cg,          \
+                     p.k_per_split, vepi)
   switch (p.cfg) {
-    case 0: TFA_G2(256, 256, 2, 2, 4); break;
-    case 1: TFA_G2(256, 192, 2, 2, 4); break;
-    case 2: TFA_G2(256, 128, 2, 2, 4); break;
-    case 3: TFA_G2(256, 64, 4, 1, 5); break;
-    case 4: TFA_G2(128, 128, 2, 2, 5); break;
-    default: TFA_G2(128, 64, 2, 2, 5); break;
+    case 0: TFA_G2(0); break;
+    case 1: TFA_G2(1); break;
+    case 2: TFA_G2(2); break;
+    case 3: TFA_G2(3); break;
+    case 4: TFA_G2(4); break;
+    default: TFA_G2(5); break;
   }
 #undef TFA_G2
 }

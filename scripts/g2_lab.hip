@@ -344,6 +344,10 @@ int main(int argc, char** argv) {
     CK(hipMemset(C, 0, (size_t)M * N * 4));
   };
   const int it = 20;
+  if (argc > 4) {  // one variant only (counter runs)
+    check("g2 256x256 s4 m3", run<256, 4, 3>(A, Bt, C, M, N, K, it));
+    return 0;
+  }
   if (N % 256 == 0) {
     check("g2 256x256 s4 m2", run<256, 4, 2>(A, Bt, C, M, N, K, it));
     check("g2 256x256 s4 m3", run<256, 4, 3>(A, Bt, C, M, N, K, it));

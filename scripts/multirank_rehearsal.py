@@ -27,6 +27,9 @@ def main():
     dev = engine.compute_device()
     rng = np.random.default_rng(0)
     out = {"world": world}
+    from tensorframes_amd._native import _C
+    pool0 = _C.device_pool_stats()
+    torch0 = torch.cuda.memory_stats(dev).get("allocation.all.allocated", 0)
 
     # reduce_blocks Sum / Min over a device-cached frame
     x = rng.standard_normal((20_000, 64)).astype(np.float32)
@@ -69,8 +72,40 @@ def main():
         np.add.at(sums, idx, pts)
         cn = sums / (np.bincount(idx, minlength=cn.shape[0]) + 1e-7)[:, None]
     out["kmeans_center_err"] = float(np.abs(c - cn).max())
+
+    # Prod / Max reducers (identity fills), groupBy().count(), long string
+    # keys (hashed, routed with their bytes), repartition of a device frame
+    with tf.Graph().as_default():
+        xi = tf.placeholder(tf.float32, [None, 64], name="x_input")
+        got = tfs.reduce_blocks(tf.reduce_max(xi, [0], name="x"), df)
+    out["reduce_max_err"] = float(np.abs(got - x.max(0)).max())
+    cnt = {int(r["key"]): int(r["count"]) for r in adf.groupBy("key").count().collect()}
+    out["count_err"] = int(sum(abs(cnt.get(k_, 0) - int(c_)) for k_, c_ in
+                               zip(*np.unique(keys, return_counts=True))))
+    skeys = np.array([f"user-{i % 97:03d}" * (1 + i % 3) for i in range(6000)])
+    sv = rng.standard_normal(6000)
+    sdf = tfs.from_columns({"k": skeys, "x": sv}, num_partitions=2 * world)
+    with tf.Graph().as_default():
+        si = tf.placeholder(tf.double, [None], name="x_input")
+        srows = tfs.aggregate(tf.reduce_sum(si, [0], name="x"), sdf.groupBy("k")).collect()
+    swant = {}
+    for k_, v_ in zip(skeys, sv):
+        swant[k_] = swant.get(k_, 0.0) + v_
+    out["string_groups"] = len(srows)
+    out["string_err"] = max(abs(r.x - swant[r.k]) for r in srows) if srows else 0.0
+    rp = adf.repartition(3 * world)
+    out["repartition_rows"] = int(rp.count())
+
+    pool1 = _C.device_pool_stats()
+    torch1 = torch.cuda.memory_stats(dev).get("allocation.all.allocated", 0)
+    stats = torch.tensor([pool1["fallbacks"] - pool0["fallbacks"], pool1["allocs"] - pool0["allocs"],
+                          torch1 - torch0], dtype=torch.int64)
+    dist.all_reduce_host_(stats, "Max")
+    out["pool_fallbacks"], out["pool_allocs"], out["framework_allocs"] = (int(v) for v in stats.tolist())
     ok = (out["reduce_sum_err"] < 1e-2 and out["reduce_min_err"] == 0.0 and out["aggregate_groups"] == 500
-          and out["aggregate_err"] < 1e-9 and out["kmeans_center_err"] < 1e-6)
+          and out["aggregate_err"] < 1e-9 and out["kmeans_center_err"] < 1e-6 and out["reduce_max_err"] == 0.0
+          and out["count_err"] == 0 and out["string_groups"] == len(swant) and out["string_err"] < 1e-9
+          and out["repartition_rows"] == 20_000 and out["pool_fallbacks"] == 0 and out["pool_allocs"] > 0)
     out["ok"] = bool(ok)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -1606,9 +1606,9 @@ def _identity(op: str, shape, dtype, dev) -> torch.Tensor:
     if op == "Sum":
         return engine.device_zeros(shape, dtype, dev)
     if op == "Prod":
-        return torch.ones(shape, dtype=dtype, device=dev)
+        return engine.device_full(shape, 1, dtype, dev)
     info = torch.finfo(dtype) if dtype.is_floating_point else torch.iinfo(dtype)
-    return torch.full(shape, info.max if op == "Min" else info.min, dtype=dtype, device=dev)
+    return engine.device_full(shape, info.max if op == "Min" else info.min, dtype, dev)
 
 
 _REDUCE_SETUP: "OrderedDict[tuple, tuple]" = OrderedDict()

@@ -266,7 +266,32 @@ def device_empty(shape, dtype: torch.dtype, device) -> torch.Tensor:
 
 
 def device_zeros(shape, dtype: torch.dtype, device) -> torch.Tensor:
-    return device_empty(shape, dtype, device).zero_()
+    """Zeroed tensor; on a GPU from the engine pool, cleared by hipMemsetAsync."""
+    device = torch.device(device)
+    if isinstance(shape, int):
+        shape = (shape,)
+    if device.type != "cuda":
+        return torch.zeros(tuple(shape), dtype=dtype, device=device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _C.device_zeros([int(d) for d in shape], dtype, idx)
+
+
+def device_full(shape, value, dtype: torch.dtype, device) -> torch.Tensor:
+    """Constant tensor; on a GPU from the engine pool, filled by the native
+    fill kernel (values a double holds exactly) or copied from the host
+    (64-bit integers beyond 2^53, e.g. the int64 Min/Max identities)."""
+    device = torch.device(device)
+    if isinstance(shape, int):
+        shape = (shape,)
+    if device.type != "cuda":
+        return torch.full(tuple(shape), value, dtype=dtype, device=device)
+    t = device_empty(shape, dtype, device)
+    if t.numel() == 0:
+        return t
+    if dtype.is_floating_point or dtype == torch.bool or abs(int(value)) <= (1 << 53):
+        return _C.fill_(t, float(value))
+    t.copy_(torch.full(tuple(shape), value, dtype=dtype))
+    return t
 
 
 def record_stream(t: torch.Tensor, stream) -> None:

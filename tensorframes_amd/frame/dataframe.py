@@ -449,7 +449,7 @@ class GroupedData:
         """Rows per key: the keys plus a column of ones go through `aggregate`
         with a Sum graph (device factorisation + segmented sum, keyed
         all-to-all across ranks); no rows are collected."""
-        from .. import core
+        from .. import core, engine
         from ..graph import dsl as tf
         keys = list(self.keys)
 
@@ -459,7 +459,7 @@ class GroupedData:
                 kc = b.columns[keys[0]]
                 dev = kc.device if isinstance(kc, torch.Tensor) else torch.device("cpu")
                 cols = {k: b.columns[k] for k in keys}
-                cols["count"] = torch.ones(b.nrows, dtype=torch.int64, device=dev)
+                cols["count"] = engine.device_full(b.nrows, 1, torch.int64, dev)
                 out[p] = Block(b.nrows, cols)
             return out
         fields = [self.df.schema[k] for k in keys] + [tensor_field("count", D.DT_INT64, [])]

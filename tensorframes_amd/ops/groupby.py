@@ -44,7 +44,7 @@ def group_ids(keys: List[torch.Tensor]) -> Tuple[torch.Tensor, List[torch.Tensor
     representative row."""
     n = keys[0].shape[0]
     if n == 0:
-        return (torch.empty(0, dtype=torch.int64, device=keys[0].device),
+        return (engine_empty(0, torch.int64, keys[0].device),
                 [k[:0] for k in keys], 0)
     if len(keys) == 1:
         ids, uniq = _C.factorize(keys[0])
@@ -79,7 +79,7 @@ def route(keys: List[torch.Tensor], cols: List[torch.Tensor], strings: Optional[
     dev = allc[0].device
     n = allc[0].shape[0]
     if dev.type == "cuda":
-        dest = _C.key_dest([k.contiguous() for k in keys], w) if n else torch.empty(0, dtype=torch.int64, device=dev)
+        dest = _C.key_dest([k.contiguous() for k in keys], w) if n else engine_empty(0, torch.int64, dev)
         perm, counts = _C.partition_rows(dest, w)
         send_rows = [int(c) for c in counts.cpu().tolist()]
     else:

@@ -359,7 +359,7 @@ def repartition_blocks(local: Dict[int, Any], names: Sequence[str], schema, npar
         if kind is not None:
             dev = devs[n]
             parts = [local[p].columns[n][st:st + ln].to(dev) for r in range(w) for (_, p, st, ln) in send[r]]
-            buf = engine.cat_rows(parts) if parts else torch.empty((0,) + kind[1], dtype=kind[0], device=dev)
+            buf = engine.cat_rows(parts) if parts else engine.device_empty((0,) + kind[1], kind[0], dev)
             got = dist.all_to_all_rows(buf, send_rows, recv_rows) if dist.is_distributed() else buf
             pos, pieces = 0, {q: [] for q in mine}
             for s in range(w):
@@ -368,7 +368,7 @@ def repartition_blocks(local: Dict[int, Any], names: Sequence[str], schema, npar
                     pos += ln
             for q in mine:
                 ps = [t for _, t in sorted(pieces[q], key=lambda x: x[0])]
-                cols_out[q][n] = engine.cat_rows(ps) if ps else torch.empty((0,) + kind[1], dtype=kind[0], device=dev)
+                cols_out[q][n] = engine.cat_rows(ps) if ps else engine.device_empty((0,) + kind[1], kind[0], dev)
         elif is_bytes_field(schema[n]) and dist.is_distributed():
             from ..frame.block import concat_columns
             from ..frame.types import BinaryType

@@ -1,6 +1,8 @@
 """Two ranks sharing the one GPU (gloo for the cross-rank exchange, since RCCL
 refuses two ranks on a device): device-resident reduce_blocks, aggregate key
-routing and K-Means agree with numpy (scripts/multirank_rehearsal.py)."""
+routing, groupBy count, long string keys, repartition and K-Means agree with
+numpy, and every device temporary of both ranks came from the engine pool
+(no fallbacks; scripts/multirank_rehearsal.py)."""
 import json
 import os
 import subprocess
@@ -30,3 +32,4 @@ def test_two_ranks_on_one_gpu_match_numpy():
     assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-3000:]
     out = json.loads(lines[0])
     assert out["ok"] and out["world"] == 2, out
+    assert out["pool_fallbacks"] == 0, out
