@@ -8,7 +8,8 @@ namespace k {
 namespace g2 {
 
 void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s) {
-  launch_cfg<A_CONV, B_RC>(p, g, cg, s);
+  if (cg.C % 16 == 0) launch_cfg<A_CONV16, B_RC>(p, g, cg, s);
+  else launch_cfg<A_CONV, B_RC>(p, g, cg, s);
 }
 
 }  // namespace g2

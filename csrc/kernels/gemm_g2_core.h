@@ -49,6 +49,11 @@ using f32core::ConvGeom;
 using f32core::F32Plan;
 
 enum BLoad { B_RC = 0, B_KC = 1 };  // B [K][N] (row-contiguous) or B^T [N][K]
+// the conv loader when C % 16 == 0: a stage's 16 k then lie in one filter tap,
+// so the tap (kh, kw) and its input offset are block-uniform scalars (no
+// per-lane carry chain) and a piece costs two bounds adds, the compares and
+// one select
+constexpr int A_CONV16 = 100;
 
 // the launcher translation units (cfg indexes kG2Tiles): k-contiguous A with
 // B [K][N] or B^T [N][K] (g.tb), and the implicit-GEMM conv (filter [K][N])
@@ -122,6 +127,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void g2_tile(GemmArgs g, int til
   // queue (vmcnt(0)) at the join, which serialises the ring.
   // A instruction q = wave*AI + i covers rows 16q .. 16q+15, lane -> row
   // 16q + lane/4, k quad koff/4 of the stage (swizzled slot).
+  constexpr bool CONV = AL == A_CONV || AL == A_CONV16, TAPU = AL == A_CONV16;
   const int koff = 4 * ((lane & 3) ^ ((lane >> 4) & 3));
   const char* abase = reinterpret_cast<const char*>(AL == A_KCONTIG ? A + m0 * g.lda + kbeg : A);
   uint32_t aoff[AI];    // k-contiguous: byte offset of the lane's row piece from abase
@@ -155,17 +161,23 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void g2_tile(GemmArgs g, int til
       ap[i] = A + n * (int64_t)cg.H * cg.W * cg.C;
       cih[i] = (int)(oh * cg.sh - cg.pt);
       ciw[i] = (int)(ow * cg.sw - cg.pl);
+      // TAPU: the lane's channel quad at the tap (0, 0) of its output pixel
+      // (only dereferenced once a tap's bounds check passed)
+      if constexpr (TAPU) ap[i] += ((int64_t)cih[i] * cg.W + ciw[i]) * cg.C + koff;
     }
   }
   // conv: this lane's k -> (kh, kw, c), advanced by BK per stage
   int kc = 0, kkw = 0, kkh = 0;
-  if constexpr (AL == A_CONV) {
-    const int k = (int)(kbeg + koff);
+  if constexpr (CONV) {
+    const int k = (int)(kbeg + (TAPU ? 0 : koff));  // TAPU: the stage's (uniform) first k
     kc = k % cg.C;
     const int t = k / cg.C;
     kkw = t % cg.KW;
     kkh = t / cg.KW;
   }
+  // TAPU: the stage's tap displacement and input offset (block-uniform)
+  int tdh = kkh * cg.dh, tdw = kkw * cg.dw;
+  int64_t toff = ((int64_t)tdh * cg.W + tdw) * cg.C + kc;
   const char* bbase = reinterpret_cast<const char*>(BL == B_KC ? B + n0 * g.ldb + kbeg : B + kbeg * g.ldb + n0);
   uint32_t boff[BI];
   bool bok[BI];
@@ -203,13 +215,32 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void g2_tile(GemmArgs g, int til
       if constexpr (AL == A_KCONTIG) {
         src = reinterpret_cast<const float*>(abase + aoff[i]);
         if constexpr (CHECK) src = (aok[i] & kok) ? src : zero;
+      } else if constexpr (TAPU) {
+        const int ih = cih[i] + tdh, iw = ciw[i] + tdw;
+        const bool ok = aok[i] & kok & ((unsigned)ih < (unsigned)cg.H) & ((unsigned)iw < (unsigned)cg.W);
+        // an arithmetic select: written as `ok ? p : zero` the compiler sinks
+        // the address math into an exec-masked branch per piece
+        const uint64_t msk = 0ull - (uint64_t)ok;
+        src = reinterpret_cast<const float*>((reinterpret_cast<uint64_t>(ap[i] + toff) & msk) |
+                                             (reinterpret_cast<uint64_t>(zero) & ~msk));
       } else {
         const int ih = cih[i] + kkh * cg.dh, iw = ciw[i] + kkw * cg.dw;
         const bool ok = aok[i] & kok & (ih >= 0) & (ih < cg.H) & (iw >= 0) & (iw < cg.W);
         src = ok ? ap[i] + ((ih * cg.W + iw) * cg.C + kc) : zero;
       }
       glds16(src, base + (wave * AI + i) * 1024);
-      if (AL == A_CONV && i == AI - 1) {
+      if (TAPU && i == AI - 1) {
+        // the next stage's tap: one step of the uniform (c0, kw, kh) counter
+        const bool wrap = kc + BK >= cg.C;
+        kc = wrap ? 0 : kc + BK;
+        const int w1 = kkw + (wrap ? 1 : 0);
+        const bool wrap2 = w1 == cg.KW;
+        kkw = wrap2 ? 0 : w1;
+        kkh = kkh + (wrap2 ? 1 : 0);
+        tdh = kkh * cg.dh;
+        tdw = kkw * cg.dw;
+        toff = ((int64_t)tdh * cg.W + tdw) * cg.C + kc;
+      } else if (CONV && i == AI - 1) {
         // advance (kc, kkw, kkh) by BK; C >= 4, so at most BK / 4 carries:
         // a fixed, select-only sequence (no data-dependent loop)
         kc += BK;
