@@ -68,6 +68,22 @@ def _launcher():
     spec.loader.exec_module(mod)
     return mod
 
+def _chosen_tiles():
+    """The f32 tiles the MatMul ran on: per GEMM shape (M, N, K) the tile in
+    force (kernels/gemm.hip autotuner, started from the shipped gfx950
+    defaults in tensorframes_amd/tiles/gfx950.json)."""
+    from tensorframes_amd import _native
+    _C = _native._C
+    out = []
+    for key, tile in _C.gemm_tune_table():
+        if key[1] == DIM and key[2] == DIM:
+            bm, bn, core = _C.gemm_tile_dims(tile)
+            dflt = [e["tile"] for e in _native.default_entries() if e["key"] == list(key)]
+            out.append({"M": key[0], "N": key[1], "K": key[2], "tile": tile, "dims": f"{bm}x{bn}",
+                        "core": "g2" if core == 2 else "round4", "default": dflt[0] if dflt else None})
+    return out
+
+
 def main():
     args = parse()
     spawn_if_needed = _launcher().spawn_if_needed
@@ -225,6 +241,7 @@ def rank_main(args):
             "gemm_tflops_device_resident": None if dev_rows_per_s is None else dev_rows_per_s * 2 * DIM * DIM / 1e12,
             "max_abs_err": err,
             "rank0_numa_bound_cpus": len(numa_cpus),
+            "gemm_tiles": _chosen_tiles() if use_gpu else None,
         }
         print(json.dumps(out))
     dist.shutdown()

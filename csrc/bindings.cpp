@@ -759,6 +759,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_direct", [](bool on) { k::set_conv_direct(on ? 1 : 0); },
         "route narrow wide-image convs (C in {32, 64}, OC <= 64) to the direct LDS-filter kernel (default on)");
   m.def("gemm_tile_count", [] { return k::gemm_tile_count(); });
+  m.def("gemm_tune_table", &k::gemm_tune_table, "the autotuner's tile picks: [(20-field shape key, tile)]");
+  m.def("gemm_tune_seed", &k::gemm_tune_seed, py::arg("key"), py::arg("tile"),
+        "a shipped default tile for a shape key (replaced only by a >= 2 % win confirmed twice)");
+  m.def("gemm_tune_reset", &k::gemm_tune_reset, "forget the autotuner's picks (the defaults stay)");
+  m.def("gemm_tile_dims", &k::gemm_tile_dims, py::arg("tile"), "{BM, BN, core}");
   m.def("roundtrip_graphdef",
         [](py::bytes b) { return py::bytes(serialize_graphdef(parse_graphdef(std::string(b)))); });
   m.def("decode_tensor_proto", [](py::bytes b) {

@@ -191,6 +191,14 @@ std::map<TuneKey, int>& tune_cache() {
   static std::map<TuneKey, int> c;
   return c;
 }
+// the shipped gfx950 defaults (tensorframes_amd/tiles/gfx950.json, seeded at
+// import): a shape with a default keeps it unless a challenger wins by >= 2 %
+// in two independent timing passes, so boxes agree on the tile (and the
+// bits) instead of following timing noise
+std::map<TuneKey, int>& tune_defaults() {
+  static std::map<TuneKey, int> d;
+  return d;
+}
 bool autotune_on() {
   static const bool v = [] {
     const char* e = std::getenv("TFA_GEMM_AUTOTUNE");
@@ -231,30 +239,58 @@ F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, co
     if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f)
       reps = std::max(3, std::min(16, (int)std::ceil(1.0f / (ms / 3))));
   }
-  float cand_ms[kNumTiles];
-  for (int c = 0; c < kNumTiles; ++c) cand_ms[c] = 1e30f;
-  for (int round = 0; round < 3; ++round) {
-    for (int c = 0; c < kNumTiles; ++c) {
-      const F32Plan q = plan_for(c, g.M, g.N, g.K, g.batch);
-      if (q.splits != 1) continue;
-      if (c >= kFirstG2 && !g2_ok(g, al, vec)) continue;
-      if (c != heur.cfg && kTiles[c][1] >= 2 * g.N && kTiles[c][1] > 32) continue;  // mostly-padding tile
-      if (round == 0) launch_plan(q, g, al, vec, cg, s);  // warm
-      (void)hipEventRecord(e0, s);
-      for (int r = 0; r < reps; ++r) launch_plan(q, g, al, vec, cg, s);
-      (void)hipEventRecord(e1, s);
-      float ms = 0.f;
-      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
-      cand_ms[c] = std::min(cand_ms[c], ms / reps);
-    }
+  int dflt = -1;
+  {
+    std::lock_guard<std::mutex> lk(tune_mu());
+    auto it = tune_defaults().find(key);
+    if (it != tune_defaults().end() && it->second >= 0 && it->second < kNumTiles &&
+        plan_for(it->second, g.M, g.N, g.K, g.batch).splits == 1 && (it->second < kFirstG2 || g2_ok(g, al, vec)))
+      dflt = it->second;
   }
-  int best = heur.cfg;
+  const int base = dflt >= 0 ? dflt : heur.cfg;
+  // times every eligible candidate (or only `only`, >= 0) `rounds` times, interleaved
+  auto time_tiles = [&](float* cand_ms, int only_a, int only_b) {
+    for (int c = 0; c < kNumTiles; ++c) cand_ms[c] = 1e30f;
+    for (int round = 0; round < 3; ++round) {
+      for (int c = 0; c < kNumTiles; ++c) {
+        if (only_a >= 0 && c != only_a && c != only_b) continue;
+        const F32Plan q = plan_for(c, g.M, g.N, g.K, g.batch);
+        if (q.splits != 1) continue;
+        if (c >= kFirstG2 && !g2_ok(g, al, vec)) continue;
+        if (c != base && kTiles[c][1] >= 2 * g.N && kTiles[c][1] > 32) continue;  // mostly-padding tile
+        if (round == 0) launch_plan(q, g, al, vec, cg, s);  // warm
+        (void)hipEventRecord(e0, s);
+        for (int r = 0; r < reps; ++r) launch_plan(q, g, al, vec, cg, s);
+        (void)hipEventRecord(e1, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+        cand_ms[c] = std::min(cand_ms[c], ms / reps);
+      }
+    }
+  };
+  float cand_ms[kNumTiles];
+  time_tiles(cand_ms, -1, -1);
+  int best = base;
   for (int c = 0; c < kNumTiles; ++c)
     if (cand_ms[c] < cand_ms[best]) best = c;
+  bool replaced = false;
+  if (dflt >= 0 && best != dflt) {
+    // a challenger to the shipped default: >= 2 % faster, and again in a
+    // second, independent pass over the two
+    bool keep = !(cand_ms[best] <= 0.98f * cand_ms[dflt]);
+    if (!keep) {
+      float again[kNumTiles];
+      time_tiles(again, dflt, best);
+      keep = !(again[best] <= 0.98f * again[dflt]);
+    }
+    replaced = !keep;
+    if (keep) best = dflt;
+  }
   static const bool log = std::getenv("TFA_GEMM_TUNE_LOG") != nullptr;
   if (log) {
-    std::fprintf(stderr, "[gemm tune] M=%lld N=%lld K=%lld al=%d conv=%dx%dx%d heur=%d best=%d |",
-                 (long long)g.M, (long long)g.N, (long long)g.K, al, cg.H, cg.W, cg.C, heur.cfg, best);
+    std::fprintf(stderr, "[gemm tune] M=%lld N=%lld K=%lld al=%d conv=%dx%dx%d heur=%d default=%d%s best=%d |",
+                 (long long)g.M, (long long)g.N, (long long)g.K, al, cg.H, cg.W, cg.C, heur.cfg, dflt,
+                 replaced ? " (replaced)" : "", best);
     for (int c = 0; c < kNumTiles; ++c)
       if (cand_ms[c] < 1e29f) std::fprintf(stderr, " %d:%.4f", c, cand_ms[c]);
     std::fprintf(stderr, "\n");
@@ -340,6 +376,32 @@ void set_gemm_tile(int cfg) {
   forced_tile().store(cfg);
 }
 int gemm_tile_count() { return kNumTiles; }
+
+std::vector<std::pair<std::vector<int64_t>, int>> gemm_tune_table() {
+  std::lock_guard<std::mutex> lk(tune_mu());
+  std::vector<std::pair<std::vector<int64_t>, int>> v;
+  for (const auto& kv : tune_cache()) v.emplace_back(std::vector<int64_t>(kv.first.begin(), kv.first.end()), kv.second);
+  return v;
+}
+
+void gemm_tune_seed(const std::vector<int64_t>& key, int cfg) {
+  TFA_CHECK(key.size() == std::tuple_size<TuneKey>::value, "gemm_tune_seed: key of ", key.size(), " fields");
+  TFA_CHECK(cfg >= 0 && cfg < kNumTiles, "gemm_tune_seed: tile ", cfg, " out of range");
+  TuneKey k;
+  std::copy(key.begin(), key.end(), k.begin());
+  std::lock_guard<std::mutex> lk(tune_mu());
+  tune_defaults()[k] = cfg;
+}
+
+void gemm_tune_reset() {
+  std::lock_guard<std::mutex> lk(tune_mu());
+  tune_cache().clear();
+}
+
+std::vector<int> gemm_tile_dims(int cfg) {
+  TFA_CHECK(cfg >= 0 && cfg < kNumTiles, "gemm_tile_dims: tile ", cfg, " out of range");
+  return {kTiles[cfg][0], kTiles[cfg][1], cfg >= kFirstG2 ? 2 : 1};
+}
 
 void set_f32_precision(int mode) {
   TFA_CHECK(mode >= 0 && mode <= 2, "precision mode must be 0 (f32), 1 (bf16) or 2 (bf16x3)");

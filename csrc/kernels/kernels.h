@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
+#include <vector>
 
 #include "../common.h"
 
@@ -229,6 +231,12 @@ void set_f32_precision(int mode);
 // Force one tile of the f32 core (-1 = heuristic + autotuner); for tests/tuning.
 void set_gemm_tile(int cfg);
 int gemm_tile_count();
+// the autotuner's picks ({20-field shape key, tile}) and the shipped defaults
+// it starts from (a default is replaced only by a >= 2 % win, confirmed twice)
+std::vector<std::pair<std::vector<int64_t>, int>> gemm_tune_table();
+void gemm_tune_seed(const std::vector<int64_t>& key, int cfg);
+void gemm_tune_reset();
+std::vector<int> gemm_tile_dims(int cfg);  // {BM, BN, core (1 round-4, 2 g2)}
 int f32_precision();
 
 // ------------------------------------------------------------ conv / pool (NHWC)

@@ -48,7 +48,9 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
     ap.add_argument("--vendor", action="store_true", help="also time MIOpen (F.conv2d, channels_last, exact f32)")
+    ap.add_argument("--only", type=int, default=-1, help="run only unique layer #i (counter runs)")
     a = ap.parse_args()
+    from tensorframes_amd._native import _C
     torch.backends.cudnn.allow_tf32 = False
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
@@ -57,7 +59,10 @@ def main():
     for l in layers:
         uniq.setdefault(l[:8], []).append(l[8])
     res, tot_ms, tot_fl = [], 0.0, 0.0
-    for (h, w, c, kh, kw, oc, s, pad), names in uniq.items():
+    for li, ((h, w, c, kh, kw, oc, s, pad), names) in enumerate(uniq.items()):
+        if a.only >= 0 and li != a.only:
+            continue
+        before = {tuple(k): t for k, t in _C.gemm_tune_table()}
         g = tf.Graph()
         with g.as_default():
             x = tf.placeholder(tf.float32, [None, h, w, c], name="x")
@@ -83,8 +88,13 @@ def main():
         n = len(names)
         tot_ms += ms * n
         tot_fl += fl * n
-        r = {"layer": names[0], "count": n, "H": h, "W": w, "C": c, "KH": kh, "KW": kw, "OC": oc, "stride": s,
-             "pad": pad, "M": a.batch * oh * ow, "K": kh * kw * c, "ms": ms, "tflops": fl / ms / 1e9}
+        new = [(k, t) for k, t in _C.gemm_tune_table() if tuple(k) not in before]
+        tile = new[0][1] if len(new) == 1 else (None if not new else [t for _, t in new])
+        dims = _C.gemm_tile_dims(tile) if isinstance(tile, int) else None
+        r = {"index": li, "layer": names[0], "count": n, "H": h, "W": w, "C": c, "KH": kh, "KW": kw, "OC": oc,
+             "stride": s, "pad": pad, "M": a.batch * oh * ow, "K": kh * kw * c, "ms": ms, "tflops": fl / ms / 1e9,
+             "tile": tile, "tile_dims": None if dims is None else f"{dims[0]}x{dims[1]}",
+             "core": None if dims is None else ("g2" if dims[2] == 2 else "round4")}
         if a.vendor:
             import torch.nn.functional as F
             xn = xin.permute(0, 3, 1, 2)
