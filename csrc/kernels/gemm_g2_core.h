@@ -64,10 +64,10 @@ void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStr
 // accumulators per lane and one block per CU; the smaller ones are sized
 // (<= 256 registers, <= 80 KB of LDS) for two, so one block's prologue and
 // epilogue overlap the other's main loop (K = 512 GEMMs, the convs)
-constexpr int kNumG2Tiles = 6;
+constexpr int kNumG2Tiles = 7;
 constexpr int kG2Tiles[kNumG2Tiles][6] = {
-    {256, 256, 2, 2, 4, 1}, {256, 192, 2, 2, 4, 1}, {256, 128, 2, 2, 3, 2},
-    {256, 64, 4, 1, 4, 2},  {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2}};
+    {256, 256, 2, 2, 4, 1}, {256, 192, 2, 2, 4, 1}, {256, 128, 2, 2, 3, 2}, {256, 64, 4, 1, 4, 2},
+    {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2},  {128, 192, 2, 2, 4, 2}};
 
 namespace {
 
@@ -478,7 +478,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 2: TFA_G2(2); break;
     case 3: TFA_G2(3); break;
     case 4: TFA_G2(4); break;
-    default: TFA_G2(5); break;
+    case 5: TFA_G2(5); break;
+    default: TFA_G2(6); break;
   }
 #undef TFA_G2
 }
