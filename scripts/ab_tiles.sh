@@ -2,7 +2,7 @@
 # round 5: forced-tile A/B of single shapes (gemm_one.py): AB="name|tiles|args;..."
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/r5/ab
+mkdir -p gpurun_out/r5/ab  # (scripts/gpu_steps.sh step `ab`)
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 if [ -n "${TESTS:-}" ]; then
   timeout -k 10 400 python -u -m pytest $TESTS -x -q --timeout 300 --timeout-method thread > gpurun_out/r5/ab/tests.log 2>&1 || { tail -20 gpurun_out/r5/ab/tests.log; exit 1; }

@@ -65,6 +65,24 @@ for s in ${STEPS:-tests}; do
     incep_sweep) for b in 256 512 1024 2048; do run incep_b$b 600 python bench/configs.py inception --source device --rows 8192 --batch $b --steps 2 --warmup 1; done ;;
     incep_host_sweep) for c in 256 1024; do run incep_host_c$c 900 python bench/configs.py inception --rows 65536 --batch 2048 --chunk-images $c --steps 1 --warmup 1; done ;;
     incep) run incep 900 python bench/configs.py inception --source device --rows ${INC_ROWS:-8192} --batch ${INC_BATCH:-512} --steps 1 --warmup 1 ;;
+    # ---- presets (the one-off round-4/5 step lists, folded in)
+    final) STEPS=smoke bash scripts/gpu_check.sh && run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
+      run bench 900 python bench.py --steps 5 --warmup 2 &&
+      run incep_dev 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
+    prec) run prec 300 python -u -m pytest tests/test_gpu_precision.py tests/test_gpu_g2.py -x -q --timeout 300 --timeout-method thread ;;
+    tile_ab) run tile_ab 900 bash scripts/tile_ab.sh ;;                    # SHAPES=<file> TILES="auto 16 28 ..."
+    ab) run ab 900 bash scripts/ab_tiles.sh ;;                             # AB="name|tiles|gemm_one args;..."
+    g2_ab) run g2_ab 1100 bash scripts/r5_g2_check.sh ;;                   # TILES / HEAD_TILES / CONV_TILES / SKIP_BENCH
+    pmc_g2) run pmc_g2 900 bash scripts/r5_pmc_g2.sh ;;                    # g2 lab vs g2 core vs round-4 counters
+    tile_table) run tile_table 1000 python scripts/tile_table.py --out gpurun_out/gfx950.json ;;
+    layers_time) PART=time run layers_time 700 bash scripts/r5_layers.sh ;;
+    layers_pmc) PART="pmc ${FIRST:-0} ${LAST:-21}" run layers_pmc 1150 bash scripts/r5_layers.sh ;;
+    img) run img_tests 300 python -u -m pytest tests/test_gpu_image_prep.py tests/test_jpeg_native.py tests/test_gpu_string_keys.py -x -v -s --timeout 200 --timeout-method thread &&
+      run read_image4k 400 python examples/read_image.py --images 4096 &&
+      TFA_PRECISION=bf16x3 run read_image4k_bf16x3 400 python examples/read_image.py --images 4096 ;;
+    decode_bench) run decode_bench 300 python scripts/decode_bench.py --images 1024 ;;
+    pool) run pool 400 python -u -m pytest tests/test_gpu_pool_accounting.py tests/test_multirank_gpu.py tests/test_gpu_engine.py -x -v --timeout 200 --timeout-method thread ;;
+    lab_g2) run lab_g2 600 bash scripts/lab_g2.sh ;;
   esac
 done
 echo "all steps done"
