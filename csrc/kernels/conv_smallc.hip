@@ -50,7 +50,9 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
   float b[KS][TN];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    const int k = 2 * s + h;
+    // k-step s pairs k = 8(s/4) + s%4 (lanes 0-31) with k + 4 (lanes 32-63),
+    // the f32 GEMM cores' order (gemm_g2_core.h), so results match them bitwise
+    const int k = 8 * (s >> 2) + (s & 3) + 4 * h;
     if (k < p.K) {
       const int c = k % p.C, t = k / p.C;
       tdy[s] = (t / p.KW) * p.dh;
@@ -182,10 +184,10 @@ void conv_smallc_launch(const ConvArgs& a, hipStream_t s) {
   p.fOW = make_fastdiv((uint32_t)a.OW);
   p.fOH = make_fastdiv((uint32_t)a.OH);
   const int tn = a.OC <= 32 ? 1 : 2;
-  const int ks = (p.K + 1) / 2;
+  const int ks = 4 * ((p.K + 7) / 8);  // whole k octets
   if (ks <= 4) launch_ks<4>(p, tn, s);
   else if (ks <= 8) launch_ks<8>(p, tn, s);
-  else if (ks <= 14) launch_ks<14>(p, tn, s);
+  else if (ks <= 12) launch_ks<12>(p, tn, s);
   else launch_ks<16>(p, tn, s);
   TFA_LAUNCH_CHECK("conv2d small-C");
 }
