@@ -64,10 +64,10 @@ void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStr
 // accumulators per lane and one block per CU; the smaller ones are sized
 // (<= 256 registers, <= 80 KB of LDS) for two, so one block's prologue and
 // epilogue overlap the other's main loop (K = 512 GEMMs, the convs)
-constexpr int kNumG2Tiles = 7;
+constexpr int kNumG2Tiles = 8;
 constexpr int kG2Tiles[kNumG2Tiles][6] = {
     {256, 256, 2, 2, 4, 1}, {256, 192, 2, 2, 4, 1}, {256, 128, 2, 2, 3, 2}, {256, 64, 4, 1, 4, 2},
-    {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2},  {128, 192, 2, 2, 4, 2}};
+    {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2},  {128, 192, 2, 2, 4, 2}, {256, 96, 4, 1, 3, 2}};
 
 namespace {
 
@@ -91,12 +91,17 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void g2_tile(GemmArgs g, int til
                                                              int64_t k_per_split, int flags) {
   constexpr int NW = WM * WN, NT = 64 * NW, BK = 16, KQ = BK / 4;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4, STAGE = A_BYTES + B_BYTES;
-  constexpr int AI = BM / 16 / NW;  // A: 16 rows per LDS-DMA instruction
-  constexpr int BI = BN / 16 / NW;  // B: 16 rows ([N][K]) or 256 floats ([K][N]) per instruction
-  constexpr int G = AI + BI;         // LDS-DMA instructions per wave per stage
+  constexpr int AI = BM / 16 / NW;        // A: 16 rows per LDS-DMA instruction
+  constexpr int BREAL = BN / 16;          // B: 16 rows ([N][K]) or 256 floats ([K][N]) per instruction
+  constexpr int BI = (BREAL + NW - 1) / NW;
+  // a B width that does not split evenly over the waves (96): the last
+  // waves issue dummy pieces into a pad area, so every wave issues the same
+  // G instructions per stage and the counted vmcnt waits stay uniform
+  constexpr int BPAD = BI * NW - BREAL;
+  constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4, STAGE = A_BYTES + B_BYTES + BPAD * 1024;
+  constexpr int G = AI + BI;              // LDS-DMA instructions per wave per stage
   constexpr int kEpi = NW * 32 * 32 * 4;
-  static_assert(NW == 4 && TM >= 1 && TN >= 1 && AI >= 1 && BI >= 1 && BM % (16 * NW) == 0 && BN % (16 * NW) == 0,
+  static_assert(NW == 4 && TM >= 1 && TN >= 1 && AI >= 1 && BI >= 1 && BM % (16 * NW) == 0 && BN % 16 == 0,
                 "4 waves, >= one 32x32 tile each, whole DMA instructions per wave");
   static_assert(STAGES >= 3 && STAGES * STAGE <= 160 * 1024 / OCC && STAGES * STAGE >= kEpi, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
@@ -185,7 +190,11 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void g2_tile(GemmArgs g, int til
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     const int q = wave * BI + i;
-    if constexpr (BL == B_KC) {
+    if (q >= BREAL) {  // a pad piece: any valid source (B's first row), or the zero page when checked
+      bok[i] = false;
+      boff[i] = 0;
+      bk_[i] = 0;
+    } else if constexpr (BL == B_KC) {
       const int r = q * 16 + lane / 4;
       bok[i] = n0 + r < N;
       boff[i] = (uint32_t)(((int64_t)r * g.ldb + koff) * 4);
@@ -479,7 +488,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 3: TFA_G2(3); break;
     case 4: TFA_G2(4); break;
     case 5: TFA_G2(5); break;
-    default: TFA_G2(6); break;
+    case 6: TFA_G2(6); break;
+    default: TFA_G2(7); break;
   }
 #undef TFA_G2
 }
