@@ -95,3 +95,28 @@ def test_non_jpeg_cells_fail_the_header_pass():
     assert not job.header_ok and job.bad_header == 2
     with pytest.raises(Exception):
         _C.jpeg_decode(buf.getvalue(), 3)
+
+
+def test_concurrent_batches_share_the_pool():
+    """Several batches in flight at once (the pre-stage keeps the next chunk
+    decoding while the current one is consumed) all complete, each into its
+    own buffer."""
+    cells = _jpegs(24, seed=11)
+    jobs = [_C.JpegBatch(cells[i::3], 3, 4, False) for i in range(3)]
+    for i, job in enumerate(jobs):
+        assert job.wait() == []
+        hb = job.buffer.numpy()
+        for j, c in enumerate(cells[i::3]):
+            want = decode_image(c, 3)
+            o = job.meta_bytes + job.pixel_offset(j)
+            assert np.array_equal(hb[o:o + want.size].reshape(want.shape), want)
+
+
+def test_batch_outlives_dropped_job():
+    """A JpegBatch dropped before wait() must not leave tasks writing into
+    freed memory: the destructor waits for its tasks."""
+    cells = _jpegs(16, seed=12)
+    for _ in range(5):
+        job = _C.JpegBatch(cells, 3, 4, False)
+        del job
+    assert _C.decode_pool_threads() >= 1
