@@ -653,11 +653,22 @@ class _ImagePrep:
         self.oy, self.ox, self.h, self.w, self.ops = oy, ox, h, w, ops
         self._inflight: List[tuple] = []  # (event, pinned buffer) of copies not yet known done
 
-    def run(self, imgs, dev) -> torch.Tensor:
+    def channels(self, hf=None) -> Optional[int]:
+        """The channel count the chain fixes (a Slice size or a per-channel
+        constant), else the decoder's (`channels` 1 / 3 / 4), else None."""
+        if self.C is not None:
+            return self.C
+        return hf.channels if hf is not None and hf.channels in (1, 3, 4) else None
+
+    def run(self, imgs, dev) -> Optional[torch.Tensor]:
+        """None when the chunk's images do not share one uint8 [H, W, C]
+        layout the chain accepts (e.g. gray and RGB files under
+        `channels=0`): the caller then runs those rows one by one."""
         arrs = [np.asarray(t) for t in imgs]
-        for a in arrs:
-            _check(a.ndim == 3 and a.shape[2] == self.C and a.dtype == np.uint8,
-                   f"image pre-stage: decoded image of shape {a.shape} / {a.dtype}, [H, W, {self.C}] uint8 expected")
+        C = self.C if self.C is not None else (arrs[0].shape[2] if arrs and arrs[0].ndim == 3 else None)
+        if C is None or any(a.ndim != 3 or a.shape[2] != C or a.dtype != np.uint8 for a in arrs) or \
+                any(len(v) not in (1, C) for _, v in self.ops):
+            return None
         sizes = np.array([a.size for a in arrs], dtype=np.int64)
         offs = np.zeros(len(arrs), dtype=np.int64)
         np.cumsum(sizes[:-1], out=offs[1:])
@@ -670,11 +681,11 @@ class _ImagePrep:
         hb[:offs.nbytes] = offs.view(np.uint8)
         hb[offs.nbytes:mbytes] = hw.reshape(-1).view(np.uint8)
         np.concatenate([a.reshape(-1) for a in arrs], out=hb[mbytes:])
-        return self.run_packed(buf, offs.nbytes, mbytes, dev)
+        return self.run_packed(buf, offs.nbytes, mbytes, dev, C)
 
-    def run_packed(self, buf: torch.Tensor, offs_nbytes: int, mbytes: int, dev) -> torch.Tensor:
+    def run_packed(self, buf: torch.Tensor, offs_nbytes: int, mbytes: int, dev, C: int) -> torch.Tensor:
         """`buf` = [int64 offsets | int32 hw pairs | pixels] in pinned memory
-        (the layout _C.JpegBatch decodes into)."""
+        (the layout _C.JpegBatch decodes into), C channels per pixel."""
         d = engine.device_empty(buf.numel(), torch.uint8, dev)
         d.copy_(buf, non_blocking=True)
         # the pinned buffer returns to its pool only once its DMA has run
@@ -683,7 +694,7 @@ class _ImagePrep:
         self._inflight = [(e, b) for e, b in self._inflight if not e.query()] + [(ev, buf)]
         doffs = d[:offs_nbytes].view(torch.int64)
         dhw = d[offs_nbytes:mbytes].view(torch.int32)
-        return _C.ragged_image_prep(d[mbytes:], doffs, dhw, self.C, self.OH, self.OW, self.mode, self.oy, self.ox,
+        return _C.ragged_image_prep(d[mbytes:], doffs, dhw, C, self.OH, self.OW, self.mode, self.oy, self.ox,
                                     self.h, self.w, self.ops)
 
 
@@ -772,8 +783,8 @@ def _match_image_prep(graph_bytes: bytes, row_feeds: List[str], cut: str) -> Opt
         cur = nd.name
     if size is None or crop is None:
         return None
-    C = C or max([len(v) for _, v in ops] + [3])
-    if any(len(v) not in (1, C) for _, v in ops):
+    C = C or (max(len(v) for _, v in ops) if any(len(v) > 1 for _, v in ops) else None)  # None: the images'
+    if C is not None and any(len(v) not in (1, C) for _, v in ops):
         return None
     oy, ox, h, w = crop
     if oy + h > size[0] or ox + w > size[1]:
@@ -964,7 +975,7 @@ class _BatchCut:
                 _finish_jpeg_batch(job, raw[0], raw[1][a:a + step])
                 t1 = time.perf_counter()
                 with torch.cuda.stream(side):
-                    cut = [prep.run_packed(job.buffer, job.offsets_bytes, job.meta_bytes, dev)]
+                    cut = [prep.run_packed(job.buffer, job.offsets_bytes, job.meta_bytes, dev, native.C)]
                 engine.record_stream(cut[0], main)
                 t_in += t1 - t0
                 t_pre += time.perf_counter() - t1
@@ -977,12 +988,14 @@ class _BatchCut:
                 imgs = [row_inputs(i)[0] for i in rows]
                 t1 = time.perf_counter()
                 with torch.cuda.stream(side):
-                    cut = [prep.run(imgs, dev)]
-                engine.record_stream(cut[0], main)
+                    c = prep.run(imgs, dev)
+                if c is not None:
+                    cut = [c]
+                    engine.record_stream(c, main)
+                    metrics.add("map_rows_batched_prestage_rows", len(imgs))
                 t_in += t1 - t0
                 t_pre += time.perf_counter() - t1
-                metrics.add("map_rows_batched_prestage_rows", len(imgs))
-            for i in (rows if prep is None else ()):
+            for i in (rows if not cut else ()):
                 t0 = time.perf_counter()
                 feeds = row_inputs(i)
                 t1 = time.perf_counter()
@@ -1027,11 +1040,13 @@ class _BatchCut:
 def _native_jpeg(prep, raw):
     """start(a, n) -> a _C.JpegBatch decoding raw cells [a, a+n) (None when a
     cell is not a JPEG the native decoder takes), or None when the native
-    decode does not apply at all."""
-    if prep is None or raw is None or not config.native_jpeg_decode or prep.C not in (1, 3):
+    decode does not apply at all. start.C: the channel count it decodes to."""
+    if prep is None or raw is None or not config.native_jpeg_decode:
         return None
     hf, cells = raw
-    if hf.op not in ("DecodeJpeg", "DecodeImage") or hf.channels != prep.C or not _C.jpeg_native_available()[0]:
+    C = prep.channels(hf)
+    if hf.op not in ("DecodeJpeg", "DecodeImage") or C not in (1, 3) or hf.channels != C or \
+            not _C.jpeg_native_available()[0]:
         return None
     threads = config.decode_threads or min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
                                            else (os.cpu_count() or 1))
@@ -1040,8 +1055,9 @@ def _native_jpeg(prep, raw):
         chunk = cells[a:a + n]
         if not all(isinstance(c, (bytes, bytearray)) for c in chunk):
             return None
-        job = _C.JpegBatch(list(chunk), prep.C, threads, True)
+        job = _C.JpegBatch(list(chunk), C, threads, True)
         return job if job.header_ok else None
+    start.C = C
     return start
 
 
