@@ -64,10 +64,11 @@ void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStr
 // accumulators per lane and one block per CU; the smaller ones are sized
 // (<= 256 registers, <= 80 KB of LDS) for two, so one block's prologue and
 // epilogue overlap the other's main loop (K = 512 GEMMs, the convs)
-constexpr int kNumG2Tiles = 8;
+constexpr int kNumG2Tiles = 9;
 constexpr int kG2Tiles[kNumG2Tiles][6] = {
     {256, 256, 2, 2, 4, 1}, {256, 192, 2, 2, 4, 1}, {256, 128, 2, 2, 3, 2}, {256, 64, 4, 1, 4, 2},
-    {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2},  {128, 192, 2, 2, 4, 2}, {256, 96, 4, 1, 3, 2}};
+    {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2},  {128, 192, 2, 2, 4, 2}, {256, 96, 4, 1, 3, 2},
+    {128, 160, 4, 1, 4, 2}};
 
 namespace {
 
@@ -489,7 +490,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 4: TFA_G2(4); break;
     case 5: TFA_G2(5); break;
     case 6: TFA_G2(6); break;
-    default: TFA_G2(7); break;
+    case 7: TFA_G2(7); break;
+    default: TFA_G2(8); break;
   }
 #undef TFA_G2
 }
