@@ -582,6 +582,14 @@ ShmComm::ShmComm(const std::string& name, int rank, int size, int64_t slot_bytes
       shm_unlink(name.c_str());
       TFA_CHECK(false, "ShmComm: ftruncate failed: ", std::strerror(e));
     }
+    // reserve the tmpfs pages now: a /dev/shm too small for the segment then
+    // fails here (the ranks agree and fall back to gloo) instead of raising
+    // SIGBUS on the first touch of an unbacked page mid-collective
+    if (const int e = posix_fallocate(fd, 0, static_cast<off_t>(bytes_)); e != 0) {
+      close(fd);
+      shm_unlink(name.c_str());
+      TFA_CHECK(false, "ShmComm: cannot reserve ", bytes_, " bytes in /dev/shm: ", std::strerror(e));
+    }
   } else {
     fd = shm_open(name.c_str(), O_RDWR, 0600);
     TFA_CHECK(fd >= 0, "ShmComm: shm_open(", name, ") failed: ", std::strerror(errno));
