@@ -53,7 +53,9 @@ class Config:
     # map_rows: run same-shaped rows as one block through the lifted row graph
     map_rows_vectorize: bool = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_VECTORIZE", True, bool))
     # map_rows batch-of-one cut: rows whose cut tensors are concatenated into one batched run
-    map_rows_batch_rows: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_BATCH", 64, int))
+    # (JPEG -> VGG-16 on MI355X, f32 / bf16x3: 64 rows 3.6 / 4.9 k img/s, 256 rows 3.9 / 6.3 k,
+    # profiles/r5_img/; the 14x14 layers only fill the CUs at a few hundred images)
+    map_rows_batch_rows: int = dataclasses.field(default_factory=lambda: _env("TFA_MAP_ROWS_BATCH", 256, int))
     # map_rows image scoring: the per-row decode -> resize -> crop -> normalise
     # part of a chunk runs as ONE ragged-batch kernel (core._ImagePrep)
     map_rows_batched_prestage: bool = dataclasses.field(
