@@ -74,10 +74,14 @@ def default_entries(path: str = TILE_TABLE) -> list:
 def _seed_tile_defaults(path: str = TILE_TABLE) -> int:
     if os.environ.get("TFA_GEMM_DEFAULTS", "1") == "0":
         return 0
-    entries = default_entries(path)
-    for e in entries:
-        _C.gemm_tune_seed([int(v) for v in e["key"]], int(e["tile"]))
-    return len(entries)
+    n = 0
+    for e in default_entries(path):
+        try:  # a table from another build (more tiles, another key layout) must not break the import
+            _C.gemm_tune_seed([int(v) for v in e["key"]], int(e["tile"]))
+            n += 1
+        except Exception:  # noqa: BLE001
+            continue
+    return n
 
 
 def _dump_tune_table(path: str) -> None:
