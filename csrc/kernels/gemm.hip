@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
 // 2.5M x 512 x 512 134.8 -> 135.6 TF; a 2x4 128x256 never beat them.
 // 21 is 256x256 as 16 waves (4x4 waves of 64x64, 1024 threads, four waves
 // per SIMD in one block): 4096^3 141.2 TF, 8192^3 142.6 TF.
-// 22-30 are the g2 core (gemm_g2_core.h: one wave per SIMD or two-block
+// 22-31 are the g2 core (gemm_g2_core.h: one wave per SIMD or two-block
 // tiles, LDS-DMA staging, k-octet b128 fragments), kG2Tiles in order; used where its loaders apply
 // (k-contiguous A or the conv im2col with C % 4 == 0, 16-byte aligned rows).
 constexpr int kFirstG2 = 22;
@@ -96,9 +96,10 @@ constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}
                                       {256, 256}, {256, 256},
                                       // g2
                                       {256, 256}, {256, 192}, {256, 128}, {256, 64}, {128, 128}, {128, 64},
-                                      {128, 192}, {256, 96}, {128, 160}};
+                                      {128, 192}, {256, 96}, {128, 160}, {192, 192}};
 static_assert(g2::kG2Tiles[0][0] == 256 && g2::kG2Tiles[0][1] == 256 && g2::kG2Tiles[5][1] == 64 &&
-                  g2::kG2Tiles[6][1] == 192 && g2::kG2Tiles[7][1] == 96 && g2::kG2Tiles[8][1] == 160,
+                  g2::kG2Tiles[6][1] == 192 && g2::kG2Tiles[7][1] == 96 && g2::kG2Tiles[8][1] == 160 &&
+                  g2::kG2Tiles[9][0] == 192,
               "kTiles' g2 rows mirror kG2Tiles");
 
 // the g2 core's loaders: k-contiguous A (or the vec conv loader), 16-byte

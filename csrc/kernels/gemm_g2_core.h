@@ -60,15 +60,16 @@ constexpr int A_CONV16 = 100;
 void launch_kc(const F32Plan& p, const GemmArgs& g, hipStream_t s);
 void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStream_t s);
 
-// {BM, BN, WM, WN, STAGES, OCC}: OCC blocks per CU. The big tiles hold 192-256
+// {BM, BN, WM, WN, STAGES, OCC}: OCC blocks per CU. (192x192: the 12x12
+// Inception layers, M = 2048 * 144, make exactly 3 waves of two-block CUs.) The big tiles hold 192-256
 // accumulators per lane and one block per CU; the smaller ones are sized
 // (<= 256 registers, <= 80 KB of LDS) for two, so one block's prologue and
 // epilogue overlap the other's main loop (K = 512 GEMMs, the convs)
-constexpr int kNumG2Tiles = 9;
+constexpr int kNumG2Tiles = 10;
 constexpr int kG2Tiles[kNumG2Tiles][6] = {
     {256, 256, 2, 2, 4, 1}, {256, 192, 2, 2, 4, 1}, {256, 128, 2, 2, 3, 2}, {256, 64, 4, 1, 4, 2},
     {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2},  {128, 192, 2, 2, 4, 2}, {256, 96, 4, 1, 3, 2},
-    {128, 160, 4, 1, 4, 2}};
+    {128, 160, 4, 1, 4, 2}, {192, 192, 2, 2, 3, 2}};
 
 namespace {
 
@@ -491,7 +492,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 5: TFA_G2(5); break;
     case 6: TFA_G2(6); break;
     case 7: TFA_G2(7); break;
-    default: TFA_G2(8); break;
+    case 8: TFA_G2(8); break;
+    default: TFA_G2(9); break;
   }
 #undef TFA_G2
 }

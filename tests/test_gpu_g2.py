@@ -42,7 +42,7 @@ def forced():
 
 
 def test_g2_tiles_exist():
-    assert len(G2_TILES) == 9
+    assert len(G2_TILES) == 10
 
 
 @pytest.mark.parametrize("tb", [False, True])
