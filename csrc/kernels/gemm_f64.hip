@@ -345,6 +345,78 @@ __global__ __launch_bounds__(256) void pool2d_kernel(PoolArgs a, I n_items, Fast
   }
 }
 
+// 3x3 windows (every pool of Inception-v3), float4 channels, 32-bit indices:
+// the nine taps are unrolled with clamped in-bounds addresses, so each lane
+// has all nine 16-byte loads in flight before the first max/add (the generic
+// kernel's data-dependent window loops issue them one at a time). Taps outside
+// the image are masked out of the result; avg divides by the valid-tap count
+// (TF semantics). Same epilogue and concat-slice output as pool2d_kernel.
+//
+// XCD: one block per 256 items, and block b runs the items of block
+// xcd_remap64(b): the hardware deals consecutive blocks round-robin over the
+// 8 XCDs, so without the remap the output rows that share an input row run on
+// different XCDs and each XCD's L2 fetches that row again; with it every XCD
+// walks one contiguous range of output rows.
+template <bool MAX, bool XCD>
+__global__ __launch_bounds__(256) void pool3x3_v4_kernel(PoolArgs a, uint32_t n_items, FastDivU32 fCV,
+                                                          FastDivU32 fOW, FastDivU32 fOH) {
+  const float* x = static_cast<const float*>(a.x);
+  float* y = static_cast<float*>(a.y);
+  const uint32_t CV = (uint32_t)(a.C >> 2), OW = (uint32_t)a.OW, OH = (uint32_t)a.OH;
+  const int H = (int)a.H, W = (int)a.W, C = (int)a.C;
+  const uint32_t stride = XCD ? n_items : gridDim.x * blockDim.x;
+  const uint32_t first = XCD ? (uint32_t)xcd_remap64((int)blockIdx.x, (int)gridDim.x) * blockDim.x + threadIdx.x
+                             : blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t i = first; i < n_items; i += stride) {
+    const uint32_t pix = fdiv(i, fCV), cv = i - pix * CV;
+    const uint32_t t2 = fdiv(pix, fOW), ow = pix - t2 * OW;
+    const uint32_t nn = fdiv(t2, fOH), oh = t2 - nn * OH;
+    const int h0 = (int)oh * (int)a.sh - (int)a.pad_t, w0 = (int)ow * (int)a.sw - (int)a.pad_l;
+    const float* base = x + (uint32_t)((int)nn * H * W * C) + cv * 4;
+    float4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int dh = 0; dh < 3; ++dh) {
+      const int ih = h0 + dh;
+      const int ihc = min(max(ih, 0), H - 1);
+#pragma unroll
+      for (int dw = 0; dw < 3; ++dw) {
+        const int iw = w0 + dw;
+        const int iwc = min(max(iw, 0), W - 1);
+        ok[dh * 3 + dw] = ih == ihc && iw == iwc;
+        v[dh * 3 + dw] = *reinterpret_cast<const float4*>(base + (uint32_t)((ihc * W + iwc) * C));
+      }
+    }
+    const float init = MAX ? -INFINITY : 0.f;
+    float4 acc = make_float4(init, init, init, init);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const float4 u = ok[j] ? v[j] : make_float4(init, init, init, init);
+      if (MAX) {
+        acc.x = fmaxf(acc.x, u.x); acc.y = fmaxf(acc.y, u.y); acc.z = fmaxf(acc.z, u.z); acc.w = fmaxf(acc.w, u.w);
+      } else {
+        acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
+      }
+    }
+    float of[4] = {acc.x, acc.y, acc.z, acc.w};
+    if (!MAX) {
+      const int cnt = (min(h0 + 3, H) - max(h0, 0)) * (min(w0 + 3, W) - max(w0, 0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) of[j] = cnt > 0 ? of[j] / (float)cnt : 0.f;
+    }
+    if (a.bias) {
+      const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(a.bias) + cv * 4);
+      of[0] = act_fast(of[0] + b.x, a.act); of[1] = act_fast(of[1] + b.y, a.act);
+      of[2] = act_fast(of[2] + b.z, a.act); of[3] = act_fast(of[3] + b.w, a.act);
+    } else if (a.act) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) of[j] = act_fast(of[j], a.act);
+    }
+    float* dst = a.ldc ? y + (uint32_t)(pix * (uint32_t)a.ldc) + cv * 4 : y + i * 4;
+    *reinterpret_cast<float4*>(dst) = make_float4(of[0], of[1], of[2], of[3]);
+  }
+}
+
 template <bool MAX>
 void pool2d_launch(const PoolArgs& a, hipStream_t s) {
   const bool v4 = a.C % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
@@ -355,6 +427,24 @@ void pool2d_launch(const PoolArgs& a, hipStream_t s) {
   const dim3 grid(ew_grid(items)), block(256);
   const FastDivU32 fCV = make_fastdiv((uint32_t)(a.C / V)), fOW = make_fastdiv((uint32_t)a.OW),
                    fOH = make_fastdiv((uint32_t)a.OH);
+  static const bool generic = [] {
+    const char* e = std::getenv("TFA_POOL_GENERIC");
+    return e && e[0] == '1';
+  }();
+  const int64_t out_span = a.ldc ? a.N * a.OH * a.OW * a.ldc : a.N * a.OH * a.OW * a.C;
+  static const bool no_xcd = [] {
+    const char* e = std::getenv("TFA_POOL_XCD");
+    return e && e[0] == '0';
+  }();
+  if (v4 && small && a.KH == 3 && a.KW == 3 && out_span < (int64_t(1) << 31) && !generic) {
+    const int64_t nblk = (items + 255) / 256;
+    if (!no_xcd && nblk < (int64_t(1) << 30))
+      hipLaunchKernelGGL((pool3x3_v4_kernel<MAX, true>), dim3((unsigned)nblk), block, 0, s, a, (uint32_t)items, fCV,
+                         fOW, fOH);
+    else
+      hipLaunchKernelGGL((pool3x3_v4_kernel<MAX, false>), grid, block, 0, s, a, (uint32_t)items, fCV, fOW, fOH);
+    return;
+  }
   if (v4 && small)
     hipLaunchKernelGGL((pool2d_kernel<MAX, 4, uint32_t>), grid, block, 0, s, a, (uint32_t)items, fCV, fOW, fOH);
   else if (v4)

@@ -83,6 +83,14 @@ for s in ${STEPS:-tests}; do
     decode_bench) run decode_bench 300 python scripts/decode_bench.py --images 1024 ;;
     pool) run pool 400 python -u -m pytest tests/test_gpu_pool_accounting.py tests/test_multirank_gpu.py tests/test_gpu_engine.py -x -v --timeout 200 --timeout-method thread ;;
     lab_g2) run lab_g2 600 bash scripts/lab_g2.sh ;;
+    poolb)
+      TFA_POOL_GENERIC=1 run pool_generic 300 python scripts/pool_bench.py &&
+      TFA_POOL_XCD=0 run pool_3x3 300 python scripts/pool_bench.py &&
+      run pool_3x3_xcd 300 python scripts/pool_bench.py ;;
+    poolk) run poolk_tests 300 python -u -m pytest tests/test_gpu_pool_fusion.py tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread &&
+      TFA_POOL_GENERIC=1 run incep_dev_poolgen 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
+      run incep_dev_pool3 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
+      export TMPDIR=/tmp && run prof_incep 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_incep" -o run -- python bench/configs.py inception --source device --rows 8192 --steps 1 --warmup 1 ;;
   esac
 done
 echo "all steps done"
