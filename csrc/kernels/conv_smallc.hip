@@ -41,7 +41,7 @@ struct SmallConv {
   FastDivU32 fOW, fOH;
 };
 
-template <int KS, int TN>
+template <int KS, int TN, bool FAST>
 __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5, col = lane & 31;
@@ -79,6 +79,93 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
   const int64_t groups = (p.M + 31) / 32;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if constexpr (FAST) {
+    // every tap of every output pixel is inside the image (no padding, checked
+    // on the host) and input and output are < 4 GiB: a tap is one 32-bit add
+    // and one load off the uniform base, pixels past M re-read pixel 0 (never
+    // stored), and the epilogue is specialised per activation with one bounds
+    // test per group. Same k order and MFMA sequence: bitwise the generic path.
+    uint32_t tb[KS];
+    bool kv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      tb[s] = (uint32_t)toff[s] * 4u;
+      kv[s] = tdy[s] < (1 << 29);
+    }
+    const char* xb = reinterpret_cast<const char*>(p.x);
+    char* yb = reinterpret_cast<char*>(p.y);
+    const uint32_t M = (uint32_t)p.M, HWC = (uint32_t)(p.H * p.W * p.C), ldc = (uint32_t)p.ldc;
+    const uint32_t rs = (uint32_t)(p.sh * p.W * p.C), cs = (uint32_t)(p.sw * p.C);
+    auto run = [&](auto act_c) __attribute__((always_inline)) {
+      constexpr int ACT = decltype(act_c)::value;
+      for (uint32_t g0 = 2 * (uint32_t)wave0; g0 < (uint32_t)groups; g0 += 2 * (uint32_t)nwaves) {
+        float a[2][KS];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t m = (g0 + q) * 32 + col;
+          const uint32_t mm = m < M ? m : 0u;
+          const uint32_t t = fdiv(mm, p.fOW);
+          const uint32_t ow = mm - t * (uint32_t)p.OW;
+          const uint32_t n = fdiv(t, p.fOH);
+          const uint32_t oh = t - n * (uint32_t)p.OH;
+          const uint32_t ob = (n * HWC + oh * rs + ow * cs) * 4u;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const float v = *reinterpret_cast<const float*>(xb + (ob + tb[s]));
+            a[q][s] = kv[s] ? v : 0.f;
+          }
+        }
+        f32x16 acc[2][TN];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[q][j][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[q][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][s], b[s][j], acc[q][j], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (g0 + q >= (uint32_t)groups) break;
+          const uint32_t m0 = (g0 + q) * 32 + 4 * h;
+          const bool full = (g0 + q + 1) * 32 <= M;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const uint32_t n = 32 * j + col;
+            if (n >= (uint32_t)p.OC) continue;
+            const uint32_t base = m0 * ldc + n;
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              v[r] = acc[q][j][r] + bv[j];
+              if (ACT == ACT_RELU) v[r] = v[r] > 0.f ? v[r] : 0.f;
+              if (ACT == ACT_RELU6) v[r] = v[r] > 0.f ? (v[r] < 6.f ? v[r] : 6.f) : 0.f;
+            }
+            if (full) {  // straight-line stores; only the last group is partial
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                *reinterpret_cast<float*>(yb + (base + (uint32_t)((r & 3) + 8 * (r >> 2)) * ldc) * 4u) = v[r];
+            } else {
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
+                if (m0 + ro < M) *reinterpret_cast<float*>(yb + (base + ro * ldc) * 4u) = v[r];
+              }
+            }
+          }
+        }
+      }
+    };
+    if (p.act == ACT_RELU) run(std::integral_constant<int, ACT_RELU>{});
+    else if (p.act == ACT_RELU6) run(std::integral_constant<int, ACT_RELU6>{});
+    else run(std::integral_constant<int, ACT_NONE>{});
+    return;
+  }
   // two 32-pixel groups per pass: 2*KS independent loads in flight per lane
   for (int64_t g0 = 2 * wave0; g0 < groups; g0 += 2 * nwaves) {
     float a[2][KS];
@@ -133,15 +220,19 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
 }
 
 template <int KS>
-void launch_ks(const SmallConv& p, int tn, hipStream_t s) {
+void launch_ks(const SmallConv& p, int tn, bool fast, hipStream_t s) {
   const int64_t groups = (p.M + 31) / 32;
   const int64_t waves = (groups + 1) / 2;
   // enough waves to fill 256 CUs x 8 waves a few times over; grid-stride beyond
   const int64_t blocks = std::min<int64_t>((waves + 3) / 4, 256 * 16);
-  if (tn == 1)
-    hipLaunchKernelGGL((conv_smallc_kernel<KS, 1>), dim3((unsigned)blocks), dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_smallc_kernel<KS, 2>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+  const dim3 g((unsigned)blocks), b(256);
+  if (fast) {
+    if (tn == 1) hipLaunchKernelGGL((conv_smallc_kernel<KS, 1, true>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((conv_smallc_kernel<KS, 2, true>), g, b, 0, s, p);
+  } else {
+    if (tn == 1) hipLaunchKernelGGL((conv_smallc_kernel<KS, 1, false>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((conv_smallc_kernel<KS, 2, false>), g, b, 0, s, p);
+  }
 }
 
 // TFA_CONV_SMALLC=0 (or set_conv_smallc(0)) sends these convs to the
@@ -185,10 +276,19 @@ void conv_smallc_launch(const ConvArgs& a, hipStream_t s) {
   p.fOH = make_fastdiv((uint32_t)a.OH);
   const int tn = a.OC <= 32 ? 1 : 2;
   const int ks = 4 * ((p.K + 7) / 8);  // whole k octets
-  if (ks <= 4) launch_ks<4>(p, tn, s);
-  else if (ks <= 8) launch_ks<8>(p, tn, s);
-  else if (ks <= 12) launch_ks<12>(p, tn, s);
-  else launch_ks<16>(p, tn, s);
+  static const bool generic = [] {
+    const char* e = std::getenv("TFA_SMALLC_GENERIC");
+    return e && e[0] == '1';
+  }();
+  // all taps in bounds (VALID-style, no padding) and 32-bit byte offsets
+  const bool fast = !generic && a.pad_t == 0 && a.pad_l == 0 &&
+                    (a.OH - 1) * a.sh + (a.KH - 1) * a.dh <= a.H - 1 &&
+                    (a.OW - 1) * a.sw + (a.KW - 1) * a.dw <= a.W - 1 &&
+                    a.N * a.H * a.W * a.C * 4 < (int64_t(1) << 32) && p.M * p.ldc * 4 < (int64_t(1) << 32);
+  if (ks <= 4) launch_ks<4>(p, tn, fast, s);
+  else if (ks <= 8) launch_ks<8>(p, tn, fast, s);
+  else if (ks <= 12) launch_ks<12>(p, tn, fast, s);
+  else launch_ks<16>(p, tn, fast, s);
   TFA_LAUNCH_CHECK("conv2d small-C");
 }
 

@@ -87,6 +87,9 @@ for s in ${STEPS:-tests}; do
       TFA_POOL_GENERIC=1 run pool_generic 300 python scripts/pool_bench.py &&
       TFA_POOL_XCD=0 run pool_3x3 300 python scripts/pool_bench.py &&
       run pool_3x3_xcd 300 python scripts/pool_bench.py ;;
+    stemx) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
+      TFA_SMALLC_GENERIC=1 run stem_gen_l0 300 python scripts/conv_layers.py --only 0 &&
+      run stem_fast_l0 300 python scripts/conv_layers.py --only 0 ;;
     poolk) run poolk_tests 300 python -u -m pytest tests/test_gpu_pool_fusion.py tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread &&
       TFA_POOL_GENERIC=1 run incep_dev_poolgen 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
       run incep_dev_pool3 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&

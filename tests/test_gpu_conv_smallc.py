@@ -47,6 +47,8 @@ CASES = [  # n, h, w, c, kh, kw, oc, stride, pad, dil, relu
     (2, 23, 23, 2, 3, 3, 48, 1, "SAME", 2, True),     # dilation
     (5, 9, 9, 4, 2, 2, 7, 3, "SAME", 1, False),       # stride 3, tiny OC
     (1, 7, 5, 3, 1, 3, 33, 1, "VALID", 1, True),      # M not a multiple of 32
+    (3, 19, 21, 3, 3, 3, 40, 2, "VALID", 1, False),   # in-bounds fast path, no activation
+    (2, 16, 16, 2, 2, 2, 32, 2, "VALID", 2, True),    # fast path with dilation
 ]
 
 
