@@ -90,6 +90,9 @@ for s in ${STEPS:-tests}; do
     stemx) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run stem_gen_l0 300 python scripts/conv_layers.py --only 0 &&
       run stem_fast_l0 300 python scripts/conv_layers.py --only 0 ;;
+    headab) for i in 1 2; do
+        run head_default_$i 600 python bench.py --steps 3 --warmup 2 &&
+        TFA_GEMM_DEFAULTS=scripts/data/gfx950_t19.json run head_t19_$i 600 python bench.py --steps 3 --warmup 2 || exit 1; done ;;
     poolk) run poolk_tests 300 python -u -m pytest tests/test_gpu_pool_fusion.py tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread &&
       TFA_POOL_GENERIC=1 run incep_dev_poolgen 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
       run incep_dev_pool3 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&

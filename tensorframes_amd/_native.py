@@ -63,15 +63,23 @@ _C = load()
 TILE_TABLE = os.path.join(_PKG_DIR, "tiles", "gfx950.json")
 
 
-def default_entries(path: str = TILE_TABLE) -> list:
+def _table_path() -> str:
+    env = os.environ.get("TFA_GEMM_DEFAULTS", "1")
+    return env if env not in ("", "0", "1") else TILE_TABLE
+
+
+def default_entries(path: str = None) -> list:
     import json
+    path = path or _table_path()
     if not os.path.exists(path):
         return []
     with open(path) as f:
         return json.load(f).get("entries", [])
 
 
-def _seed_tile_defaults(path: str = TILE_TABLE) -> int:
+def _seed_tile_defaults(path: str = None) -> int:
+    """Seed the tuner with the shipped table, or with the table file that
+    TFA_GEMM_DEFAULTS names (A/B of entries); TFA_GEMM_DEFAULTS=0: none."""
     if os.environ.get("TFA_GEMM_DEFAULTS", "1") == "0":
         return 0
     n = 0
