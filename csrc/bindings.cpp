@@ -758,6 +758,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "route tiny-reduction convs (KH*KW*C <= 32) to the direct kernel (default on)");
   m.def("set_conv_direct", [](bool on) { k::set_conv_direct(on ? 1 : 0); },
         "route narrow wide-image convs (C in {32, 64}, OC <= 64) to the direct LDS-filter kernel (default on)");
+  m.def("set_conv_wino", [](bool on) { k::set_conv_wino(on ? 1 : 0); },
+        "Winograd F(2x2,3x3) for 3x3 stride-1 convs with constant filters (default on; TFA_CONV_ALGO=direct "
+        "turns it off). Plans built while it is off carry no Winograd filters.");
+  m.def("conv_wino_enabled", [] { return k::conv_wino_enabled(); });
+  m.def("set_wino_tile", [](int v) { k::set_wino_tile(v); },
+        "force the Winograd kernel variant: -1 auto, 0 = 64 tiles x 64 oc, 1 = 128 tiles x 32 oc");
+  m.def("conv_wino_filter", [](const at::Tensor& w) {
+          TFA_CHECK(w.dim() == 4 && w.size(0) == 3 && w.size(1) == 3 && w.scalar_type() == at::kFloat,
+                    "conv_wino_filter: HWIO [3,3,C,OC] float32");
+          at::Tensor wc = w.cpu().contiguous();
+          at::Tensor u = at::empty({16 * wc.size(2) * k::conv_wino_ocp(wc.size(3))}, wc.options());
+          k::conv_wino_filter(wc.data_ptr<float>(), wc.size(2), wc.size(3), u.data_ptr<float>());
+          return u;
+        }, "the planner's Winograd filter transform (fp64), [C/4][16][OCP][4] flattened (tests)");
   m.def("gemm_tile_count", [] { return k::gemm_tile_count(); });
   m.def("gemm_tune_table", &k::gemm_tune_table, "the autotuner's tile picks: [(20-field shape key, tile)]");
   m.def("gemm_tune_seed", &k::gemm_tune_seed, py::arg("key"), py::arg("tile"),

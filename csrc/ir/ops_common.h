@@ -88,10 +88,13 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
               const at::Tensor* bias, int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
 // sibling convs fused along OC (GPU): w0 = the members' filters concatenated
 // along OC, outs[k] = member k's output (NHWC, possibly a channel slice)
+// wino: the planner's Winograd F(2x2,3x3) filter of w0 (conv_wino_filter), or null
 void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,
-                         std::vector<at::Tensor>& outs, const std::vector<int>& acts);
+                         std::vector<at::Tensor>& outs, const std::vector<int>& acts,
+                         const at::Tensor* wino = nullptr);
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
-                int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr);
+                int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr,
+                const at::Tensor* wino = nullptr);
 // MaxPool/AvgPool with a fused bias + activation, into `out` (GPU; `out` may
 // be a channel slice of a concat output)
 void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Tensor* bias, int act,

@@ -85,6 +85,14 @@ void rows_batch(InferCtx& c) {
   for (auto& o : c.out) o.row = ok ? RowClass::ROW : RowClass::MIXED;
 }
 
+// the planner's Winograd filter: device-resident, f32, [C/4][16][OCP][4]
+const void* wino_filter_ptr(const at::Tensor& u, int64_t C, int64_t OC) {
+  TFA_CHECK(u.is_cuda() && u.scalar_type() == at::kFloat && u.is_contiguous() &&
+                u.numel() == 16 * C * k::conv_wino_ocp(OC),
+            "internal: Winograd filter layout");
+  return u.data_ptr();
+}
+
 }  // namespace
 
 // planner-fused pool step (GPU): Pool -> BiasAdd -> Relu/Relu6 in one pass,
@@ -117,7 +125,7 @@ void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Ten
 
 // shared with the planner's fused conv epilogue
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
-                int act, at::Tensor& out, const std::vector<EpiStep>* epi) {
+                int act, at::Tensor& out, const std::vector<EpiStep>* epi, const at::Tensor* wino) {
   Conv2DGeom g = conv_geom(c.node, x0.sizes().vec(), w0.sizes().vec());
   if (!c.gpu) {
     at::Tensor x = x0.permute({0, 3, 1, 2});
@@ -149,6 +157,7 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
                 out.stride(0) == out.size(1) * out.stride(1),
             "Conv2D: output must be NHWC-contiguous up to the channel stride");
   a.ldc = out.stride(2);
+  if (wino) a.wino = wino_filter_ptr(*wino, g.C, g.OC);
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
     work = c.alloc({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
@@ -158,7 +167,7 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
 }
 
 void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,
-                         std::vector<at::Tensor>& outs, const std::vector<int>& acts) {
+                         std::vector<at::Tensor>& outs, const std::vector<int>& acts, const at::Tensor* wino) {
   TFA_CHECK(c.gpu, "Conv2D siblings: GPU plans only");
   TFA_CHECK(!outs.empty() && outs.size() <= static_cast<size_t>(k::kMaxOutSegs), "Conv2D siblings: 1..",
             k::kMaxOutSegs, " outputs");
@@ -190,6 +199,7 @@ void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0,
   TFA_CHECK(begin == g.OC, "Conv2D siblings: outputs cover ", begin, " channels of ", g.OC);
   a.y = outs[0].data_ptr();
   a.ldc = outs[0].stride(2);
+  if (wino) a.wino = wino_filter_ptr(*wino, g.C, g.OC);
   if (g.N * g.OH * g.OW == 0) return;
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {

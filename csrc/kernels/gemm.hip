@@ -465,6 +465,10 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     bf16_gemm_launch(f32_precision(), g, !conv_is_pointwise(a), cg, s);
     return;
   }
+  if (conv_wino_eligible(a)) {  // 3x3 stride 1 with a planner-made Winograd filter
+    conv_wino_launch(a, s);
+    return;
+  }
   if (!conv_is_pointwise(a) && conv_smallc_eligible(a)) {  // RGB stems: filter in registers, no LDS
     conv_smallc_launch(a, s);
     return;

@@ -25,5 +25,9 @@ void conv_smallc_launch(const ConvArgs& a, hipStream_t s);
 // filter in LDS, A straight to registers; chosen by shape only
 bool conv_direct_eligible(const ConvArgs& a);
 void conv_direct_launch(const ConvArgs& a, hipStream_t s);
+// Winograd F(2x2,3x3) (conv_wino.hip): a.wino set by the planner, 3x3/s1,
+// C % 4 == 0, OC % 4 == 0, cheap epilogue, 16-byte aligned outputs
+bool conv_wino_eligible(const ConvArgs& a);
+void conv_wino_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace k
 }  // namespace tfa

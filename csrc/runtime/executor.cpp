@@ -187,6 +187,9 @@ struct Program::Step {
     int act;  // this member's epilogue activation (members may differ)
   };
   std::vector<Sib> sibs;
+  // Winograd F(2x2,3x3) filter of this CONV step (plan-made constant slot, or
+  // -1): 3x3 stride-1 convs whose filter is a constant (conv_wino.hip)
+  int wino_slot = -1;
 };
 
 struct Program::Plan {
@@ -217,6 +220,7 @@ struct Program::Plan {
   std::map<int, std::set<void*>> used_streams;
   int fused = 0;
   int fused_siblings = 0;  // convs folded into sibling-fused steps
+  int wino_convs = 0;      // Winograd filters made (one per distinct 3x3 s1 filter)
   // fused elementwise regions (GPU plans): generated source + loaded kernel per device
   struct Fused {
     FusedRegion region;
@@ -1042,11 +1046,58 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     }
   }
 
+  // ---- Winograd filters (GPU plans): every 3x3 stride-1 CONV step with a
+  // constant f32 filter and a cheap epilogue gets its F(2x2,3x3) transform
+  // (fp64 on the host, once per plan) as a plan-made constant; the kernel
+  // layer runs conv_wino.hip with it unless TFA_CONV_ALGO=direct
+  if (gpu_plan && k::conv_wino_enabled()) {
+    std::map<int, TensorRef> const_ref;
+    for (auto& cs : p->const_slots) const_ref[cs.first] = cs.second;
+    auto filt = [&](int slot) -> const at::Tensor* {
+      auto sc = p->synth_consts.find(slot);
+      if (sc != p->synth_consts.end()) return &sc->second;
+      auto it = const_ref.find(slot);
+      if (it == const_ref.end()) return nullptr;
+      const auto& v = infos[it->second.node][it->second.index].value;
+      return v ? &*v : nullptr;
+    };
+    std::map<int, int> made;  // filter slot -> Winograd slot (convs sharing a filter share it)
+    for (auto& st : p->steps) {
+      if (st.kind != Step::CONV || !st.epi.empty() || st.in_slots.size() != 2 || st.act > k::ACT_RELU6) continue;
+      bool acts_ok = true;
+      for (const auto& sb : st.sibs) acts_ok = acts_ok && sb.act <= k::ACT_RELU6;
+      if (!acts_ok) continue;
+      const Node& nd = g_->node(st.node);
+      if (nd.op != "Conv2D" || nd.attr_s("data_format", std::string("NHWC")) != "NHWC") continue;
+      const std::vector<int64_t> one{1, 1, 1, 1};
+      const auto strides = nd.attr_ilist("strides", one), dil = nd.attr_ilist("dilations", one);
+      if (strides != one || !(dil == one || dil.empty())) continue;
+      const at::Tensor* w = filt(st.in_slots[1]);
+      if (!w || w->dim() != 4 || w->scalar_type() != at::kFloat) continue;
+      if (!k::conv_wino_shape_ok(w->size(0), w->size(1), 1, 1, 1, 1, w->size(2), w->size(3))) continue;
+      auto hit = made.find(st.in_slots[1]);
+      if (hit != made.end()) {
+        st.wino_slot = hit->second;
+        continue;
+      }
+      const at::Tensor wc = w->contiguous();
+      at::Tensor u = at::empty({16 * wc.size(2) * k::conv_wino_ocp(wc.size(3))}, wc.options());
+      k::conv_wino_filter(wc.data_ptr<float>(), wc.size(2), wc.size(3), u.data_ptr<float>());
+      const int slot = p->nslots++;
+      p->synth_consts[slot] = u;
+      made[st.in_slots[1]] = slot;
+      st.wino_slot = slot;
+      ++p->wino_convs;
+    }
+  }
+  phase("winograd");
+
   // liveness: release each slot after its last reading step (fetches/consts are kept)
   std::vector<int> last(p->nslots, -1);
   for (size_t i = 0; i < p->steps.size(); ++i) {
     for (int s : p->steps[i].in_slots) last[s] = static_cast<int>(i);
     if (p->steps[i].bias_slot >= 0) last[p->steps[i].bias_slot] = static_cast<int>(i);
+    if (p->steps[i].wino_slot >= 0) last[p->steps[i].wino_slot] = static_cast<int>(i);
     for (auto& e : p->steps[i].epi)
       if (e.slot >= 0) last[e.slot] = static_cast<int>(i);
   }
@@ -1485,7 +1536,8 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           if (st.bias_slot >= 0) bias = slots[st.bias_slot];
           std::vector<int> acts;
           for (const auto& sb : st.sibs) acts.push_back(sb.act);
-          run_conv2d_siblings(c, c.in[0], c.in[1], st.bias_slot >= 0 ? &bias : nullptr, st.act, outs, acts);
+          run_conv2d_siblings(c, c.in[0], c.in[1], st.bias_slot >= 0 ? &bias : nullptr, st.act, outs, acts,
+                              st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr);
           for (size_t k = 0; k < outs.size(); ++k) c.out[k] = outs[k];
         } else if (gpu && st.alias_slot >= 0) {
           at::Tensor& whole = slots[st.alias_slot];
@@ -1502,7 +1554,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
             run_gemm(c, c.in[0], c.in[1], gemm_ta(nd), gemm_tb(nd), bp, st.act, out,
                      epp);
           else
-            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out, epp);
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr);
           c.out[0] = out;
         } else {
           at::Tensor out = gpu ? c.alloc_out(0) : at::Tensor();
@@ -1519,7 +1571,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
             run_gemm(c, c.in[0], c.in[1], gemm_ta(nd), gemm_tb(nd), bp, st.act,
                      kout, epp);
           else
-            run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout, epp);
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr);
           c.out[0] = viewed ? kout.reshape(st.out_info[0].shape.dims) : kout;
         }
       } catch (const GraphError& e) {
@@ -2346,6 +2398,7 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
   os << "plan: " << p->steps.size() << " steps, " << p->const_slots.size() << " constants, "
      << p->fused << " fused epilogues, " << p->fused_regions.size() << " fused regions";
   if (p->fused_siblings) os << ", " << p->fused_siblings << " sibling convs fused";
+  if (p->wino_convs) os << ", " << p->wino_convs << " Winograd filters";
   {
     const std::string why = graph_blocker(*p);
     os << (why.empty() ? ", graphable" : ", not graphable (" + why + ")");
@@ -2376,6 +2429,7 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
       os << "]";
     }
     if (st.alias_slot >= 0) os << " ->concat-slice@" << st.alias_offset;
+    if (st.wino_slot >= 0) os << " +winograd";
     if (!st.sibs.empty()) {
       os << " siblings[";
       for (size_t k = 0; k < st.sibs.size(); ++k) {

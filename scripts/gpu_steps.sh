@@ -59,6 +59,7 @@ for s in ${STEPS:-tests}; do
     cfg_plumbing) run cfg_plumbing 300 python bench/configs.py plumbing ;;
     cfg_reduce) run cfg_reduce 900 python bench/configs.py reduce ;;
     bench) run bench 900 python bench.py --steps 5 --warmup 2 ;;
+    smi) run smi_$(date +%H%M%S) 60 rocm-smi --showclocks --showpower --showtemp --showuse ;;
     rehearse2) TFA_DIST_BACKEND=gloo run rehearse2 600 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 scripts/multirank_rehearsal.py ;;
     incep_sweep2) for b in 2048 4096 8192; do run incep_b$b 600 python bench/configs.py inception --source device --rows 16384 --batch $b --steps 2 --warmup 1; done ;;
     incep_host_sweep2) for c in 1024 2048; do run incep_host_c$c 900 python bench/configs.py inception --rows 65536 --batch 4096 --chunk-images $c --steps 1 --warmup 1; done ;;

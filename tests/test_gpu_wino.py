@@ -1,0 +1,147 @@
+"""The Winograd F(2x2,3x3) conv kernel (csrc/kernels/conv_wino.hip) on the GPU
+against a float64 host reference, on Inception-v3 / VGG-16 layer geometries
+and odd edge shapes, both kernel variants (64 tiles x 64 oc, 128 tiles x 32
+oc), with bias + ReLU, concat slices and sibling-fused convs.
+
+Accuracy gate (per layer): max |y - ref| / sum|a*b| <= 1e-5, and <= 4x the
+error the exact implicit-GEMM path measures on the same data (the same plan run
+with the Winograd switch off). Reference workload: BASELINE config 5 and
+src/main/python/tensorframes_snippets/read_image.py:62-71 (VGG-16)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from tensorframes_amd import engine, tf  # noqa: E402
+from tensorframes_amd._native import _C  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def run(g, fetches, feeds):
+    names = list(feeds)
+    prog = engine.program(g.serialize(), fetches, names)
+    ins = [torch.as_tensor(np.asarray(feeds[n])) for n in names]
+    return prog, [o.cpu().numpy() for o in engine.run_program(prog, ins, DEV)]
+
+
+def ref_conv(x, f, pad):
+    xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
+    ft = torch.from_numpy(f).double().permute(3, 2, 0, 1)
+    p = 1 if pad == "SAME" else 0
+    y = torch.nn.functional.conv2d(xt, ft, padding=p).permute(0, 2, 3, 1).numpy()
+    s = torch.nn.functional.conv2d(xt.abs(), ft.abs(), padding=p).permute(0, 2, 3, 1).numpy()
+    return y, s
+
+
+@pytest.fixture
+def variant():
+    def force(v):
+        _C.set_wino_tile(v)
+    yield force
+    _C.set_wino_tile(-1)
+    _C.set_conv_wino(True)
+
+
+GEOMS = [  # N, H, W, C, OC, padding
+    (8, 25, 25, 64, 96, "SAME"),     # Inception Mixed_5x b2_3x3a
+    (8, 25, 25, 96, 96, "SAME"),     # b2_3x3b
+    (2, 54, 54, 80, 192, "VALID"),   # Conv2d_4a
+    (1, 111, 111, 32, 32, "VALID"),  # Conv2d_2a
+    (1, 109, 109, 32, 64, "SAME"),   # Conv2d_2b
+    (16, 5, 5, 448, 384, "SAME"),    # Mixed_7x b2_3x3
+    (2, 28, 28, 256, 512, "SAME"),   # VGG-16 conv4_1
+    (3, 13, 11, 36, 52, "SAME"),     # odd sizes, OC tail inside a block
+    (2, 7, 9, 4, 8, "VALID"),        # one k step, tiny
+]
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_wino_matches_fp64_and_gate(variant, geom):
+    nb, h, w, c, oc, pad = geom
+    rng = np.random.default_rng(h * w + c + oc)
+    x = rng.uniform(-1, 1, (nb, h, w, c)).astype(np.float32)
+    f = rng.uniform(-1, 1, (3, 3, c, oc)).astype(np.float32)
+    bias = rng.uniform(-1, 1, oc).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        xi = tf.placeholder(tf.float32, [None, h, w, c], name="x")
+        cv = tf.nn.conv2d(xi, tf.constant(f), [1, 1, 1, 1], pad)
+        tf.identity(tf.nn.bias_add(cv, tf.constant(bias)), name="y")
+    ref, scale = ref_conv(x, f, pad)
+    want = ref + bias
+    scale = scale + np.abs(bias)
+    prog, _ = run(g, ["y"], {"x": x})
+    assert "+winograd" in prog.describe([torch.from_numpy(x)], True)
+    _C.set_conv_wino(False)
+    _, (yd,) = run(g, ["y"], {"x": x})
+    _C.set_conv_wino(True)
+    err_direct = np.max(np.abs(yd - want) / scale)
+    for v in (0, 1):
+        variant(v)
+        _, (y,) = run(g, ["y"], {"x": x})
+        assert y.shape == want.shape
+        err = np.max(np.abs(y - want) / scale)
+        assert err <= 1e-5, f"variant {v}: {err}"
+        assert err <= 4 * max(err_direct, 1e-7), f"variant {v}: {err} vs direct {err_direct}"
+        # Winograd really ran (it does not give the direct path's bits)
+        assert not np.array_equal(y, yd)
+        # deterministic: the same conv gives the same bits
+        _, (y2,) = run(g, ["y"], {"x": x})
+        assert np.array_equal(y, y2)
+
+
+def test_wino_relu_concat_slice_and_siblings():
+    """An Inception mixed block: two sibling 3x3 s1 convs of one input (fused
+    along OC into one Winograd launch, per-member ReLU) writing straight into
+    their channel slices of a ConcatV2 with a 1x1 branch."""
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, (4, 17, 17, 32)).astype(np.float32)
+    fa = rng.uniform(-1, 1, (3, 3, 32, 48)).astype(np.float32)
+    fb = rng.uniform(-1, 1, (3, 3, 32, 64)).astype(np.float32)
+    fc = rng.uniform(-1, 1, (1, 1, 32, 16)).astype(np.float32)
+    ba = rng.uniform(-1, 1, 48).astype(np.float32)
+    bb = rng.uniform(-1, 1, 64).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        xi = tf.placeholder(tf.float32, [None, 17, 17, 32], name="x")
+        a = tf.nn.relu(tf.nn.bias_add(tf.nn.conv2d(xi, tf.constant(fa), [1, 1, 1, 1], "SAME"), tf.constant(ba)))
+        b = tf.nn.bias_add(tf.nn.conv2d(xi, tf.constant(fb), [1, 1, 1, 1], "SAME"), tf.constant(bb))
+        c = tf.nn.conv2d(xi, tf.constant(fc), [1, 1, 1, 1], "SAME")
+        tf.concat([c, a, b], 3, name="y")
+    prog, (y,) = run(g, ["y"], {"x": x})
+    desc = prog.describe([torch.from_numpy(x)], True)
+    assert "+winograd" in desc and "siblings[" in desc, desc
+    ra, sa = ref_conv(x, fa, "SAME")
+    rb, sb = ref_conv(x, fb, "SAME")
+    rc, _ = ref_conv(x, fc, "SAME")
+    want = np.concatenate([rc, np.maximum(ra + ba, 0), rb + bb], 3)
+    scale = np.concatenate([np.ones_like(rc), sa + np.abs(ba), sb + np.abs(bb)], 3)
+    assert np.max(np.abs(y - want) / scale) < 1e-5
+
+
+def test_direct_switch_restores_exact_path():
+    """TFA_CONV_ALGO=direct (set_conv_wino(False)) runs the same plan on the
+    implicit-GEMM core, bitwise equal to a plan built with the switch off."""
+    rng = np.random.default_rng(9)
+    x = rng.uniform(-1, 1, (4, 12, 12, 16)).astype(np.float32)
+    f = rng.uniform(-1, 1, (3, 3, 16, 32)).astype(np.float32)
+    g = tf.Graph()
+    with g.as_default():
+        xi = tf.placeholder(tf.float32, [None, 12, 12, 16], name="x")
+        tf.nn.conv2d(xi, tf.constant(f), [1, 1, 1, 1], "SAME", name="y")
+    _C.set_conv_wino(False)
+    try:
+        _, (a,) = run(g, ["y"], {"x": x})
+        g2 = tf.Graph()
+        with g2.as_default():
+            xi = tf.placeholder(tf.float32, [None, 12, 12, 16], name="x")
+            tf.nn.conv2d(xi, tf.constant(f), [1, 1, 1, 1], "SAME", name="y2")
+        _, (b,) = run(g2, ["y2"], {"x": x})
+    finally:
+        _C.set_conv_wino(True)
+    assert np.array_equal(a, b)
