@@ -56,12 +56,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 struct WinoGeom {
   int H, W, C, OH, OW, pt, pl, TH, TW, OCP, KT;
   int64_t ntiles;
+  int64_t img_floats;    // H * W * C
+  int64_t u_bytes;       // the whole transformed filter
   FastDivU32 fTW, fTH;
 };
-
-__device__ __forceinline__ void wglds16(const void* gp, void* lds) {
-  __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
-}
 
 template <int N>
 __device__ __forceinline__ void wwait_vm() {
@@ -69,80 +67,102 @@ __device__ __forceinline__ void wwait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-__device__ __forceinline__ const float* sel_ptr(const float* p, const float* z, bool ok) {
-  // an arithmetic select: a ternary here becomes an exec-masked branch per
-  // piece, and a branch between LDS-DMA issues drains the queue (vmcnt(0))
-  const uint64_t m = 0ull - (uint64_t)ok;
-  return reinterpret_cast<const float*>((reinterpret_cast<uint64_t>(p) & m) | (reinterpret_cast<uint64_t>(z) & ~m));
+// a raw buffer descriptor (gfx9 dword 3); bases and sizes must be provably
+// uniform (readfirstlane) or every buffer op becomes a waterfall loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-template <int T, int BN, int S>
-__global__ __launch_bounds__(256, 1) void wino23_kernel(GemmArgs g, WinoGeom q, int nbn) {
-  constexpr int TG = T / 16, CG = BN / 16;                    // 16x16 MFMA tiles: tile groups, oc groups
+// 16 bytes per lane global -> LDS (lane i lands at lds + 16 i); a lane whose
+// offset is past the descriptor's size reads zeros (padding taps, tiles past
+// the end): no per-lane select, no branch between DMA issues
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ float act3(float v, int a) {  // none / ReLU / ReLU6 as selects
+  float r = (a != 0 && !(v > 0.f)) ? 0.f : v;
+  return (a == ACT_RELU6 && r > 6.f) ? 6.f : r;
+}
+
+constexpr uint32_t kOOB = 0x80000000u;  // an offset past every input descriptor
+
+// NW = 4: one wave per SIMD, 4 * T * BN / 64 accumulators per lane; NW = 8:
+// two waves per SIMD splitting the tiles (half the accumulators each, so one
+// wave's LDS waits and barrier skew are covered by its partner's MFMAs)
+template <int T, int BN, int S, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom q, int nbn) {
+  constexpr int NTP = NW / 4;                                  // tile parts (waves per xi row)
+  constexpr int TWV = T / NTP;                                 // tiles per wave
+  constexpr int TG = TWV / 16, CG = BN / 16;                   // 16x16 MFMA tiles per wave
   constexpr int IN_BYTES = 16 * T * 16, U_BYTES = 16 * BN * 16, STAGE = IN_BYTES + U_BYTES;
-  constexpr int GI = T / 16, GU = BN / 16, G = GI + GU;       // DMA pieces per wave per stage
-  constexpr int EP = BN + 4;                                  // epilogue row pitch (floats)
+  constexpr int GI = 16 * (T / 64) / NW, GU = 16 * (BN / 64) / NW, G = GI + GU;  // DMA pieces per wave
+  constexpr int EP = BN + 4;                                   // epilogue row pitch (floats)
   constexpr int E_BYTES = 4 * 2 * T * EP * 4;
   constexpr int SMEM = S * STAGE > E_BYTES ? S * STAGE : E_BYTES;
-  static_assert(T % 64 == 0 && BN % 32 == 0 && S >= 3, "whole DMA pieces per wave, >= 3 stages");
+  static_assert(T % 64 == 0 && BN % 64 == 0 && S >= 3 && (NW == 4 || NW == 8), "tile shape");
+  static_assert(GI >= 1 && GU >= 1 && GI * NW == 16 * (T / 64) && GU * NW == 16 * (BN / 64), "whole DMA pieces");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
-  static_assert(4 * TG * CG * 4 <= 256, "accumulators");
+  static_assert(4 * TG * CG * 4 * NTP <= 256, "accumulators");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int xr = wave & 3, tp = wave >> 2;  // xi row, tile part
   const int li = lane & 15, lq = lane >> 4;
   const int nwg = gridDim.x;
   const int wg = f32core::xcd_remap(blockIdx.x, nwg);
   const int64_t t0 = (int64_t)(wg / nbn) * T;
   const int n0 = (wg % nbn) * BN;
-  const float* x = static_cast<const float*>(g.A);
-  const float* u = static_cast<const float*>(g.B);
-  const float* zero = f32core::kZeroPage;
   const int KT = q.KT;
 
-  // ---- DMA sources. Input piece i of wave w: patch row py = w, column
-  // px = i / (T/64), tiles (i % (T/64)) * 64 + lane; fixed per lane except
-  // for the channel offset (advanced by 4 floats per stage).
-  const float* isrc[GI];
-  bool iok[GI];
+  // ---- descriptors: the input from the block's first image on (every valid
+  // tap of the block lies within 2^31 bytes of it: conv_wino_eligible), the
+  // whole filter, and an empty one (stages past the end)
+  const uint32_t nb0 = (uint32_t)(t0 / ((int64_t)q.TH * q.TW));
+  const __amdgpu_buffer_rsrc_t rin = wrsrc(static_cast<const float*>(g.A) + (int64_t)nb0 * q.img_floats, kOOB);
+  const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (uint32_t)q.u_bytes);
+  const __amdgpu_buffer_rsrc_t rnil = wrsrc(g.B, 0u);
+  // input piece p = wave * GI + i: patch position p / (T/64) (= 4 py + px),
+  // tiles (p % (T/64)) * 64 + lane; byte offset per lane fixed for the loop
+  uint32_t ioff[GI];
 #pragma unroll
   for (int i = 0; i < GI; ++i) {
-    const int px = i / (T / 64), sub = i % (T / 64);
+    const int p = wave * GI + i, pos = p / (T / 64), sub = p % (T / 64);
+    const int py = pos >> 2, px = pos & 3;
     const int64_t t = t0 + sub * 64 + lane;
     const bool live = t < q.ntiles;
     const uint32_t tc = live ? (uint32_t)t : 0u;
     const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
     const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
-    const int ih = 2 * (int)ty - q.pt + wave, iw = 2 * (int)tx - q.pl + px;
-    iok[i] = live & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
-    const int64_t off = iok[i] ? (((int64_t)n * q.H + ih) * q.W + iw) * q.C : 0;
-    isrc[i] = x + off;
+    const int ih = 2 * (int)ty - q.pt + py, iw = 2 * (int)tx - q.pl + px;
+    const bool ok = live & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
+    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4) : kOOB;
   }
-  // filter piece i of wave w: elements i*64 + lane of the wave's [4 xi][BN]
+  // filter piece p = wave * GU + i: elements p * 64 + lane of [16 xi][BN]
   uint32_t uoff[GU];
 #pragma unroll
   for (int i = 0; i < GU; ++i) {
-    const int e = i * 64 + lane, xl = e / BN, oc = e % BN;
-    uoff[i] = (uint32_t)((xl * q.OCP + oc) * 4);
+    const int e = (wave * GU + i) * 64 + lane, xi = e / BN, oc = e % BN;
+    uoff[i] = (uint32_t)((xi * q.OCP + n0 + oc) * 16);
   }
-  const float* ubase = u + ((int64_t)(4 * wave) * q.OCP + n0) * 4;
-  const int64_t ustep = (int64_t)16 * q.OCP * 4;  // floats per channel quad
-  int64_t coff = 0;                               // input channel offset of the next stage to issue
-  int kiss = 0;                                   // index of the next stage to issue
+  const uint32_t ustep = (uint32_t)(16 * q.OCP * 16);  // bytes per channel quad
+  int kiss = 0;                                        // index of the next stage to issue
 
   auto issue = [&](int slot) __attribute__((always_inline)) {
     char* base = smem + slot * STAGE;
     const bool live = kiss < KT;
+    const __amdgpu_buffer_rsrc_t ri = live ? rin : rnil, rf = live ? ru : rnil;
+    const uint32_t is = (uint32_t)kiss * 16u, us = (uint32_t)kiss * ustep;
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int px = i / (T / 64), sub = i % (T / 64);
-      wglds16(sel_ptr(isrc[i] + coff, zero, iok[i] & live), base + ((wave * 4 + px) * T + sub * 64) * 16);
+      const int p = wave * GI + i, pos = p / (T / 64), sub = p % (T / 64);
+      bdma16(ri, ioff[i], is, base + (pos * T + sub * 64) * 16);
     }
 #pragma unroll
-    for (int i = 0; i < GU; ++i)
-      wglds16(sel_ptr(ubase + uoff[i], zero, live), base + IN_BYTES + (4 * wave * BN + i * 64) * 16);
-    coff += 4;
-    ubase += ustep;
+    for (int i = 0; i < GU; ++i) bdma16(rf, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
     ++kiss;
   };
 
@@ -151,17 +171,17 @@ __global__ __launch_bounds__(256, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
     float a[4][TG];
     float b[4][CG];
   };
-  // B^T row `wave`: t = d[ra] + sgn * d[rb]
-  const int ra = wave == 0 ? 0 : (wave == 2 ? 2 : 1);
-  const int rb = wave == 0 ? 2 : (wave == 1 ? 2 : (wave == 2 ? 1 : 3));
-  const float sgn = wave == 1 ? 1.f : -1.f;
+  // B^T row xr: t = d[ra] + sgn * d[rb]
+  const int ra = xr == 0 ? 0 : (xr == 2 ? 2 : 1);
+  const int rb = xr == 0 ? 2 : (xr == 1 ? 2 : (xr == 2 ? 1 : 3));
+  const float sgn = xr == 1 ? 1.f : -1.f;
   auto read = [&](int kt, Frag& f) __attribute__((always_inline)) {
     const char* st = smem + (kt % S) * STAGE;
     const float* in = reinterpret_cast<const float*>(st);
     const float* us = reinterpret_cast<const float*>(st + IN_BYTES);
 #pragma unroll
     for (int gi = 0; gi < TG; ++gi) {
-      const int tile = 16 * gi + li;
+      const int tile = tp * TWV + 16 * gi + li;
       float t[4];
 #pragma unroll
       for (int px = 0; px < 4; ++px) {
@@ -177,7 +197,7 @@ __global__ __launch_bounds__(256, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int cg = 0; cg < CG; ++cg) f.b[j][cg] = us[((4 * wave + j) * BN + 16 * cg + li) * 4 + lq];
+      for (int cg = 0; cg < CG; ++cg) f.b[j][cg] = us[((4 * xr + j) * BN + 16 * cg + li) * 4 + lq];
   };
 
   f32x4 acc[4][TG][CG];
@@ -190,18 +210,6 @@ __global__ __launch_bounds__(256, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
 
   constexpr int NM = 4 * TG * CG;          // MFMAs per stage
   constexpr int NR = 8 * TG + 4 * CG;      // LDS reads per stage
-  auto stage = [&](int kt, auto do_issue, auto do_read) __attribute__((always_inline)) {
-    constexpr bool ISSUE = decltype(do_issue)::value, READ = decltype(do_read)::value;
-    if constexpr (ISSUE) wwait_vm<G * (S - 3)>();  // stage kt+1 landed (kt+2 .. kt+S-2 may fly)
-    else wwait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    if constexpr (ISSUE) issue((kt + S - 1) % S);
-    Frag nxt;
-    if constexpr (READ) read(kt + 1, nxt);
-    (void)nxt;
-    return nxt;
-  };
-  Frag cur;
   auto compute = [&](const Frag& f) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -212,31 +220,42 @@ __global__ __launch_bounds__(256, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
           acc[j][gi][cg] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[j][gi], f.b[j][cg], acc[j][gi][cg], 0, 0, 0);
   };
 
-  // prologue: stages 0 .. S-2 (stages past KT read zero pages only)
+  // prologue: stages 0 .. S-2 (stages past KT read through the empty descriptor)
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) issue(s);
   wwait_vm<G * (S - 2)>();  // stage 0 landed
   __builtin_amdgcn_s_barrier();
+  Frag cur;
   read(0, cur);
   int kt = 0;
+  // One stage: stage kt+1 retired for every wave (counted wait + barrier),
+  // which also frees the slot of stage kt-1 for the DMA of stage kt+S-1;
+  // then the stage's MFMAs with the next stage's fragment reads (and its
+  // input transform) in their shadow.
   for (; kt + S - 1 < KT; ++kt) {
-    Frag nxt = stage(kt, std::true_type{}, std::true_type{});
+    wwait_vm<G * (S - 3)>();  // stage kt+1 landed (kt+2 .. kt+S-2 may fly)
+    __builtin_amdgcn_s_barrier();
+    issue((kt + S - 1) % S);
+    Frag nxt;
+    read(kt + 1, nxt);
     compute(cur);
     // MFMA, DMA piece, MFMA, ..., then MFMA, LDS read, MFMA, LDS read, ...
     f32core::sched_interleave<0, NM, G + NR, G, f32core::kSchedVmemRead, f32core::kSchedDsRead>();
     cur = nxt;
   }
   for (; kt + 1 < KT; ++kt) {
-    Frag nxt = stage(kt, std::false_type{}, std::true_type{});
+    wwait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    Frag nxt;
+    read(kt + 1, nxt);
     compute(cur);
     f32core::sched_interleave<0, NM, NR, 0, f32core::kSchedVmemRead, f32core::kSchedDsRead>();
     cur = nxt;
   }
-  (void)stage(kt, std::false_type{}, std::false_type{});
   compute(cur);
   __syncthreads();  // every wave is done with the ring: it becomes the epilogue exchange
 
-  // ---- epilogue. A^T along x: this wave's rows m'[w][px] (C/D layout of
+  // ---- epilogue. A^T along x: this wave's rows m'[xr][px] (C/D layout of
   // 16x16x4: oc = 16 cg + (l & 15), tile = 16 gi + 4 (l >> 4) + r)
   float* E = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -247,26 +266,25 @@ __global__ __launch_bounds__(256, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
       for (int r = 0; r < 4; ++r) {
         const float m0 = (acc[0][gi][cg][r] + acc[1][gi][cg][r]) + acc[2][gi][cg][r];
         const float m1 = (acc[1][gi][cg][r] - acc[2][gi][cg][r]) - acc[3][gi][cg][r];
-        const int tile = 16 * gi + 4 * lq + r, oc = 16 * cg + li;
-        E[((wave * 2 + 0) * T + tile) * EP + oc] = m0;
-        E[((wave * 2 + 1) * T + tile) * EP + oc] = m1;
+        const int tile = tp * TWV + 16 * gi + 4 * lq + r, oc = 16 * cg + li;
+        E[((xr * 2 + 0) * T + tile) * EP + oc] = m0;
+        E[((xr * 2 + 1) * T + tile) * EP + oc] = m1;
       }
   __syncthreads();
-  // A^T along y over the 4 waves' rows; wave w writes tiles [w T/4, (w+1) T/4)
+  // A^T along y over the 4 xi rows; wave w writes tiles [w T/NW, (w+1) T/NW)
   constexpr int LPT = BN / 4, TPP = 64 / LPT;  // lanes per tile (float4 of oc), tiles per pass
   const int cq = lane % LPT, tr = lane / LPT;
   const int64_t col = n0 + 4 * cq;
   if (col >= g.N) return;
-  float* Cb = static_cast<float*>(g.C);
   float* cbase;
   int64_t cld;
   int cact;
-  f32core::out_col(g, Cb, col, cbase, cld, cact);
+  f32core::out_col(g, static_cast<float*>(g.C), col, cbase, cld, cact);
   const float* bias = static_cast<const float*>(g.bias);
   const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int ps = 0; ps < T / 4 / TPP; ++ps) {
-    const int tile = wave * (T / 4) + ps * TPP + tr;
+  for (int ps = 0; ps < T / NW / TPP; ++ps) {
+    const int tile = wave * (T / NW) + ps * TPP + tr;
     const int64_t t = t0 + tile;
     if (t >= q.ntiles) continue;
     const uint32_t tc = (uint32_t)t, qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
@@ -279,19 +297,17 @@ __global__ __launch_bounds__(256, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
       for (int w = 0; w < 4; ++w) e[w] = *reinterpret_cast<const f32x4*>(&E[((w * 2 + px) * T + tile) * EP + 4 * cq]);
       const f32x4 y0 = (e[0] + e[1]) + e[2];
       const f32x4 y1 = (e[1] - e[2]) - e[3];
-      if (ow >= q.OW) continue;
 #pragma unroll
       for (int py = 0; py < 2; ++py) {
         const int oh = 2 * (int)ty + py;
-        if (oh >= q.OH) continue;
         const f32x4 v = py ? y1 : y0;
         float4 o;
-        o.x = act_fast(v[0] + bv.x, cact);
-        o.y = act_fast(v[1] + bv.y, cact);
-        o.z = act_fast(v[2] + bv.z, cact);
-        o.w = act_fast(v[3] + bv.w, cact);
+        o.x = act3(v[0] + bv.x, cact);
+        o.y = act3(v[1] + bv.y, cact);
+        o.z = act3(v[2] + bv.z, cact);
+        o.w = act3(v[3] + bv.w, cact);
         const int64_t row = ((int64_t)n * q.OH + oh) * q.OW + ow;
-        *reinterpret_cast<float4*>(cbase + row * cld) = o;
+        if (ow < q.OW && oh < q.OH) *reinterpret_cast<float4*>(cbase + row * cld) = o;
       }
     }
   }
@@ -305,7 +321,7 @@ std::atomic<int>& wino_state() {
   return v;
 }
 
-// forced variant (-1 auto, 0: 64 tiles x 64 oc, 1: 128 tiles x 32 oc)
+// forced variant (-1 auto, 0: 4 waves (one per SIMD), 1: 8 waves; both 64 tiles x 64 oc)
 std::atomic<int>& wino_variant() {
   static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_WINO_TILE");
@@ -354,8 +370,12 @@ bool conv_wino_eligible(const ConvArgs& a) {
   if (!conv_wino_shape_ok(a.KH, a.KW, a.sh, a.sw, a.dh, a.dw, a.C, a.OC)) return false;
   if (a.epi.n != 0 || a.act > ACT_RELU6) return false;
   if (!al16p(a.x) || !al16p(a.wino) || (a.bias && !al16p(a.bias))) return false;
-  const int64_t ntiles = a.N * ((a.OH + 1) / 2) * ((a.OW + 1) / 2);
+  const int64_t tpi = ((a.OH + 1) / 2) * ((a.OW + 1) / 2), ntiles = a.N * tpi;
   if (ntiles >= (int64_t(1) << 31)) return false;
+  // a block's taps lie within (images a block spans + 1) images of its first
+  // image: under 2^31 bytes for the input descriptor's 32-bit offsets
+  if ((128 / tpi + 2) * a.H * a.W * a.C * 4 >= (int64_t(1) << 31)) return false;
+  if (16 * a.C * conv_wino_ocp(a.OC) * 4 >= (int64_t(1) << 31)) return false;
   if (a.seg.n == 0) return al16p(a.y) && (a.ldc > 0 ? a.ldc : a.OC) % 4 == 0;
   for (int s = 0; s < a.seg.n; ++s) {
     if (a.seg.begin[s] % 4 != 0 || a.seg.ldc[s] % 4 != 0 || !al16p(a.seg.ptr[s])) return false;
@@ -372,6 +392,8 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   q.OCP = (int)conv_wino_ocp(a.OC);
   q.KT = (int)(a.C / 4);
   q.ntiles = a.N * q.TH * q.TW;
+  q.img_floats = a.H * a.W * a.C;
+  q.u_bytes = 16 * a.C * q.OCP * 4;
   q.fTW = make_fastdiv((uint32_t)q.TW);
   q.fTH = make_fastdiv((uint32_t)q.TH);
   GemmArgs g{};
@@ -387,15 +409,15 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   g.batch = 1;
   g.seg = a.seg;
   int v = wino_variant().load();
-  if (v < 0) v = a.OC <= 32 ? 1 : 0;
-  const int T = v == 1 ? 128 : 64, BN = v == 1 ? 32 : 64;
+  if (v < 0) v = 1;
+  const int T = 64, BN = 64;
   const int64_t nbt = (q.ntiles + T - 1) / T, nbn = (a.OC + BN - 1) / BN;
   TFA_CHECK(nbt * nbn < (int64_t(1) << 31), "conv_wino: grid too large");
   const dim3 grid((unsigned)(nbt * nbn));
-  if (v == 1)
-    hipLaunchKernelGGL((wino23_kernel<128, 32, 3>), grid, dim3(256), 0, s, g, q, (int)nbn);
+  if (v == 0)
+    hipLaunchKernelGGL((wino23_kernel<64, 64, 4, 4>), grid, dim3(256), 0, s, g, q, (int)nbn);
   else
-    hipLaunchKernelGGL((wino23_kernel<64, 64, 4>), grid, dim3(256), 0, s, g, q, (int)nbn);
+    hipLaunchKernelGGL((wino23_kernel<64, 64, 4, 8>), grid, dim3(512), 0, s, g, q, (int)nbn);
   TFA_LAUNCH_CHECK("conv_wino");
 }
 

@@ -66,6 +66,21 @@ for s in ${STEPS:-tests}; do
     incep_sweep) for b in 256 512 1024 2048; do run incep_b$b 600 python bench/configs.py inception --source device --rows 8192 --batch $b --steps 2 --warmup 1; done ;;
     incep_host_sweep) for c in 256 1024; do run incep_host_c$c 900 python bench/configs.py inception --rows 65536 --batch 2048 --chunk-images $c --steps 1 --warmup 1; done ;;
     incep) run incep 900 python bench/configs.py inception --source device --rows ${INC_ROWS:-8192} --batch ${INC_BATCH:-512} --steps 1 --warmup 1 ;;
+    wino) run wino_tests 400 python -u -m pytest tests/test_gpu_wino.py -x -v --timeout 200 --timeout-method thread &&
+      run layers_wino 700 python scripts/conv_layers.py --json gpurun_out/layers_wino.json &&
+      TFA_CONV_ALGO=direct run layers_direct 700 python scripts/conv_layers.py --json gpurun_out/layers_direct.json ;;
+    wino_pmc) export TMPDIR=/tmp
+      for spec in ${WINO_PMC:-4:0 4:1 8:1 2:1}; do set -- ${spec/:/ }
+        for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+                    "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+                    "TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"; do
+          tag=l$1_v$2_$(echo $pass | cut -c1-6)
+          TFA_WINO_TILE=$2 run pmc_$tag 120 rocprofv3 --pmc $pass --output-format csv -d "$PWD/gpurun_out/wino_pmc/$tag" -o run -- python scripts/conv_layers.py --only $1 --iters 2 || exit 1
+        done
+      done ;;
+    wtest) run wino_tests 400 python -u -m pytest tests/test_gpu_wino.py -x -v --timeout 200 --timeout-method thread ;;
+    layers_v1) TFA_WINO_TILE=1 run layers_wino_v1 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v1.json ;;
+    layers_v0) TFA_WINO_TILE=0 run layers_wino_v0 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v0.json ;;
     # ---- presets (the one-off round-4/5 step lists, folded in)
     final) STEPS=smoke bash scripts/gpu_check.sh && run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
       run bench 900 python bench.py --steps 5 --warmup 2 &&

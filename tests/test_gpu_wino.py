@@ -1,7 +1,8 @@
 """The Winograd F(2x2,3x3) conv kernel (csrc/kernels/conv_wino.hip) on the GPU
 against a float64 host reference, on Inception-v3 / VGG-16 layer geometries
-and odd edge shapes, both kernel variants (64 tiles x 64 oc, 128 tiles x 32
-oc), with bias + ReLU, concat slices and sibling-fused convs.
+and odd edge shapes, both kernel variants (4 waves = one per SIMD, 8 waves =
+two per SIMD; 64 tiles x 64 oc each), with bias + ReLU, concat slices and
+sibling-fused convs.
 
 Accuracy gate (per layer): max |y - ref| / sum|a*b| <= 1e-5, and <= 4x the
 error the exact implicit-GEMM path measures on the same data (the same plan run
@@ -32,7 +33,7 @@ def run(g, fetches, feeds):
 def ref_conv(x, f, pad):
     xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
     ft = torch.from_numpy(f).double().permute(3, 2, 0, 1)
-    p = 1 if pad == "SAME" else 0
+    p = (f.shape[0] // 2) if pad == "SAME" else 0
     y = torch.nn.functional.conv2d(xt, ft, padding=p).permute(0, 2, 3, 1).numpy()
     s = torch.nn.functional.conv2d(xt.abs(), ft.abs(), padding=p).permute(0, 2, 3, 1).numpy()
     return y, s
