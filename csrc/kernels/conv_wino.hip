@@ -52,12 +52,14 @@ namespace k {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 struct WinoGeom {
   int H, W, C, OH, OW, pt, pl, TH, TW, OCP, KT;
   int64_t ntiles;
   int64_t img_floats;    // H * W * C
   int64_t u_bytes;       // the whole transformed filter
+  int dbg;               // timing experiments (TFA_WINO_DEBUG): 1 no filter traffic, 2 no input traffic, 4 no stores
   FastDivU32 fTW, fTH;
 };
 
@@ -90,28 +92,25 @@ __device__ __forceinline__ float act3(float v, int a) {  // none / ReLU / ReLU6 
 
 constexpr uint32_t kOOB = 0x80000000u;  // an offset past every input descriptor
 
-// NW = 4: one wave per SIMD, 4 * T * BN / 64 accumulators per lane; NW = 8:
-// two waves per SIMD splitting the tiles (half the accumulators each, so one
-// wave's LDS waits and barrier skew are covered by its partner's MFMAs)
-template <int T, int BN, int S, int NW>
+// NW = 4: one wave per SIMD (256 accumulators per lane); NW = 8: two waves
+// per SIMD splitting the block's tiles (128 each), so one wave's fragment
+// reads at a stage start are covered by its partner's MFMAs
+template <int NW>
 __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom q, int nbn) {
-  constexpr int NTP = NW / 4;                                  // tile parts (waves per xi row)
-  constexpr int TWV = T / NTP;                                 // tiles per wave
-  constexpr int TG = TWV / 16, CG = BN / 16;                   // 16x16 MFMA tiles per wave
-  constexpr int IN_BYTES = 16 * T * 16, U_BYTES = 16 * BN * 16, STAGE = IN_BYTES + U_BYTES;
-  constexpr int GI = 16 * (T / 64) / NW, GU = 16 * (BN / 64) / NW, G = GI + GU;  // DMA pieces per wave
+  constexpr int T = 64, BN = 64;                               // tiles x output channels per block
+  constexpr int NTP = NW / 4, TWV = T / NTP, TM = TWV / 32;    // tile parts, tiles per wave, 32-row MFMA tiles
+  constexpr int IN_BYTES = 16 * 2 * T * 16, U_BYTES = 16 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
+  constexpr int GI = 32 / NW, GU = 32 / NW, G = GI + GU;       // DMA pieces per wave per stage
   constexpr int EP = BN + 4;                                   // epilogue row pitch (floats)
   constexpr int E_BYTES = 4 * 2 * T * EP * 4;
-  constexpr int SMEM = S * STAGE > E_BYTES ? S * STAGE : E_BYTES;
-  static_assert(T % 64 == 0 && BN % 64 == 0 && S >= 3 && (NW == 4 || NW == 8), "tile shape");
-  static_assert(GI >= 1 && GU >= 1 && GI * NW == 16 * (T / 64) && GU * NW == 16 * (BN / 64), "whole DMA pieces");
+  constexpr int SMEM = 2 * STAGE > E_BYTES ? 2 * STAGE : E_BYTES;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
-  static_assert(4 * TG * CG * 4 * NTP <= 256, "accumulators");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int xr = wave & 3, tp = wave >> 2;  // xi row, tile part
-  const int li = lane & 15, lq = lane >> 4;
+  const int h = lane >> 5, r32 = lane & 31;
   const int nwg = gridDim.x;
   const int wg = f32core::xcd_remap(blockIdx.x, nwg);
   const int64_t t0 = (int64_t)(wg / nbn) * T;
@@ -119,154 +118,122 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
   const int KT = q.KT;
 
   // ---- descriptors: the input from the block's first image on (every valid
-  // tap of the block lies within 2^31 bytes of it: conv_wino_eligible), the
-  // whole filter, and an empty one (stages past the end)
+  // tap of the block lies within 2^31 bytes of it: conv_wino_eligible) and
+  // the whole filter
   const uint32_t nb0 = (uint32_t)(t0 / ((int64_t)q.TH * q.TW));
-  const __amdgpu_buffer_rsrc_t rin = wrsrc(static_cast<const float*>(g.A) + (int64_t)nb0 * q.img_floats, kOOB);
-  const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (uint32_t)q.u_bytes);
-  const __amdgpu_buffer_rsrc_t rnil = wrsrc(g.B, 0u);
-  // input piece p = wave * GI + i: patch position p / (T/64) (= 4 py + px),
-  // tiles (p % (T/64)) * 64 + lane; byte offset per lane fixed for the loop
+  const __amdgpu_buffer_rsrc_t rin = wrsrc(static_cast<const float*>(g.A) + (int64_t)nb0 * q.img_floats,
+                                            (q.dbg & 2) ? 0u : kOOB);
+  const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
+  // input piece p = wave * GI + i: patch position pos = p >> 1 (= 4 py + px),
+  // channel quad p & 1 of the stage, tiles 0..63 (lane); the lane's byte
+  // offset is fixed for the loop (out of range: a padding tap / past the end)
   uint32_t ioff[GI];
 #pragma unroll
   for (int i = 0; i < GI; ++i) {
-    const int p = wave * GI + i, pos = p / (T / 64), sub = p % (T / 64);
-    const int py = pos >> 2, px = pos & 3;
-    const int64_t t = t0 + sub * 64 + lane;
+    const int p = wave * GI + i, pos = p >> 1, py = pos >> 2, px = pos & 3;
+    const int64_t t = t0 + lane;
     const bool live = t < q.ntiles;
     const uint32_t tc = live ? (uint32_t)t : 0u;
     const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
     const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
     const int ih = 2 * (int)ty - q.pt + py, iw = 2 * (int)tx - q.pl + px;
     const bool ok = live & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
-    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4) : kOOB;
+    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + (p & 1) * 16) : kOOB;
   }
-  // filter piece p = wave * GU + i: elements p * 64 + lane of [16 xi][BN]
+  // filter piece p = wave * GU + i: (xi, quad) = (p >> 1, p & 1), oc n0 + lane
   uint32_t uoff[GU];
 #pragma unroll
   for (int i = 0; i < GU; ++i) {
-    const int e = (wave * GU + i) * 64 + lane, xi = e / BN, oc = e % BN;
-    uoff[i] = (uint32_t)((xi * q.OCP + n0 + oc) * 16);
+    const int p = wave * GU + i;
+    uoff[i] = (uint32_t)((p * q.OCP + lane) * 16);
   }
-  const uint32_t ustep = (uint32_t)(16 * q.OCP * 16);  // bytes per channel quad
-  int kiss = 0;                                        // index of the next stage to issue
+  const uint32_t ustep = (uint32_t)(32 * q.OCP * 16);  // filter bytes per 8-channel stage
+  const uint32_t ubase = (uint32_t)(n0 * 16);
 
-  auto issue = [&](int slot) __attribute__((always_inline)) {
-    char* base = smem + slot * STAGE;
-    const bool live = kiss < KT;
-    const __amdgpu_buffer_rsrc_t ri = live ? rin : rnil, rf = live ? ru : rnil;
-    const uint32_t is = (uint32_t)kiss * 16u, us = (uint32_t)kiss * ustep;
+  // stage kt -> slot kt & 1: input [pos][quad][tile][4 c], filter [xi][quad][oc][4 c]
+  auto issue = [&](int kt) __attribute__((always_inline)) {
+    char* base = smem + (kt & 1) * STAGE;
+    const uint32_t is = (uint32_t)kt * 32u, us = ubase + (uint32_t)kt * ustep;
 #pragma unroll
-    for (int i = 0; i < GI; ++i) {
-      const int p = wave * GI + i, pos = p / (T / 64), sub = p % (T / 64);
-      bdma16(ri, ioff[i], is, base + (pos * T + sub * 64) * 16);
-    }
+    for (int i = 0; i < GI; ++i) bdma16(rin, ioff[i], is, base + (wave * GI + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < GU; ++i) bdma16(rf, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
-    ++kiss;
+    for (int i = 0; i < GU; ++i) bdma16(ru, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
   };
 
-  // ---- fragments of one stage: A[xi_x][tile group], B[xi_x][oc group]
-  struct Frag {
-    float a[4][TG];
-    float b[4][CG];
-  };
+  // ---- fragments: lane (h, r32) holds tile r32 (of a 32-tile group) and oc
+  // r32 (of a 32-oc half), channel quad h; MFMA step s takes channel 4h + s.
   // B^T row xr: t = d[ra] + sgn * d[rb]
   const int ra = xr == 0 ? 0 : (xr == 2 ? 2 : 1);
   const int rb = xr == 0 ? 2 : (xr == 1 ? 2 : (xr == 2 ? 1 : 3));
   const float sgn = xr == 1 ? 1.f : -1.f;
-  auto read = [&](int kt, Frag& f) __attribute__((always_inline)) {
-    const char* st = smem + (kt % S) * STAGE;
-    const float* in = reinterpret_cast<const float*>(st);
-    const float* us = reinterpret_cast<const float*>(st + IN_BYTES);
+  f32x4 av[4][TM];   // A: [xi_x][tile group] -> 4 steps
+  f32x4 bv[4][2];    // B: [xi_x][oc half] -> 4 steps
+  auto read = [&](int kt) __attribute__((always_inline)) {
+    const char* st = smem + (kt & 1) * STAGE;
 #pragma unroll
-    for (int gi = 0; gi < TG; ++gi) {
-      const int tile = tp * TWV + 16 * gi + li;
-      float t[4];
+    for (int gi = 0; gi < TM; ++gi) {
+      const int tile = tp * TWV + 32 * gi + r32;
+      f32x4 t[4];
 #pragma unroll
       for (int px = 0; px < 4; ++px) {
-        const float a = in[((ra * 4 + px) * T + tile) * 4 + lq];
-        const float b = in[((rb * 4 + px) * T + tile) * 4 + lq];
-        t[px] = __builtin_fmaf(sgn, b, a);  // exact a +- b, one rounding
+        const f32x4 a = *reinterpret_cast<const f32x4*>(st + (((ra * 4 + px) * 2 + h) * T + tile) * 16);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(st + (((rb * 4 + px) * 2 + h) * T + tile) * 16);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[px][c] = __builtin_fmaf(sgn, b[c], a[c]);  // exact a +- b
       }
-      f.a[0][gi] = t[0] - t[2];
-      f.a[1][gi] = t[1] + t[2];
-      f.a[2][gi] = t[2] - t[1];
-      f.a[3][gi] = t[1] - t[3];
+      av[0][gi] = t[0] - t[2];
+      av[1][gi] = t[1] + t[2];
+      av[2][gi] = t[2] - t[1];
+      av[3][gi] = t[1] - t[3];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int cg = 0; cg < CG; ++cg) f.b[j][cg] = us[((4 * xr + j) * BN + 16 * cg + li) * 4 + lq];
+      for (int nh = 0; nh < 2; ++nh)
+        bv[j][nh] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + (((4 * xr + j) * 2 + h) * BN + nh * 32 + r32) * 16);
   };
 
-  f32x4 acc[4][TG][CG];
+  f32x16 acc[4][TM][2];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int gi = 0; gi < TG; ++gi)
+    for (int gi = 0; gi < TM; ++gi)
 #pragma unroll
-      for (int cg = 0; cg < CG; ++cg) acc[j][gi][cg] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int nh = 0; nh < 2; ++nh) acc[j][gi][nh] = (f32x16){};
 
-  constexpr int NM = 4 * TG * CG;          // MFMAs per stage
-  constexpr int NR = 8 * TG + 4 * CG;      // LDS reads per stage
-  auto compute = [&](const Frag& f) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int gi = 0; gi < TG; ++gi)
-#pragma unroll
-        for (int cg = 0; cg < CG; ++cg)
-          acc[j][gi][cg] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[j][gi], f.b[j][cg], acc[j][gi][cg], 0, 0, 0);
-  };
-
-  // prologue: stages 0 .. S-2 (stages past KT read through the empty descriptor)
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s) issue(s);
-  wwait_vm<G * (S - 2)>();  // stage 0 landed
-  __builtin_amdgcn_s_barrier();
-  Frag cur;
-  read(0, cur);
-  int kt = 0;
-  // One stage: stage kt+1 retired for every wave (counted wait + barrier),
-  // which also frees the slot of stage kt-1 for the DMA of stage kt+S-1;
-  // then the stage's MFMAs with the next stage's fragment reads (and its
-  // input transform) in their shadow.
-  for (; kt + S - 1 < KT; ++kt) {
-    wwait_vm<G * (S - 3)>();  // stage kt+1 landed (kt+2 .. kt+S-2 may fly)
-    __builtin_amdgcn_s_barrier();
-    issue((kt + S - 1) % S);
-    Frag nxt;
-    read(kt + 1, nxt);
-    compute(cur);
-    // MFMA, DMA piece, MFMA, ..., then MFMA, LDS read, MFMA, LDS read, ...
-    f32core::sched_interleave<0, NM, G + NR, G, f32core::kSchedVmemRead, f32core::kSchedDsRead>();
-    cur = nxt;
-  }
-  for (; kt + 1 < KT; ++kt) {
+  // One stage: my DMA of stage kt retired, barrier (everyone's landed, and
+  // everyone is done reading slot kt-1), DMA of stage kt+1 into that slot,
+  // then the fragment reads + input transform and 32 * TM MFMAs of stage kt.
+  issue(0);
+  for (int kt = 0; kt < KT; ++kt) {
     wwait_vm<0>();
     __builtin_amdgcn_s_barrier();
-    Frag nxt;
-    read(kt + 1, nxt);
-    compute(cur);
-    f32core::sched_interleave<0, NM, NR, 0, f32core::kSchedVmemRead, f32core::kSchedDsRead>();
-    cur = nxt;
+    if (kt + 1 < KT) issue(kt + 1);
+    read(kt);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int gi = 0; gi < TM; ++gi)
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+            acc[j][gi][nh] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j][gi][s], bv[j][nh][s], acc[j][gi][nh], 0, 0, 0);
   }
-  compute(cur);
-  __syncthreads();  // every wave is done with the ring: it becomes the epilogue exchange
+  __syncthreads();  // every wave is done with the stages: the LDS becomes the epilogue exchange
 
   // ---- epilogue. A^T along x: this wave's rows m'[xr][px] (C/D layout of
-  // 16x16x4: oc = 16 cg + (l & 15), tile = 16 gi + 4 (l >> 4) + r)
+  // 32x32x2: oc = 32 nh + (l & 31), tile = 32 gi + (r & 3) + 8 (r >> 2) + 4 h)
   float* E = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int gi = 0; gi < TG; ++gi)
+  for (int gi = 0; gi < TM; ++gi)
 #pragma unroll
-    for (int cg = 0; cg < CG; ++cg)
+    for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float m0 = (acc[0][gi][cg][r] + acc[1][gi][cg][r]) + acc[2][gi][cg][r];
-        const float m1 = (acc[1][gi][cg][r] - acc[2][gi][cg][r]) - acc[3][gi][cg][r];
-        const int tile = tp * TWV + 16 * gi + 4 * lq + r, oc = 16 * cg + li;
+      for (int r = 0; r < 16; ++r) {
+        const float m0 = (acc[0][gi][nh][r] + acc[1][gi][nh][r]) + acc[2][gi][nh][r];
+        const float m1 = (acc[1][gi][nh][r] - acc[2][gi][nh][r]) - acc[3][gi][nh][r];
+        const int tile = tp * TWV + 32 * gi + (r & 3) + 8 * (r >> 2) + 4 * h, oc = 32 * nh + r32;
         E[((xr * 2 + 0) * T + tile) * EP + oc] = m0;
         E[((xr * 2 + 1) * T + tile) * EP + oc] = m1;
       }
@@ -281,7 +248,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
   int cact;
   f32core::out_col(g, static_cast<float*>(g.C), col, cbase, cld, cact);
   const float* bias = static_cast<const float*>(g.bias);
-  const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 bvv = bias ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int ps = 0; ps < T / NW / TPP; ++ps) {
     const int tile = wave * (T / NW) + ps * TPP + tr;
@@ -302,12 +269,12 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
         const int oh = 2 * (int)ty + py;
         const f32x4 v = py ? y1 : y0;
         float4 o;
-        o.x = act3(v[0] + bv.x, cact);
-        o.y = act3(v[1] + bv.y, cact);
-        o.z = act3(v[2] + bv.z, cact);
-        o.w = act3(v[3] + bv.w, cact);
+        o.x = act3(v[0] + bvv.x, cact);
+        o.y = act3(v[1] + bvv.y, cact);
+        o.z = act3(v[2] + bvv.z, cact);
+        o.w = act3(v[3] + bvv.w, cact);
         const int64_t row = ((int64_t)n * q.OH + oh) * q.OW + ow;
-        if (ow < q.OW && oh < q.OH) *reinterpret_cast<float4*>(cbase + row * cld) = o;
+        if (ow < q.OW && oh < q.OH && !(q.dbg & 4)) *reinterpret_cast<float4*>(cbase + row * cld) = o;
       }
     }
   }
@@ -340,7 +307,7 @@ void set_wino_tile(int v) { wino_variant().store(v); }
 
 int64_t conv_wino_ocp(int64_t OC) { return (OC + 63) / 64 * 64; }
 
-// U = G g G^T per (c, oc) in fp64, rounded once to f32, into [C/4][16 xi][OCP][4 c]
+// U = G g G^T per (c, oc) in fp64, rounded once to f32, into [C/8][16 xi][2][OCP][4 c]
 void conv_wino_filter(const float* w, int64_t C, int64_t OC, float* u) {
   static const double G[4][3] = {{1, 0, 0}, {.5, .5, .5}, {.5, -.5, .5}, {0, 0, 1}};
   const int64_t OCP = conv_wino_ocp(OC);
@@ -355,13 +322,13 @@ void conv_wino_filter(const float* w, int64_t C, int64_t OC, float* u) {
       for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
           const double v = t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2];
-          u[(((c / 4) * 16 + i * 4 + j) * OCP + o) * 4 + c % 4] = static_cast<float>(v);
+          u[((((c / 8) * 16 + i * 4 + j) * 2 + (c / 4) % 2) * OCP + o) * 4 + c % 4] = static_cast<float>(v);
         }
     }
 }
 
 bool conv_wino_shape_ok(int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t C, int64_t OC) {
-  return KH == 3 && KW == 3 && sh == 1 && sw == 1 && dh == 1 && dw == 1 && C % 4 == 0 && OC % 4 == 0 && C > 0 &&
+  return KH == 3 && KW == 3 && sh == 1 && sw == 1 && dh == 1 && dw == 1 && C % 8 == 0 && OC % 4 == 0 && C > 0 &&
          OC > 0;
 }
 
@@ -369,12 +336,15 @@ bool conv_wino_eligible(const ConvArgs& a) {
   if (!a.wino || !conv_wino_enabled()) return false;
   if (!conv_wino_shape_ok(a.KH, a.KW, a.sh, a.sw, a.dh, a.dw, a.C, a.OC)) return false;
   if (a.epi.n != 0 || a.act > ACT_RELU6) return false;
+  // a 64-wide oc block on OC <= 32 wastes half the MFMAs: the direct kernels
+  // win there (Conv2d_2a, OC = 32: 77 vs 101 TF/s, profiles/r6_wino/)
+  if (a.OC <= 32 && wino_variant().load() < 0) return false;
   if (!al16p(a.x) || !al16p(a.wino) || (a.bias && !al16p(a.bias))) return false;
   const int64_t tpi = ((a.OH + 1) / 2) * ((a.OW + 1) / 2), ntiles = a.N * tpi;
   if (ntiles >= (int64_t(1) << 31)) return false;
   // a block's taps lie within (images a block spans + 1) images of its first
   // image: under 2^31 bytes for the input descriptor's 32-bit offsets
-  if ((128 / tpi + 2) * a.H * a.W * a.C * 4 >= (int64_t(1) << 31)) return false;
+  if ((64 / tpi + 2) * a.H * a.W * a.C * 4 >= (int64_t(1) << 31)) return false;
   if (16 * a.C * conv_wino_ocp(a.OC) * 4 >= (int64_t(1) << 31)) return false;
   if (a.seg.n == 0) return al16p(a.y) && (a.ldc > 0 ? a.ldc : a.OC) % 4 == 0;
   for (int s = 0; s < a.seg.n; ++s) {
@@ -390,10 +360,15 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   q.pt = (int)a.pad_t; q.pl = (int)a.pad_l;
   q.TH = (int)((a.OH + 1) / 2); q.TW = (int)((a.OW + 1) / 2);
   q.OCP = (int)conv_wino_ocp(a.OC);
-  q.KT = (int)(a.C / 4);
+  q.KT = (int)(a.C / 8);
   q.ntiles = a.N * q.TH * q.TW;
   q.img_floats = a.H * a.W * a.C;
   q.u_bytes = 16 * a.C * q.OCP * 4;
+  static const int dbg = [] {
+    const char* e = std::getenv("TFA_WINO_DEBUG");
+    return e ? std::atoi(e) : 0;
+  }();
+  q.dbg = dbg;
   q.fTW = make_fastdiv((uint32_t)q.TW);
   q.fTH = make_fastdiv((uint32_t)q.TH);
   GemmArgs g{};
@@ -410,14 +385,13 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   g.seg = a.seg;
   int v = wino_variant().load();
   if (v < 0) v = 1;
-  const int T = 64, BN = 64;
-  const int64_t nbt = (q.ntiles + T - 1) / T, nbn = (a.OC + BN - 1) / BN;
+  const int64_t nbt = (q.ntiles + 63) / 64, nbn = (a.OC + 63) / 64;
   TFA_CHECK(nbt * nbn < (int64_t(1) << 31), "conv_wino: grid too large");
   const dim3 grid((unsigned)(nbt * nbn));
   if (v == 0)
-    hipLaunchKernelGGL((wino23_kernel<64, 64, 4, 4>), grid, dim3(256), 0, s, g, q, (int)nbn);
+    hipLaunchKernelGGL((wino23_kernel<4>), grid, dim3(256), 0, s, g, q, (int)nbn);
   else
-    hipLaunchKernelGGL((wino23_kernel<64, 64, 4, 8>), grid, dim3(512), 0, s, g, q, (int)nbn);
+    hipLaunchKernelGGL((wino23_kernel<8>), grid, dim3(512), 0, s, g, q, (int)nbn);
   TFA_LAUNCH_CHECK("conv_wino");
 }
 

@@ -56,8 +56,8 @@ GEOMS = [  # N, H, W, C, OC, padding
     (1, 109, 109, 32, 64, "SAME"),   # Conv2d_2b
     (16, 5, 5, 448, 384, "SAME"),    # Mixed_7x b2_3x3
     (2, 28, 28, 256, 512, "SAME"),   # VGG-16 conv4_1
-    (3, 13, 11, 36, 52, "SAME"),     # odd sizes, OC tail inside a block
-    (2, 7, 9, 4, 8, "VALID"),        # one k step, tiny
+    (3, 13, 11, 40, 52, "SAME"),     # odd sizes, OC tail inside a block
+    (2, 7, 9, 8, 8, "VALID"),        # one k step, tiny
 ]
 
 
@@ -146,3 +146,28 @@ def test_direct_switch_restores_exact_path():
     finally:
         _C.set_conv_wino(True)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("model", ["inception_v3", "vgg16"])
+def test_full_models_top5_identical(model):
+    """Full-width Inception-v3 / VGG-16 at 224x224 (random-init frozen graphs,
+    synthetic images): the Winograd plan and the exact implicit-GEMM plan give
+    the same top-5 classes for every image, and close probabilities."""
+    from tensorframes_amd.models import cnn
+    kw = dict(image_size=224)
+    if model == "vgg16":
+        kw["fc_width"] = 1024
+    g, iname, oname = getattr(cnn, model)(**kw)
+    vals, idx = cnn.top_k_classes(g, oname, k=5)
+    x = np.random.default_rng(3).random((8, 224, 224, 3), dtype=np.float32)
+    fetches = [oname, idx.op.name]
+    prog = engine.program(g.serialize(), fetches, [iname])
+    assert "+winograd" in prog.describe([torch.from_numpy(x)], True)
+    pw, iw = [o.cpu().numpy() for o in engine.run_program(prog, [torch.from_numpy(x)], DEV)]
+    _C.set_conv_wino(False)
+    try:
+        pd, idd = [o.cpu().numpy() for o in engine.run_program(prog, [torch.from_numpy(x)], DEV)]
+    finally:
+        _C.set_conv_wino(True)
+    np.testing.assert_array_equal(iw, idd)
+    np.testing.assert_allclose(pw, pd, rtol=1e-3, atol=1e-6)

@@ -1,5 +1,5 @@
 """Winograd F(2x2,3x3) conv path, host side (no GPU): the planner's filter
-transform (conv_wino_filter, fp64 -> f32, layout [C/4][16][OCP][4]) driven
+transform (conv_wino_filter, fp64 -> f32, layout [C/8][16][2][OCP][4]) driven
 through a numpy emulation of exactly the kernel's algorithm (B^T d B per wave
 row, M = sum_c V U, A^T M A) must reproduce a float64 direct convolution, and
 a GPU plan must carry one Winograd filter per distinct 3x3 stride-1 filter.
@@ -31,15 +31,13 @@ def direct(x, f, pad):
 def emulate(x, u_flat, oc, pad):
     n, h, w, c = x.shape
     ocp = -(-oc // 64) * 64
-    u = u_flat.astype(np.float64).reshape(c // 4, 16, ocp, 4).transpose(1, 0, 3, 2).reshape(16, c, ocp)
+    u = u_flat.astype(np.float64).reshape(c // 8, 16, 2, ocp, 4).transpose(1, 0, 2, 4, 3).reshape(16, c, ocp)
     p = 1 if pad == "SAME" else 0
     oh, ow = h + 2 * p - 2, w + 2 * p - 2
     th, tw = -(-oh // 2), -(-ow // 2)
     # zero padding that covers the patch of every (partial) edge tile
     xp = np.zeros((n, 2 * th + 2, 2 * tw + 2, c))
-    src = x[:, max(0, -p + 0):, :, :]
-    xp[:, p:p + h, p:p + w, :] = x[:, : 2 * th + 2 - p, : 2 * tw + 2 - p, :][:, :h, :w]
-    del src
+    xp[:, p:p + h, p:p + w, :] = x
     y = np.zeros((n, 2 * th, 2 * tw, oc))
     for ty in range(th):
         for tx in range(tw):
@@ -50,7 +48,7 @@ def emulate(x, u_flat, oc, pad):
     return y[:, :oh, :ow, :]
 
 
-@pytest.mark.parametrize("geom", [(2, 6, 6, 4, 8, "SAME"), (1, 7, 9, 8, 12, "VALID"), (2, 5, 5, 12, 68, "SAME")])
+@pytest.mark.parametrize("geom", [(2, 6, 6, 8, 8, "SAME"), (1, 7, 9, 8, 12, "VALID"), (2, 5, 5, 24, 68, "SAME")])
 def test_filter_transform_and_algorithm_match_direct(geom):
     n, h, w, c, oc, pad = geom
     rng = np.random.default_rng(h * w + c)
@@ -67,12 +65,12 @@ def test_filter_transform_and_algorithm_match_direct(geom):
 
 def test_filter_padding_is_zero():
     import torch
-    f = np.ones((3, 3, 4, 10), np.float32)
-    u = _C.conv_wino_filter(torch.from_numpy(f)).numpy().reshape(1, 16, 64, 4)
-    assert np.all(u[:, :, 10:, :] == 0)
+    f = np.ones((3, 3, 8, 10), np.float32)
+    u = _C.conv_wino_filter(torch.from_numpy(f)).numpy().reshape(1, 16, 2, 64, 4)
+    assert np.all(u[:, :, :, 10:, :] == 0)
     # xi (0,0) is g[0][0]; xi (1,1) is (sum over the 3x3) / 4
-    assert np.allclose(u[0, 0, :10], 1.0)
-    assert np.allclose(u[0, 5, :10], 9 / 4)
+    assert np.allclose(u[0, 0, :, :10], 1.0)
+    assert np.allclose(u[0, 5, :, :10], 9 / 4)
 
 
 def _inception_like_graph():
@@ -96,7 +94,6 @@ def test_gpu_plan_carries_winograd_filters_only_for_3x3_stride1():
     desc = prog.describe([torch.zeros(2, 9, 9, 8)], True)
     assert "1 Winograd filters" in desc, desc
     assert desc.count("+winograd") == 1, desc
-    assert "+winograd" not in desc.split("\n")[0] or True
     # host plans never carry one; with the switch off GPU plans do not either
     assert "+winograd" not in prog.describe([torch.zeros(2, 9, 9, 8)], False)
     _C.set_conv_wino(False)
