@@ -957,6 +957,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              py::arg("size"), py::arg("slot_bytes"), py::arg("create"), GR())
         .def("unlink", &comm::ShmComm::unlink)
         .def("set_timeout", &comm::ShmComm::set_timeout, py::arg("seconds"))
+        .def("poison", &comm::ShmComm::poison, "make every rank's current / next collective raise")
+        .def("reset_after_failure", &comm::ShmComm::reset_after_failure,
+             "clear the barrier state (only once every rank has left the communicator)")
+        .def_property_readonly("poisoned", &comm::ShmComm::poisoned)
         .def_property_readonly("slot_bytes", &comm::ShmComm::slot_bytes)
         .def_property_readonly("attached", &comm::ShmComm::attached);
     m.attr("EXIT_COLLECTIVE_TIMEOUT") = comm::kExitCollectiveTimeout;

@@ -634,6 +634,16 @@ void ShmComm::fail_all(const std::string& why) {
   throw CollectiveError(why);
 }
 
+void ShmComm::poison() { reinterpret_cast<Ctrl*>(base_)->broken.store(1, std::memory_order_release); }
+
+bool ShmComm::poisoned() const { return reinterpret_cast<Ctrl*>(base_)->broken.load(std::memory_order_acquire) != 0; }
+
+void ShmComm::reset_after_failure() {
+  Ctrl* c = reinterpret_cast<Ctrl*>(base_);
+  c->arrived.store(0, std::memory_order_relaxed);
+  c->broken.store(0, std::memory_order_release);
+}
+
 void ShmComm::barrier() {
   Ctrl* c = reinterpret_cast<Ctrl*>(base_);
   if (c->broken.load(std::memory_order_acquire))

@@ -239,6 +239,13 @@ class ShmComm : public Comm {
   void barrier() override;
   void unlink();
   void set_timeout(double seconds) { timeout_s_ = seconds; }
+  // failure agreement (parallel/dist.agreed): a rank whose local phase
+  // failed poisons the segment, so every rank waiting in (or entering) a
+  // collective raises at once; once every rank has left the communicator
+  // (synchronised on another channel) rank 0 clears the barrier state
+  void poison();
+  void reset_after_failure();
+  bool poisoned() const;
   int64_t slot_bytes() const { return slot_; }
   int attached() const;  // ranks that have mapped the segment so far
 

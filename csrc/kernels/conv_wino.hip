@@ -125,20 +125,23 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
                                             (q.dbg & 2) ? 0u : kOOB);
   const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
   // input piece p = wave * GI + i: patch position pos = p >> 1 (= 4 py + px),
-  // channel quad p & 1 of the stage, tiles 0..63 (lane); the lane's byte
-  // offset is fixed for the loop (out of range: a padding tap / past the end)
+  // tile half th = p & 1; lane L takes tile 32 th + (L & 31), channel quad
+  // L >> 5, so the two 16-byte quads of one pixel are one 32-byte access of
+  // one instruction (half the distinct lines of one-quad-per-instruction).
+  // The lane's byte offset is fixed for the loop (out of range: a padding
+  // tap / a tile past the end). LDS image: [pos][th][quad][32 tiles][16 B].
   uint32_t ioff[GI];
 #pragma unroll
   for (int i = 0; i < GI; ++i) {
     const int p = wave * GI + i, pos = p >> 1, py = pos >> 2, px = pos & 3;
-    const int64_t t = t0 + lane;
+    const int64_t t = t0 + (p & 1) * 32 + r32;
     const bool live = t < q.ntiles;
     const uint32_t tc = live ? (uint32_t)t : 0u;
     const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
     const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
     const int ih = 2 * (int)ty - q.pt + py, iw = 2 * (int)tx - q.pl + px;
     const bool ok = live & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
-    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + (p & 1) * 16) : kOOB;
+    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
   }
   // filter piece p = wave * GU + i: (xi, quad) = (p >> 1, p & 1), oc n0 + lane
   uint32_t uoff[GU];
@@ -168,29 +171,50 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
   const float sgn = xr == 1 ? 1.f : -1.f;
   f32x4 av[4][TM];   // A: [xi_x][tile group] -> 4 steps
   f32x4 bv[4][2];    // B: [xi_x][oc half] -> 4 steps
+  // reads in the order the xi_x columns need them (V_0 = t0 - t2, then t1,
+  // then t3), so the first MFMAs wait for 6 of the 16 reads only
   auto read = [&](int kt) __attribute__((always_inline)) {
     const char* st = smem + (kt & 1) * STAGE;
+    auto inp = [&](int r, int px, int gi) __attribute__((always_inline)) {
+      const int th = tp * TM + gi;
+      return *reinterpret_cast<const f32x4*>(st + (((r * 4 + px) * 2 + th) * 2 + h) * 512 + r32 * 16);
+    };
+    auto filt = [&](int j, int nh) __attribute__((always_inline)) {
+      bv[j][nh] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + (((4 * xr + j) * 2 + h) * BN + nh * 32 + r32) * 16);
+    };
+    auto tr = [&](f32x4 a, f32x4 b) __attribute__((always_inline)) {
+      f32x4 t;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[c] = __builtin_fmaf(sgn, b[c], a[c]);  // exact a +- b
+      return t;
+    };
+    f32x4 t[4][TM];
 #pragma unroll
     for (int gi = 0; gi < TM; ++gi) {
-      const int tile = tp * TWV + 32 * gi + r32;
-      f32x4 t[4];
-#pragma unroll
-      for (int px = 0; px < 4; ++px) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(st + (((ra * 4 + px) * 2 + h) * T + tile) * 16);
-        const f32x4 b = *reinterpret_cast<const f32x4*>(st + (((rb * 4 + px) * 2 + h) * T + tile) * 16);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) t[px][c] = __builtin_fmaf(sgn, b[c], a[c]);  // exact a +- b
-      }
-      av[0][gi] = t[0] - t[2];
-      av[1][gi] = t[1] + t[2];
-      av[2][gi] = t[2] - t[1];
-      av[3][gi] = t[1] - t[3];
+      t[0][gi] = tr(inp(ra, 0, gi), inp(rb, 0, gi));
+      t[2][gi] = tr(inp(ra, 2, gi), inp(rb, 2, gi));
     }
+    filt(0, 0);
+    filt(0, 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int gi = 0; gi < TM; ++gi) {
+      av[0][gi] = t[0][gi] - t[2][gi];
+      t[1][gi] = tr(inp(ra, 1, gi), inp(rb, 1, gi));
+    }
+    filt(1, 0);
+    filt(1, 1);
+    filt(2, 0);
+    filt(2, 1);
 #pragma unroll
-      for (int nh = 0; nh < 2; ++nh)
-        bv[j][nh] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + (((4 * xr + j) * 2 + h) * BN + nh * 32 + r32) * 16);
+    for (int gi = 0; gi < TM; ++gi) {
+      av[1][gi] = t[1][gi] + t[2][gi];
+      av[2][gi] = t[2][gi] - t[1][gi];
+      t[3][gi] = tr(inp(ra, 3, gi), inp(rb, 3, gi));
+    }
+    filt(3, 0);
+    filt(3, 1);
+#pragma unroll
+    for (int gi = 0; gi < TM; ++gi) av[3][gi] = t[1][gi] - t[3][gi];
   };
 
   f32x16 acc[4][TM][2];
@@ -204,22 +228,35 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
   // One stage: my DMA of stage kt retired, barrier (everyone's landed, and
   // everyone is done reading slot kt-1), DMA of stage kt+1 into that slot,
   // then the fragment reads + input transform and 32 * TM MFMAs of stage kt.
+  // The xi_x = 3 column's MFMAs of stage kt are deferred into stage kt+1:
+  // issued right after its barrier, they keep the matrix pipe busy while
+  // that stage's fragment reads and input transform are in flight.
+  auto mfma_cols = [&](int j0, int j1, const f32x4 (&a)[4][TM], const f32x4 (&b)[4][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = j0; j < j1; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int gi = 0; gi < TM; ++gi)
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+            acc[j][gi][nh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][gi][s], b[j][nh][s], acc[j][gi][nh], 0, 0, 0);
+  };
+  f32x4 pa[4][TM], pb[4][2];  // the deferred column (only [3] is live)
   issue(0);
   for (int kt = 0; kt < KT; ++kt) {
     wwait_vm<0>();
     __builtin_amdgcn_s_barrier();
     if (kt + 1 < KT) issue(kt + 1);
+    if (kt > 0) mfma_cols(3, 4, pa, pb);
     read(kt);
+    mfma_cols(0, 3, av, bv);
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int gi = 0; gi < TM; ++gi)
-#pragma unroll
-          for (int nh = 0; nh < 2; ++nh)
-            acc[j][gi][nh] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j][gi][s], bv[j][nh][s], acc[j][gi][nh], 0, 0, 0);
+    for (int gi = 0; gi < TM; ++gi) pa[3][gi] = av[3][gi];
+    pb[3][0] = bv[3][0];
+    pb[3][1] = bv[3][1];
   }
+  mfma_cols(3, 4, pa, pb);
   __syncthreads();  // every wave is done with the stages: the LDS becomes the epilogue exchange
 
   // ---- epilogue. A^T along x: this wave's rows m'[xr][px] (C/D layout of
@@ -280,6 +317,155 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
   }
 }
 
+// Register-epilogue variant: 4 waves (one per SIMD), wave w owns ALL 16 xi
+// of a 32-tile x 32-oc quadrant (tile half w & 1, oc half w >> 1): 16 32x32
+// accumulators = 256 registers per lane. Each wave transforms the whole 4x4
+// patch of its tiles (the two oc-half waves repeat it: 32 VALU per 64 MFMAs),
+// and A^T M A is done in registers at the end: no LDS exchange, no epilogue
+// barrier, scalar 4-byte stores that cover 32 consecutive oc per half wave.
+__global__ __launch_bounds__(256, 1) void wino23_reg_kernel(GemmArgs g, WinoGeom q, int nbn) {
+  constexpr int T = 64, BN = 64;
+  constexpr int IN_BYTES = 16 * 2 * T * 16, U_BYTES = 16 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
+  constexpr int GI = 8, GU = 8;  // DMA pieces per wave per stage (32 + 32 per block)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int th = wave & 1, oh = wave >> 1;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int nwg = gridDim.x;
+  const int wg = f32core::xcd_remap(blockIdx.x, nwg);
+  const int64_t t0 = (int64_t)(wg / nbn) * T;
+  const int n0 = (wg % nbn) * BN;
+  const int KT = q.KT;
+
+  const uint32_t nb0 = (uint32_t)(t0 / ((int64_t)q.TH * q.TW));
+  const __amdgpu_buffer_rsrc_t rin = wrsrc(static_cast<const float*>(g.A) + (int64_t)nb0 * q.img_floats,
+                                            (q.dbg & 2) ? 0u : kOOB);
+  const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
+  // input piece p = wave * GI + i: patch position p >> 1, tile half p & 1;
+  // lane L: tile 32 (p & 1) + (L & 31), channel quad L >> 5 (as wino23_kernel)
+  uint32_t ioff[GI];
+#pragma unroll
+  for (int i = 0; i < GI; ++i) {
+    const int p = wave * GI + i, pos = p >> 1, py = pos >> 2, px = pos & 3;
+    const int64_t t = t0 + (p & 1) * 32 + r32;
+    const bool live = t < q.ntiles;
+    const uint32_t tc = live ? (uint32_t)t : 0u;
+    const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
+    const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
+    const int ih = 2 * (int)ty - q.pt + py, iw = 2 * (int)tx - q.pl + px;
+    const bool ok = live & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
+    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
+  }
+  uint32_t uoff[GU];
+#pragma unroll
+  for (int i = 0; i < GU; ++i) uoff[i] = (uint32_t)(((wave * GU + i) * q.OCP + lane) * 16);
+  const uint32_t ustep = (uint32_t)(32 * q.OCP * 16);
+  const uint32_t ubase = (uint32_t)(n0 * 16);
+  auto issue = [&](int kt) __attribute__((always_inline)) {
+    char* base = smem + (kt & 1) * STAGE;
+    const uint32_t is = (uint32_t)kt * 32u, us = ubase + (uint32_t)kt * ustep;
+#pragma unroll
+    for (int i = 0; i < GI; ++i) bdma16(rin, ioff[i], is, base + (wave * GI + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < GU; ++i) bdma16(ru, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
+  };
+
+  f32x16 acc[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) acc[x] = (f32x16){};
+
+  // one stage: patch rows in the order the xi rows need them (row 0 = d0-d2,
+  // rows 1, 2 = d1 +- d2, row 3 = d1 - d3), each xi row's 16 MFMAs as soon as
+  // its transform is done
+  auto stage = [&](int kt) __attribute__((always_inline)) {
+    const char* st = smem + (kt & 1) * STAGE;
+    auto inp = [&](int py, int px) __attribute__((always_inline)) {
+      return *reinterpret_cast<const f32x4*>(st + ((((py * 4 + px) * 2 + th) * 2 + h) * 512) + r32 * 16);
+    };
+    auto filt = [&](int x) __attribute__((always_inline)) {
+      return *reinterpret_cast<const f32x4*>(st + IN_BYTES + ((x * 2 + h) * BN + oh * 32 + r32) * 16);
+    };
+    auto row_mfma = [&](int y, const f32x4 (&t)[4]) __attribute__((always_inline)) {
+      f32x4 v[4];
+      v[0] = t[0] - t[2];
+      v[1] = t[1] + t[2];
+      v[2] = t[2] - t[1];
+      v[3] = t[1] - t[3];
+#pragma unroll
+      for (int xx = 0; xx < 4; ++xx) {
+        const f32x4 b = filt(4 * y + xx);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[4 * y + xx] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[xx][s], b[s], acc[4 * y + xx], 0, 0, 0);
+      }
+    };
+    f32x4 d0[4], d1[4], d2[4], d3[4], t[4];
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      d0[px] = inp(0, px);
+      d2[px] = inp(2, px);
+    }
+#pragma unroll
+    for (int px = 0; px < 4; ++px) t[px] = d0[px] - d2[px];
+    row_mfma(0, t);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) d1[px] = inp(1, px);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) t[px] = d1[px] + d2[px];
+    row_mfma(1, t);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) t[px] = d2[px] - d1[px];
+    row_mfma(2, t);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) d3[px] = inp(3, px);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) t[px] = d1[px] - d3[px];
+    row_mfma(3, t);
+  };
+
+  issue(0);
+  for (int kt = 0; kt < KT; ++kt) {
+    wwait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < KT) issue(kt + 1);
+    stage(kt);
+  }
+
+  // ---- epilogue in registers: C/D row r -> tile 32 th + (r & 3) + 8 (r >> 2) + 4 h
+  const int64_t col = n0 + oh * 32 + r32;
+  if (col >= g.N) return;
+  float* cbase;
+  int64_t cld;
+  int cact;
+  f32core::out_col(g, static_cast<float*>(g.C), col, cbase, cld, cact);
+  const float bias = g.bias ? static_cast<const float*>(g.bias)[col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t t = t0 + th * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    float m[4][2];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      m[y][0] = (acc[4 * y + 0][r] + acc[4 * y + 1][r]) + acc[4 * y + 2][r];
+      m[y][1] = (acc[4 * y + 1][r] - acc[4 * y + 2][r]) - acc[4 * y + 3][r];
+    }
+    if (t >= q.ntiles || (q.dbg & 4)) continue;
+    const uint32_t tc = (uint32_t)t, qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
+    const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      const float y0 = (m[0][px] + m[1][px]) + m[2][px];
+      const float y1 = (m[1][px] - m[2][px]) - m[3][px];
+      const int ow = 2 * (int)tx + px;
+      const int64_t row = ((int64_t)n * q.OH + 2 * (int)ty) * q.OW + ow;
+      if (ow < q.OW) {
+        cbase[row * cld] = act3(y0 + bias, cact);
+        if (2 * (int)ty + 1 < q.OH) cbase[(row + q.OW) * cld] = act3(y1 + bias, cact);
+      }
+    }
+  }
+}
+
 std::atomic<int>& wino_state() {
   static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_CONV_ALGO");
@@ -288,7 +474,8 @@ std::atomic<int>& wino_state() {
   return v;
 }
 
-// forced variant (-1 auto, 0: 4 waves (one per SIMD), 1: 8 waves; both 64 tiles x 64 oc)
+// forced variant (-1 auto, 1: 8 waves with the LDS-exchange epilogue, 2: 4 waves with the register
+// epilogue; both 64 tiles x 64 oc)
 std::atomic<int>& wino_variant() {
   static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_WINO_TILE");
@@ -388,8 +575,8 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   const int64_t nbt = (q.ntiles + 63) / 64, nbn = (a.OC + 63) / 64;
   TFA_CHECK(nbt * nbn < (int64_t(1) << 31), "conv_wino: grid too large");
   const dim3 grid((unsigned)(nbt * nbn));
-  if (v == 0)
-    hipLaunchKernelGGL((wino23_kernel<4>), grid, dim3(256), 0, s, g, q, (int)nbn);
+  if (v == 2)
+    hipLaunchKernelGGL(wino23_reg_kernel, grid, dim3(256), 0, s, g, q, (int)nbn);
   else
     hipLaunchKernelGGL((wino23_kernel<8>), grid, dim3(512), 0, s, g, q, (int)nbn);
   TFA_LAUNCH_CHECK("conv_wino");

@@ -82,6 +82,8 @@ for s in ${STEPS:-tests}; do
     layers_v1) TFA_WINO_TILE=1 run layers_wino_v1 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v1.json ;;
     wdbg) for d in ${WDBG:-0 1 2 3 4}; do TFA_WINO_DEBUG=$d run wdbg_l${WL:-4}_d$d 120 python scripts/conv_layers.py --only ${WL:-4} --iters 5 || exit 1; grep -h TF gpurun_out/wdbg_l${WL:-4}_d$d.log | tail -1; done ;;
     wsweep) run wsweep 300 python scripts/wino_sweep.py ;;
+    wsweep2) TFA_WINO_TILE=2 run wsweep2 300 python scripts/wino_sweep.py ;;
+    layers_v2) TFA_WINO_TILE=2 run layers_wino_v2 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v2.json ;;
     layers_v0) TFA_WINO_TILE=0 run layers_wino_v0 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v0.json ;;
     # ---- presets (the one-off round-4/5 step lists, folded in)
     final) STEPS=smoke bash scripts/gpu_check.sh && run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&

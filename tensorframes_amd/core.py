@@ -28,7 +28,7 @@ from .config import config
 from .frame.block import (Block, ObjectColumn, RaggedColumn, StringColumn, build_column, column_tf_dtype,
                           column_values, concat_blocks, is_dense)
 from .frame.column_info import ColumnInformation, SparkTFColInfo, explain_schema
-from .frame.dataframe import DataFrame, GroupedData, _Derived, _Materialized, _sort_key
+from .frame.dataframe import DataFrame, GroupedData, _Derived, _Failed, _Materialized, _sort_key
 from .frame.types import (BinaryType, NumericType, Row, StringType, StructField, StructType, sql_type_for_tf)
 from .graph import dsl
 from .graph import proto as P
@@ -447,7 +447,15 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
         # setting up the next operator -- while the GPU runs them; an iterative
         # workload's consumer then finds them computed (K-Means: the reduce
         # graph is built under the partition kernels)
-        res = run(src)
+        try:
+            res = run(src)
+        except Exception as e:  # noqa: BLE001
+            if not dist.is_distributed():
+                raise
+            # SPMD: raising here on one rank would leave the others in the
+            # next collective; the error is raised by the action that reads
+            # this frame, inside its agreed local phase (dist.agreed)
+            return DataFrame(out_schema, _Failed(e), dframe.num_partitions)
         df = DataFrame(out_schema, _Materialized(res), dframe.num_partitions)
         df._persist = True
         df._cached = res
@@ -1719,7 +1727,10 @@ def reduce_blocks(fetches, dframe: DataFrame, graph=None, shape_hints=None):
             else:
                 res[pid] = engine.run_program(prog, ins, ins[0].device if on_device else None)
         return res
-    per_part = faults.with_retries("reduce_blocks", task)(dframe.local_blocks())
+    # the local phase is agreed across ranks: a rank that fails here makes
+    # every rank raise instead of leaving the others in the combine below
+    per_part = dist.agreed("reduce_blocks",
+                           lambda: faults.with_retries("reduce_blocks", task)(dframe.local_blocks()))
     for pid in sorted(per_part):
         for j, o in enumerate(per_part[pid]):
             partials[j].append(o)
@@ -1820,7 +1831,8 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
                         row[n] = folded[names.index(n)]
                 res[pid] = row
             return res
-        per_part = faults.with_retries("reduce_rows", task)(dframe.local_blocks())
+        per_part = dist.agreed("reduce_rows",
+                               lambda: faults.with_retries("reduce_rows", task)(dframe.local_blocks()))
         for pid in sorted(per_part):
             for n in names:
                 partials[n].append(per_part[pid][n])
@@ -1849,13 +1861,16 @@ def reduce_rows(fetches, dframe: DataFrame, graph=None, shape_hints=None):
 
     def fold_task(blocks):
         return {pid: fold_block([b.columns[n] for n in names]) for pid, b in sorted(blocks.items()) if b.nrows > 0}
-    per_part = faults.with_retries("reduce_rows", fold_task)(dframe.local_blocks())
-    partials_rows = [per_part[pid] for pid in sorted(per_part)]
-    # this rank's partials folded as a tree too, then the per-rank partials gathered
-    local: Dict[str, Optional[torch.Tensor]] = {n: None for n in names}
-    if partials_rows:
-        acc = partials_rows[0] if len(partials_rows) == 1 else _fold_partials(fold_block, partials_rows)
-        local = dict(zip(names, acc))
+    def fold_local():
+        per_part = faults.with_retries("reduce_rows", fold_task)(dframe.local_blocks())
+        partials_rows = [per_part[pid] for pid in sorted(per_part)]
+        # this rank's partials folded as a tree too, then the per-rank partials gathered
+        local: Dict[str, Optional[torch.Tensor]] = {n: None for n in names}
+        if partials_rows:
+            acc = partials_rows[0] if len(partials_rows) == 1 else _fold_partials(fold_block, partials_rows)
+            local = dict(zip(names, acc))
+        return local
+    local = dist.agreed("reduce_rows", fold_local)
     static = {n: None for n in names}  # generic pair graphs: shapes agreed at run time
     allp = _gather_rank_values(local, static, {n: summary[n].tf_dtype for n in names})
     _check(all(allp[n] for n in names), "Cannot reduce an empty DataFrame")
@@ -2430,17 +2445,20 @@ def aggregate(fetches, grouped_data: GroupedData, graph=None, shape_hints=None) 
         shape = (o.shape if o.shape is not None else Shape()).prepend(UNKNOWN)
         out_fields.append(ColumnInformation.struct_field(n, o.tf_dtype, shape))
     def compute_keys_checked(blocks):
+        """One aggregation attempt, agreed across ranks: a rank that fails
+        makes every rank raise; a (2^-62 per pair of long keys) hash collision
+        on any rank makes every rank redo the aggregation on exact key words."""
         from .ops import groupby as G
-        try:
+
+        def attempt():
+            faults.check("aggregate", blocks.keys())
             return compute(blocks)
-        except G.StringKeyCollision as e:
-            # 2^-62 per pair of distinct long keys: a rank alone cannot redo a
-            # collective aggregation, so only a single process falls back
-            if dist.is_distributed():
-                raise TensorFramesError(f"aggregate: {e}; rerun with TFA_STRING_KEY_HASH=0") from e
+        try:
+            return dist.agreed("aggregate", attempt, soft=(G.StringKeyCollision,))
+        except (G.StringKeyCollision, dist.AgreedSoftFailure):
             metrics.add("aggregate_string_key_collisions")
             exact_string_keys[0] = True
-            return compute(blocks)
+            return dist.agreed("aggregate", attempt)
 
     return DataFrame(StructType(out_fields), _Derived(df, compute_keys_checked, streamable=False),
                      max(1, dist.world_size()))
@@ -2467,18 +2485,22 @@ def analyze(dframe: DataFrame) -> DataFrame:
     partitions agree (else unknown), cell dims that vary become unknown
     (reference: src/main/scala/org/tensorframes/ExperimentalOperations.scala:35-157)."""
     dframe = _frame(dframe)
-    local = {}
-    for pid, b in dframe.local_blocks().items():
-        if b.nrows == 0:
-            continue
-        shapes = {}
-        for f in dframe.schema.fields:
-            col = b.columns[f.name]
-            if is_dense(col):
-                shapes[f.name] = list(col.shape)
-            elif isinstance(col, RaggedColumn):
-                shapes[f.name] = [b.nrows] + _merged_cell_dims(col.cells)
-        local[pid] = shapes
+
+    def scan():
+        local = {}
+        for pid, b in dframe.local_blocks().items():
+            if b.nrows == 0:
+                continue
+            shapes = {}
+            for f in dframe.schema.fields:
+                col = b.columns[f.name]
+                if is_dense(col):
+                    shapes[f.name] = list(col.shape)
+                elif isinstance(col, RaggedColumn):
+                    shapes[f.name] = [b.nrows] + _merged_cell_dims(col.cells)
+            local[pid] = shapes
+        return local
+    local = dist.agreed("analyze", scan)
     merged: Dict[str, Optional[Shape]] = {}
     for chunk in dist.all_gather_object(local):
         for pid, shapes in chunk.items():

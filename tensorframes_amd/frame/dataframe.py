@@ -47,6 +47,18 @@ class _Materialized(_Source):
         return self._blocks
 
 
+class _Failed(_Source):
+    """A frame whose (eager) computation failed on this rank: the error is
+    raised when an action evaluates it, inside the action's agreed local phase
+    (parallel/dist.agreed), so every rank raises together."""
+
+    def __init__(self, err: BaseException):
+        self._err = err
+
+    def compute(self):
+        raise self._err
+
+
 class _Generated(_Source):
     def __init__(self, num_partitions: int, fn: Callable[[int], Block]):
         self._n = num_partitions
@@ -287,7 +299,9 @@ class DataFrame:
         names = self._schema.names
         if to is None and config.collect_to != "all":
             to = int(config.collect_to) if str(config.collect_to).isdigit() else 0
-        local = list(self._iter_blocks())  # evaluated once, partition by partition
+        # evaluated once, partition by partition; agreed across ranks (a rank
+        # that fails makes every rank raise, none waits in the gather)
+        local = dist.agreed("collect", lambda: list(self._iter_blocks()))
         if not dist.is_distributed():
             return build_rows(names, [(b.nrows, [self._column_payload(b.columns[n]) for n in names])
                                       for _, b in local if b.nrows])
@@ -298,7 +312,8 @@ class DataFrame:
 
     def count(self) -> int:
         """Rows over all ranks: one int64 all-reduce."""
-        n = torch.tensor([sum(b.nrows for _, b in self._iter_blocks())], dtype=torch.int64)
+        n = torch.tensor([dist.agreed("count", lambda: sum(b.nrows for _, b in self._iter_blocks()))],
+                         dtype=torch.int64)
         return int(dist.all_reduce_host_(n, "Sum").item())
 
     def first(self) -> Optional[Row]:
@@ -333,7 +348,7 @@ class DataFrame:
         """All rows of a column as one array, on every rank (dense columns are
         gathered as tensors)."""
         from ..parallel import frame_comm
-        blocks = self._blocks()
+        blocks = dist.agreed("to_numpy", self._blocks)
         local = [(pid, blocks[pid]) for pid in sorted(blocks)]
         if not dist.is_distributed():
             parts = [(pid, b.nrows, [self._column_payload(b.columns[column])]) for pid, b in local if b.nrows]

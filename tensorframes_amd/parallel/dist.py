@@ -464,14 +464,19 @@ def broadcast_tensor(t: Optional[torch.Tensor], shape: tuple, dtype: torch.dtype
     return buf
 
 
+# dtypes the shared-memory communicator folds (csrc/comm ShmComm fold_into);
+# half / bfloat16 / bool reductions go to gloo
+_SHM_REDUCE_DTYPES = {torch.float32, torch.float64, torch.int32, torch.int64, torch.int16, torch.uint8, torch.int8}
+
+
 def all_reduce_host_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
     """In-place all-reduce of a host tensor: the shared-memory communicator
-    when the ranks share a node, else the gloo group."""
+    when the ranks share a node (and it folds the dtype), else the gloo group."""
     if not is_distributed():
         return t
     _ensure_groups()
     shm = _host_comm()
-    if shm is not None and t.is_contiguous():
+    if shm is not None and t.is_contiguous() and t.dtype in _SHM_REDUCE_DTYPES:
         with _traced("shm_all_reduce", _nbytes(t)):
             shm.all_reduce(t, op)
         return t
@@ -575,7 +580,7 @@ def all_reduce_(t: torch.Tensor, op: str = "Sum") -> torch.Tensor:
             return ec.all_reduce_(t.contiguous() if not t.is_contiguous() else t, op)
     if t.is_cuda and not gpu_collectives():  # gloo rehearsal: stage through the host
         return t.copy_(all_reduce_(t.cpu(), op))
-    if not t.is_cuda and _host_comm() is not None and t.is_contiguous():
+    if not t.is_cuda and _host_comm() is not None and t.is_contiguous() and t.dtype in _SHM_REDUCE_DTYPES:
         with _traced("shm_all_reduce", _nbytes(t)):
             _host_comm().all_reduce(t, op)
         return t
@@ -609,3 +614,114 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     with _traced("all_gather", _nbytes(t)):
         dist.all_gather(parts, t, group=_state["cpu_group"])
     return torch.stack(parts, 0)
+
+
+# -- collective failure agreement
+class RemoteRankError(RuntimeError):
+    """Another rank failed in the local phase of a collective operator; this
+    rank raises too instead of waiting in the next collective for
+    `collective_timeout_s` (Spark fails the whole job on a task failure:
+    reference DebugRowOps.scala:500, :524-525, :576)."""
+
+
+class AgreedSoftFailure(RuntimeError):
+    """Some rank hit a recoverable condition (a `soft` exception of `agreed`):
+    every rank raises this so that all of them redo the operator together."""
+
+
+def _raise_agreed(site: str, mine: Optional[BaseException], mine_status: int, statuses: List[tuple]):
+    """statuses[r] = (status, kind, type name, message); 0 ok, 1 soft, 2 failed,
+    3 only raised because another rank poisoned the communicator."""
+    from ..utils.logging import metrics
+    if any(st == 2 for st, *_ in statuses):
+        metrics.add("collective_failures_agreed")
+        if mine_status == 2:
+            raise mine
+        r, (_, kind, tname, text) = next((r, v) for r, v in enumerate(statuses) if v[0] == 2)
+        if kind == "validation":
+            from ..core import TensorFramesError
+            raise TensorFramesError(f"{site} failed on rank {r}: {tname}: {text}")
+        raise RemoteRankError(f"{site} failed on rank {r}: {tname}: {text}")
+    metrics.add("collective_soft_failures")
+    if mine_status == 1:
+        raise mine
+    raise AgreedSoftFailure(f"{site}: a rank asked for a collective retry")
+
+
+def agreed(site: str, fn, soft: tuple = ()):
+    """Runs `fn` -- the local phase of an SPMD operator, which may itself hold
+    collectives; every rank calls this at the same point -- and agrees on the
+    outcome, so that a rank that fails never leaves the others waiting in a
+    collective for `collective_timeout_s`:
+
+    * the common case costs ONE int64 Max all-reduce of a status word;
+    * a rank whose `fn` raises poisons the shared-memory communicator at
+      once, so every other rank's current or next host collective raises
+      too; every rank then meets on the gloo bootstrap group, exchanges
+      (status, error) and rank 0 clears the segment's barrier state;
+    * a failure makes the failing rank re-raise its own error and every
+      other rank raise RemoteRankError (TensorFramesError for a validation
+      error) naming it; a `soft` exception on any rank (and no failure) makes
+      every rank raise AgreedSoftFailure, so the caller redoes the operator
+      together (the string-key collision fallback of aggregate).
+
+    Without the shared-memory communicator (TFA_SHM_COLLECTIVES=0) the
+    agreement is the status all-reduce alone, which covers failures that
+    happen before `fn`'s first collective."""
+    if not is_distributed():
+        return fn()
+    _ensure_groups()
+    shm = _host_comm()
+    res, err, status = None, None, 0
+    try:
+        res = fn()
+    except BaseException as e:  # noqa: BLE001 - re-raised below on every rank
+        err = e
+        induced = shm is not None and shm.poisoned and isinstance(e, _C_collective_error())
+        status = 3 if induced else (1 if soft and isinstance(e, soft) else 2)
+        if shm is not None and status != 3:
+            shm.poison()
+    if shm is None:
+        flag = torch.tensor([status], dtype=torch.int64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=_state["cpu_group"])
+        if int(flag.item()) == 0:
+            return res
+        text = "" if err is None else str(err)
+        kind = "" if err is None else _classify(err)
+        stats = [None] * world_size()
+        dist.all_gather_object(stats, (status, kind, type(err).__name__ if err else "", text[:_MSG_BYTES]),
+                               group=_state["cpu_group"])
+        _raise_agreed(site, err, status, stats)
+    if status == 0:
+        try:
+            flag = torch.tensor([0], dtype=torch.int64)
+            shm.all_reduce(flag, "Max")
+            if int(flag.item()) == 0:
+                return res
+        except _C_collective_error() as e:  # another rank failed and poisoned the segment
+            err, status = e, 3
+    # recovery on the bootstrap (gloo) group: every rank is out of the shm
+    # communicator once it is here
+    text = "" if err is None else str(err)
+    kind = "" if err is None or status == 3 else _classify(err)
+    stats = [None] * world_size()
+    dist.all_gather_object(stats, (status, kind, type(err).__name__ if err else "", text[:_MSG_BYTES]),
+                           group=_state["cpu_group"])
+    dist.barrier(group=_state["cpu_group"])
+    if rank() == 0:
+        shm.reset_after_failure()
+    dist.barrier(group=_state["cpu_group"])
+    _raise_agreed(site, err, status, stats)
+
+
+def _C_collective_error():
+    from .comm import CollectiveError
+    return CollectiveError
+
+
+def _classify(e: BaseException) -> str:
+    from ..utils import faults
+    return faults.classify(e)
+
+
+_MSG_BYTES = 1024
