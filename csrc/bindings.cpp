@@ -950,7 +950,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("wait", &comm::RcclComm::wait, GR(), "bounded wait for every collective issued so far")
         .def("check", &comm::RcclComm::check, "raises CollectiveError if the communicator failed")
         .def_property_readonly("failed", &comm::RcclComm::failed)
-        .def_property_readonly("inflight", &comm::RcclComm::inflight);
+        .def_property_readonly("inflight", &comm::RcclComm::inflight)
+        .def("set_test_stall", &comm::RcclComm::set_test_stall, py::arg("seconds"),
+             "tests: a spin kernel inside each all_reduce, after its start event");
     py::class_<comm::ShmComm, Comm, std::shared_ptr<comm::ShmComm>>(m, "ShmComm",
         "host tensors of the ranks of one node through a POSIX shared-memory segment")
         .def(py::init<const std::string&, int, int, int64_t, bool>(), py::arg("name"), py::arg("rank"),

@@ -207,7 +207,10 @@ RcclComm::~RcclComm() {
     if (failed_) (void)ncclCommAbort(static_cast<ncclComm_t>(comm_));
     else (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
   }
-  for (auto& f : inflight_) (void)hipEventDestroy(f.ev);
+  for (auto& f : inflight_) {
+    (void)hipEventDestroy(f.ev);
+    if (f.start) (void)hipEventDestroy(f.start);
+  }
   for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
   (void)hipGetLastError();
 }
@@ -218,7 +221,7 @@ void RcclComm::set_timeout(double seconds, bool exit_on_timeout) {
   exit_on_timeout_ = exit_on_timeout;
 }
 
-void RcclComm::track(hipStream_t s) {
+hipEvent_t RcclComm::take_event() {
   hipEvent_t e = nullptr;
   {
     std::lock_guard<std::mutex> lk(wmu_);
@@ -229,14 +232,58 @@ void RcclComm::track(hipStream_t s) {
   }
   if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
     (void)hipGetLastError();
-    return;  // no event: this collective is not watched (never fails the call)
+    return nullptr;
+  }
+  return e;
+}
+
+hipEvent_t RcclComm::begin(hipStream_t s) {
+  hipEvent_t e = take_event();
+  if (e) (void)hipEventRecord(e, s);
+  return e;
+}
+
+void RcclComm::track(hipStream_t s, hipEvent_t start) {
+  hipEvent_t e = take_event();
+  if (!e) {  // no event: this collective is not watched (never fails the call)
+    if (start) {
+      std::lock_guard<std::mutex> lk(wmu_);
+      free_events_.push_back(start);
+    }
+    return;
   }
   (void)hipEventRecord(e, s);
   {
     std::lock_guard<std::mutex> lk(wmu_);
-    inflight_.push_back({e, std::chrono::steady_clock::now()});
+    inflight_.push_back({e, start, std::chrono::steady_clock::now(), start == nullptr});
   }
   wcv_.notify_one();
+}
+
+double RcclComm::front_age() {
+  if (inflight_.empty()) return 0;
+  Inflight& f = inflight_.front();
+  const auto now = std::chrono::steady_clock::now();
+  if (!f.started) {
+    if (hipEventQuery(f.start) == hipErrorNotReady) return 0;
+    f.started = true;
+    f.t0 = now;
+  }
+  return std::chrono::duration<double>(now - f.t0).count();
+}
+
+void RcclComm::abort_comm(std::unique_lock<std::mutex>& held) {
+  ncclComm_t c = static_cast<ncclComm_t>(comm_);
+  comm_ = nullptr;
+  if (!c) return;
+  held.unlock();
+  auto done = std::make_shared<std::atomic<bool>>(false);
+  std::thread([c, done] {
+    (void)ncclCommAbort(c);
+    done->store(true);
+  }).detach();
+  for (int i = 0; i < 100 && !done->load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  held.lock();
 }
 
 int64_t RcclComm::inflight() const {
@@ -270,6 +317,7 @@ void RcclComm::wait() {
         const hipError_t q = hipEventQuery(inflight_.front().ev);
         if (q == hipErrorNotReady) break;
         free_events_.push_back(inflight_.front().ev);
+        if (inflight_.front().start) free_events_.push_back(inflight_.front().start);
         inflight_.pop_front();
       }
       if (inflight_.empty()) {
@@ -279,12 +327,26 @@ void RcclComm::wait() {
       front = inflight_.front();
       tmo = timeout_s_;
     }
-    const double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - front.t0).count();
+    double age;
+    {
+      std::lock_guard<std::mutex> lk(wmu_);
+      age = front_age();
+    }
     if (tmo > 0 && age > tmo) {
       const std::string why = str_cat("a collective did not complete within ", tmo,
-                                      " s (collective_timeout_s): a peer rank is missing, stuck, or issued a "
-                                      "different collective sequence");
-      fail(why);
+                                      " s of starting (collective_timeout_s): a peer rank is missing, stuck, or "
+                                      "issued a different collective sequence");
+      {
+        std::unique_lock<std::mutex> lk(wmu_);
+        if (!failed_) {
+          fail_msg_ = why;
+          failed_ = true;
+        }
+        // release the stuck collective kernel: without the abort the next
+        // synchronisation of this stream (a retry, the combine's sync) would
+        // block forever
+        abort_comm(lk);
+      }
       throw CollectiveError(str_cat("RCCL collective timed out on rank ", rank_, " of ", size_, ": ", why));
     }
     if (spins < 64) std::this_thread::yield();
@@ -302,10 +364,11 @@ void RcclComm::watchdog() {
       const hipError_t q = hipEventQuery(inflight_.front().ev);
       if (q == hipErrorNotReady) break;
       free_events_.push_back(inflight_.front().ev);
+      if (inflight_.front().start) free_events_.push_back(inflight_.front().start);
       inflight_.pop_front();
     }
     (void)hipGetLastError();
-    if (failed_ || !comm_) continue;  // already reported to the main thread
+    if (failed_ || !comm_) continue;  // already reported to the main thread (and aborted)
     std::string why;
     ncclResult_t ae = ncclSuccess;
     if (ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &ae) == ncclSuccess && ae != ncclSuccess &&
@@ -315,8 +378,7 @@ void RcclComm::watchdog() {
       // the main thread's own wait() raises at the timeout; past it plus a
       // grace period nobody is polling: the main thread is stuck elsewhere
       const double grace = std::min(60.0, std::max(1.0, 0.5 * timeout_s_));
-      const double age =
-          std::chrono::duration<double>(std::chrono::steady_clock::now() - inflight_.front().t0).count();
+      const double age = front_age();
       if (age > timeout_s_ + grace)
         why = str_cat("a collective has not completed after ", age, " s (collective_timeout_s = ", timeout_s_, ")");
     }
@@ -324,6 +386,7 @@ void RcclComm::watchdog() {
     if (!exit_on_timeout_) {
       fail_msg_ = why;
       failed_ = true;
+      abort_comm(lk);  // a thread blocked in a sync on this stream is released
       continue;
     }
     std::fprintf(stderr,
@@ -346,9 +409,11 @@ void RcclComm::all_reduce(at::Tensor& t, k::RedOp op) {
   check();
   ++calls_;
   c10::hip::HIPGuard guard(t.device().index());
+  hipEvent_t st = begin(cur_stream(t));
+  if (test_stall_s_ > 0) k::device_stall(static_cast<uint64_t>(test_stall_s_ * 1e6), cur_stream(t));
   TFA_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), nccl_op(op),
                          static_cast<ncclComm_t>(comm_), cur_stream(t)));
-  track(cur_stream(t));
+  track(cur_stream(t), st);
 }
 
 at::Tensor RcclComm::all_gather(const at::Tensor& t0) {
@@ -360,9 +425,10 @@ at::Tensor RcclComm::all_gather(const at::Tensor& t0) {
   std::vector<int64_t> sz = t.sizes().vec();
   sz.insert(sz.begin(), size_);
   at::Tensor out = pool_empty(sz, t.options());
+  hipEvent_t st = begin(cur_stream(t));
   TFA_NCCL(ncclAllGather(t.data_ptr(), out.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()),
                          static_cast<ncclComm_t>(comm_), cur_stream(t)));
-  track(cur_stream(t));
+  track(cur_stream(t), st);
   return out;
 }
 
@@ -384,6 +450,7 @@ at::Tensor RcclComm::all_to_all_v(const at::Tensor& x0, const std::vector<int64_
   const hipStream_t s = cur_stream(x);
   // one grouped launch: every peer pair moves its rows over its own xGMI link
   // (the groupBy shuffle, reference DebugRowOps.scala:576)
+  hipEvent_t st = begin(s);
   TFA_NCCL(ncclGroupStart());
   int64_t so = 0, ro = 0;
   for (int r = 0; r < size_; ++r) {
@@ -397,7 +464,7 @@ at::Tensor RcclComm::all_to_all_v(const at::Tensor& x0, const std::vector<int64_
     ro += recv_rows[r];
   }
   TFA_NCCL(ncclGroupEnd());
-  track(s);
+  track(s, st);
   return out;
 }
 
@@ -406,9 +473,10 @@ void RcclComm::broadcast(at::Tensor& t, int root) {
   check();
   ++calls_;
   c10::hip::HIPGuard guard(t.device().index());
+  hipEvent_t st = begin(cur_stream(t));
   TFA_NCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), root,
                          static_cast<ncclComm_t>(comm_), cur_stream(t)));
-  track(cur_stream(t));
+  track(cur_stream(t), st);
 }
 
 void RcclComm::barrier() {

@@ -158,19 +158,36 @@ class RcclComm : public Comm {
   void check();
   bool failed() const { return failed_.load(); }
   int64_t inflight() const;
+  // tests: all_reduce runs a spin kernel of this many seconds between its
+  // start event and the RCCL call (a collective that started but does not
+  // finish; RCCL refuses the two ranks on one device a real hang needs)
+  void set_test_stall(double seconds) { test_stall_s_ = seconds; }
 
  private:
-  void track(hipStream_t s);   // event after a collective, for wait() and the watchdog
+  // events around a collective, for wait() and the watchdog: a collective's
+  // age counts from when its start event completed (the work queued ahead of
+  // it on the stream has finished), not from when it was enqueued
+  hipEvent_t begin(hipStream_t s);
+  void track(hipStream_t s, hipEvent_t start);
   void fail(const std::string& why);
+  // ncclCommAbort on a helper thread, given 2 s (releases a collective kernel
+  // that waits for a peer); the communicator is unusable afterwards
+  void abort_comm(std::unique_lock<std::mutex>& held);
   void watchdog();
   void* comm_ = nullptr;  // ncclComm_t
   int rank_, size_, device_;
   double timeout_s_ = 0;
   bool exit_on_timeout_ = true;
+  double test_stall_s_ = 0;
   struct Inflight {
-    hipEvent_t ev;
-    std::chrono::steady_clock::time_point t0;
+    hipEvent_t ev;     // after the collective
+    hipEvent_t start;  // before it (null: counted from enqueue)
+    std::chrono::steady_clock::time_point t0;  // enqueue, then the first time start was seen complete
+    bool started;
   };
+  hipEvent_t take_event();
+  // the age of the oldest in-flight collective (0 while it has not started); wmu_ held
+  double front_age();
   mutable std::mutex wmu_;
   std::condition_variable wcv_;
   std::deque<Inflight> inflight_;

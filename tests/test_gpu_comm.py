@@ -201,10 +201,10 @@ def test_oneshot_self_test_and_forced_fallback(monkeypatch):
         config.force_collectives = old
 
 
-def test_rccl_wait_times_out_behind_a_stalled_stream():
-    """A collective that cannot complete (here: queued behind a 3 s stall
-    kernel) raises CollectiveError at the 0.5 s timeout, not at completion;
-    the communicator is then failed and refuses new collectives."""
+def test_rccl_queued_collective_does_not_time_out_behind_compute():
+    """A collective queued behind 2 s of other work on its stream is NOT timed
+    out at 0.5 s: its clock starts when it starts (a start event before it),
+    so a backed-up stream never trips the watchdog of a healthy rank."""
     _need_gpu()
     import time
 
@@ -213,15 +213,38 @@ def test_rccl_wait_times_out_behind_a_stalled_stream():
     c.set_timeout(0.5, False)
     x = torch.ones(1 << 20, device="cuda")
     torch.cuda.synchronize()
-    _C.device_stall(3.0)
+    _C.device_stall(2.0)
+    c.all_reduce(x, "Sum")
+    t0 = time.time()
+    c.wait()
+    assert time.time() - t0 > 1.0 and not c.failed and c.inflight == 0
+
+
+def test_rccl_wait_times_out_and_aborts_a_started_collective():
+    """A collective that started and does not finish (test stall inside it)
+    raises CollectiveError at the 0.5 s timeout; the communicator is aborted
+    (ncclCommAbort releases a collective kernel waiting for a peer), so a later
+    device synchronisation returns in bounded time, and it refuses new
+    collectives."""
+    _need_gpu()
+    import time
+
+    from tensorframes_amd._native import _C
+    c = _C.RcclComm(_C.rccl_unique_id(), 0, 1, 0)
+    c.set_timeout(0.5, False)
+    x = torch.ones(1 << 20, device="cuda")
+    torch.cuda.synchronize()
+    c.set_test_stall(3.0)
     c.all_reduce(x, "Sum")
     t0 = time.time()
     with pytest.raises(_C.CollectiveError, match="timed out"):
         c.wait()
     waited = time.time() - t0
-    assert waited < 2.0, waited
-    torch.cuda.synchronize()  # the stall ends; the queued collective completes
-    assert c.failed
+    assert waited < 3.0, waited
+    t1 = time.time()
+    torch.cuda.synchronize()
+    assert time.time() - t1 < 10.0
+    assert c.failed and c.async_error() == "aborted"
     with pytest.raises(_C.CollectiveError):
         c.all_reduce(x, "Sum")
     # a healthy communicator: wait() returns once the work is done
@@ -233,8 +256,9 @@ def test_rccl_wait_times_out_behind_a_stalled_stream():
 
 
 def test_rccl_watchdog_ends_a_stuck_process(tmp_path):
-    """The main thread blocks in an unbounded synchronisation behind a stalled
-    collective: the watchdog aborts the communicator and exits with 76."""
+    """The main thread blocks in an unbounded synchronisation on a collective
+    that started and does not finish: the watchdog aborts the communicator
+    and exits with 76."""
     _need_gpu()
     import subprocess
     import sys
@@ -247,7 +271,7 @@ def test_rccl_watchdog_ends_a_stuck_process(tmp_path):
         "c.set_timeout(0.3, True)\n"
         "x = torch.ones(1 << 20, device='cuda'); torch.cuda.synchronize()\n"
         "print('T0', time.time(), flush=True)\n"
-        "_C.device_stall(12.0)\n"
+        "c.set_test_stall(12.0)\n"
         "c.all_reduce(x, 'Sum')\n"
         "torch.cuda.synchronize()\n"
         "print('NOT REACHED')\n" % repo)
