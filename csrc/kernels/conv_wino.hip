@@ -40,6 +40,7 @@
 //     its concat channel slice, or the sibling-conv segments).
 // Summation order is fixed (no atomics): a given conv always gives the same
 // bits. Numerics: tests/test_gpu_wino.py gates the error against fp64.
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -92,92 +93,103 @@ __device__ __forceinline__ float act3(float v, int a) {  // none / ReLU / ReLU6 
 
 constexpr uint32_t kOOB = 0x80000000u;  // an offset past every input descriptor
 
-// NW = 4: one wave per SIMD (256 accumulators per lane); NW = 8: two waves
-// per SIMD splitting the block's tiles (128 each), so one wave's fragment
-// reads at a stage start are covered by its partner's MFMAs
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom q, int nbn) {
-  constexpr int T = 64, BN = 64;                               // tiles x output channels per block
-  constexpr int NTP = NW / 4, TWV = T / NTP, TM = TWV / 32;    // tile parts, tiles per wave, 32-row MFMA tiles
+// epilogue stores of rows past the end (tiles past the last, odd output
+// edges, oc past OC) land here, so every lane issues the same stores (the
+// next item's first wait counts them: no branch around a store)
+__device__ __attribute__((aligned(16))) float4 kWinoTrash[64];
+
+// Persistent: one block of 8 waves (two per SIMD) per CU, each taking work
+// items (64 tiles x 64 oc) b', b' + G, ... (b' = XCD remap of its index, so
+// the 32 blocks of one XCD hold 32 consecutive items: the oc blocks of a tile
+// block, and neighbouring tile blocks, share L2). The DMA of the next item's
+// first stage is issued before this item's epilogue, which hides its latency.
+// Wave w owns the xi row xr = w & 3 of tiles [32 (w >> 2), +32) x 64 oc:
+// acc[xi_x][oc half] = 4 x 2 32x32 accumulators = 128 registers per lane.
+__global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, int nbn, int nwork) {
+  constexpr int T = 64, BN = 64, TWV = 32;
   constexpr int IN_BYTES = 16 * 2 * T * 16, U_BYTES = 16 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
-  constexpr int GI = 32 / NW, GU = 32 / NW, G = GI + GU;       // DMA pieces per wave per stage
-  constexpr int EP = BN + 4;                                   // epilogue row pitch (floats)
-  constexpr int E_BYTES = 4 * 2 * T * EP * 4;
-  constexpr int SMEM = 2 * STAGE > E_BYTES ? 2 * STAGE : E_BYTES;
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  constexpr int GI = 4, GU = 4;                // DMA pieces per wave per stage (32 + 32 per block)
+  constexpr int EP = BN + 4;                   // exchange row pitch (floats): conflict-free ds_write_b32
+  constexpr int EH_BYTES = 4 * T * EP * 4;     // one px plane of the exchange
+  constexpr int SMEM = STAGE + EH_BYTES;       // slot 0 | slot 1, the exchange plane over slot 1 and past it
+  constexpr int LPT = BN / 4, TPP = 64 / LPT;  // epilogue: lanes per tile (float4 of oc), tiles per pass
+  constexpr int NPASS = T / 8 / TPP;           // passes over the wave's T/8 tiles
+  constexpr int NST = NPASS * 2 * 2;           // stores per lane per item (unconditional)
+  static_assert(2 * STAGE <= SMEM && SMEM <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int xr = wave & 3, tp = wave >> 2;  // xi row, tile part
   const int h = lane >> 5, r32 = lane & 31;
-  const int nwg = gridDim.x;
-  const int wg = f32core::xcd_remap(blockIdx.x, nwg);
-  const int64_t t0 = (int64_t)(wg / nbn) * T;
-  const int n0 = (wg % nbn) * BN;
+  const int G = gridDim.x;
   const int KT = q.KT;
-
-  // ---- descriptors: the input from the block's first image on (every valid
-  // tap of the block lies within 2^31 bytes of it: conv_wino_eligible) and
-  // the whole filter
-  const uint32_t nb0 = (uint32_t)(t0 / ((int64_t)q.TH * q.TW));
-  const __amdgpu_buffer_rsrc_t rin = wrsrc(static_cast<const float*>(g.A) + (int64_t)nb0 * q.img_floats,
-                                            (q.dbg & 2) ? 0u : kOOB);
+  const float* x = static_cast<const float*>(g.A);
   const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
-  // input piece p = wave * GI + i: patch position pos = p >> 1 (= 4 py + px),
-  // tile half th = p & 1; lane L takes tile 32 th + (L & 31), channel quad
-  // L >> 5, so the two 16-byte quads of one pixel are one 32-byte access of
-  // one instruction (half the distinct lines of one-quad-per-instruction).
-  // The lane's byte offset is fixed for the loop (out of range: a padding
-  // tap / a tile past the end). LDS image: [pos][th][quad][32 tiles][16 B].
-  uint32_t ioff[GI];
-#pragma unroll
-  for (int i = 0; i < GI; ++i) {
-    const int p = wave * GI + i, pos = p >> 1, py = pos >> 2, px = pos & 3;
-    const int64_t t = t0 + (p & 1) * 32 + r32;
-    const bool live = t < q.ntiles;
-    const uint32_t tc = live ? (uint32_t)t : 0u;
-    const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
-    const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
-    const int ih = 2 * (int)ty - q.pt + py, iw = 2 * (int)tx - q.pl + px;
-    const bool ok = live & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
-    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
-  }
+  const __amdgpu_buffer_rsrc_t rnil = wrsrc(g.B, 0u);
   // filter piece p = wave * GU + i: (xi, quad) = (p >> 1, p & 1), oc n0 + lane
   uint32_t uoff[GU];
 #pragma unroll
-  for (int i = 0; i < GU; ++i) {
-    const int p = wave * GU + i;
-    uoff[i] = (uint32_t)((p * q.OCP + lane) * 16);
-  }
+  for (int i = 0; i < GU; ++i) uoff[i] = (uint32_t)(((wave * GU + i) * q.OCP + lane) * 16);
   const uint32_t ustep = (uint32_t)(32 * q.OCP * 16);  // filter bytes per 8-channel stage
-  const uint32_t ubase = (uint32_t)(n0 * 16);
 
-  // stage kt -> slot kt & 1: input [pos][quad][tile][4 c], filter [xi][quad][oc][4 c]
-  auto issue = [&](int kt) __attribute__((always_inline)) {
+  // ---- one work item's DMA state. Input: the descriptor starts at the
+  // item's first image (every valid tap lies within 2^31 bytes of it:
+  // conv_wino_eligible); piece p = wave * GI + i: patch position p >> 1
+  // (= 4 py + px), tile half p & 1, lane L: tile 32 (p & 1) + (L & 31),
+  // channel quad L >> 5 (a pixel's two quads are one 32-byte access). A
+  // padding tap or a tile past the end has an out-of-range offset (zeros).
+  // An item past the end (the prefetch after a block's last item) reads
+  // through the empty descriptor.
+  struct Item {
+    int64_t t0;
+    int n0;
+    __amdgpu_buffer_rsrc_t rin, rf;
+    uint32_t ioff[GI];
+  };
+  auto setup = [&](int item, bool live, Item& it) __attribute__((always_inline)) {
+    const int itc = live ? item : 0;
+    it.t0 = (int64_t)(itc / nbn) * T;
+    it.n0 = (itc % nbn) * BN;
+    const uint32_t nb0 = (uint32_t)(it.t0 / ((int64_t)q.TH * q.TW));
+    const __amdgpu_buffer_rsrc_t r = wrsrc(x + (int64_t)nb0 * q.img_floats, (q.dbg & 2) ? 0u : kOOB);
+    it.rin = live ? r : rnil;
+    it.rf = live ? ru : rnil;
+#pragma unroll
+    for (int i = 0; i < GI; ++i) {
+      const int p = wave * GI + i, pos = p >> 1, py = pos >> 2, px = pos & 3;
+      const int64_t t = it.t0 + (p & 1) * 32 + r32;
+      const bool tl = t < q.ntiles;
+      const uint32_t tc = tl ? (uint32_t)t : 0u;
+      const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
+      const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
+      const int ih = 2 * (int)ty - q.pt + py, iw = 2 * (int)tx - q.pl + px;
+      const bool ok = tl & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
+      it.ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
+    }
+  };
+  // stage kt -> slot kt & 1: input [pos][th][quad][32 tiles][16 B], filter [xi][quad][oc][16 B]
+  auto issue = [&](const Item& it, int kt) __attribute__((always_inline)) {
     char* base = smem + (kt & 1) * STAGE;
-    const uint32_t is = (uint32_t)kt * 32u, us = ubase + (uint32_t)kt * ustep;
+    const uint32_t is = (uint32_t)kt * 32u, us = (uint32_t)(it.n0 * 16) + (uint32_t)kt * ustep;
 #pragma unroll
-    for (int i = 0; i < GI; ++i) bdma16(rin, ioff[i], is, base + (wave * GI + i) * 1024);
+    for (int i = 0; i < GI; ++i) bdma16(it.rin, it.ioff[i], is, base + (wave * GI + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < GU; ++i) bdma16(ru, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
+    for (int i = 0; i < GU; ++i) bdma16(it.rf, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
   };
 
-  // ---- fragments: lane (h, r32) holds tile r32 (of a 32-tile group) and oc
-  // r32 (of a 32-oc half), channel quad h; MFMA step s takes channel 4h + s.
+  // ---- fragments: lane (h, r32) holds tile r32 of the wave's 32 and oc r32
+  // of a 32-oc half, channel quad h; MFMA step s takes channel 4h + s.
   // B^T row xr: t = d[ra] + sgn * d[rb]
   const int ra = xr == 0 ? 0 : (xr == 2 ? 2 : 1);
   const int rb = xr == 0 ? 2 : (xr == 1 ? 2 : (xr == 2 ? 1 : 3));
   const float sgn = xr == 1 ? 1.f : -1.f;
-  f32x4 av[4][TM];   // A: [xi_x][tile group] -> 4 steps
-  f32x4 bv[4][2];    // B: [xi_x][oc half] -> 4 steps
+  f32x4 av[4], bv[4][2];
   // reads in the order the xi_x columns need them (V_0 = t0 - t2, then t1,
   // then t3), so the first MFMAs wait for 6 of the 16 reads only
   auto read = [&](int kt) __attribute__((always_inline)) {
     const char* st = smem + (kt & 1) * STAGE;
-    auto inp = [&](int r, int px, int gi) __attribute__((always_inline)) {
-      const int th = tp * TM + gi;
-      return *reinterpret_cast<const f32x4*>(st + (((r * 4 + px) * 2 + th) * 2 + h) * 512 + r32 * 16);
+    auto inp = [&](int r, int px) __attribute__((always_inline)) {
+      return *reinterpret_cast<const f32x4*>(st + (((r * 4 + px) * 2 + tp) * 2 + h) * 512 + r32 * 16);
     };
     auto filt = [&](int j, int nh) __attribute__((always_inline)) {
       bv[j][nh] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + (((4 * xr + j) * 2 + h) * BN + nh * 32 + r32) * 16);
@@ -188,281 +200,131 @@ __global__ __launch_bounds__(64 * NW, 1) void wino23_kernel(GemmArgs g, WinoGeom
       for (int c = 0; c < 4; ++c) t[c] = __builtin_fmaf(sgn, b[c], a[c]);  // exact a +- b
       return t;
     };
-    f32x4 t[4][TM];
-#pragma unroll
-    for (int gi = 0; gi < TM; ++gi) {
-      t[0][gi] = tr(inp(ra, 0, gi), inp(rb, 0, gi));
-      t[2][gi] = tr(inp(ra, 2, gi), inp(rb, 2, gi));
-    }
+    const f32x4 t0v = tr(inp(ra, 0), inp(rb, 0));
+    const f32x4 t2v = tr(inp(ra, 2), inp(rb, 2));
     filt(0, 0);
     filt(0, 1);
-#pragma unroll
-    for (int gi = 0; gi < TM; ++gi) {
-      av[0][gi] = t[0][gi] - t[2][gi];
-      t[1][gi] = tr(inp(ra, 1, gi), inp(rb, 1, gi));
-    }
+    av[0] = t0v - t2v;
+    const f32x4 t1v = tr(inp(ra, 1), inp(rb, 1));
     filt(1, 0);
     filt(1, 1);
     filt(2, 0);
     filt(2, 1);
-#pragma unroll
-    for (int gi = 0; gi < TM; ++gi) {
-      av[1][gi] = t[1][gi] + t[2][gi];
-      av[2][gi] = t[2][gi] - t[1][gi];
-      t[3][gi] = tr(inp(ra, 3, gi), inp(rb, 3, gi));
-    }
+    av[1] = t1v + t2v;
+    av[2] = t2v - t1v;
+    const f32x4 t3v = tr(inp(ra, 3), inp(rb, 3));
     filt(3, 0);
     filt(3, 1);
-#pragma unroll
-    for (int gi = 0; gi < TM; ++gi) av[3][gi] = t[1][gi] - t[3][gi];
+    av[3] = t1v - t3v;
   };
 
-  f32x16 acc[4][TM][2];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int gi = 0; gi < TM; ++gi)
-#pragma unroll
-      for (int nh = 0; nh < 2; ++nh) acc[j][gi][nh] = (f32x16){};
-
-  // One stage: my DMA of stage kt retired, barrier (everyone's landed, and
-  // everyone is done reading slot kt-1), DMA of stage kt+1 into that slot,
-  // then the fragment reads + input transform and 32 * TM MFMAs of stage kt.
-  // The xi_x = 3 column's MFMAs of stage kt are deferred into stage kt+1:
-  // issued right after its barrier, they keep the matrix pipe busy while
-  // that stage's fragment reads and input transform are in flight.
-  auto mfma_cols = [&](int j0, int j1, const f32x4 (&a)[4][TM], const f32x4 (&b)[4][2]) __attribute__((always_inline)) {
+  f32x16 acc[4][2];
+  auto mfma_cols = [&](int j0, int j1, const f32x4 (&a)[4], const f32x4 (&b)[4][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = j0; j < j1; ++j)
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int gi = 0; gi < TM; ++gi)
-#pragma unroll
-          for (int nh = 0; nh < 2; ++nh)
-            acc[j][gi][nh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][gi][s], b[j][nh][s], acc[j][gi][nh], 0, 0, 0);
+        for (int nh = 0; nh < 2; ++nh)
+          acc[j][nh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][s], b[j][nh][s], acc[j][nh], 0, 0, 0);
   };
-  f32x4 pa[4][TM], pb[4][2];  // the deferred column (only [3] is live)
-  issue(0);
-  for (int kt = 0; kt < KT; ++kt) {
-    wwait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kt + 1 < KT) issue(kt + 1);
-    if (kt > 0) mfma_cols(3, 4, pa, pb);
-    read(kt);
-    mfma_cols(0, 3, av, bv);
-#pragma unroll
-    for (int gi = 0; gi < TM; ++gi) pa[3][gi] = av[3][gi];
-    pb[3][0] = bv[3][0];
-    pb[3][1] = bv[3][1];
-  }
-  mfma_cols(3, 4, pa, pb);
-  __syncthreads();  // every wave is done with the stages: the LDS becomes the epilogue exchange
+  f32x4 pa[4], pb[4][2];  // the deferred xi_x = 3 column (only [3] is live)
+  float* E = reinterpret_cast<float*>(smem + STAGE);
 
-  // ---- epilogue. A^T along x: this wave's rows m'[xr][px] (C/D layout of
-  // 32x32x2: oc = 32 nh + (l & 31), tile = 32 gi + (r & 3) + 8 (r >> 2) + 4 h)
-  float* E = reinterpret_cast<float*>(smem);
+  int item = f32core::xcd_remap(blockIdx.x, G);
+  if (item >= nwork) return;
+  Item cur;
+  setup(item, true, cur);
+  issue(cur, 0);
+  for (bool first = true;; first = false) {
 #pragma unroll
-  for (int gi = 0; gi < TM; ++gi)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float m0 = (acc[0][gi][nh][r] + acc[1][gi][nh][r]) + acc[2][gi][nh][r];
-        const float m1 = (acc[1][gi][nh][r] - acc[2][gi][nh][r]) - acc[3][gi][nh][r];
-        const int tile = tp * TWV + 32 * gi + (r & 3) + 8 * (r >> 2) + 4 * h, oc = 32 * nh + r32;
-        E[((xr * 2 + 0) * T + tile) * EP + oc] = m0;
-        E[((xr * 2 + 1) * T + tile) * EP + oc] = m1;
-      }
-  __syncthreads();
-  // A^T along y over the 4 xi rows; wave w writes tiles [w T/NW, (w+1) T/NW)
-  constexpr int LPT = BN / 4, TPP = 64 / LPT;  // lanes per tile (float4 of oc), tiles per pass
-  const int cq = lane % LPT, tr = lane / LPT;
-  const int64_t col = n0 + 4 * cq;
-  if (col >= g.N) return;
-  float* cbase;
-  int64_t cld;
-  int cact;
-  f32core::out_col(g, static_cast<float*>(g.C), col, cbase, cld, cact);
-  const float* bias = static_cast<const float*>(g.bias);
-  const float4 bvv = bias ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int ps = 0; ps < T / NW / TPP; ++ps) {
-    const int tile = wave * (T / NW) + ps * TPP + tr;
-    const int64_t t = t0 + tile;
-    if (t >= q.ntiles) continue;
-    const uint32_t tc = (uint32_t)t, qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
-    const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
+      for (int nh = 0; nh < 2; ++nh) acc[j][nh] = (f32x16){};
+    // The xi_x = 3 column's MFMAs of stage kt run right after stage kt+1's
+    // barrier: they keep the matrix pipe busy while that stage's fragment
+    // reads and input transform are in flight.
+    for (int kt = 0; kt < KT; ++kt) {
+      if (kt == 0 && !first) wwait_vm<NST>();  // the previous epilogue's stores may still fly
+      else wwait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + 1 < KT) issue(cur, kt + 1);
+      if (kt > 0) mfma_cols(3, 4, pa, pb);
+      read(kt);
+      mfma_cols(0, 3, av, bv);
+      pa[3] = av[3];
+      pb[3][0] = bv[3][0];
+      pb[3][1] = bv[3][1];
+    }
+    mfma_cols(3, 4, pa, pb);
+    // the epilogue's per-lane column, its activation and bias (loaded before
+    // the barrier, whose vmcnt(0) it then costs nothing)
+    const int cq = lane % LPT, trr = lane / LPT;
+    const int64_t col = cur.n0 + 4 * cq;
+    const bool colok = col < g.N;
+    float* cbase;
+    int64_t cld;
+    int cact;
+    f32core::out_col(g, static_cast<float*>(g.C), colok ? col : 0, cbase, cld, cact);
+    const float* bias = static_cast<const float*>(g.bias);
+    const float4 bvv = (bias && colok) ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();  // the ring is free: slot 0 takes the next item's first stage, slot 1 the exchange
+    const int next = item + G;
+    const bool live = next < nwork;
+    Item nx;
+    setup(next, live, nx);
+    issue(nx, 0);
+    // ---- epilogue, one output column px at a time. A^T along x in
+    // registers: m'[xr][px] (C/D layout of 32x32x2: oc = 32 nh + (l & 31),
+    // tile = (r & 3) + 8 (r >> 2) + 4 h of the wave's 32); the 4 xi rows
+    // through LDS; A^T along y; bias + activation; float4 stores.
 #pragma unroll
     for (int px = 0; px < 2; ++px) {
-      const int ow = 2 * (int)tx + px;
-      f32x4 e[4];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) e[w] = *reinterpret_cast<const f32x4*>(&E[((w * 2 + px) * T + tile) * EP + 4 * cq]);
-      const f32x4 y0 = (e[0] + e[1]) + e[2];
-      const f32x4 y1 = (e[1] - e[2]) - e[3];
+      for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-      for (int py = 0; py < 2; ++py) {
-        const int oh = 2 * (int)ty + py;
-        const f32x4 v = py ? y1 : y0;
-        float4 o;
-        o.x = act3(v[0] + bvv.x, cact);
-        o.y = act3(v[1] + bvv.y, cact);
-        o.z = act3(v[2] + bvv.z, cact);
-        o.w = act3(v[3] + bvv.w, cact);
-        const int64_t row = ((int64_t)n * q.OH + oh) * q.OW + ow;
-        if (ow < q.OW && oh < q.OH && !(q.dbg & 4)) *reinterpret_cast<float4*>(cbase + row * cld) = o;
+        for (int r = 0; r < 16; ++r) {
+          const float m = px == 0 ? (acc[0][nh][r] + acc[1][nh][r]) + acc[2][nh][r]
+                                  : (acc[1][nh][r] - acc[2][nh][r]) - acc[3][nh][r];
+          const int tile = tp * TWV + (r & 3) + 8 * (r >> 2) + 4 * h;
+          E[(xr * T + tile) * EP + 32 * nh + r32] = m;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int ps = 0; ps < NPASS; ++ps) {
+        const int tile = wave * (T / 8) + ps * TPP + trr;
+        const int64_t t = cur.t0 + tile;
+        const bool tl = t < q.ntiles;
+        const uint32_t tc = tl ? (uint32_t)t : 0u, qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
+        const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
+        f32x4 e[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) e[w] = *reinterpret_cast<const f32x4*>(&E[(w * T + tile) * EP + 4 * cq]);
+        const f32x4 y0 = (e[0] + e[1]) + e[2];
+        const f32x4 y1 = (e[1] - e[2]) - e[3];
+        const int ow = 2 * (int)tx + px;
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+          const int oh = 2 * (int)ty + py;
+          const f32x4 v = py ? y1 : y0;
+          float4 o;
+          o.x = act3(v[0] + bvv.x, cact);
+          o.y = act3(v[1] + bvv.y, cact);
+          o.z = act3(v[2] + bvv.z, cact);
+          o.w = act3(v[3] + bvv.w, cact);
+          const bool ok = tl && colok && ow < q.OW && oh < q.OH && !(q.dbg & 4);
+          const int64_t row = ((int64_t)n * q.OH + oh) * q.OW + ow;
+          float4* dst = ok ? reinterpret_cast<float4*>(cbase + (ok ? row : 0) * cld) : &kWinoTrash[lane];
+          *dst = o;
+        }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // the plane is read: the next one may overwrite it
     }
-  }
-}
-
-// Register-epilogue variant: 4 waves (one per SIMD), wave w owns ALL 16 xi
-// of a 32-tile x 32-oc quadrant (tile half w & 1, oc half w >> 1): 16 32x32
-// accumulators = 256 registers per lane. Each wave transforms the whole 4x4
-// patch of its tiles (the two oc-half waves repeat it: 32 VALU per 64 MFMAs),
-// and A^T M A is done in registers at the end: no LDS exchange, no epilogue
-// barrier, scalar 4-byte stores that cover 32 consecutive oc per half wave.
-__global__ __launch_bounds__(256, 1) void wino23_reg_kernel(GemmArgs g, WinoGeom q, int nbn) {
-  constexpr int T = 64, BN = 64;
-  constexpr int IN_BYTES = 16 * 2 * T * 16, U_BYTES = 16 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
-  constexpr int GI = 8, GU = 8;  // DMA pieces per wave per stage (32 + 32 per block)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int th = wave & 1, oh = wave >> 1;
-  const int h = lane >> 5, r32 = lane & 31;
-  const int nwg = gridDim.x;
-  const int wg = f32core::xcd_remap(blockIdx.x, nwg);
-  const int64_t t0 = (int64_t)(wg / nbn) * T;
-  const int n0 = (wg % nbn) * BN;
-  const int KT = q.KT;
-
-  const uint32_t nb0 = (uint32_t)(t0 / ((int64_t)q.TH * q.TW));
-  const __amdgpu_buffer_rsrc_t rin = wrsrc(static_cast<const float*>(g.A) + (int64_t)nb0 * q.img_floats,
-                                            (q.dbg & 2) ? 0u : kOOB);
-  const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
-  // input piece p = wave * GI + i: patch position p >> 1, tile half p & 1;
-  // lane L: tile 32 (p & 1) + (L & 31), channel quad L >> 5 (as wino23_kernel)
-  uint32_t ioff[GI];
-#pragma unroll
-  for (int i = 0; i < GI; ++i) {
-    const int p = wave * GI + i, pos = p >> 1, py = pos >> 2, px = pos & 3;
-    const int64_t t = t0 + (p & 1) * 32 + r32;
-    const bool live = t < q.ntiles;
-    const uint32_t tc = live ? (uint32_t)t : 0u;
-    const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
-    const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
-    const int ih = 2 * (int)ty - q.pt + py, iw = 2 * (int)tx - q.pl + px;
-    const bool ok = live & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
-    ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
-  }
-  uint32_t uoff[GU];
-#pragma unroll
-  for (int i = 0; i < GU; ++i) uoff[i] = (uint32_t)(((wave * GU + i) * q.OCP + lane) * 16);
-  const uint32_t ustep = (uint32_t)(32 * q.OCP * 16);
-  const uint32_t ubase = (uint32_t)(n0 * 16);
-  auto issue = [&](int kt) __attribute__((always_inline)) {
-    char* base = smem + (kt & 1) * STAGE;
-    const uint32_t is = (uint32_t)kt * 32u, us = ubase + (uint32_t)kt * ustep;
-#pragma unroll
-    for (int i = 0; i < GI; ++i) bdma16(rin, ioff[i], is, base + (wave * GI + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < GU; ++i) bdma16(ru, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
-  };
-
-  f32x16 acc[16];
-#pragma unroll
-  for (int x = 0; x < 16; ++x) acc[x] = (f32x16){};
-
-  // one stage: patch rows in the order the xi rows need them (row 0 = d0-d2,
-  // rows 1, 2 = d1 +- d2, row 3 = d1 - d3), each xi row's 16 MFMAs as soon as
-  // its transform is done
-  auto stage = [&](int kt) __attribute__((always_inline)) {
-    const char* st = smem + (kt & 1) * STAGE;
-    auto inp = [&](int py, int px) __attribute__((always_inline)) {
-      return *reinterpret_cast<const f32x4*>(st + ((((py * 4 + px) * 2 + th) * 2 + h) * 512) + r32 * 16);
-    };
-    auto filt = [&](int x) __attribute__((always_inline)) {
-      return *reinterpret_cast<const f32x4*>(st + IN_BYTES + ((x * 2 + h) * BN + oh * 32 + r32) * 16);
-    };
-    auto row_mfma = [&](int y, const f32x4 (&t)[4]) __attribute__((always_inline)) {
-      f32x4 v[4];
-      v[0] = t[0] - t[2];
-      v[1] = t[1] + t[2];
-      v[2] = t[2] - t[1];
-      v[3] = t[1] - t[3];
-#pragma unroll
-      for (int xx = 0; xx < 4; ++xx) {
-        const f32x4 b = filt(4 * y + xx);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          acc[4 * y + xx] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[xx][s], b[s], acc[4 * y + xx], 0, 0, 0);
-      }
-    };
-    f32x4 d0[4], d1[4], d2[4], d3[4], t[4];
-#pragma unroll
-    for (int px = 0; px < 4; ++px) {
-      d0[px] = inp(0, px);
-      d2[px] = inp(2, px);
-    }
-#pragma unroll
-    for (int px = 0; px < 4; ++px) t[px] = d0[px] - d2[px];
-    row_mfma(0, t);
-#pragma unroll
-    for (int px = 0; px < 4; ++px) d1[px] = inp(1, px);
-#pragma unroll
-    for (int px = 0; px < 4; ++px) t[px] = d1[px] + d2[px];
-    row_mfma(1, t);
-#pragma unroll
-    for (int px = 0; px < 4; ++px) t[px] = d2[px] - d1[px];
-    row_mfma(2, t);
-#pragma unroll
-    for (int px = 0; px < 4; ++px) d3[px] = inp(3, px);
-#pragma unroll
-    for (int px = 0; px < 4; ++px) t[px] = d1[px] - d3[px];
-    row_mfma(3, t);
-  };
-
-  issue(0);
-  for (int kt = 0; kt < KT; ++kt) {
-    wwait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kt + 1 < KT) issue(kt + 1);
-    stage(kt);
-  }
-
-  // ---- epilogue in registers: C/D row r -> tile 32 th + (r & 3) + 8 (r >> 2) + 4 h
-  const int64_t col = n0 + oh * 32 + r32;
-  if (col >= g.N) return;
-  float* cbase;
-  int64_t cld;
-  int cact;
-  f32core::out_col(g, static_cast<float*>(g.C), col, cbase, cld, cact);
-  const float bias = g.bias ? static_cast<const float*>(g.bias)[col] : 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t t = t0 + th * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    float m[4][2];
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      m[y][0] = (acc[4 * y + 0][r] + acc[4 * y + 1][r]) + acc[4 * y + 2][r];
-      m[y][1] = (acc[4 * y + 1][r] - acc[4 * y + 2][r]) - acc[4 * y + 3][r];
-    }
-    if (t >= q.ntiles || (q.dbg & 4)) continue;
-    const uint32_t tc = (uint32_t)t, qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
-    const uint32_t n = fdiv(qa, q.fTH), ty = qa - n * (uint32_t)q.TH;
-#pragma unroll
-    for (int px = 0; px < 2; ++px) {
-      const float y0 = (m[0][px] + m[1][px]) + m[2][px];
-      const float y1 = (m[1][px] - m[2][px]) - m[3][px];
-      const int ow = 2 * (int)tx + px;
-      const int64_t row = ((int64_t)n * q.OH + 2 * (int)ty) * q.OW + ow;
-      if (ow < q.OW) {
-        cbase[row * cld] = act3(y0 + bias, cact);
-        if (2 * (int)ty + 1 < q.OH) cbase[(row + q.OW) * cld] = act3(y1 + bias, cact);
-      }
-    }
+    if (!live) break;
+    item = next;
+    cur = nx;
   }
 }
 
@@ -474,8 +336,8 @@ std::atomic<int>& wino_state() {
   return v;
 }
 
-// forced variant (-1 auto, 1: 8 waves with the LDS-exchange epilogue, 2: 4 waves with the register
-// epilogue; both 64 tiles x 64 oc)
+// forced variant (-1 auto: persistent blocks, 3: one work item per block, for A/B; the
+// OC <= 32 shapes only run Winograd when a variant is forced)
 std::atomic<int>& wino_variant() {
   static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_WINO_TILE");
@@ -570,15 +432,19 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   g.act = a.act;
   g.batch = 1;
   g.seg = a.seg;
-  int v = wino_variant().load();
-  if (v < 0) v = 1;
   const int64_t nbt = (q.ntiles + 63) / 64, nbn = (a.OC + 63) / 64;
   TFA_CHECK(nbt * nbn < (int64_t(1) << 31), "conv_wino: grid too large");
-  const dim3 grid((unsigned)(nbt * nbn));
-  if (v == 2)
-    hipLaunchKernelGGL(wino23_reg_kernel, grid, dim3(256), 0, s, g, q, (int)nbn);
-  else
-    hipLaunchKernelGGL((wino23_kernel<8>), grid, dim3(512), 0, s, g, q, (int)nbn);
+  const int nwork = (int)(nbt * nbn);
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    (void)hipGetLastError();
+    return n > 0 ? n : 256;
+  }();
+  const int per_cu = wino_variant().load() == 3 ? 0 : 1;  // 3: one item per block (no persistence), for A/B
+  const int grid = per_cu ? std::min(nwork, ncu) : nwork;
+  hipLaunchKernelGGL(wino23_kernel, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   TFA_LAUNCH_CHECK("conv_wino");
 }
 

@@ -79,10 +79,10 @@ for s in ${STEPS:-tests}; do
         done
       done ;;
     wtest) run wino_tests 400 python -u -m pytest tests/test_gpu_wino.py -x -v --timeout 200 --timeout-method thread ;;
-    layers_v1) TFA_WINO_TILE=1 run layers_wino_v1 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v1.json ;;
+    layers_v1) run layers_wino_v1 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v1.json ;;
     wdbg) for d in ${WDBG:-0 1 2 3 4}; do TFA_WINO_DEBUG=$d run wdbg_l${WL:-4}_d$d 120 python scripts/conv_layers.py --only ${WL:-4} --iters 5 || exit 1; grep -h TF gpurun_out/wdbg_l${WL:-4}_d$d.log | tail -1; done ;;
     wsweep) run wsweep 300 python scripts/wino_sweep.py ;;
-    wsweep2) TFA_WINO_TILE=2 run wsweep2 300 python scripts/wino_sweep.py ;;
+    wsweep3) TFA_WINO_TILE=3 run wsweep3 300 python scripts/wino_sweep.py ;;
     layers_v2) TFA_WINO_TILE=2 run layers_wino_v2 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v2.json ;;
     layers_v0) TFA_WINO_TILE=0 run layers_wino_v0 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v0.json ;;
     # ---- presets (the one-off round-4/5 step lists, folded in)
