@@ -759,19 +759,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_direct", [](bool on) { k::set_conv_direct(on ? 1 : 0); },
         "route narrow wide-image convs (C in {32, 64}, OC <= 64) to the direct LDS-filter kernel (default on)");
   m.def("set_conv_wino", [](bool on) { k::set_conv_wino(on ? 1 : 0); },
-        "Winograd F(2x2,3x3) for 3x3 stride-1 convs with constant filters (default on; TFA_CONV_ALGO=direct "
+        "Winograd F(2x2,3x3) / F(2,7) for 3x3 / 1x7 / 7x1 stride-1 convs with constant filters (default on; TFA_CONV_ALGO=direct "
         "turns it off). Plans built while it is off carry no Winograd filters.");
   m.def("conv_wino_enabled", [] { return k::conv_wino_enabled(); });
   m.def("set_wino_tile", [](int v) { k::set_wino_tile(v); },
         "force the Winograd kernel variant: -1 auto, 0 = 64 tiles x 64 oc, 1 = 128 tiles x 32 oc");
   m.def("conv_wino_filter", [](const at::Tensor& w) {
-          TFA_CHECK(w.dim() == 4 && w.size(0) == 3 && w.size(1) == 3 && w.scalar_type() == at::kFloat,
-                    "conv_wino_filter: HWIO [3,3,C,OC] float32");
+          TFA_CHECK(w.dim() == 4 && w.scalar_type() == at::kFloat, "conv_wino_filter: HWIO float32 filter");
+          const int kind = k::conv_wino_kind(w.size(0), w.size(1), 1, 1, 1, 1, w.size(2), w.size(3));
+          TFA_CHECK(kind != 0, "conv_wino_filter: 3x3, 1x7 or 7x1 with C % 8 == 0 and OC % 4 == 0");
           at::Tensor wc = w.cpu().contiguous();
-          at::Tensor u = at::empty({16 * wc.size(2) * k::conv_wino_ocp(wc.size(3))}, wc.options());
-          k::conv_wino_filter(wc.data_ptr<float>(), wc.size(2), wc.size(3), u.data_ptr<float>());
+          at::Tensor u = at::empty({k::conv_wino_filter_elems(kind, wc.size(2), wc.size(3))}, wc.options());
+          k::conv_wino_filter(kind, wc.data_ptr<float>(), wc.size(2), wc.size(3), u.data_ptr<float>());
           return u;
-        }, "the planner's Winograd filter transform (fp64), [C/4][16][OCP][4] flattened (tests)");
+        }, "the planner's Winograd filter transform (fp64): 3x3 -> [C/8][16][2][OCP][4], 1x7 / 7x1 -> "
+           "[C/8][8][2][OCP][4], flattened (tests)");
   m.def("gemm_tile_count", [] { return k::gemm_tile_count(); });
   m.def("gemm_tune_table", &k::gemm_tune_table, "the autotuner's tile picks: [(20-field shape key, tile)]");
   m.def("gemm_tune_seed", &k::gemm_tune_seed, py::arg("key"), py::arg("tile"),

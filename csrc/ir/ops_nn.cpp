@@ -86,9 +86,10 @@ void rows_batch(InferCtx& c) {
 }
 
 // the planner's Winograd filter: device-resident, f32, [C/4][16][OCP][4]
-const void* wino_filter_ptr(const at::Tensor& u, int64_t C, int64_t OC) {
-  TFA_CHECK(u.is_cuda() && u.scalar_type() == at::kFloat && u.is_contiguous() &&
-                u.numel() == 16 * C * k::conv_wino_ocp(OC),
+const void* wino_filter_ptr(const at::Tensor& u, int64_t KH, int64_t KW, int64_t C, int64_t OC) {
+  const int kind = k::conv_wino_kind(KH, KW, 1, 1, 1, 1, C, OC);
+  TFA_CHECK(kind != 0 && u.is_cuda() && u.scalar_type() == at::kFloat && u.is_contiguous() &&
+                u.numel() == k::conv_wino_filter_elems(kind, C, OC),
             "internal: Winograd filter layout");
   return u.data_ptr();
 }
@@ -157,7 +158,7 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
                 out.stride(0) == out.size(1) * out.stride(1),
             "Conv2D: output must be NHWC-contiguous up to the channel stride");
   a.ldc = out.stride(2);
-  if (wino) a.wino = wino_filter_ptr(*wino, g.C, g.OC);
+  if (wino) a.wino = wino_filter_ptr(*wino, g.KH, g.KW, g.C, g.OC);
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
     work = c.alloc({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
@@ -199,7 +200,7 @@ void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0,
   TFA_CHECK(begin == g.OC, "Conv2D siblings: outputs cover ", begin, " channels of ", g.OC);
   a.y = outs[0].data_ptr();
   a.ldc = outs[0].stride(2);
-  if (wino) a.wino = wino_filter_ptr(*wino, g.C, g.OC);
+  if (wino) a.wino = wino_filter_ptr(*wino, g.KH, g.KW, g.C, g.OC);
   if (g.N * g.OH * g.OW == 0) return;
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {

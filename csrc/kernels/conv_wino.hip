@@ -61,6 +61,10 @@ struct WinoGeom {
   int64_t img_floats;    // H * W * C
   int64_t u_bytes;       // the whole transformed filter
   int dbg;               // timing experiments (TFA_WINO_DEBUG): 1 no filter traffic, 2 no input traffic, 4 no stores
+  // F(2,7) (1x7 / 7x1): tile t -> (n, i0, i1) over (D0, D1); the conv axis
+  // is W (axis 0: tile = 2 outputs along W) or H (axis 1)
+  int axis, D0, D1;
+  FastDivU32 fD0, fD1;
   FastDivU32 fTW, fTH;
 };
 
@@ -328,6 +332,191 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
   }
 }
 
+// ---------------------------------------------------------------- F(2,7)
+// 1x7 / 7x1 convs (Inception-v3 Mixed_6x: ~25 % of its conv time): a tile is
+// 2 outputs along the conv axis, its patch 8 inputs; 8 transform points
+// {0, +-1, +-2, +-1/2, inf} (tests/test_wino.py derives and checks the
+// matrices):
+//   V = B^T d: V0 = (d6 - d0) + 21/4 (d2 - d4), V7 = (d7 - d1) + 21/4 (d3 - d5),
+//     V1,2 = E1 +- O1 (E1 = d2 - 17/4 d4 + d6, O1 = d1 - 17/4 d3 + d5),
+//     V3,4 = E3 +- O3 (E3 = d2/4 - 5/4 d4 + d6, O3 = d1/2 - 5/2 d3 + 2 d5),
+//     V5,6 = E5 +- O5 (E5 = 4 d2 - 5 d4 + d6, O5 = 2 d1 - 5/2 d3 + d5/2)
+//   Y0 = M0 + ... + M6,  Y1 = (M1 - M2) + 2 (M3 - M4) + (M5 - M6) / 2 + M7
+// 8 products per 2 outputs instead of 14 (1.75x fewer MFMA FLOPs); f32 error
+// ~1.7x the direct path's (the gate in tests/test_gpu_wino.py).
+//
+// With 8 transform points a wave holds ALL of them for a 32-tile x 32-oc
+// quadrant (8 accumulators of 32x32 = 128 registers per lane, two waves per
+// SIMD), so the output transform is in registers: no LDS exchange, no
+// epilogue barrier. Block: 8 waves = 4 tile quarters x 2 oc halves = 128
+// tiles x 64 oc; 8-channel stages of 48 KB (input [8 pos][4 tq][2 quads][32
+// tiles][16 B], filter [8 xi][2 quads][64 oc][16 B]) in a ring of 3, DMA two
+// stages ahead; persistent blocks prefetch the next item's first stage under
+// the epilogue (as wino23_kernel).
+__global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, int nbn, int nwork) {
+  constexpr int T = 128, BN = 64;
+  constexpr int IN_BYTES = 8 * 2 * T * 16, U_BYTES = 8 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
+  constexpr int S = 3;
+  constexpr int GI = 4, GU = 2, G = GI + GU;  // DMA pieces per wave per stage (32 + 16 per block)
+  constexpr int NST = 32;                     // stores per lane per item (unconditional)
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
+
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int tq = wave & 3, nh = wave >> 2;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int Gd = gridDim.x;
+  const int KT = q.KT;
+  const int dh = q.axis, dw = 1 - q.axis;  // the conv axis: H (7x1) or W (1x7)
+  const float* x = static_cast<const float*>(g.A);
+  const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
+  const __amdgpu_buffer_rsrc_t rnil = wrsrc(g.B, 0u);
+  // filter piece p = wave * GU + i: (xi, quad) = (p >> 1, p & 1), oc n0 + lane
+  uint32_t uoff[GU];
+#pragma unroll
+  for (int i = 0; i < GU; ++i) uoff[i] = (uint32_t)(((wave * GU + i) * q.OCP + lane) * 16);
+  const uint32_t ustep = (uint32_t)(16 * q.OCP * 16);  // filter bytes per 8-channel stage
+
+  auto tile_of = [&](uint32_t tc, uint32_t& n, int& o_h, int& o_w) __attribute__((always_inline)) {
+    const uint32_t qa = fdiv(tc, q.fD1), i1 = tc - qa * (uint32_t)q.D1;
+    n = fdiv(qa, q.fD0);
+    const uint32_t i0 = qa - n * (uint32_t)q.D0;
+    o_h = dh ? 2 * (int)i0 : (int)i0;   // the tile's first output pixel
+    o_w = dh ? (int)i1 : 2 * (int)i1;
+  };
+  // input piece p = wave * GI + i: patch position p >> 2, tile quarter p & 3;
+  // lane L: tile 32 (p & 3) + (L & 31), channel quad L >> 5
+  struct Item {
+    int64_t t0;
+    int n0;
+    __amdgpu_buffer_rsrc_t rin, rf;
+    uint32_t ioff[GI];
+  };
+  auto setup = [&](int item, bool live, Item& it) __attribute__((always_inline)) {
+    const int itc = live ? item : 0;
+    it.t0 = (int64_t)(itc / nbn) * T;
+    it.n0 = (itc % nbn) * BN;
+    const uint32_t nb0 = (uint32_t)(it.t0 / ((int64_t)q.D0 * q.D1));
+    const __amdgpu_buffer_rsrc_t r = wrsrc(x + (int64_t)nb0 * q.img_floats, (q.dbg & 2) ? 0u : kOOB);
+    it.rin = live ? r : rnil;
+    it.rf = live ? ru : rnil;
+#pragma unroll
+    for (int i = 0; i < GI; ++i) {
+      const int p = wave * GI + i, pos = p >> 2;
+      const int64_t t = it.t0 + (p & 3) * 32 + r32;
+      const bool tl = t < q.ntiles;
+      uint32_t n;
+      int oh, ow;
+      tile_of(tl ? (uint32_t)t : 0u, n, oh, ow);
+      const int ih = oh - q.pt + pos * dh, iw = ow - q.pl + pos * dw;
+      const bool ok = tl & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
+      it.ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
+    }
+  };
+  auto issue = [&](const Item& it, int kt) __attribute__((always_inline)) {
+    char* base = smem + (kt % S) * STAGE;
+    const uint32_t is = (uint32_t)kt * 32u, us = (uint32_t)(it.n0 * 16) + (uint32_t)kt * ustep;
+#pragma unroll
+    for (int i = 0; i < GI; ++i) bdma16(it.rin, it.ioff[i], is, base + (wave * GI + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < GU; ++i) bdma16(it.rf, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
+  };
+
+  // ---- fragments: lane (h, r32): tile r32 of the wave's 32, oc r32 of its
+  // half, channel quad h; MFMA step s takes channel 4h + s
+  f32x4 av[8], bv[8];
+  auto read = [&](int kt) __attribute__((always_inline)) {
+    const char* st = smem + (kt % S) * STAGE;
+    f32x4 d[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      d[p] = *reinterpret_cast<const f32x4*>(st + (((p * 4 + tq) * 2 + h) * 512) + r32 * 16);
+#pragma unroll
+    for (int xi = 0; xi < 8; ++xi)
+      bv[xi] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + ((xi * 2 + h) * BN + nh * 32 + r32) * 16);
+    const f32x4 c21 = 5.25f, c17 = 4.25f, c5q = 1.25f, c5h = 2.5f, c5 = 5.f;
+    av[0] = (d[6] - d[0]) + c21 * (d[2] - d[4]);
+    av[7] = (d[7] - d[1]) + c21 * (d[3] - d[5]);
+    const f32x4 e1 = (d[2] + d[6]) - c17 * d[4], o1 = (d[1] + d[5]) - c17 * d[3];
+    av[1] = e1 + o1;
+    av[2] = e1 - o1;
+    const f32x4 e3 = (0.25f * d[2] + d[6]) - c5q * d[4], o3 = (0.5f * d[1] + 2.f * d[5]) - c5h * d[3];
+    av[3] = e3 + o3;
+    av[4] = e3 - o3;
+    const f32x4 e5 = (4.f * d[2] + d[6]) - c5 * d[4], o5 = (2.f * d[1] + 0.5f * d[5]) - c5h * d[3];
+    av[5] = e5 + o5;
+    av[6] = e5 - o5;
+  };
+
+  f32x16 acc[8];
+  int item = f32core::xcd_remap(blockIdx.x, Gd);
+  if (item >= nwork) return;
+  Item cur;
+  setup(item, true, cur);
+  issue(cur, 0);
+  for (bool first = true;; first = false) {
+#pragma unroll
+    for (int xi = 0; xi < 8; ++xi) acc[xi] = (f32x16){};
+    if (KT > 1) issue(cur, 1);
+    for (int kt = 0; kt < KT; ++kt) {
+      // stage kt landed: newer ops that may fly are stage kt+1's DMA and, in
+      // an item's first stage, the previous item's epilogue stores (older
+      // than stage 1's DMA, newer than stage 0's)
+      const bool more = kt + 1 < KT;
+      if (kt == 0 && !first) {
+        if (more) wwait_vm<NST + G>();
+        else wwait_vm<NST>();
+      } else if (more) {
+        wwait_vm<G>();
+      } else {
+        wwait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < KT) issue(cur, kt + 2);  // into the slot of stage kt-1, read before this barrier
+      read(kt);
+#pragma unroll
+      for (int xi = 0; xi < 8; ++xi)
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+          acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[xi][st], bv[xi][st], acc[xi], 0, 0, 0);
+    }
+    const int64_t col = cur.n0 + nh * 32 + r32;
+    const bool colok = col < g.N;
+    float* cbase;
+    int64_t cld;
+    int cact;
+    f32core::out_col(g, static_cast<float*>(g.C), colok ? col : 0, cbase, cld, cact);
+    const float bias = (g.bias && colok) ? static_cast<const float*>(g.bias)[col] : 0.f;
+    __syncthreads();  // the ring is free: slot 0 takes the next item's first stage
+    const int next = item + Gd;
+    const bool live = next < nwork;
+    Item nx;
+    setup(next, live, nx);
+    issue(nx, 0);
+    // ---- epilogue in registers: C/D row r -> tile 32 tq + (r & 3) + 8 (r >> 2) + 4 h
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float y0 = ((((acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r])) + (acc[4][r] + acc[5][r])) + acc[6][r]);
+      const float y1 = (((acc[1][r] - acc[2][r]) + 2.f * (acc[3][r] - acc[4][r])) + 0.5f * (acc[5][r] - acc[6][r])) +
+                       acc[7][r];
+      const int64_t t = cur.t0 + tq * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const bool tl = t < q.ntiles;
+      uint32_t n;
+      int oh, ow;
+      tile_of(tl ? (uint32_t)t : 0u, n, oh, ow);
+      const int64_t row0 = ((int64_t)n * q.OH + oh) * q.OW + ow, step = dh ? q.OW : 1;
+      const bool ok0 = tl && colok && !(q.dbg & 4);
+      const bool ok1 = ok0 && (dh ? oh + 1 < q.OH : ow + 1 < q.OW);
+      float* p0 = ok0 ? cbase + (ok0 ? row0 : 0) * cld : reinterpret_cast<float*>(&kWinoTrash[lane]);
+      float* p1 = ok1 ? cbase + (ok1 ? row0 + step : 0) * cld : reinterpret_cast<float*>(&kWinoTrash[lane]) + 1;
+      *p0 = act3(y0 + bias, cact);
+      *p1 = act3(y1 + bias, cact);
+    }
+    if (!live) break;
+    item = next;
+    cur = nx;
+  }
+}
+
 std::atomic<int>& wino_state() {
   static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_CONV_ALGO");
@@ -356,45 +545,80 @@ void set_wino_tile(int v) { wino_variant().store(v); }
 
 int64_t conv_wino_ocp(int64_t OC) { return (OC + 63) / 64 * 64; }
 
-// U = G g G^T per (c, oc) in fp64, rounded once to f32, into [C/8][16 xi][2][OCP][4 c]
-void conv_wino_filter(const float* w, int64_t C, int64_t OC, float* u) {
-  static const double G[4][3] = {{1, 0, 0}, {.5, .5, .5}, {.5, -.5, .5}, {0, 0, 1}};
-  const int64_t OCP = conv_wino_ocp(OC);
-  std::memset(u, 0, sizeof(float) * 16 * C * OCP);
-  for (int64_t c = 0; c < C; ++c)
-    for (int64_t o = 0; o < OC; ++o) {
-      double gg[3][3], t[4][3];
-      for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) gg[a][b] = w[((a * 3 + b) * C + c) * OC + o];
-      for (int i = 0; i < 4; ++i)
-        for (int b = 0; b < 3; ++b) t[i][b] = G[i][0] * gg[0][b] + G[i][1] * gg[1][b] + G[i][2] * gg[2][b];
-      for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) {
-          const double v = t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2];
-          u[((((c / 8) * 16 + i * 4 + j) * 2 + (c / 4) % 2) * OCP + o) * 4 + c % 4] = static_cast<float>(v);
-        }
-    }
+int conv_wino_kind(int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t C, int64_t OC) {
+  if (sh != 1 || sw != 1 || dh != 1 || dw != 1 || C <= 0 || OC <= 0 || C % 8 != 0 || OC % 4 != 0) return 0;
+  if (KH == 3 && KW == 3) return 1;
+  if (KH == 1 && KW == 7) return 2;
+  if (KH == 7 && KW == 1) return 3;
+  return 0;
 }
 
-bool conv_wino_shape_ok(int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t C, int64_t OC) {
-  return KH == 3 && KW == 3 && sh == 1 && sw == 1 && dh == 1 && dw == 1 && C % 8 == 0 && OC % 4 == 0 && C > 0 &&
-         OC > 0;
+int64_t conv_wino_filter_elems(int kind, int64_t C, int64_t OC) {
+  return (kind == 1 ? 16 : 8) * C * conv_wino_ocp(OC);
+}
+
+// kind 1: U = G g G^T per (c, oc) into [C/8][16 xi][2][OCP][4 c];
+// kinds 2/3: U = G7 g into [C/8][8 xi][2][OCP][4 c]. fp64, rounded once to f32.
+void conv_wino_filter(int kind, const float* w, int64_t C, int64_t OC, float* u) {
+  static const double G[4][3] = {{1, 0, 0}, {.5, .5, .5}, {.5, -.5, .5}, {0, 0, 1}};
+  // F(2,7), points {0, 1, -1, 2, -2, 1/2, -1/2, inf} (rows of G7: tests/test_wino.py)
+  static const double G7[8][7] = {
+      {-1, 0, 0, 0, 0, 0, 0},
+      {-2. / 9, -2. / 9, -2. / 9, -2. / 9, -2. / 9, -2. / 9, -2. / 9},
+      {-2. / 9, 2. / 9, -2. / 9, 2. / 9, -2. / 9, 2. / 9, -2. / 9},
+      {1. / 90, 1. / 45, 2. / 45, 4. / 45, 8. / 45, 16. / 45, 32. / 45},
+      {1. / 90, -1. / 45, 2. / 45, -4. / 45, 8. / 45, -16. / 45, 32. / 45},
+      {32. / 45, 16. / 45, 8. / 45, 4. / 45, 2. / 45, 1. / 45, 1. / 90},
+      {32. / 45, -16. / 45, 8. / 45, -4. / 45, 2. / 45, -1. / 45, 1. / 90},
+      {0, 0, 0, 0, 0, 0, 1}};
+  const int64_t OCP = conv_wino_ocp(OC);
+  std::memset(u, 0, sizeof(float) * conv_wino_filter_elems(kind, C, OC));
+  for (int64_t c = 0; c < C; ++c)
+    for (int64_t o = 0; o < OC; ++o) {
+      if (kind == 1) {
+        double gg[3][3], t[4][3];
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) gg[a][b] = w[((a * 3 + b) * C + c) * OC + o];
+        for (int i = 0; i < 4; ++i)
+          for (int b = 0; b < 3; ++b) t[i][b] = G[i][0] * gg[0][b] + G[i][1] * gg[1][b] + G[i][2] * gg[2][b];
+        for (int i = 0; i < 4; ++i)
+          for (int j = 0; j < 4; ++j) {
+            const double v = t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2];
+            u[((((c / 8) * 16 + i * 4 + j) * 2 + (c / 4) % 2) * OCP + o) * 4 + c % 4] = static_cast<float>(v);
+          }
+      } else {
+        // HWIO [1][7] or [7][1]: tap k at w[(k * C + c) * OC + o] either way
+        for (int i = 0; i < 8; ++i) {
+          double v = 0;
+          for (int k = 0; k < 7; ++k) v += G7[i][k] * w[(k * C + c) * OC + o];
+          u[((((c / 8) * 8 + i) * 2 + (c / 4) % 2) * OCP + o) * 4 + c % 4] = static_cast<float>(v);
+        }
+      }
+    }
 }
 
 bool conv_wino_eligible(const ConvArgs& a) {
   if (!a.wino || !conv_wino_enabled()) return false;
-  if (!conv_wino_shape_ok(a.KH, a.KW, a.sh, a.sw, a.dh, a.dw, a.C, a.OC)) return false;
+  const int kind = conv_wino_kind(a.KH, a.KW, a.sh, a.sw, a.dh, a.dw, a.C, a.OC);
+  if (kind == 0) return false;
   if (a.epi.n != 0 || a.act > ACT_RELU6) return false;
   // a 64-wide oc block on OC <= 32 wastes half the MFMAs: the direct kernels
-  // win there (Conv2d_2a, OC = 32: 77 vs 101 TF/s, profiles/r6_wino/)
+  // win there (Conv2d_2a, OC = 32: 78 vs 105 TF/s, profiles/r6_wino/)
   if (a.OC <= 32 && wino_variant().load() < 0) return false;
   if (!al16p(a.x) || !al16p(a.wino) || (a.bias && !al16p(a.bias))) return false;
-  const int64_t tpi = ((a.OH + 1) / 2) * ((a.OW + 1) / 2), ntiles = a.N * tpi;
+  const int64_t tpi = kind == 1 ? ((a.OH + 1) / 2) * ((a.OW + 1) / 2)
+                                : (kind == 2 ? a.OH * ((a.OW + 1) / 2) : ((a.OH + 1) / 2) * a.OW);
+  const int64_t T = kind == 1 ? 64 : 128, ntiles = a.N * tpi;
   if (ntiles >= (int64_t(1) << 31)) return false;
   // a block's taps lie within (images a block spans + 1) images of its first
   // image: under 2^31 bytes for the input descriptor's 32-bit offsets
-  if ((64 / tpi + 2) * a.H * a.W * a.C * 4 >= (int64_t(1) << 31)) return false;
-  if (16 * a.C * conv_wino_ocp(a.OC) * 4 >= (int64_t(1) << 31)) return false;
+  if ((T / tpi + 2) * a.H * a.W * a.C * 4 >= (int64_t(1) << 31)) return false;
+  if (conv_wino_filter_elems(kind, a.C, a.OC) * 4 >= (int64_t(1) << 31)) return false;
+  if (kind != 1) {  // scalar stores
+    for (int s = 0; s < a.seg.n; ++s)
+      if (a.seg.act[s] > ACT_RELU6) return false;
+    return true;
+  }
   if (a.seg.n == 0) return al16p(a.y) && (a.ldc > 0 ? a.ldc : a.OC) % 4 == 0;
   for (int s = 0; s < a.seg.n; ++s) {
     if (a.seg.begin[s] % 4 != 0 || a.seg.ldc[s] % 4 != 0 || !al16p(a.seg.ptr[s])) return false;
@@ -410,9 +634,15 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   q.TH = (int)((a.OH + 1) / 2); q.TW = (int)((a.OW + 1) / 2);
   q.OCP = (int)conv_wino_ocp(a.OC);
   q.KT = (int)(a.C / 8);
-  q.ntiles = a.N * q.TH * q.TW;
+  const int kind = conv_wino_kind(a.KH, a.KW, a.sh, a.sw, a.dh, a.dw, a.C, a.OC);
+  q.axis = kind == 3 ? 1 : 0;
+  q.D0 = kind == 2 ? (int)a.OH : q.TH;       // F(2,7): tiles (n, i0, i1) over (D0, D1)
+  q.D1 = kind == 3 ? (int)a.OW : q.TW;
+  q.fD0 = make_fastdiv((uint32_t)q.D0);
+  q.fD1 = make_fastdiv((uint32_t)q.D1);
+  q.ntiles = kind == 1 ? a.N * q.TH * q.TW : a.N * (int64_t)q.D0 * q.D1;
   q.img_floats = a.H * a.W * a.C;
-  q.u_bytes = 16 * a.C * q.OCP * 4;
+  q.u_bytes = conv_wino_filter_elems(kind, a.C, a.OC) * 4;
   static const int dbg = [] {
     const char* e = std::getenv("TFA_WINO_DEBUG");
     return e ? std::atoi(e) : 0;
@@ -423,7 +653,7 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   GemmArgs g{};
   g.M = a.N * a.OH * a.OW;
   g.N = a.OC;
-  g.K = 9 * a.C;
+  g.K = a.KH * a.KW * a.C;
   g.A = a.x;
   g.B = a.wino;
   g.C = a.y;
@@ -432,7 +662,8 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   g.act = a.act;
   g.batch = 1;
   g.seg = a.seg;
-  const int64_t nbt = (q.ntiles + 63) / 64, nbn = (a.OC + 63) / 64;
+  const int64_t TB = kind == 1 ? 64 : 128;
+  const int64_t nbt = (q.ntiles + TB - 1) / TB, nbn = (a.OC + 63) / 64;
   TFA_CHECK(nbt * nbn < (int64_t(1) << 31), "conv_wino: grid too large");
   const int nwork = (int)(nbt * nbn);
   static const int ncu = [] {
@@ -444,7 +675,10 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   }();
   const int per_cu = wino_variant().load() == 3 ? 0 : 1;  // 3: one item per block (no persistence), for A/B
   const int grid = per_cu ? std::min(nwork, ncu) : nwork;
-  hipLaunchKernelGGL(wino23_kernel, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  if (kind == 1)
+    hipLaunchKernelGGL(wino23_kernel, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  else
+    hipLaunchKernelGGL(wino27_kernel, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   TFA_LAUNCH_CHECK("conv_wino");
 }
 

@@ -252,8 +252,8 @@ struct ConvArgs {
   int64_t ldc = 0;  // output pixel stride in elements (0 = OC; > OC writes a channel slice)
   EpiProg epi;      // absorbed elementwise chain over the [N*OH*OW, OC] output
   OutSegs seg;      // sibling convs fused along OC: per-sibling outputs (seg.n == 0: y / ldc)
-  // Winograd F(2x2,3x3) filter (conv_wino_filter layout) when the planner made
-  // one: 3x3 stride-1 convs then run conv_wino.hip unless TFA_CONV_ALGO=direct
+  // Winograd filter (conv_wino_filter layout) when the planner made one:
+  // 3x3 / 1x7 / 7x1 stride-1 convs then run conv_wino.hip unless TFA_CONV_ALGO=direct
   const void* wino = nullptr;
 };
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a);
@@ -269,13 +269,15 @@ struct PoolArgs {
   int64_t ldc = 0;             // 0 = C
 };
 void pool2d_nhwc(DType dt, const PoolArgs& a, hipStream_t s);
-// Winograd F(2x2,3x3) path (conv_wino.hip): shape test used by the planner,
-// padded filter width, runtime switch (TFA_CONV_ALGO=direct turns it off) and
-// forced kernel variant (-1 auto, 0: 64 tiles x 64 oc, 1: 128 tiles x 32 oc)
-bool conv_wino_shape_ok(int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t C, int64_t OC);
+// Winograd paths (conv_wino.hip): the planner's shape test (0 none, 1
+// F(2x2,3x3), 2 F(2,7) along W (1x7), 3 F(2,7) along H (7x1)), padded filter
+// width, runtime switch (TFA_CONV_ALGO=direct turns it off) and forced
+// kernel variant (-1 auto; >= 0 also runs OC <= 32; 3 one item per block)
+int conv_wino_kind(int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t C, int64_t OC);
 int64_t conv_wino_ocp(int64_t OC);
-// host: HWIO [3][3][C][OC] f32 filter -> u [C/4][16][conv_wino_ocp(OC)][4] (fp64 transform)
-void conv_wino_filter(const float* w, int64_t C, int64_t OC, float* u);
+int64_t conv_wino_filter_elems(int kind, int64_t C, int64_t OC);
+// host: HWIO f32 filter -> the transformed filter (fp64 transform, rounded once)
+void conv_wino_filter(int kind, const float* w, int64_t C, int64_t OC, float* u);
 void set_conv_wino(int on);
 bool conv_wino_enabled();
 void set_wino_tile(int v);

@@ -1046,8 +1046,9 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
     }
   }
 
-  // ---- Winograd filters (GPU plans): every 3x3 stride-1 CONV step with a
-  // constant f32 filter and a cheap epilogue gets its F(2x2,3x3) transform
+  // ---- Winograd filters (GPU plans): every 3x3 / 1x7 / 7x1 stride-1 CONV
+  // step with a constant f32 filter and a cheap epilogue gets its F(2x2,3x3)
+  // or F(2,7) transform
   // (fp64 on the host, once per plan) as a plan-made constant; the kernel
   // layer runs conv_wino.hip with it unless TFA_CONV_ALGO=direct
   if (gpu_plan && k::conv_wino_enabled()) {
@@ -1074,15 +1075,16 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
       if (strides != one || !(dil == one || dil.empty())) continue;
       const at::Tensor* w = filt(st.in_slots[1]);
       if (!w || w->dim() != 4 || w->scalar_type() != at::kFloat) continue;
-      if (!k::conv_wino_shape_ok(w->size(0), w->size(1), 1, 1, 1, 1, w->size(2), w->size(3))) continue;
+      const int kind = k::conv_wino_kind(w->size(0), w->size(1), 1, 1, 1, 1, w->size(2), w->size(3));
+      if (kind == 0) continue;
       auto hit = made.find(st.in_slots[1]);
       if (hit != made.end()) {
         st.wino_slot = hit->second;
         continue;
       }
       const at::Tensor wc = w->contiguous();
-      at::Tensor u = at::empty({16 * wc.size(2) * k::conv_wino_ocp(wc.size(3))}, wc.options());
-      k::conv_wino_filter(wc.data_ptr<float>(), wc.size(2), wc.size(3), u.data_ptr<float>());
+      at::Tensor u = at::empty({k::conv_wino_filter_elems(kind, wc.size(2), wc.size(3))}, wc.options());
+      k::conv_wino_filter(kind, wc.data_ptr<float>(), wc.size(2), wc.size(3), u.data_ptr<float>());
       const int slot = p->nslots++;
       p->synth_consts[slot] = u;
       made[st.in_slots[1]] = slot;

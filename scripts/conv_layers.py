@@ -95,6 +95,13 @@ def main():
              "stride": s, "pad": pad, "M": a.batch * oh * ow, "K": kh * kw * c, "ms": ms, "tflops": fl / ms / 1e9,
              "tile": tile, "tile_dims": None if dims is None else f"{dims[0]}x{dims[1]}",
              "core": None if dims is None else ("g2" if dims[2] == 2 else "round4")}
+        # the algorithm that ran: the plan carries a Winograd filter for 3x3 /
+        # 1x7 / 7x1 stride-1 convs; the kernel layer declines OC <= 32 unless
+        # a Winograd variant is forced (conv_wino.hip conv_wino_eligible)
+        wino = "+winograd" in prog.describe([xin[:1].cpu()], True) and _C.conv_wino_enabled() and (
+            oc > 32 or os.environ.get("TFA_WINO_TILE") not in (None, "", "-1"))
+        r["algo"] = ("wino_f23" if kh == 3 else "wino_f27") if wino else (
+            "direct" if dims is None else f"gemm {r['core']} {r['tile_dims']}")
         if a.vendor:
             import torch.nn.functional as F
             xn = xin.permute(0, 3, 1, 2)
@@ -126,8 +133,8 @@ def main():
             "fraction_of_f32_peak": tot_fl / tot_ms / 1e9 / F32_PEAK_TF,
             "images_per_s_conv_only": a.batch / tot_ms * 1e3}
     print(json.dumps(summ), flush=True)
-    for r in sorted(res, key=lambda r: -r["share"])[:15]:
-        print(f"{r['share'] * 100:5.1f}%  {r['tflops']:6.1f} TF  {r['layer']:>14s} x{r['count']}  "
+    for r in sorted(res, key=lambda r: -r["share"]):
+        print(f"{r['share'] * 100:5.1f}%  {r['tflops']:6.1f} TF  {r.get('algo', ''):>18s} {r['layer']:>14s} x{r['count']}  "
               f"{r['H']}x{r['W']}x{r['C']} k{r['KH']}x{r['KW']} s{r['stride']} -> {r['OC']}  M={r['M']} K={r['K']}",
               flush=True)
     if a.json:

@@ -1,4 +1,4 @@
-"""The Winograd F(2x2,3x3) conv kernel (csrc/kernels/conv_wino.hip) on the GPU
+"""The Winograd F(2x2,3x3) and F(2,7) conv kernels (csrc/kernels/conv_wino.hip) on the GPU
 against a float64 host reference, on Inception-v3 / VGG-16 layer geometries
 and odd edge shapes, persistent blocks (the default) and one work item per
 block, with bias + ReLU, concat slices and sibling-fused convs.
@@ -32,7 +32,7 @@ def run(g, fetches, feeds):
 def ref_conv(x, f, pad):
     xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
     ft = torch.from_numpy(f).double().permute(3, 2, 0, 1)
-    p = (f.shape[0] // 2) if pad == "SAME" else 0
+    p = (f.shape[0] // 2, f.shape[1] // 2) if pad == "SAME" else 0
     y = torch.nn.functional.conv2d(xt, ft, padding=p).permute(0, 2, 3, 1).numpy()
     s = torch.nn.functional.conv2d(xt.abs(), ft.abs(), padding=p).permute(0, 2, 3, 1).numpy()
     return y, s
@@ -47,7 +47,15 @@ def variant():
     _C.set_conv_wino(True)
 
 
-GEOMS = [  # N, H, W, C, OC, padding
+# (the F(2,7) layers at a batch whose direct GEMM is not split along K, as at
+# the production batch: a split-K reference has shorter accumulation chains,
+# so its error, and the 4x gate, would be artificially tight)
+GEOMS = [  # N, H, W, C, OC, padding[, KH, KW]
+    (128, 12, 12, 160, 160, "SAME", 1, 7),  # Inception Mixed_6x b1_1x7 (F(2,7))
+    (128, 12, 12, 128, 192, "SAME", 7, 1),  # Mixed_6x b1_7x1
+    (4, 17, 13, 40, 52, "SAME", 1, 7),      # odd sizes, OC tail
+    (3, 9, 11, 16, 44, "SAME", 7, 1),
+    (2, 15, 14, 24, 64, "VALID", 1, 7),
     (8, 25, 25, 64, 96, "SAME"),     # Inception Mixed_5x b2_3x3a
     (8, 25, 25, 96, 96, "SAME"),     # b2_3x3b
     (2, 54, 54, 80, 192, "VALID"),   # Conv2d_4a
@@ -62,10 +70,11 @@ GEOMS = [  # N, H, W, C, OC, padding
 
 @pytest.mark.parametrize("geom", GEOMS)
 def test_wino_matches_fp64_and_gate(variant, geom):
-    nb, h, w, c, oc, pad = geom
+    nb, h, w, c, oc, pad = geom[:6]
+    kh, kw = geom[6:] if len(geom) > 6 else (3, 3)
     rng = np.random.default_rng(h * w + c + oc)
     x = rng.uniform(-1, 1, (nb, h, w, c)).astype(np.float32)
-    f = rng.uniform(-1, 1, (3, 3, c, oc)).astype(np.float32)
+    f = rng.uniform(-1, 1, (kh, kw, c, oc)).astype(np.float32)
     bias = rng.uniform(-1, 1, oc).astype(np.float32)
     g = tf.Graph()
     with g.as_default():

@@ -65,12 +65,80 @@ def test_filter_transform_and_algorithm_match_direct(geom):
 
 def test_filter_padding_is_zero():
     import torch
-    f = np.ones((3, 3, 8, 10), np.float32)
+    f = np.ones((3, 3, 8, 12), np.float32)
     u = _C.conv_wino_filter(torch.from_numpy(f)).numpy().reshape(1, 16, 2, 64, 4)
-    assert np.all(u[:, :, :, 10:, :] == 0)
+    assert np.all(u[:, :, :, 12:, :] == 0)
     # xi (0,0) is g[0][0]; xi (1,1) is (sum over the 3x3) / 4
-    assert np.allclose(u[0, 0, :, :10], 1.0)
-    assert np.allclose(u[0, 5, :, :10], 9 / 4)
+    assert np.allclose(u[0, 0, :, :12], 1.0)
+    assert np.allclose(u[0, 5, :, :12], 9 / 4)
+
+
+def emulate27(x, u_flat, oc, axis):
+    """The F(2,7) kernel's algorithm (its exact input-transform formulas) on a
+    1x7 (axis 0, along W) or 7x1 (axis 1, along H) SAME conv."""
+    n, h, w, c = x.shape
+    ocp = -(-oc // 64) * 64
+    u = u_flat.astype(np.float64).reshape(c // 8, 8, 2, ocp, 4).transpose(1, 0, 2, 4, 3).reshape(8, c, ocp)[:, :, :oc]
+    xs = x if axis == 0 else x.transpose(0, 2, 1, 3)      # conv along the W axis of xs
+    L = xs.shape[2]
+    nt = -(-L // 2)
+    xp = np.zeros((n, xs.shape[1], 2 * nt + 6, c))
+    xp[:, :, 3:3 + L, :] = xs
+    y = np.zeros((n, xs.shape[1], 2 * nt, oc))
+    for t in range(nt):
+        d = [xp[:, :, 2 * t + p, :] for p in range(8)]
+        v = [None] * 8
+        v[0] = (d[6] - d[0]) + 5.25 * (d[2] - d[4])
+        v[7] = (d[7] - d[1]) + 5.25 * (d[3] - d[5])
+        e1, o1 = (d[2] + d[6]) - 4.25 * d[4], (d[1] + d[5]) - 4.25 * d[3]
+        v[1], v[2] = e1 + o1, e1 - o1
+        e3, o3 = (0.25 * d[2] + d[6]) - 1.25 * d[4], (0.5 * d[1] + 2 * d[5]) - 2.5 * d[3]
+        v[3], v[4] = e3 + o3, e3 - o3
+        e5, o5 = (4 * d[2] + d[6]) - 5 * d[4], (2 * d[1] + 0.5 * d[5]) - 2.5 * d[3]
+        v[5], v[6] = e5 + o5, e5 - o5
+        m = [np.einsum("nhc,co->nho", v[i], u[i]) for i in range(8)]
+        y[:, :, 2 * t] = m[0] + m[1] + m[2] + m[3] + m[4] + m[5] + m[6]
+        y[:, :, 2 * t + 1] = (m[1] - m[2]) + 2 * (m[3] - m[4]) + 0.5 * (m[5] - m[6]) + m[7]
+    y = y[:, :, :L]
+    return y if axis == 0 else y.transpose(0, 2, 1, 3)
+
+
+@pytest.mark.parametrize("axis", [0, 1])
+def test_f27_transform_and_algorithm_match_direct(axis):
+    import torch
+    rng = np.random.default_rng(7 + axis)
+    x = rng.uniform(-1, 1, (2, 6, 9, 16))
+    kshape = (1, 7, 16, 12) if axis == 0 else (7, 1, 16, 12)
+    f = rng.uniform(-1, 1, kshape).astype(np.float32)
+    u = _C.conv_wino_filter(torch.from_numpy(f)).numpy()
+    assert u.shape == (8 * 16 * 64,)
+    xt = torch.from_numpy(x).permute(0, 3, 1, 2)
+    ft = torch.from_numpy(f.astype(np.float64)).permute(3, 2, 0, 1)
+    pad = (0, 3) if axis == 0 else (3, 0)
+    want = torch.nn.functional.conv2d(xt, ft, padding=pad).permute(0, 2, 3, 1).numpy()
+    got = emulate27(x, u, 12, axis)
+    scale = torch.nn.functional.conv2d(xt.abs(), ft.abs(), padding=pad).permute(0, 2, 3, 1).numpy()
+    assert np.max(np.abs(got - want) / (scale + 1)) < 1e-6
+
+
+def test_f27_matrices_from_toom_cook():
+    """The kernel's B^T / A^T and the host's G7 reproduce 1-D correlation for
+    every (d, g): sum_i A^T[j][i] G[i][k] B^T[i][l] == [l == j + k]."""
+    from fractions import Fraction as F
+    G7 = [[-1, 0, 0, 0, 0, 0, 0], [F(-2, 9)] * 7, [F(-2, 9) * (-1) ** k for k in range(7)],
+          [F(1, 90) * 2 ** k for k in range(7)], [F(1, 90) * (-2) ** k for k in range(7)],
+          [F(32, 45) / 2 ** k for k in range(7)], [F(32, 45) * F(-1, 2) ** k for k in range(7)],
+          [0, 0, 0, 0, 0, 0, 1]]
+    BT = [[-1, 0, F(21, 4), 0, F(-21, 4), 0, 1, 0], [0, 1, 1, F(-17, 4), F(-17, 4), 1, 1, 0],
+          [0, -1, 1, F(17, 4), F(-17, 4), -1, 1, 0], [0, F(1, 2), F(1, 4), F(-5, 2), F(-5, 4), 2, 1, 0],
+          [0, F(-1, 2), F(1, 4), F(5, 2), F(-5, 4), -2, 1, 0], [0, 2, 4, F(-5, 2), -5, F(1, 2), 1, 0],
+          [0, -2, 4, F(5, 2), -5, F(-1, 2), 1, 0], [0, -1, 0, F(21, 4), 0, F(-21, 4), 0, 1]]
+    AT = [[1, 1, 1, 1, 1, 1, 1, 0], [0, 1, -1, 2, -2, F(1, 2), F(-1, 2), 1]]
+    for j in range(2):
+        for k in range(7):
+            for l in range(8):
+                v = sum(F(AT[j][i]) * F(G7[i][k]) * F(BT[i][l]) for i in range(8))
+                assert v == (1 if l == j + k else 0), (j, k, l, v)
 
 
 def _inception_like_graph():
