@@ -448,6 +448,13 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
   };
 
   f32x16 acc[8];
+  auto mfma_pts = [&](int x0, int x1, const f32x4 (&a)[8], const f32x4 (&b)[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int xi = x0; xi < x1; ++xi)
+#pragma unroll
+      for (int st = 0; st < 4; ++st) acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[xi][st], b[xi][st], acc[xi], 0, 0, 0);
+  };
+  f32x4 pa[8], pb[8];  // the deferred points 6, 7 of the previous stage (only [6], [7] are live)
   int item = f32core::xcd_remap(blockIdx.x, Gd);
   if (item >= nwork) return;
   Item cur;
@@ -472,13 +479,18 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
       }
       __builtin_amdgcn_s_barrier();
       if (kt + 2 < KT) issue(cur, kt + 2);  // into the slot of stage kt-1, read before this barrier
+      // the last two transform points' MFMAs of stage kt-1 run here, in the
+      // shadow of this stage's fragment reads and input transform
+      if (kt > 0) mfma_pts(6, 8, pa, pb);
       read(kt);
+      mfma_pts(0, 6, av, bv);
 #pragma unroll
-      for (int xi = 0; xi < 8; ++xi)
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-          acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[xi][st], bv[xi][st], acc[xi], 0, 0, 0);
+      for (int xi = 6; xi < 8; ++xi) {
+        pa[xi] = av[xi];
+        pb[xi] = bv[xi];
+      }
     }
+    mfma_pts(6, 8, pa, pb);
     const int64_t col = cur.n0 + nh * 32 + r32;
     const bool colok = col < g.N;
     float* cbase;
