@@ -672,6 +672,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     bool ok = tfa::jpeg_native_available(&why);
     return py::make_tuple(ok, why);
   });
+  m.def("jpeg_native_info", [] {
+    tfa::JpegLibInfo i = tfa::jpeg_native_info();
+    py::dict d;
+    d["ok"] = i.ok;
+    d["version"] = i.version;
+    d["struct_size"] = i.struct_size;
+    d["soname"] = i.soname;
+    d["why"] = i.why;
+    return d;
+  }, "the loaded libjpeg: its own version and decompressor size, and whether that layout is a known one");
+  m.def("jpeg_force_version", &tfa::jpeg_force_version, py::arg("version"),
+        "tests: treat the loaded libjpeg as this version (0 = its real one); unknown layouts disable the native path");
   m.def("jpeg_decode", [](const py::buffer& data, int channels) {
     auto v = data.request();
     tfa::JpegHeader h;

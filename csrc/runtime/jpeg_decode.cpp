@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <csetjmp>
 #include <cstring>
 #include <deque>
@@ -80,9 +81,34 @@ struct Lib {
   int (*finish)(void*) = nullptr;
   int version = 0;
   size_t struct_size = 0;
+  std::string soname;
   bool ok = false;
   std::string why;
 };
+
+// The (JPEG_LIB_VERSION, sizeof(jpeg_decompress_struct)) pairs of the LP64
+// builds whose leading-field layout (DecompHead) has been verified: the
+// library reported the pair itself and its decodes matched PIL bit for bit
+// (tests/test_jpeg_native.py). Only libjpeg-turbo's libjpeg.so.8 (8 API) on
+// this image so far; any other pair is refused and the Python decoder takes
+// over (metric jpeg_native_unavailable), until it is verified and added here.
+struct KnownLayout {
+  int version;
+  size_t struct_size;
+};
+constexpr KnownLayout kKnownLayouts[] = {{80, 656}};
+
+bool known_layout(int version, size_t size) {
+  for (const KnownLayout& k : kKnownLayouts)
+    if (k.version == version && k.struct_size == size) return true;
+  return false;
+}
+
+// tests: make the probe see another library version (0 = the real one)
+std::atomic<int>& forced_version() {
+  static std::atomic<int> v(0);
+  return v;
+}
 
 struct Ctx {  // per-decode: error manager + jump buffer + the decompressor storage
   ErrorMgr err;
@@ -119,7 +145,10 @@ Lib probe() {
   Lib L;
   void* h = nullptr;
   for (const char* name : {"libjpeg.so.8", "libjpeg.so.62", "libjpeg.so"}) {
-    if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+    if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) {
+      L.soname = name;
+      break;
+    }
   }
   if (!h) {
     L.why = "libjpeg not found";
@@ -156,18 +185,34 @@ Lib probe() {
     L.why = "libjpeg struct size probe failed";
     return L;
   }
-  if (version != 62 && version != 70 && version != 80 && version != 90) {
-    L.why = "unknown libjpeg version " + std::to_string(version);
+  L.version = version;
+  if (!known_layout(version, L.struct_size)) {
+    L.why = "unknown libjpeg layout (version " + std::to_string(version) + ", decompressor struct " +
+            std::to_string(L.struct_size) + " bytes)";
     return L;
   }
-  L.version = version;
   L.ok = true;
   return L;
 }
 
-const Lib& lib() {
+const Lib& probed() {
   static Lib L = probe();
   return L;
+}
+
+// the probed library, or (tests) the same library seen as another version,
+// which the layout table then accepts or refuses
+const Lib& lib() {
+  const int fv = forced_version().load();
+  if (fv == 0) return probed();
+  thread_local Lib F;
+  F = probed();
+  F.version = fv;
+  F.ok = F.struct_size && known_layout(fv, F.struct_size);
+  if (!F.ok)
+    F.why = "unknown libjpeg layout (version " + std::to_string(fv) + ", decompressor struct " +
+            std::to_string(F.struct_size) + " bytes)";
+  return F;
 }
 
 // ---- the decode pool --------------------------------------------------------
@@ -254,6 +299,13 @@ bool jpeg_native_available(std::string* why) {
   if (why) *why = L.ok ? "libjpeg " + std::to_string(L.version) : L.why;
   return L.ok;
 }
+
+JpegLibInfo jpeg_native_info() {
+  const Lib& L = lib();
+  return {L.ok, L.version, static_cast<int64_t>(L.struct_size), L.soname, L.ok ? "" : L.why};
+}
+
+void jpeg_force_version(int version) { forced_version().store(version); }
 
 bool jpeg_decode_into(const uint8_t* data, size_t len, int out_c, uint8_t* dst, size_t dst_bytes,
                       std::string* err) {

@@ -41,6 +41,20 @@ bool jpeg_parse_header(const uint8_t* data, size_t len, JpegHeader* h);
 // True when libjpeg could be loaded and its ABI matched (probed once).
 bool jpeg_native_available(std::string* why = nullptr);
 
+// What the probe found: the library's own version (JPEG_LIB_VERSION, read
+// from the version-mismatch error jpeg_CreateDecompress raises) and
+// decompressor struct size (the size-mismatch error), the soname loaded, and
+// whether that (version, size) pair is a known layout (else `why`).
+struct JpegLibInfo {
+  bool ok;
+  int version;
+  int64_t struct_size;
+  std::string soname, why;
+};
+JpegLibInfo jpeg_native_info();
+// tests: see the loaded library as another version (0 = the real one)
+void jpeg_force_version(int version);
+
 // Decode one JPEG into `dst` (height x width x out_c uint8, row-major).
 // out_c: 3 (RGB; grayscale files are replicated) or 1 (grayscale files only).
 // Returns false (with a reason) on any error or libjpeg warning.

@@ -15,6 +15,7 @@ import functools
 from collections import OrderedDict
 import os
 import time
+import warnings
 import zlib
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
@@ -1053,8 +1054,10 @@ def _native_jpeg(prep, raw):
         return None
     hf, cells = raw
     C = prep.channels(hf)
-    if hf.op not in ("DecodeJpeg", "DecodeImage") or C not in (1, 3) or hf.channels != C or \
-            not _C.jpeg_native_available()[0]:
+    if hf.op not in ("DecodeJpeg", "DecodeImage") or C not in (1, 3) or hf.channels != C:
+        return None
+    if not jpeg_native_usable():
+        metrics.add("jpeg_native_unavailable", 1)
         return None
     threads = config.decode_threads or min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
                                            else (os.cpu_count() or 1))
@@ -1067,6 +1070,57 @@ def _native_jpeg(prep, raw):
         return job if job.header_ok else None
     start.C = C
     return start
+
+
+_JPEG_CHECKED: Dict[tuple, bool] = {}  # (version, struct size, soname) -> the self-check passed
+
+
+def jpeg_native_usable() -> bool:
+    """The native libjpeg decoder may run: the library's own (version,
+    decompressor size) pair is a known layout (jpeg_decode.cpp refuses any
+    other) AND, checked once per loaded library, its pixels equal the Python
+    decoder's on a few PIL-encoded files (baseline 4:2:0, 4:4:4, progressive,
+    grayscale). Otherwise the Python decoder takes every image, with a
+    warning and the jpeg_native_disabled metric."""
+    info = _C.jpeg_native_info()
+    if not info["ok"]:
+        return False
+    key = (info["version"], info["struct_size"], info["soname"])
+    ok = _JPEG_CHECKED.get(key)
+    if ok is None:
+        ok, why = _jpeg_self_check()
+        _JPEG_CHECKED[key] = ok
+        metrics.set("jpeg_native_version", info["version"])
+        if not ok:
+            metrics.add("jpeg_native_disabled", 1)
+            warnings.warn(f"native JPEG decode disabled ({info['soname']}, version {info['version']}): {why}; "
+                          "images go through the Python decoder", RuntimeWarning, stacklevel=3)
+    return ok
+
+
+def _jpeg_self_check():
+    from .ops.host_ops import decode_image
+    try:
+        from PIL import Image
+    except ImportError:
+        return False, "Pillow missing, nothing to check the native decoder against"
+    import io
+    rng = np.random.default_rng(0)
+    for i, kw in enumerate(({"subsampling": 2}, {"subsampling": 0}, {"progressive": True}, {})):
+        a = rng.integers(0, 255, (21 + i, 34 - i, 3), dtype=np.uint8)
+        im = Image.fromarray(a if i < 3 else a[..., 0])
+        buf = io.BytesIO()
+        im.save(buf, format="JPEG", quality=85, **kw)
+        d = buf.getvalue()
+        for c in ((3,) if i < 3 else (1, 3)):  # (color -> 1 channel is the Python decoder's)
+            try:
+                got = _C.jpeg_decode(d, c).numpy()
+            except Exception as e:  # noqa: BLE001
+                return False, f"decode raised {type(e).__name__}: {e}"
+            want = decode_image(d, c)
+            if got.shape != want.shape or not np.array_equal(got, want):
+                return False, f"pixels differ from the Python decoder (file {i}, {c} channels)"
+    return True, ""
 
 
 def _finish_jpeg_batch(job, hf, cells) -> None:

@@ -31,6 +31,11 @@ class Metrics:
         with self._lock:
             self.counters[key] += v
 
+    def set(self, key: str, v: float):
+        """a gauge (e.g. a library version), not a counter"""
+        with self._lock:
+            self.counters[key] = v
+
     @contextmanager
     def timer(self, key: str):
         t0 = time.perf_counter()

@@ -92,6 +92,37 @@ def test_batched_prestage_equals_per_row_scoring(native):
         assert np.array_equal(np.asarray(a["value"]), np.asarray(b["value"]))
 
 
+def test_unknown_libjpeg_version_falls_back_with_identical_topk():
+    """The loaded libjpeg seen as an unknown version (jpeg_force_version): the
+    pre-stage refuses the native decoder (jpeg_native_unavailable), decodes
+    through the Python decoder and gives the native run's top-k bit for bit."""
+    from tensorframes_amd import core
+    rng = np.random.default_rng(6)
+    jpgs = _jpegs(40, rng)
+    df = tfs.create_dataframe([Row(uri=f"img{i}", image_data=b) for i, b in enumerate(jpgs)], num_partitions=1)
+    g = cnn.jpeg_scoring_graph("vgg16", contents=bytes(jpgs[0]), width=0.125)
+    res, snaps = {}, {}
+    try:
+        for forced in (0, 99):
+            _C.jpeg_force_version(forced)
+            tfs.metrics.reset()
+            with g.as_default():
+                pred = tfs.map_rows(["index", "value"], df, feed_dict={"DecodeJpeg/contents": "image_data"})
+                res[forced] = pred.select("uri", "index", "value").collect()
+            snaps[forced] = tfs.metrics.snapshot()
+    finally:
+        _C.jpeg_force_version(0)
+        core._JPEG_CHECKED.clear()
+    assert snaps[0].get("map_rows_native_decode_rows", 0) == len(jpgs)
+    assert snaps[99].get("map_rows_native_decode_rows", 0) == 0
+    assert snaps[99].get("jpeg_native_unavailable", 0) >= 1
+    assert snaps[99].get("map_rows_batched_prestage_rows", 0) == len(jpgs)
+    for a, b in zip(res[0], res[99]):
+        assert a.uri == b.uri
+        assert list(a["index"]) == list(b["index"])
+        assert np.array_equal(np.asarray(a["value"]), np.asarray(b["value"]))
+
+
 def test_native_decode_falls_back_for_truncated_files():
     """A truncated JPEG in a chunk: the native decoder reports it, the Python
     decoder then raises its own error, as on the per-row path."""
