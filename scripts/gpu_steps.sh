@@ -91,12 +91,34 @@ for s in ${STEPS:-tests}; do
       run incep_dev 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
     prec) run prec 300 python -u -m pytest tests/test_gpu_precision.py tests/test_gpu_g2.py -x -q --timeout 300 --timeout-method thread ;;
     tile_ab) run tile_ab 900 bash scripts/tile_ab.sh ;;                    # SHAPES=<file> TILES="auto 16 28 ..."
-    ab) run ab 900 bash scripts/ab_tiles.sh ;;                             # AB="name|tiles|gemm_one args;..."
-    g2_ab) run g2_ab 1100 bash scripts/r5_g2_check.sh ;;                   # TILES / HEAD_TILES / CONV_TILES / SKIP_BENCH
-    pmc_g2) run pmc_g2 900 bash scripts/r5_pmc_g2.sh ;;                    # g2 lab vs g2 core vs round-4 counters
+    ab2)  # forced-tile A/B of single shapes: AB="name|tiles|gemm_one args;..."
+      IFS=';' read -ra items <<< "${AB:-}"
+      for it in "${items[@]}"; do IFS='|' read -r nm tiles args <<< "$it"
+        for t in $tiles; do TFA_GEMM_TILE=$t run ab_${nm}_t$t 120 python scripts/gemm_one.py $args --iters 10 || exit 1; done
+      done ;;
+    g2_ab)  # g2 core correctness, then forced-tile A/B: TILES / HEAD_TILES / CONV_TILES
+      run g2_tests 400 python -u -m pytest tests/test_gpu_g2.py tests/test_gpu_precision.py -x -q --timeout 300 --timeout-method thread || exit 1
+      for t in ${TILES:-21 22 23 24}; do
+        TFA_GEMM_TILE=$t run ab_4096_t$t 120 python scripts/gemm_one.py gemm 4096 4096 4096 --iters 30 &&
+        TFA_GEMM_TILE=$t run ab_4096tb_t$t 120 python scripts/gemm_one.py gemm 4096 4096 4096 --iters 30 --tb &&
+        TFA_GEMM_TILE=$t run ab_8192_t$t 120 python scripts/gemm_one.py gemm 8192 8192 8192 --iters 10 || exit 1
+      done
+      for t in ${HEAD_TILES:-13 22 23 24 25}; do TFA_GEMM_TILE=$t run ab_head_t$t 120 python scripts/gemm_one.py gemm 2500000 512 512 --iters 20 || exit 1; done
+      for t in ${CONV_TILES:-16 23 24 25 26}; do TFA_GEMM_TILE=$t run ab_conv4a_t$t 120 python scripts/gemm_one.py conv 2048 54 54 80 3 3 192 1 VALID --iters 10 || exit 1; done ;;
+    lab_g2)  # the g2 GEMM lab kernel (scripts/g2_lab.hip) on G2_SHAPES; counters with PMC=1
+      export TMPDIR=/tmp
+      hipcc -O3 --offload-arch=gfx950 -std=c++17 scripts/g2_lab.hip -o /tmp/g2_lab || exit 3
+      for shape in ${G2_SHAPES:-"4096 4096 4096" "8192 8192 8192" "2560000 512 512"}; do
+        run lab_g2_${shape// /x} 120 /tmp/g2_lab $shape || exit 1; done
+      if [ -n "${PMC:-}" ]; then
+        PA="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
+        PB="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"
+        timeout -s KILL 90 rocprofv3 --pmc $PA --output-format csv -d "$PWD/gpurun_out/lab_pmc/a" -o run -- /tmp/g2_lab 4096 4096 4096 one > gpurun_out/lab_pmc_a.log 2>&1 &&
+        timeout -s KILL 90 rocprofv3 --pmc $PB --output-format csv -d "$PWD/gpurun_out/lab_pmc/b" -o run -- /tmp/g2_lab 4096 4096 4096 one > gpurun_out/lab_pmc_b.log 2>&1 || exit 1
+      fi ;;
     tile_table) run tile_table 1000 python scripts/tile_table.py --out gpurun_out/gfx950.json ;;
-    layers_time) PART=time run layers_time 700 bash scripts/r5_layers.sh ;;
-    layers_pmc) PART="pmc ${FIRST:-0} ${LAST:-21}" run layers_pmc 1150 bash scripts/r5_layers.sh ;;
+    layers_time) run layers_time 700 python scripts/conv_layers.py --json gpurun_out/layers.json ;;
+    layers_pmc) run layers_pmc 1150 python scripts/layers_pmc.py --layers scripts/data/inception_layers.json --out gpurun_out/layers_pmc --first ${FIRST:-0} --last ${LAST:-21} ;;
     img) run img_tests 300 python -u -m pytest tests/test_gpu_image_prep.py tests/test_jpeg_native.py tests/test_gpu_string_keys.py -x -v -s --timeout 200 --timeout-method thread &&
       run read_image4k 400 python examples/read_image.py --images 4096 &&
       TFA_PRECISION=bf16x3 run read_image4k_bf16x3 400 python examples/read_image.py --images 4096 ;;
