@@ -77,10 +77,44 @@ def default_entries(path: str = None) -> list:
         return json.load(f).get("entries", [])
 
 
+def _kfd_archs() -> set:
+    """The gfx names of this machine's GPUs, read from the KFD topology in
+    sysfs (gfx_target_version 90500 -> gfx950) so that the import does not
+    initialise HIP; empty when there is no GPU (or no sysfs)."""
+    archs = set()
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return archs
+    for nd in nodes:
+        try:
+            with open(os.path.join(root, nd, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version" and int(v) > 0:
+                        t = int(v)
+                        archs.add(f"gfx{t // 10000}{(t // 100) % 100:x}{t % 100:x}")
+        except (OSError, ValueError):
+            continue
+    return archs
+
+
 def _seed_tile_defaults(path: str = None) -> int:
     """Seed the tuner with the shipped table, or with the table file that
-    TFA_GEMM_DEFAULTS names (A/B of entries); TFA_GEMM_DEFAULTS=0: none."""
+    TFA_GEMM_DEFAULTS names (A/B of entries); TFA_GEMM_DEFAULTS=0: none.
+    A table whose "arch" is not this machine's GPU is not seeded: its tiles
+    were timed on another chip, and the 2 %-twice rule would keep them."""
     if os.environ.get("TFA_GEMM_DEFAULTS", "1") == "0":
+        return 0
+    import json
+    path = path or _table_path()
+    if not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        arch = json.load(f).get("arch")
+    gpus = _kfd_archs()
+    if arch and gpus and arch not in gpus:
         return 0
     n = 0
     for e in default_entries(path):

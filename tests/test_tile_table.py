@@ -38,3 +38,14 @@ def test_dump_merges(tmp_path):
     _native._dump_tune_table(str(p))
     got = json.loads(p.read_text())
     assert got["arch"] == "gfx950" and [1] * 20 in [e["key"] for e in got["entries"]]
+
+
+def test_table_seeded_only_on_its_arch(monkeypatch):
+    """gfx950.json is not seeded on another GPU: its tiles
+    were timed on gfx950. No GPU (this container) or a gfx950 seeds it."""
+    monkeypatch.setattr(_native, "_kfd_archs", lambda: {"gfx942"})
+    assert _native._seed_tile_defaults() == 0
+    monkeypatch.setattr(_native, "_kfd_archs", lambda: {"gfx950"})
+    assert _native._seed_tile_defaults() == len(_native.default_entries())
+    monkeypatch.setattr(_native, "_kfd_archs", lambda: set())
+    assert _native._seed_tile_defaults() == len(_native.default_entries())
