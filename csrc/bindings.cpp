@@ -703,7 +703,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_pool_threads", &tfa::decode_pool_threads);
   m.def("ragged_image_prep", [](const at::Tensor& data, const at::Tensor& offs, const at::Tensor& hw, int C, int OH,
                                  int OW, int mode, int oy, int ox, int h, int w,
-                                 const std::vector<std::pair<int, std::vector<float>>>& ops) {
+                                 const std::vector<std::pair<int, std::vector<float>>>& ops,
+                                 std::optional<at::Tensor> row_params) {
     // the batched map_rows image pre-stage (kernels/image.hip ragged_prep_kernel)
     TFA_CHECK(data.is_cuda() && data.scalar_type() == at::kByte && data.dim() == 1 && data.is_contiguous(),
               "ragged_image_prep: data must be a contiguous uint8 device buffer");
@@ -716,7 +717,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     a.n = n; a.C = C; a.OH = OH; a.OW = OW; a.mode = mode; a.oy = oy; a.ox = ox; a.h = h; a.w = w;
     a.nops = static_cast<int>(ops.size());
     for (size_t q = 0; q < ops.size(); ++q) {
-      TFA_CHECK(ops[q].first >= 0 && ops[q].first <= 2, "ragged_image_prep: step kind must be 0 add, 1 sub, 2 mul");
+      TFA_CHECK(ops[q].first >= 0 && ops[q].first <= 3,
+                "ragged_image_prep: step kind must be 0 add, 1 sub, 2 mul, 3 div");
       const auto& v = ops[q].second;
       TFA_CHECK(v.size() == 1 || static_cast<int>(v.size()) == C, "ragged_image_prep: step constant of ", v.size(),
                 " values for ", C, " channels");
@@ -725,6 +727,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       for (size_t c = 0; c < v.size(); ++c) a.op_val[q][c] = v[c];
     }
     c10::hip::HIPGuard guard(data.device().index());
+    at::Tensor rp;
+    if (row_params) {
+      // per-row (OH, OW, oy, ox): checked here on the host copy (the kernel
+      // trusts them), then copied to the device on the stream
+      const at::Tensor& hp = *row_params;
+      TFA_CHECK(!hp.is_cuda() && hp.scalar_type() == at::kInt && hp.is_contiguous() && hp.numel() == 4 * n,
+                "ragged_image_prep: row_params must be a host int32 [n, 4] tensor");
+      const int32_t* p = hp.data_ptr<int32_t>();
+      for (int64_t r = 0; r < n; ++r) {
+        const int32_t RH = p[4 * r], RW = p[4 * r + 1], py = p[4 * r + 2], px = p[4 * r + 3];
+        TFA_CHECK(RH > 0 && RW > 0 && py >= 0 && px >= 0 && py + h <= RH && px + w <= RW, "ragged_image_prep: row ",
+                  r, ": crop ", h, "x", w, " at (", py, ", ", px, ") outside its ", RH, "x", RW, " resize");
+      }
+      rp = pool_empty({n, 4}, data.options().dtype(at::kInt));
+      rp.copy_(hp, /*non_blocking=*/hp.is_pinned());
+      a.rp = rp.data_ptr<int32_t>();
+    }
     at::Tensor y = pool_empty({n, h, w, C}, data.options().dtype(at::kFloat));
     a.x = data.data_ptr<uint8_t>();
     a.offs = offs.data_ptr<int64_t>();
@@ -734,7 +753,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return y;
   }, py::arg("data"), py::arg("offsets"), py::arg("hw"), py::arg("channels"), py::arg("resize_h"),
         py::arg("resize_w"), py::arg("mode"), py::arg("crop_y"), py::arg("crop_x"), py::arg("crop_h"),
-        py::arg("crop_w"), py::arg("ops"),
+        py::arg("crop_w"), py::arg("ops"), py::arg("row_params") = py::none(),
         "n ragged uint8 HWC images -> f32 [n, crop_h, crop_w, C]: bilinear resize, crop, elementwise steps");
   m.def("gather_rows", [](const at::Tensor& x0, const at::Tensor& idx) {
     TFA_CHECK(x0.is_cuda() && idx.is_cuda() && idx.scalar_type() == at::kLong, "gather_rows: device tensors");

@@ -395,7 +395,8 @@ void register_array_ops(OpRegistry& r) {
     std::vector<bool> drop(rk, false);
     if (axes.empty()) {
       for (int i = 0; i < rk; ++i) {
-        TFA_CHECK(x.shape.dims[i] >= 0, "Squeeze with no axes needs a known shape, got ", x.shape.str());
+        // an unknown dim may or may not be 1: the rank is unknown until run time (as in TF)
+        if (x.shape.dims[i] < 0) { c.set(0, x.dtype, Shape::unknown()); return; }
         drop[i] = x.shape.dims[i] == 1;
       }
     } else {
@@ -709,6 +710,17 @@ void register_array_ops(OpRegistry& r) {
   slice.infer = [](InferCtx& c) {
     const TensorInfo& x = c.input(0);
     auto bv = c.ivalue(1), sv = c.ivalue(2);
+    if (sv && (x.shape.unknown_rank || !bv)) {
+      // begin computed per row (a central crop's offsets) or an input of
+      // unknown rank: the sizes given as numbers are still static
+      if (!x.shape.unknown_rank)
+        TFA_CHECK(static_cast<int>(sv->size()) == x.shape.rank(), "Slice: size has ", sv->size(),
+                  " entries for a rank-", x.shape.rank(), " input");
+      std::vector<int64_t> d;
+      for (int64_t s : *sv) d.push_back(s >= 0 ? s : -1);
+      c.set(0, x.dtype, Shape(d));
+      return;
+    }
     if (x.shape.unknown_rank || !bv || !sv) {
       c.set(0, x.dtype, x.shape.unknown_rank ? Shape::unknown()
                                              : Shape(std::vector<int64_t>(x.shape.rank(), -1)));

@@ -18,13 +18,17 @@ namespace k {
 
 namespace {
 
+// Both helpers round after every operation (no fused multiply-add), as the
+// host oracle (ir/ops_nn.cpp, one ATen op per step) does: the GPU resize, the
+// batched pre-stage and the CPU executor give the same bits.
 __device__ __forceinline__ float src_coord(int64_t dst, float scale, int mode) {
+#pragma clang fp contract(off)
   return mode == 2 ? ((float)dst + 0.5f) * scale - 0.5f : (float)dst * scale;
 }
 
-// the bilinear blend shared by both resize paths (one expression: one rounding
-// / contraction pattern for both)
+// the bilinear blend shared by both resize paths
 __device__ __forceinline__ float bilerp(float tl, float tr, float bl, float br, float lx, float ly) {
+#pragma clang fp contract(off)
   const float top = tl + (tr - tl) * lx;
   const float bot = bl + (br - bl) * lx;
   return top + (bot - top) * ly;
@@ -44,8 +48,8 @@ __global__ __launch_bounds__(256) void resize_bilinear_kernel(ResizeArgs a, int6
     const int64_t nn = t / a.OH;
     const float iy = src_coord(oh, a.sh, a.mode), ix = src_coord(ow, a.sw, a.mode);
     const float fy = floorf(iy), fx = floorf(ix);
-    const int64_t y0 = max((int64_t)fy, (int64_t)0), y1 = min((int64_t)ceilf(iy), a.H - 1);
-    const int64_t x0 = max((int64_t)fx, (int64_t)0), x1 = min((int64_t)ceilf(ix), a.W - 1);
+    const int64_t y0 = min(max((int64_t)fy, (int64_t)0), a.H - 1), y1 = min((int64_t)ceilf(iy), a.H - 1);
+    const int64_t x0 = min(max((int64_t)fx, (int64_t)0), a.W - 1), x1 = min((int64_t)ceilf(ix), a.W - 1);
     const float ly = iy - fy, lx = ix - fx;
     const T* base = x + nn * a.H * a.W * a.C + c;
     const float tl = (float)base[(y0 * a.W + x0) * a.C], tr = (float)base[(y0 * a.W + x1) * a.C];
@@ -58,8 +62,11 @@ __global__ __launch_bounds__(256) void resize_bilinear_kernel(ResizeArgs a, int6
 // batched pre-stage: the bilinear sample of the resized image at
 // (oy + yy, ox + xx), computed exactly as resize_bilinear_kernel does on the
 // cast image (so a batch equals the per-row program bit for bit), then the
-// elementwise steps in graph order
+// elementwise steps in graph order. With a.rp the resize size and crop offset
+// are the row's own (rp[4n..4n+3] = OH, OW, oy, ox: an aspect-preserving
+// resize and its central crop, evaluated per row on the host).
 __global__ __launch_bounds__(256) void ragged_prep_kernel(RaggedPrepArgs a, int64_t total) {
+#pragma clang fp contract(off)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const int c = (int)(i % a.C);
@@ -69,12 +76,17 @@ __global__ __launch_bounds__(256) void ragged_prep_kernel(RaggedPrepArgs a, int6
     const int yy = (int)(t % a.h);
     const int64_t nn = t / a.h;
     const int64_t H = a.hw[2 * nn], W = a.hw[2 * nn + 1];
-    const float sh = (a.mode == 1 && a.OH > 1) ? float(H - 1) / float(a.OH - 1) : float(H) / float(a.OH);
-    const float sw = (a.mode == 1 && a.OW > 1) ? float(W - 1) / float(a.OW - 1) : float(W) / float(a.OW);
-    const float iy = src_coord(a.oy + yy, sh, a.mode), ix = src_coord(a.ox + xx, sw, a.mode);
+    int OH = a.OH, OW = a.OW, oy = a.oy, ox = a.ox;
+    if (a.rp) {
+      const int4 p = reinterpret_cast<const int4*>(a.rp)[nn];
+      OH = p.x; OW = p.y; oy = p.z; ox = p.w;
+    }
+    const float sh = (a.mode == 1 && OH > 1) ? float(H - 1) / float(OH - 1) : float(H) / float(OH);
+    const float sw = (a.mode == 1 && OW > 1) ? float(W - 1) / float(OW - 1) : float(W) / float(OW);
+    const float iy = src_coord(oy + yy, sh, a.mode), ix = src_coord(ox + xx, sw, a.mode);
     const float fy = floorf(iy), fx = floorf(ix);
-    const int64_t y0 = max((int64_t)fy, (int64_t)0), y1 = min((int64_t)ceilf(iy), H - 1);
-    const int64_t x0 = max((int64_t)fx, (int64_t)0), x1 = min((int64_t)ceilf(ix), W - 1);
+    const int64_t y0 = min(max((int64_t)fy, (int64_t)0), H - 1), y1 = min((int64_t)ceilf(iy), H - 1);
+    const int64_t x0 = min(max((int64_t)fx, (int64_t)0), W - 1), x1 = min((int64_t)ceilf(ix), W - 1);
     const float ly = iy - fy, lx = ix - fx;
     const uint8_t* base = a.x + a.offs[nn] + c;
     const float tl = (float)base[(y0 * W + x0) * a.C], tr = (float)base[(y0 * W + x1) * a.C];
@@ -85,7 +97,8 @@ __global__ __launch_bounds__(256) void ragged_prep_kernel(RaggedPrepArgs a, int6
       switch (a.op_kind[q]) {
         case 0: v = v + k; break;
         case 1: v = v - k; break;
-        default: v = v * k; break;
+        case 2: v = v * k; break;
+        default: v = v / k; break;
       }
     }
     a.y[i] = v;
@@ -142,8 +155,10 @@ void resize_bilinear(DType dt, const ResizeArgs& a, hipStream_t s) {
 void ragged_image_prep(const RaggedPrepArgs& a, hipStream_t s) {
   const int64_t total = a.n * a.h * a.w * a.C;
   if (total <= 0) return;
-  TFA_CHECK(a.C >= 1 && a.C <= 4 && a.nops >= 0 && a.nops <= 4 && a.OH > 0 && a.OW > 0, "ragged_image_prep: bad args");
-  TFA_CHECK(a.oy >= 0 && a.ox >= 0 && a.oy + a.h <= a.OH && a.ox + a.w <= a.OW, "ragged_image_prep: crop outside");
+  TFA_CHECK(a.C >= 1 && a.C <= 4 && a.nops >= 0 && a.nops <= 4, "ragged_image_prep: bad args");
+  // per-row sizes and offsets (a.rp) are checked by the caller, on the host copy
+  TFA_CHECK(a.rp || (a.OH > 0 && a.OW > 0 && a.oy >= 0 && a.ox >= 0 && a.oy + a.h <= a.OH && a.ox + a.w <= a.OW),
+            "ragged_image_prep: crop outside");
   hipLaunchKernelGGL(ragged_prep_kernel, dim3(ew_grid(total)), dim3(256), 0, s, a, total);
   TFA_LAUNCH_CHECK("ragged_image_prep");
 }

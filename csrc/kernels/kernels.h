@@ -293,8 +293,9 @@ void resize_nearest(int64_t elem_size, const ResizeArgs& a, hipStream_t s);
 // batched ragged image pre-stage: n uint8 HWC images of their own sizes (byte
 // offsets offs[n], (H, W) pairs hw[2n]) -> f32 [n, h, w, C]: bilinear resize
 // to OH x OW (mode 0 default, 1 align_corners, 2 half_pixel_centers), crop at
-// (oy, ox), then up to 4 elementwise steps (0 add, 1 sub, 2 mul; a scalar or
-// per-channel constant)
+// (oy, ox), then up to 4 elementwise steps (0 add, 1 sub, 2 mul, 3 div; a
+// scalar or per-channel constant). rp (optional, int32 [n][4]): each row's
+// own OH, OW, oy, ox instead of the shared ones.
 struct RaggedPrepArgs {
   int64_t n = 0;
   int C = 3, OH = 0, OW = 0, oy = 0, ox = 0, h = 0, w = 0, mode = 0;
@@ -304,6 +305,7 @@ struct RaggedPrepArgs {
   const uint8_t* x = nullptr;
   const int64_t* offs = nullptr;
   const int32_t* hw = nullptr;
+  const int32_t* rp = nullptr;
   float* y = nullptr;
 };
 void ragged_image_prep(const RaggedPrepArgs& a, hipStream_t s);

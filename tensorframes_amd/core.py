@@ -33,7 +33,7 @@ from .frame.dataframe import DataFrame, GroupedData, _Derived, _Failed, _Materia
 from .frame.types import (BinaryType, NumericType, Row, StringType, StructField, StructType, sql_type_for_tf)
 from .graph import dsl
 from .graph import proto as P
-from .ops import host_ops
+from .ops import host_ops, image_prep
 from .parallel import dist
 from .utils import dtypes as D
 from .utils import faults
@@ -645,160 +645,13 @@ def _host_contents(spec: GraphSpec, host) -> List[str]:
     return [g.node_inputs(hf.node)[0].split(":")[0] for hf in host]
 
 
-class _ImagePrep:
-    """The per-row part of the reference's JPEG scoring graph, recognised and
-    run for a whole chunk of rows at once (reference
-    src/main/python/tensorframes_snippets/read_image.py:35-75): decoded uint8
-    image -> Cast float -> ResizeBilinear (const size) -> Slice (central crop)
-    -> up to 4 Add / Sub / Mul by a constant -> ExpandDims(0), the row's cut
-    tensor. The decoded images of a chunk (each its own H x W) are packed into
-    one page-locked buffer, copied in one DMA, and ONE kernel
-    (kernels/image.hip ragged_prep_kernel) writes the [rows, h, w, C] batch
-    the CNN reads, with the same arithmetic as the per-row ops (bit-identical
-    results)."""
-
-    def __init__(self, C, OH, OW, mode, oy, ox, h, w, ops):
-        self.C, self.OH, self.OW, self.mode = C, OH, OW, mode
-        self.oy, self.ox, self.h, self.w, self.ops = oy, ox, h, w, ops
-        self._inflight: List[tuple] = []  # (event, pinned buffer) of copies not yet known done
-
-    def channels(self, hf=None) -> Optional[int]:
-        """The channel count the chain fixes (a Slice size or a per-channel
-        constant), else the decoder's (`channels` 1 / 3 / 4), else None."""
-        if self.C is not None:
-            return self.C
-        return hf.channels if hf is not None and hf.channels in (1, 3, 4) else None
-
-    def run(self, imgs, dev) -> Optional[torch.Tensor]:
-        """None when the chunk's images do not share one uint8 [H, W, C]
-        layout the chain accepts (e.g. gray and RGB files under
-        `channels=0`): the caller then runs those rows one by one."""
-        arrs = [np.asarray(t) for t in imgs]
-        C = self.C if self.C is not None else (arrs[0].shape[2] if arrs and arrs[0].ndim == 3 else None)
-        if C is None or any(a.ndim != 3 or a.shape[2] != C or a.dtype != np.uint8 for a in arrs) or \
-                any(len(v) not in (1, C) for _, v in self.ops):
-            return None
-        sizes = np.array([a.size for a in arrs], dtype=np.int64)
-        offs = np.zeros(len(arrs), dtype=np.int64)
-        np.cumsum(sizes[:-1], out=offs[1:])
-        hw = np.array([[a.shape[0], a.shape[1]] for a in arrs], dtype=np.int32)
-        total = int(sizes.sum())
-        # meta (offsets, sizes) and pixels in one page-locked buffer, one DMA
-        mbytes = offs.nbytes + hw.nbytes
-        buf = _C.empty_pinned([mbytes + total], torch.uint8)
-        hb = buf.numpy()
-        hb[:offs.nbytes] = offs.view(np.uint8)
-        hb[offs.nbytes:mbytes] = hw.reshape(-1).view(np.uint8)
-        np.concatenate([a.reshape(-1) for a in arrs], out=hb[mbytes:])
-        return self.run_packed(buf, offs.nbytes, mbytes, dev, C)
-
-    def run_packed(self, buf: torch.Tensor, offs_nbytes: int, mbytes: int, dev, C: int) -> torch.Tensor:
-        """`buf` = [int64 offsets | int32 hw pairs | pixels] in pinned memory
-        (the layout _C.JpegBatch decodes into), C channels per pixel."""
-        d = engine.device_empty(buf.numel(), torch.uint8, dev)
-        d.copy_(buf, non_blocking=True)
-        # the pinned buffer returns to its pool only once its DMA has run
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        self._inflight = [(e, b) for e, b in self._inflight if not e.query()] + [(ev, buf)]
-        doffs = d[:offs_nbytes].view(torch.int64)
-        dhw = d[offs_nbytes:mbytes].view(torch.int32)
-        return _C.ragged_image_prep(d[mbytes:], doffs, dhw, C, self.OH, self.OW, self.mode, self.oy, self.ox,
-                                    self.h, self.w, self.ops)
+# the batched image pre-stage (recognition, per-row shape part, kernel call)
+_ImagePrep = image_prep.ImagePrep
 
 
-def _match_image_prep(graph_bytes: bytes, row_feeds: List[str], cut: str) -> Optional[_ImagePrep]:
-    """The chain feed -> cut as an _ImagePrep, or None when it is anything else."""
-    if len(row_feeds) != 1:
-        return None
-    try:
-        light = P.parse_graphdef(_C.light_graphdef(graph_bytes, 4096))
-    except Exception:  # noqa: BLE001 - not recognisable: the per-row path stays
-        return None
-    by_name = {nd.name: nd for nd in light.node}
-    consumers: Dict[str, List[str]] = {}
-    for nd in light.node:
-        for i in nd.input:
-            consumers.setdefault(i.split(":")[0].lstrip("^"), []).append(nd.name)
-
-    def const(name):
-        nd = by_name.get(name.split(":")[0])
-        if nd is None or nd.op != "Const" or "value" not in nd.attr:
-            return None
-        try:
-            return nd.attr["value"].value.to_numpy()
-        except Exception:  # noqa: BLE001
-            return None
-
-    def attr_b(nd, k):
-        a = nd.attr.get(k)
-        return bool(a.value) if a is not None else False
-
-    cur = row_feeds[0].split(":")[0]
-    size = crop = None
-    mode, C, ops, saw_cast = 0, None, [], False
-    while cur != cut:
-        nxt = consumers.get(cur, [])
-        if len(nxt) != 1:
-            return None
-        nd = by_name[nxt[0]]
-        ins = [i.split(":")[0] for i in nd.input if not i.startswith("^")]
-        if not ins or ins[0] != cur and nd.op not in ("Add", "AddV2", "Sub", "Mul"):
-            return None
-        if nd.op == "Cast":
-            if saw_cast or nd.attr.get("DstT") is None or nd.attr["DstT"].value != D.DT_FLOAT:
-                return None
-            saw_cast = True
-        elif nd.op == "ExpandDims":
-            dim = const(nd.input[1])
-            if dim is None or int(np.asarray(dim).reshape(-1)[0]) != 0:
-                return None
-        elif nd.op == "Squeeze":
-            a = nd.attr.get("squeeze_dims")
-            if a is None or list(a.value.get("i", [])) not in ([0],):
-                return None
-        elif nd.op == "ResizeBilinear":
-            if not saw_cast or size is not None or crop is not None:
-                return None
-            sz = const(nd.input[1])
-            if sz is None or np.asarray(sz).size != 2:
-                return None
-            size = [int(v) for v in np.asarray(sz).reshape(-1)]
-            align, half = attr_b(nd, "align_corners"), attr_b(nd, "half_pixel_centers")
-            mode = 1 if align else (2 if half else 0)
-        elif nd.op == "Slice":
-            b, sz = const(nd.input[1]), const(nd.input[2])
-            if size is None or crop is not None or ops or b is None or sz is None:
-                return None
-            b, sz = [int(v) for v in np.asarray(b).reshape(-1)], [int(v) for v in np.asarray(sz).reshape(-1)]
-            if len(b) != 3 or len(sz) != 3 or b[2] != 0 or sz[0] < 0 or sz[1] < 0:
-                return None
-            crop = (b[0], b[1], sz[0], sz[1])
-            if sz[2] >= 0:
-                C = sz[2]
-        elif nd.op in ("Add", "AddV2", "Sub", "Mul"):
-            other = [i for i in ins if i != cur]
-            if len(ins) != 2 or len(other) != 1 or (nd.op == "Sub" and ins[0] != cur):
-                return None
-            v = const(other[0])
-            if v is None or crop is None or len(ops) == 4 or np.asarray(v).dtype != np.float32:
-                return None
-            v = np.asarray(v, dtype=np.float32).reshape(-1)
-            if v.size > 4:
-                return None
-            ops.append((0 if nd.op in ("Add", "AddV2") else 1 if nd.op == "Sub" else 2, [float(x) for x in v]))
-        else:
-            return None
-        cur = nd.name
-    if size is None or crop is None:
-        return None
-    C = C or (max(len(v) for _, v in ops) if any(len(v) > 1 for _, v in ops) else None)  # None: the images'
-    if C is not None and any(len(v) not in (1, C) for _, v in ops):
-        return None
-    oy, ox, h, w = crop
-    if oy + h > size[0] or ox + w > size[1]:
-        return None
-    return _ImagePrep(C, size[0], size[1], mode, oy, ox, h, w, ops)
+def _match_image_prep(graph_bytes: bytes, row_feeds: List[str], cut: str, cut_shape=None):
+    """The chain feed -> cut as an ImagePrep, or None (ops/image_prep.py)."""
+    return image_prep.match(graph_bytes, row_feeds, cut, cut_shape)
 
 
 class _BatchCut:
@@ -949,7 +802,7 @@ class _BatchCut:
         self.modes = modes
         self.pre = engine.program(self.graph_bytes, [node + ":0"], self.row_feeds)
         self.post = prog
-        self.image_prep = _match_image_prep(self.graph_bytes, self.row_feeds, node)
+        self.image_prep = _match_image_prep(self.graph_bytes, self.row_feeds, node, list(shp))
         return True
 
     def run(self, nrows: int, row_inputs, dev, per_out, raw=None) -> Optional[List[torch.Tensor]]:
@@ -984,12 +837,16 @@ class _BatchCut:
                 _finish_jpeg_batch(job, raw[0], raw[1][a:a + step])
                 t1 = time.perf_counter()
                 with torch.cuda.stream(side):
-                    cut = [prep.run_packed(job.buffer, job.offsets_bytes, job.meta_bytes, dev, native.C)]
-                engine.record_stream(cut[0], main)
+                    c = prep.run_packed(job.buffer, job.offsets_bytes, job.meta_bytes, dev, native.C)
                 t_in += t1 - t0
                 t_pre += time.perf_counter() - t1
-                metrics.add("map_rows_batched_prestage_rows", len(rows))
-                metrics.add("map_rows_native_decode_rows", len(rows))
+                if c is not None:
+                    cut = [c]
+                    engine.record_stream(c, main)
+                    metrics.add("map_rows_batched_prestage_rows", len(rows))
+                    metrics.add("map_rows_native_decode_rows", len(rows))
+                    if prep.dyn is not None:
+                        metrics.add("map_rows_prestage_row_params_rows", len(rows))
             elif prep is not None:
                 # the whole chunk's pre-stage in one kernel: every decoded
                 # image in ONE pinned ragged buffer, one copy, one launch
@@ -1002,6 +859,8 @@ class _BatchCut:
                     cut = [c]
                     engine.record_stream(c, main)
                     metrics.add("map_rows_batched_prestage_rows", len(imgs))
+                    if prep.dyn is not None:
+                        metrics.add("map_rows_prestage_row_params_rows", len(imgs))
                 t_in += t1 - t0
                 t_pre += time.perf_counter() - t1
             for i in (rows if not cut else ()):

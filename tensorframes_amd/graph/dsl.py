@@ -1246,10 +1246,19 @@ def transpose(a, perm=None, name="transpose"):
 builtin_range = _builtins.range
 
 
+def _int_vector(v):
+    """An int32 vector operand given as numbers, a Tensor, or a list mixing
+    both (packed, as TF does for a computed crop offset)."""
+    if isinstance(v, Tensor):
+        return v
+    if isinstance(v, (list, tuple)) and any(isinstance(e, Tensor) for e in v):
+        return stack([e if isinstance(e, Tensor) else np.int32(e) for e in v])
+    return np.asarray(v, dtype=np.int32)
+
+
 def slice(input_, begin, size, name=None):  # noqa: A001
     x = convert_to_tensor(input_)
-    return _op("Slice", [("input", x), ("begin", np.asarray(begin, dtype=np.int32)),
-                         ("size", np.asarray(size, dtype=np.int32))],
+    return _op("Slice", [("input", x), ("begin", _int_vector(begin)), ("size", _int_vector(size))],
                {"T": P.AttrValue.type(x.dtype), "Index": P.AttrValue.type(int32)}, name,
                out_dtypes=[x.dtype]).outputs[0]
 
@@ -1621,7 +1630,7 @@ class _Image:
     @staticmethod
     def resize_bilinear(images, size, align_corners=False, half_pixel_centers=False, name=None):
         x = convert_to_tensor(images)
-        return _op("ResizeBilinear", [("images", x), ("size", np.asarray(size, dtype=np.int32))],
+        return _op("ResizeBilinear", [("images", x), ("size", _int_vector(size))],
                    {"T": P.AttrValue.type(x.dtype), "align_corners": P.AttrValue.b(align_corners),
                     "half_pixel_centers": P.AttrValue.b(half_pixel_centers)}, name,
                    out_dtypes=[float32]).outputs[0]
@@ -1629,7 +1638,7 @@ class _Image:
     @staticmethod
     def resize_nearest_neighbor(images, size, align_corners=False, half_pixel_centers=False, name=None):
         x = convert_to_tensor(images)
-        return _op("ResizeNearestNeighbor", [("images", x), ("size", np.asarray(size, dtype=np.int32))],
+        return _op("ResizeNearestNeighbor", [("images", x), ("size", _int_vector(size))],
                    {"T": P.AttrValue.type(x.dtype), "align_corners": P.AttrValue.b(align_corners),
                     "half_pixel_centers": P.AttrValue.b(half_pixel_centers)}, name,
                    out_dtypes=[x.dtype]).outputs[0]

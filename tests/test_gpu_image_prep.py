@@ -4,7 +4,9 @@ kernels/image.hip ragged_prep_kernel): the reference's JPEG scoring graph
 run with the per-row pre-program and with the ragged-batch kernel must give
 bit-identical top-k values and indices; the kernel alone against the per-image
 CPU-oracle ops (Cast -> ResizeBilinear -> Slice -> Sub) on images of mixed
-sizes and every resize mode."""
+sizes and every resize mode; the slim-style eval preprocessing (aspect-preserving
+resize computed from each image's shape, central crop, per-channel mean
+through split/concat) against the CPU executor, bit for bit."""
 import io
 
 import numpy as np
@@ -50,7 +52,10 @@ def test_ragged_kernel_matches_per_image_ops(mode):
         y = tf.slice(tf.squeeze(y, [0]), [oy, ox, 0], [h, w, -1])
         tf.multiply(tf.subtract(y, tf.constant(np.array(mean, np.float32))), 0.5, name="out")
     prog = engine.program(g.serialize(), ["out"], ["x"])
-    want = [engine.run_program(prog, [torch.from_numpy(a)], DEV)[0].cpu() for a in imgs]
+    # the oracle is the CPU executor; the GPU per-row program gives the same bits
+    want = [engine.run_program(prog, [torch.from_numpy(a)], torch.device("cpu"))[0] for a in imgs]
+    for a, wnt in zip(imgs[:3], want):
+        assert torch.equal(engine.run_program(prog, [torch.from_numpy(a)], DEV)[0].cpu(), wnt)
     sizes = np.array([a.size for a in imgs])
     offs = torch.from_numpy(np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)).to(DEV)
     hw = torch.tensor([[a.shape[0], a.shape[1]] for a in imgs], dtype=torch.int32, device=DEV)
@@ -133,3 +138,62 @@ def test_native_decode_falls_back_for_truncated_files():
     g = cnn.jpeg_scoring_graph("vgg16", contents=bytes(jpgs[0]), width=0.125)
     with g.as_default(), pytest.raises(Exception, match="(?i)truncated"):
         tfs.map_rows(["index", "value"], df, feed_dict={"DecodeJpeg/contents": "image_data"}).collect()
+
+
+def _slim_graph(**kw):
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_image_prestage_match import slim_eval_graph
+    return slim_eval_graph(**kw)
+
+
+def test_slim_prestage_equals_cpu_executor():
+    """Per-row resize sizes and crop offsets (from each image's own shape)
+    through the ragged kernel: bit-identical to the CPU executor running the
+    graph's pre-part on each image."""
+    from tensorframes_amd import core
+    g = _slim_graph(with_cnn=False)
+    prep = core._match_image_prep(g.serialize(), ["DecodeJpeg"], "prepped", [1, 224, 224, 3])
+    assert prep is not None and prep.dyn is not None
+    rng = np.random.default_rng(4)
+    shapes = [(224, 224), (256, 300), (480, 270), (231, 999), (640, 480), (225, 227)]
+    imgs = [rng.integers(0, 255, (h, w, 3), dtype=np.uint8) for h, w in shapes]
+    got = prep.run(imgs, DEV).cpu()
+    prog = engine.program(g.serialize(), ["prepped:0"], ["DecodeJpeg"])
+    for i, a in enumerate(imgs):
+        want = engine.run_program(prog, [torch.from_numpy(a)], torch.device("cpu"))[0]
+        assert want.shape == (1, 224, 224, 3)
+        assert torch.equal(got[i:i + 1], want), f"image {shapes[i]}: max diff {(got[i] - want[0]).abs().max().item()}"
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_slim_scoring_batched_equals_per_row(native):
+    """The slim-style graph through map_rows: the batched pre-stage runs
+    (metric counters) and gives the per-row path's top-k bit for bit."""
+    from PIL import Image
+    rng = np.random.default_rng(8)
+    jpgs = []
+    for _ in range(24):
+        h, w = (int(v) for v in rng.integers(224, 400, 2))
+        buf = io.BytesIO()
+        Image.fromarray(rng.integers(0, 255, (h, w, 3), dtype=np.uint8)).save(buf, format="JPEG", quality=90)
+        jpgs.append(bytearray(buf.getvalue()))
+    df = tfs.create_dataframe([Row(uri=f"img{i}", image_data=b) for i, b in enumerate(jpgs)], num_partitions=1)
+    g = _slim_graph()
+    res = {}
+    try:
+        for on in (False, True):
+            tfs.set_config(map_rows_batched_prestage=on, native_jpeg_decode=native)
+            tfs.metrics.reset()
+            with g.as_default():
+                rows = tfs.map_rows(["s"], df, feed_dict={"data": "image_data"}).select("uri", "s").collect()
+            res[on] = rows
+            m = tfs.metrics.snapshot()
+            assert (m.get("map_rows_batched_prestage_rows", 0) == len(jpgs)) == on, m
+            assert (m.get("map_rows_prestage_row_params_rows", 0) == len(jpgs)) == on, m
+    finally:
+        tfs.set_config(map_rows_batched_prestage=True, native_jpeg_decode=True)
+    for a, b in zip(res[False], res[True]):
+        assert a.uri == b.uri
+        assert np.array_equal(np.asarray(a["s"]), np.asarray(b["s"]))

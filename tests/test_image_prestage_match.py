@@ -4,8 +4,10 @@ core._match_image_prep on the reference's JPEG scoring chain
 resize -> central crop -> mean subtraction -> expand_dims) and on variants it
 must take (channel count from the decoder) or refuse (ops it does not model)."""
 import numpy as np
+import pytest
 
 from tensorframes_amd import core, tf
+from tensorframes_amd.ops import image_prep
 from tensorframes_amd.models import cnn
 
 
@@ -62,3 +64,86 @@ def test_per_channel_constants_fix_the_channel_count():
 def test_unmodelled_ops_are_refused():
     g = _chain(3, lambda x: tf.nn.relu(x))
     assert _cut(g, ["s"]).image_prep is None
+
+
+def slim_eval_graph(side=256, crop=224, means=(123.68, 116.78, 103.94), with_cnn=True):
+    """slim-style eval preprocessing (vgg_preprocessing.preprocess_for_eval):
+    aspect-preserving resize of the uint8 image to smallest side `side`,
+    central crop computed from the resized shape, per-channel mean
+    subtraction through split / concat, then a batch of one."""
+    g = tf.Graph()
+    with g.as_default():
+        data = tf.placeholder(tf.string, [], name="data")
+        im = tf.image.decode_jpeg(data, channels=3, name="DecodeJpeg")
+        shp = tf.shape(im)
+        hf, wf = tf.cast(shp[0], tf.float32), tf.cast(shp[1], tf.float32)
+        scale = tf.where(tf.greater(hf, wf), float(side) / wf, float(side) / hf)
+        nh = tf.cast(tf.round(hf * scale), tf.int32, name="new_h")
+        nw = tf.cast(tf.round(wf * scale), tf.int32, name="new_w")
+        x = tf.squeeze(tf.image.resize_bilinear(tf.expand_dims(im, 0), [nh, nw]))
+        rs = tf.shape(x)
+        oy = tf.identity((rs[0] - crop) // 2, name="off_h")
+        ox = tf.identity((rs[1] - crop) // 2, name="off_w")
+        x = tf.slice(x, [oy, ox, 0], [crop, crop, 3])
+        x = tf.cast(x, tf.float32)
+        r, gch, b = tf.split(x, 3, axis=2)
+        x = tf.concat([r - means[0], gch - means[1], b - means[2]], 2)
+        x = tf.expand_dims(x, 0, name="prepped")
+        if with_cnn:
+            y = tf.nn.conv2d(x, tf.constant(np.ones((3, 3, 3, 4), np.float32) * 1e-3), [1, 1, 1, 1], "SAME")
+            tf.reduce_sum(tf.nn.relu(y), [1, 2], name="s")
+    return g
+
+
+def test_slim_style_chain_is_recognised_with_per_row_sizes():
+    g = slim_eval_graph()
+    bc = _cut(g, ["s"])
+    assert bc.cut == "prepped"
+    p = bc.image_prep
+    assert p is not None and p.dyn is not None
+    assert (p.h, p.w, p.C, p.mode) == (224, 224, 3, 0)
+    assert p.ops == [(1, [np.float32(123.68), np.float32(116.78), np.float32(103.94)])]
+
+
+def test_per_row_sizes_match_the_cpu_executor():
+    """The host evaluation of the shape-only part gives, for every image
+    size, the resize size and crop offset the graph itself computes on the
+    CPU executor."""
+    import torch
+
+    from tensorframes_amd import engine
+    g = slim_eval_graph(with_cnn=False)
+    p = _cut_prep(g)
+    rng = np.random.default_rng(0)
+    hw = np.concatenate([rng.integers(224, 900, (40, 2)), [[224, 224], [256, 1000], [1001, 257], [300, 300]]])
+    got = p.row_params(hw.astype(np.int32))
+    prog = engine.program(g.serialize(), ["new_h:0", "new_w:0", "off_h:0", "off_w:0"], ["DecodeJpeg"])
+    for (H, W), row in zip(hw, got):
+        img = torch.zeros((int(H), int(W), 3), dtype=torch.uint8)
+        want = [int(t.item()) for t in engine.run_program(prog, [img], torch.device("cpu"))]
+        assert list(row) == want, (H, W, row, want)
+
+
+def _cut_prep(g):
+    # the pre-stage of a graph whose cut is its `prepped` batch of one
+    return core._match_image_prep(g.serialize(), ["DecodeJpeg"], "prepped", [1, 224, 224, 3])
+
+
+def test_small_image_rows_fall_back():
+    """A row whose central crop would fall outside its resize (the graph's
+    own Slice would fail there) is not batched: the chunk runs per row."""
+    p = _cut_prep(slim_eval_graph(side=200, with_cnn=False))
+    with pytest.raises(image_prep.Unsupported):
+        p.row_params(np.array([[300, 400]], np.int32))
+
+
+def test_split_branches_with_different_steps_are_refused():
+    g = tf.Graph()
+    with g.as_default():
+        data = tf.placeholder(tf.string, [], name="data")
+        x = tf.cast(tf.image.decode_jpeg(data, channels=3, name="DecodeJpeg"), tf.float32)
+        x = tf.slice(tf.squeeze(tf.image.resize_bilinear(tf.expand_dims(x, 0), [40, 40]), [0]), [4, 4, 0],
+                     [32, 32, 3])
+        r, gc, b = tf.split(x, 3, axis=2)
+        x = tf.expand_dims(tf.concat([r - 1.0, gc * 2.0, b - 3.0], 2), 0, name="prepped")
+    assert core._match_image_prep(g.serialize(), ["DecodeJpeg"], "prepped", [1, 32, 32, 3]) is None
