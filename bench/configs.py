@@ -53,11 +53,13 @@ def timed(fn, steps, warmup):
     for _ in range(warmup):
         fn()
     sync()
+    _C.roctx_push("tfa.timed_steps")  # rocprofv3 --marker-trace: the timed window
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
     sync()
     dt = time.perf_counter() - t0
+    _C.roctx_pop()
     if dist.is_distributed():
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce_(t, "Max")
@@ -295,6 +297,10 @@ def cfg_inception(a):
     metrics.reset()
     dt = timed(lambda: run(df), a.steps, 0)
     m = metrics.snapshot()
+    if a.step_profile:  # one more, untimed step with per-step device timing
+        from tensorframes_amd.utils.profiling import step_profile
+        step_profile(lambda: run(df), a.step_profile,
+                     f"Inception-v3, {images} images ({a.source}-resident, batch {batch}): per-layer device time")
     flops_per_image = _inception_flops(size)
     in_bytes = images * size * size * 3 * (1 if u8 else 4)
     emit({"config": f"5: {images}-row {size}x{size}x3 {a.input_dtype} image column ({a.source}-resident), "
@@ -374,6 +380,8 @@ def main():
     ap.add_argument("--batch", type=int, default=2048,
                     help="rows per partition (inception: 2048 fills the chip; measured 17.7k vs 16.6k img/s at 512)")
     ap.add_argument("--source", choices=["host", "device"], default="host", help="inception: where the column lives")
+    ap.add_argument("--step-profile", default="", help="inception: after the timed steps, one more step with "
+                    "per-step device timing, written to this JSON (+ .md)")
     ap.add_argument("--input-dtype", choices=["float32", "uint8"], default="float32", help="inception image dtype")
     ap.add_argument("--chunk-images", type=int, default=1024,
                     help="inception (host): images per pipelined chunk (1024: 16.8k vs 15.2k img/s at 256)")

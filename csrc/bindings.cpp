@@ -14,6 +14,7 @@
 #include "runtime/executor.h"
 #include "runtime/jit.h"
 #include "runtime/jpeg_decode.h"
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 namespace py = pybind11;
 using namespace tfa;
@@ -672,6 +673,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     bool ok = tfa::jpeg_native_available(&why);
     return py::make_tuple(ok, why);
   });
+  m.def("set_step_timing", &tfa::set_step_timing, py::arg("on"),
+        "time every step of GPU plan runs (a hipEvent pair each) until turned off");
+  m.def("read_step_timing", [] {
+    py::list out;
+    for (const auto& r : tfa::read_step_timing()) {
+      py::dict d;
+      d["node"] = r.node;
+      d["op"] = r.op;
+      d["label"] = r.label;
+      d["flops"] = r.flops;
+      d["ms"] = r.ms;
+      out.append(d);
+    }
+    return out;
+  }, "wait for and drain the step records: [{node, op, label, flops, ms}] in launch order");
+  m.def("roctx_push", [](const std::string& name) { roctxRangePushA(name.c_str()); }, py::arg("name"),
+        "open a roctx range (rocprofv3 --marker-trace)");
+  m.def("roctx_pop", [] { roctxRangePop(); });
   m.def("jpeg_native_info", [] {
     tfa::JpegLibInfo i = tfa::jpeg_native_info();
     py::dict d;

@@ -57,6 +57,19 @@ struct RangeGuard {
   ~RangeGuard() { roctxRangePop(); }
 };
 
+// Step timing (set_step_timing): a hipEvent pair around every step of every
+// GPU plan run while it is on, read back (device ms, FLOPs, the step's label)
+// by read_step_timing: the per-layer table of the plan that really ran
+// (sibling-fused convs, Winograd or implicit GEMM), not of isolated layers.
+std::atomic<bool> g_step_timing{false};
+struct StepRec {
+  std::string node, op, label;
+  double flops = 0;
+  hipEvent_t a = nullptr, b = nullptr;
+};
+std::mutex g_step_mu;
+std::vector<StepRec> g_step_recs;
+
 // TFA_STAGE_TIMERS=0 turns off the per-chunk hipEvent stage timers of run_chunked
 bool stage_timers_enabled() {
   static const bool on = [] {
@@ -1442,11 +1455,19 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
     if (it == m.end()) it = m.emplace(sc.first, dev.is_cuda() ? sc.second.to(dev) : sc.second).first;
     slots[sc.first] = it->second;
   }
+  const bool timing = gpu && g_step_timing.load(std::memory_order_relaxed) &&
+                      !dev_stream_capturing(static_cast<hipStream_t>(stream));
   for (auto& st : p.steps) {
     const Node& nd = g_->node(st.node);
     ExecCtx c{nd, {}, {}, &st.out_info, &st.in_info, gpu, stream};
     for (int s : st.in_slots) c.in.push_back(slots[s]);
     c.out.resize(st.out_info.size());
+    StepRec rec;
+    if (timing) {
+      TFA_CHECK(hipEventCreate(&rec.a) == hipSuccess, "hipEventCreate failed");
+      TFA_CHECK(hipEventCreate(&rec.b) == hipSuccess, "hipEventCreate failed");
+      TFA_CHECK(hipEventRecord(rec.a, static_cast<hipStream_t>(stream)) == hipSuccess, "hipEventRecord failed");
+    }
     {
       std::unique_ptr<RangeGuard> rg;
       if (gpu) rg = std::make_unique<RangeGuard>(nd.op + ":" + nd.name);
@@ -1600,6 +1621,33 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
                 "' produced shape ", shape_of(o).str(), " but inference said ", want.str());
       slots[st.out_slots[k]] = o;
     }
+    if (timing) {
+      TFA_CHECK(hipEventRecord(rec.b, static_cast<hipStream_t>(stream)) == hipSuccess, "hipEventRecord failed");
+      rec.node = g_->node(st.out_node >= 0 ? st.out_node : st.node).name;
+      rec.op = nd.op;
+      if (st.kind == Step::CONV || st.kind == Step::GEMM) {
+        // 2 * output elements * reduction length, summed over sibling outputs
+        int64_t outs_n = 0;
+        for (auto& o : c.out) outs_n += o.numel();
+        int64_t red = 0;
+        if (st.kind == Step::CONV) {
+          const at::Tensor& f = c.in[1];
+          red = f.dim() == 4 ? f.size(0) * f.size(1) * f.size(2) : 0;
+        } else {
+          const at::Tensor& a = c.in[0];
+          red = a.dim() >= 2 ? (gemm_ta(nd) ? a.size(a.dim() - 2) : a.size(a.dim() - 1)) : 0;
+        }
+        rec.flops = 2.0 * static_cast<double>(outs_n) * static_cast<double>(red);
+        rec.label = st.kind == Step::GEMM ? "gemm"
+                    : st.wino_slot >= 0  ? (c.in[1].size(0) == 3 && c.in[1].size(1) == 3 ? "wino_f23" : "wino_f27")
+                                         : "implicit_gemm";
+        if (!st.sibs.empty()) rec.label += str_cat("+siblings", st.sibs.size());
+      } else {
+        rec.label = st.kind == Step::FUSED ? "fused" : "op";
+      }
+      std::lock_guard<std::mutex> lk(g_step_mu);
+      g_step_recs.push_back(std::move(rec));
+    }
     for (int s : st.release) slots[s] = at::Tensor();
     stats_.kernels++;
   }
@@ -1631,7 +1679,7 @@ int hip_graphs_mode() {
     const std::string v(e);
     return v == "0" ? 0 : (v == "2" ? 2 : 1);
   }();
-  return debug_sync() ? 0 : mode;
+  return (debug_sync() || g_step_timing.load()) ? 0 : mode;  // step timing needs the eager path
 }
 bool hip_graphs_enabled() { return hip_graphs_mode() != 0; }
 int64_t now_ns() {
@@ -1645,6 +1693,27 @@ int64_t hip_graph_max_bytes() {
 }  // namespace
 
 bool Program::graphable(const Plan& p) const { return graph_blocker(p).empty(); }
+
+void set_step_timing(bool on) { g_step_timing.store(on); }
+bool step_timing() { return g_step_timing.load(); }
+
+std::vector<StepTiming> read_step_timing() {
+  std::vector<StepRec> recs;
+  {
+    std::lock_guard<std::mutex> lk(g_step_mu);
+    recs.swap(g_step_recs);
+  }
+  std::vector<StepTiming> out;
+  for (auto& r : recs) {
+    float ms = 0;
+    TFA_CHECK(hipEventSynchronize(r.b) == hipSuccess, "hipEventSynchronize failed");
+    TFA_CHECK(hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess, "hipEventElapsedTime failed");
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+    out.push_back({r.node, r.op, r.label, r.flops, ms});
+  }
+  return out;
+}
 
 // why a plan cannot be captured into a HIP graph ("" = it can)
 std::string Program::graph_blocker(const Plan& p) const {

@@ -181,6 +181,17 @@ class Program {
   void drop_pipe(bool synced);
 };
 
+// per-step device time of GPU plan runs while on (tools: the per-layer table
+// of the plan that ran); read_step_timing waits for and drains the records
+struct StepTiming {
+  std::string node, op, label;
+  double flops;
+  float ms;
+};
+void set_step_timing(bool on);
+bool step_timing();
+std::vector<StepTiming> read_step_timing();
+
 // waits for (and releases) an event handle returned by run_chunked(wait=false)
 void pipeline_wait(int64_t handle);
 

@@ -38,7 +38,10 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
 }
 
 std::vector<std::string> options() {
-  return {std::string("--offload-arch=") + kArch, "-O3", "-std=c++17"};
+  // no fused multiply-add in the generated elementwise kernels: they round
+  // after every op like the CPU executor (and the image pre-stage kernel),
+  // so a fused chain gives the host oracle's bits; they are memory-bound
+  return {std::string("--offload-arch=") + kArch, "-O3", "-std=c++17", "-ffp-contract=off"};
 }
 
 std::string key_of(const std::string& src) {

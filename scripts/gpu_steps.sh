@@ -5,6 +5,13 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+# clocks / power / temperature every 5 s next to every number this call
+# measures (gpurun_out/smi_trace.log); SMI=0 turns it off
+if [ "${SMI:-1}" = 1 ]; then
+  ( while true; do echo "== $(date +%T)"; rocm-smi --showclocks --showpower --showtemp --showuse 2>&1 | grep -E "GPU\[|sclk|mclk|fclk|Power|Temperature|use"; sleep 5; done ) >> gpurun_out/smi_trace.log 2>&1 &
+  SMI_PID=$!
+  trap 'kill $SMI_PID 2>/dev/null' EXIT
+fi
 run() {
   local name=$1; shift
   local secs=$1; shift
@@ -85,6 +92,16 @@ for s in ${STEPS:-tests}; do
     wsweep3) TFA_WINO_TILE=3 run wsweep3 300 python scripts/wino_sweep.py ;;
     layers_v2) TFA_WINO_TILE=2 run layers_wino_v2 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v2.json ;;
     layers_v0) TFA_WINO_TILE=0 run layers_wino_v0 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v0.json ;;
+    # ---- round 6: the executed plan (per-step device time) and one timed window's kernel trace
+    layers_exec)
+      run layers_exec_incep 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_exec_incep.json &&
+      run layers_exec_vgg 600 python examples/read_image.py --images 4096 --step-profile gpurun_out/layers_exec_vgg.json ;;
+    trace_incep) export TMPDIR=/tmp
+      run trace_incep 900 rocprofv3 --kernel-trace --marker-trace --output-format csv -d "$PWD/gpurun_out/trace_incep" -o run -- python bench/configs.py inception --source device --rows 16384 --steps 1 --warmup 1 &&
+      run trace_incep_window 120 python scripts/trace_window.py gpurun_out/trace_incep --out gpurun_out/trace_incep_step.md --title "Inception-v3, 16384 device-resident images: one timed step" ;;
+    trace_vgg) export TMPDIR=/tmp
+      run trace_vgg 600 rocprofv3 --kernel-trace --marker-trace --output-format csv -d "$PWD/gpurun_out/trace_vgg" -o run -- python examples/read_image.py --images 4096 &&
+      run trace_vgg_window 120 python scripts/trace_window.py gpurun_out/trace_vgg --out gpurun_out/trace_vgg_step.md --title "VGG-16 JPEG scoring (read_image), 4096 images: the steady-state pass" ;;
     # ---- presets (the one-off round-4/5 step lists, folded in)
     final) STEPS=smoke bash scripts/gpu_check.sh && run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
       run bench 900 python bench.py --steps 5 --warmup 2 &&

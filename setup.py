@@ -32,7 +32,7 @@ HIP_FLAGS = [
     "-std=c++17",
     f"--offload-arch={ARCH}",
     "-fPIC",
-    "-ffp-contract=fast",
+    "-ffp-contract=fast-honor-pragmas",  # contraction on, except where a kernel turns it off
     "-munsafe-fp-atomics",
     "-Wno-unused-result",
 ]

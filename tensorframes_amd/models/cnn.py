@@ -181,14 +181,36 @@ def top_k_classes(graph: tf.Graph, output_name: str = "prob", k: int = 5, name: 
 _RGB_MEANS = np.array([123.68, 116.78, 103.94], np.float32)
 
 
+def slim_eval_preprocess(im, image_size: int = 224, resize_side: int = 256):
+    """The slim-style eval preprocessing (vgg_preprocessing.preprocess_for_eval,
+    the graphs the reference's users score with): aspect-preserving bilinear
+    resize of the uint8 image so its smaller side is `resize_side` (sizes
+    computed from the image's own shape, rounded half to even), a central
+    `image_size` crop whose offsets come from the resized shape, float, and the
+    per-channel mean subtracted channel by channel (split / concat)."""
+    shp = tf.shape(im)
+    hf, wf = tf.cast(shp[0], tf.float32), tf.cast(shp[1], tf.float32)
+    scale = tf.where(tf.greater(hf, wf), float(resize_side) / wf, float(resize_side) / hf)
+    nh = tf.cast(tf.round(hf * scale), tf.int32)
+    nw = tf.cast(tf.round(wf * scale), tf.int32)
+    x = tf.squeeze(tf.image.resize_bilinear(tf.expand_dims(im, 0), [nh, nw]), [0])
+    rs = tf.shape(x)
+    oy, ox = (rs[0] - image_size) // 2, (rs[1] - image_size) // 2
+    x = tf.cast(tf.slice(x, [oy, ox, 0], [image_size, image_size, 3]), tf.float32)
+    chans = tf.split(x, 3, axis=2)
+    return tf.concat([c - m for c, m in zip(chans, _RGB_MEANS)], 2)
+
+
 def jpeg_scoring_graph(model: str = "vgg16", image_size: int = 224, resize_to: Optional[int] = None,
-                       contents=None, k: int = 5, **model_kw) -> tf.Graph:
+                       contents=None, k: int = 5, preprocessing: str = "reference", **model_kw) -> tf.Graph:
     """The reference's image-scoring graph (read_image.py:35-75): JPEG bytes ->
     ``DecodeJpeg`` (host stage) -> float -> resize -> central crop -> mean
     subtraction -> batch of one -> CNN -> softmax -> ``top_predictions``
     (TopKV2). `contents` (bytes) becomes the ``DecodeJpeg/contents`` constant
     that ``map_rows(..., feed_dict={'DecodeJpeg/contents': <binary column>})``
     replaces row by row; None makes it a string placeholder of that name.
+    preprocessing="slim": slim_eval_preprocess (aspect-preserving resize to
+    `resize_to`, default 256) instead of the square resize.
     Outputs: ``index`` (int32 [k]) and ``value`` (float32 [k])."""
     g = tf.Graph()
     resize_to = resize_to or image_size + 32
@@ -197,10 +219,13 @@ def jpeg_scoring_graph(model: str = "vgg16", image_size: int = 224, resize_to: O
             with tf.name_scope("DecodeJpeg/"):
                 contents = tf.placeholder(tf.string, [], name="contents")
         im = tf.image.decode_jpeg(contents, channels=3)
-        x = tf.cast(im, tf.float32)
-        x = tf.image.resize_images(x, [resize_to, resize_to])
-        x = tf.image.central_crop_to(x, image_size, image_size)
-        x = tf.subtract(x, tf.constant(_RGB_MEANS))
+        if preprocessing == "slim":
+            x = slim_eval_preprocess(im, image_size, resize_to)
+        else:
+            x = tf.cast(im, tf.float32)
+            x = tf.image.resize_images(x, [resize_to, resize_to])
+            x = tf.image.central_crop_to(x, image_size, image_size)
+            x = tf.subtract(x, tf.constant(_RGB_MEANS))
         x = tf.expand_dims(x, 0)
         build = {"vgg16": vgg16, "inception_v3": inception_v3}[model]
         build(image_size=image_size, inputs=x, graph=g, **model_kw)
