@@ -449,6 +449,11 @@ void gemm(DType dt, const GemmArgs& g, hipStream_t s) {
   TFA_LAUNCH_CHECK("gemm");
 }
 
+namespace {
+thread_local const char* t_conv_algo = "";
+}
+const char* last_conv_algo() { return t_conv_algo; }
+
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
   TFA_CHECK(dt == DType::F32, "conv2d: f32 only");
   TFA_CHECK(a.N > 0 && a.OH > 0 && a.OW > 0 && a.OC > 0, "conv2d: empty output");
@@ -462,22 +467,27 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     cg.OH = (int)a.OH; cg.OW = (int)a.OW;
     cg.sh = (int)a.sh; cg.sw = (int)a.sw; cg.dh = (int)a.dh; cg.dw = (int)a.dw;
     cg.pt = (int)a.pad_t; cg.pl = (int)a.pad_l;
+    t_conv_algo = f32_precision() == 1 ? "bf16" : "bf16x3";
     bf16_gemm_launch(f32_precision(), g, !conv_is_pointwise(a), cg, s);
     return;
   }
   if (conv_wino_eligible(a)) {  // 3x3 stride 1 with a planner-made Winograd filter
+    t_conv_algo = a.KH == 3 ? "wino_f23" : "wino_f27";
     conv_wino_launch(a, s);
     return;
   }
   if (!conv_is_pointwise(a) && conv_smallc_eligible(a)) {  // RGB stems: filter in registers, no LDS
+    t_conv_algo = "direct_smallc";
     conv_smallc_launch(a, s);
     return;
   }
   if (conv_direct_eligible(a)) {  // narrow stem convs: filter in LDS, A to registers
+    t_conv_algo = "direct";
     conv_direct_launch(a, s);
     return;
   }
   if (conv_is_pointwise(a)) {  // 1x1/s1: x is already the [N*H*W, C] A matrix
+    t_conv_algo = "gemm_1x1";
     bool vec = al16(a.x) && al16(a.w) && a.C % 4 == 0 && a.OC % 4 == 0;
     run_f32(g, A_KCONTIG, vec, ConvGeom{}, s);
   } else {
@@ -489,6 +499,7 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     cg.fast = g.M < (int64_t(1) << 32);
     cg.fOW = make_fastdiv((uint32_t)a.OW);
     cg.fOH = make_fastdiv((uint32_t)a.OH);
+    t_conv_algo = "implicit_gemm";
     bool vec = a.C % 4 == 0 && al16(a.x) && al16(a.w) && a.OC % 4 == 0;
     run_f32(g, A_CONV, vec, cg, s);
   }

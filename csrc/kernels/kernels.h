@@ -258,6 +258,9 @@ struct ConvArgs {
 };
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a);
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s);
+// the kernel family the calling thread's last conv2d_nhwc ran ("wino_f23",
+// "implicit_gemm", "gemm_1x1", "direct", ...): step-timing labels
+const char* last_conv_algo();
 struct PoolArgs {
   int64_t N, H, W, C, OH, OW, KH, KW, sh, sw, pad_t, pad_l;
   bool is_max;

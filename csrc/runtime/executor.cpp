@@ -1638,9 +1638,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           red = a.dim() >= 2 ? (gemm_ta(nd) ? a.size(a.dim() - 2) : a.size(a.dim() - 1)) : 0;
         }
         rec.flops = 2.0 * static_cast<double>(outs_n) * static_cast<double>(red);
-        rec.label = st.kind == Step::GEMM ? "gemm"
-                    : st.wino_slot >= 0  ? (c.in[1].size(0) == 3 && c.in[1].size(1) == 3 ? "wino_f23" : "wino_f27")
-                                         : "implicit_gemm";
+        rec.label = st.kind == Step::GEMM ? "gemm" : k::last_conv_algo();
         if (!st.sibs.empty()) rec.label += str_cat("+siblings", st.sibs.size());
       } else {
         rec.label = st.kind == Step::FUSED ? "fused" : "op";

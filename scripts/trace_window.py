@@ -42,8 +42,19 @@ def window(marker_csv, marker):
 
 
 def short(name):
-    name = re.sub(r"\(.*", "", name)  # drop the argument list
-    return name[:110]
+    """the kernel name with its template arguments, without the parameter list"""
+    name = name.replace("(anonymous namespace)::", "")
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            name = name[:i]
+            break
+    name = re.sub(r"^void ", "", name)
+    return name[:160]
 
 
 def main():
