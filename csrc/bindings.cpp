@@ -812,6 +812,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "Winograd F(2x2,3x3) / F(2,7) for 3x3 / 1x7 / 7x1 stride-1 convs with constant filters (default on; TFA_CONV_ALGO=direct "
         "turns it off). Plans built while it is off carry no Winograd filters.");
   m.def("conv_wino_enabled", [] { return k::conv_wino_enabled(); });
+  m.def("set_wino_bn", &tfa::k::set_wino_bn, py::arg("bn"), "F(2x2,3x3) oc block: 0 auto (32 for OC <= 32), 32 or 64");
   m.def("set_wino_tile", [](int v) { k::set_wino_tile(v); },
         "force the Winograd kernel variant: -1 auto, 0 = 64 tiles x 64 oc, 1 = 128 tiles x 32 oc");
   m.def("conv_wino_filter", [](const at::Tensor& w) {

@@ -103,23 +103,29 @@ constexpr uint32_t kOOB = 0x80000000u;  // an offset past every input descriptor
 __device__ __attribute__((aligned(16))) float4 kWinoTrash[64];
 
 // Persistent: one block of 8 waves (two per SIMD) per CU, each taking work
-// items (64 tiles x 64 oc) b', b' + G, ... (b' = XCD remap of its index, so
+// items (T tiles x BN oc) b', b' + G, ... (b' = XCD remap of its index, so
 // the 32 blocks of one XCD hold 32 consecutive items: the oc blocks of a tile
 // block, and neighbouring tile blocks, share L2). The DMA of the next item's
 // first stage is issued before this item's epilogue, which hides its latency.
-// Wave w owns the xi row xr = w & 3 of tiles [32 (w >> 2), +32) x 64 oc:
-// acc[xi_x][oc half] = 4 x 2 32x32 accumulators = 128 registers per lane.
+// BN = 64 (T = 64): wave w owns the xi row xr = w & 3 of tiles
+// [32 (w >> 2), +32) x 64 oc. BN = 32 (T = 128, OC <= 32 layers such as
+// Inception's Conv2d_2a: no padded oc half): tiles [64 (w >> 2), +64) x 32 oc.
+// Either way acc[xi_x][2] = 4 x 2 32x32 accumulators = 128 registers per lane.
+template <int BN>
 __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, int nbn, int nwork) {
-  constexpr int T = 64, BN = 64, TWV = 32;
+  constexpr int T = 4096 / BN, TWV = 32;
+  constexpr int NG = T / 32;                   // 32-tile groups per block
+  constexpr int MT = T / 64, NT = BN / 32;     // a wave's tile groups and 32-oc halves (MT * NT = 2)
+  static_assert(MT * NT == 2, "two 32x32 accumulators per xi column");
   constexpr int IN_BYTES = 16 * 2 * T * 16, U_BYTES = 16 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
-  constexpr int GI = 4, GU = 4;                // DMA pieces per wave per stage (32 + 32 per block)
+  constexpr int GI = 2 * NG, GU = BN / 16;     // DMA pieces per wave per stage
   constexpr int EP = BN + 4;                   // exchange row pitch (floats): conflict-free ds_write_b32
   constexpr int EH_BYTES = 4 * T * EP * 4;     // one px plane of the exchange
-  constexpr int SMEM = STAGE + EH_BYTES;       // slot 0 | slot 1, the exchange plane over slot 1 and past it
+  constexpr int SMEM = (2 * STAGE > STAGE + EH_BYTES) ? 2 * STAGE : STAGE + EH_BYTES;  // slot 0 | slot 1 (+ exchange)
   constexpr int LPT = BN / 4, TPP = 64 / LPT;  // epilogue: lanes per tile (float4 of oc), tiles per pass
   constexpr int NPASS = T / 8 / TPP;           // passes over the wave's T/8 tiles
   constexpr int NST = NPASS * 2 * 2;           // stores per lane per item (unconditional)
-  static_assert(2 * STAGE <= SMEM && SMEM <= 160 * 1024, "LDS budget");
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -130,16 +136,18 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
   const float* x = static_cast<const float*>(g.A);
   const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
   const __amdgpu_buffer_rsrc_t rnil = wrsrc(g.B, 0u);
-  // filter piece p = wave * GU + i: (xi, quad) = (p >> 1, p & 1), oc n0 + lane
+  // filter piece p = wave * GU + i covers (xi, quad) rows p * (64 / BN) + lane / BN,
+  // oc n0 + lane % BN (global layout [C/8][16 xi][2 quads][OCP][4 c])
   uint32_t uoff[GU];
 #pragma unroll
-  for (int i = 0; i < GU; ++i) uoff[i] = (uint32_t)(((wave * GU + i) * q.OCP + lane) * 16);
+  for (int i = 0; i < GU; ++i)
+    uoff[i] = (uint32_t)((((wave * GU + i) * (64 / BN) + lane / BN) * q.OCP + lane % BN) * 16);
   const uint32_t ustep = (uint32_t)(32 * q.OCP * 16);  // filter bytes per 8-channel stage
 
   // ---- one work item's DMA state. Input: the descriptor starts at the
   // item's first image (every valid tap lies within 2^31 bytes of it:
-  // conv_wino_eligible); piece p = wave * GI + i: patch position p >> 1
-  // (= 4 py + px), tile half p & 1, lane L: tile 32 (p & 1) + (L & 31),
+  // conv_wino_eligible); piece p = wave * GI + i: patch position p / NG
+  // (= 4 py + px), tile group p % NG, lane L: tile 32 (p % NG) + (L & 31),
   // channel quad L >> 5 (a pixel's two quads are one 32-byte access). A
   // padding tap or a tile past the end has an out-of-range offset (zeros).
   // An item past the end (the prefetch after a block's last item) reads
@@ -160,8 +168,8 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
     it.rf = live ? ru : rnil;
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int p = wave * GI + i, pos = p >> 1, py = pos >> 2, px = pos & 3;
-      const int64_t t = it.t0 + (p & 1) * 32 + r32;
+      const int p = wave * GI + i, pos = p / NG, py = pos >> 2, px = pos & 3;
+      const int64_t t = it.t0 + (p % NG) * 32 + r32;
       const bool tl = t < q.ntiles;
       const uint32_t tc = tl ? (uint32_t)t : 0u;
       const uint32_t qa = fdiv(tc, q.fTW), tx = tc - qa * (uint32_t)q.TW;
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
       it.ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
     }
   };
-  // stage kt -> slot kt & 1: input [pos][th][quad][32 tiles][16 B], filter [xi][quad][oc][16 B]
+  // stage kt -> slot kt & 1: input [pos][group][quad][32 tiles][16 B], filter [xi][quad][oc][16 B]
   auto issue = [&](const Item& it, int kt) __attribute__((always_inline)) {
     char* base = smem + (kt & 1) * STAGE;
     const uint32_t is = (uint32_t)kt * 32u, us = (uint32_t)(it.n0 * 16) + (uint32_t)kt * ustep;
@@ -181,22 +189,24 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
     for (int i = 0; i < GU; ++i) bdma16(it.rf, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
   };
 
-  // ---- fragments: lane (h, r32) holds tile r32 of the wave's 32 and oc r32
-  // of a 32-oc half, channel quad h; MFMA step s takes channel 4h + s.
+  // ---- fragments: lane (h, r32) holds tile r32 of a 32-tile group and oc
+  // r32 of a 32-oc half, channel quad h; MFMA step s takes channel 4h + s.
   // B^T row xr: t = d[ra] + sgn * d[rb]
   const int ra = xr == 0 ? 0 : (xr == 2 ? 2 : 1);
   const int rb = xr == 0 ? 2 : (xr == 1 ? 2 : (xr == 2 ? 1 : 3));
   const float sgn = xr == 1 ? 1.f : -1.f;
-  f32x4 av[4], bv[4][2];
+  f32x4 av[4][MT], bv[4][NT];
   // reads in the order the xi_x columns need them (V_0 = t0 - t2, then t1,
-  // then t3), so the first MFMAs wait for 6 of the 16 reads only
+  // then t3), so the first MFMAs wait for part of the reads only
   auto read = [&](int kt) __attribute__((always_inline)) {
     const char* st = smem + (kt & 1) * STAGE;
-    auto inp = [&](int r, int px) __attribute__((always_inline)) {
-      return *reinterpret_cast<const f32x4*>(st + (((r * 4 + px) * 2 + tp) * 2 + h) * 512 + r32 * 16);
+    auto inp = [&](int r, int px, int m) __attribute__((always_inline)) {
+      return *reinterpret_cast<const f32x4*>(st + (((r * 4 + px) * NG + tp * MT + m) * 2 + h) * 512 + r32 * 16);
     };
-    auto filt = [&](int j, int nh) __attribute__((always_inline)) {
-      bv[j][nh] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + (((4 * xr + j) * 2 + h) * BN + nh * 32 + r32) * 16);
+    auto filt = [&](int j) __attribute__((always_inline)) {
+#pragma unroll
+      for (int nh = 0; nh < NT; ++nh)
+        bv[j][nh] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + (((4 * xr + j) * 2 + h) * BN + nh * 32 + r32) * 16);
     };
     auto tr = [&](f32x4 a, f32x4 b) __attribute__((always_inline)) {
       f32x4 t;
@@ -204,35 +214,43 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
       for (int c = 0; c < 4; ++c) t[c] = __builtin_fmaf(sgn, b[c], a[c]);  // exact a +- b
       return t;
     };
-    const f32x4 t0v = tr(inp(ra, 0), inp(rb, 0));
-    const f32x4 t2v = tr(inp(ra, 2), inp(rb, 2));
-    filt(0, 0);
-    filt(0, 1);
-    av[0] = t0v - t2v;
-    const f32x4 t1v = tr(inp(ra, 1), inp(rb, 1));
-    filt(1, 0);
-    filt(1, 1);
-    filt(2, 0);
-    filt(2, 1);
-    av[1] = t1v + t2v;
-    av[2] = t2v - t1v;
-    const f32x4 t3v = tr(inp(ra, 3), inp(rb, 3));
-    filt(3, 0);
-    filt(3, 1);
-    av[3] = t1v - t3v;
+    f32x4 t1v[MT], t2v[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const f32x4 t0v = tr(inp(ra, 0, m), inp(rb, 0, m));
+      t2v[m] = tr(inp(ra, 2, m), inp(rb, 2, m));
+      av[0][m] = t0v - t2v[m];
+    }
+    filt(0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      t1v[m] = tr(inp(ra, 1, m), inp(rb, 1, m));
+      av[1][m] = t1v[m] + t2v[m];
+      av[2][m] = t2v[m] - t1v[m];
+    }
+    filt(1);
+    filt(2);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const f32x4 t3v = tr(inp(ra, 3, m), inp(rb, 3, m));
+      av[3][m] = t1v[m] - t3v;
+    }
+    filt(3);
   };
 
-  f32x16 acc[4][2];
-  auto mfma_cols = [&](int j0, int j1, const f32x4 (&a)[4], const f32x4 (&b)[4][2]) __attribute__((always_inline)) {
+  f32x16 acc[4][2];  // [xi_x][m * NT + nh]
+  auto mfma_cols = [&](int j0, int j1, const f32x4 (&a)[4][MT], const f32x4 (&b)[4][NT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = j0; j < j1; ++j)
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
-          acc[j][nh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][s], b[j][nh][s], acc[j][nh], 0, 0, 0);
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int nh = 0; nh < NT; ++nh)
+            acc[j][m * NT + nh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][m][s], b[j][nh][s], acc[j][m * NT + nh], 0, 0, 0);
   };
-  f32x4 pa[4], pb[4][2];  // the deferred xi_x = 3 column (only [3] is live)
+  f32x4 pa[4][MT], pb[4][NT];  // the deferred xi_x = 3 column (only [3] is live)
   float* E = reinterpret_cast<float*>(smem + STAGE);
 
   int item = f32core::xcd_remap(blockIdx.x, G);
@@ -244,7 +262,7 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int nh = 0; nh < 2; ++nh) acc[j][nh] = (f32x16){};
+      for (int k2 = 0; k2 < 2; ++k2) acc[j][k2] = (f32x16){};
     // The xi_x = 3 column's MFMAs of stage kt run right after stage kt+1's
     // barrier: they keep the matrix pipe busy while that stage's fragment
     // reads and input transform are in flight.
@@ -256,9 +274,10 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
       if (kt > 0) mfma_cols(3, 4, pa, pb);
       read(kt);
       mfma_cols(0, 3, av, bv);
-      pa[3] = av[3];
-      pb[3][0] = bv[3][0];
-      pb[3][1] = bv[3][1];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) pa[3][m] = av[3][m];
+#pragma unroll
+      for (int nh = 0; nh < NT; ++nh) pb[3][nh] = bv[3][nh];
     }
     mfma_cols(3, 4, pa, pb);
     // the epilogue's per-lane column, its activation and bias (loaded before
@@ -280,19 +299,22 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
     issue(nx, 0);
     // ---- epilogue, one output column px at a time. A^T along x in
     // registers: m'[xr][px] (C/D layout of 32x32x2: oc = 32 nh + (l & 31),
-    // tile = (r & 3) + 8 (r >> 2) + 4 h of the wave's 32); the 4 xi rows
+    // tile = (r & 3) + 8 (r >> 2) + 4 h of a 32-tile group); the 4 xi rows
     // through LDS; A^T along y; bias + activation; float4 stores.
 #pragma unroll
     for (int px = 0; px < 2; ++px) {
 #pragma unroll
-      for (int nh = 0; nh < 2; ++nh)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float m = px == 0 ? (acc[0][nh][r] + acc[1][nh][r]) + acc[2][nh][r]
-                                  : (acc[1][nh][r] - acc[2][nh][r]) - acc[3][nh][r];
-          const int tile = tp * TWV + (r & 3) + 8 * (r >> 2) + 4 * h;
-          E[(xr * T + tile) * EP + 32 * nh + r32] = m;
-        }
+        for (int nh = 0; nh < NT; ++nh)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int k2 = m * NT + nh;
+            const float mv = px == 0 ? (acc[0][k2][r] + acc[1][k2][r]) + acc[2][k2][r]
+                                     : (acc[1][k2][r] - acc[2][k2][r]) - acc[3][k2][r];
+            const int tile = (tp * MT + m) * TWV + (r & 3) + 8 * (r >> 2) + 4 * h;
+            E[(xr * T + tile) * EP + 32 * nh + r32] = mv;
+          }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -537,8 +559,7 @@ std::atomic<int>& wino_state() {
   return v;
 }
 
-// forced variant (-1 auto: persistent blocks, 3: one work item per block, for A/B; the
-// OC <= 32 shapes only run Winograd when a variant is forced)
+// forced variant (-1 auto: persistent blocks, 3: one work item per block, for A/B)
 std::atomic<int>& wino_variant() {
   static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_WINO_TILE");
@@ -549,11 +570,34 @@ std::atomic<int>& wino_variant() {
 
 bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// F(2x2,3x3) oc block: 32 (128 tiles per item) when a 64-wide block would
+// leave at least half of the last block empty (OC <= 32, OC = 96, 160, ...),
+// else 64 (64 tiles). Measured per layer (profiles/r6_wino/layers_bn32.json):
+// Conv2d_2a (OC 32) 4.33 ms direct -> 3.42 ms, Mixed_5x 3x3 OC 96 1.006 ->
+// 0.905 and 1.436 -> 1.284 ms; OC 64 / 192 / 384 lose with 32 (5.51 -> 6.69,
+// 7.26 -> 8.93, 0.92 -> 1.07 ms). TFA_WINO_BN=32/64 (or set_wino_bn) forces one.
+std::atomic<int>& wino_bn_forced() {
+  static std::atomic<int> v([] {
+    const char* e = std::getenv("TFA_WINO_BN");
+    const int b = e ? std::atoi(e) : 0;
+    return (b == 32 || b == 64) ? b : 0;
+  }());
+  return v;
+}
+int wino23_bn(int64_t OC) {
+  const int forced = wino_bn_forced().load();
+  return forced ? forced : ((OC % 64 != 0 && OC % 64 <= 32) ? 32 : 64);
+}
+
 }  // namespace
 
 void set_conv_wino(int on) { wino_state().store(on ? 1 : 0); }
 bool conv_wino_enabled() { return wino_state().load() != 0; }
 void set_wino_tile(int v) { wino_variant().store(v); }
+void set_wino_bn(int bn) {
+  TFA_CHECK(bn == 0 || bn == 32 || bn == 64, "set_wino_bn: 0 (auto), 32 or 64");
+  wino_bn_forced().store(bn);
+}
 
 int64_t conv_wino_ocp(int64_t OC) { return (OC + 63) / 64 * 64; }
 
@@ -614,13 +658,10 @@ bool conv_wino_eligible(const ConvArgs& a) {
   const int kind = conv_wino_kind(a.KH, a.KW, a.sh, a.sw, a.dh, a.dw, a.C, a.OC);
   if (kind == 0) return false;
   if (a.epi.n != 0 || a.act > ACT_RELU6) return false;
-  // a 64-wide oc block on OC <= 32 wastes half the MFMAs: the direct kernels
-  // win there (Conv2d_2a, OC = 32: 78 vs 105 TF/s, profiles/r6_wino/)
-  if (a.OC <= 32 && wino_variant().load() < 0) return false;
   if (!al16p(a.x) || !al16p(a.wino) || (a.bias && !al16p(a.bias))) return false;
   const int64_t tpi = kind == 1 ? ((a.OH + 1) / 2) * ((a.OW + 1) / 2)
                                 : (kind == 2 ? a.OH * ((a.OW + 1) / 2) : ((a.OH + 1) / 2) * a.OW);
-  const int64_t T = kind == 1 ? 64 : 128, ntiles = a.N * tpi;
+  const int64_t T = kind == 1 ? 4096 / wino23_bn(a.OC) : 128, ntiles = a.N * tpi;
   if (ntiles >= (int64_t(1) << 31)) return false;
   // a block's taps lie within (images a block spans + 1) images of its first
   // image: under 2^31 bytes for the input descriptor's 32-bit offsets
@@ -674,8 +715,9 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   g.act = a.act;
   g.batch = 1;
   g.seg = a.seg;
-  const int64_t TB = kind == 1 ? 64 : 128;
-  const int64_t nbt = (q.ntiles + TB - 1) / TB, nbn = (a.OC + 63) / 64;
+  const int bn = kind == 1 ? wino23_bn(a.OC) : 64;
+  const int64_t TB = kind == 1 ? 4096 / bn : 128;
+  const int64_t nbt = (q.ntiles + TB - 1) / TB, nbn = (a.OC + bn - 1) / bn;
   TFA_CHECK(nbt * nbn < (int64_t(1) << 31), "conv_wino: grid too large");
   const int nwork = (int)(nbt * nbn);
   static const int ncu = [] {
@@ -687,8 +729,10 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   }();
   const int per_cu = wino_variant().load() == 3 ? 0 : 1;  // 3: one item per block (no persistence), for A/B
   const int grid = per_cu ? std::min(nwork, ncu) : nwork;
-  if (kind == 1)
-    hipLaunchKernelGGL(wino23_kernel, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  if (kind == 1 && bn == 32)
+    hipLaunchKernelGGL(wino23_kernel<32>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  else if (kind == 1)
+    hipLaunchKernelGGL(wino23_kernel<64>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   else
     hipLaunchKernelGGL(wino27_kernel, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   TFA_LAUNCH_CHECK("conv_wino");

@@ -284,6 +284,7 @@ void conv_wino_filter(int kind, const float* w, int64_t C, int64_t OC, float* u)
 void set_conv_wino(int on);
 bool conv_wino_enabled();
 void set_wino_tile(int v);
+void set_wino_bn(int bn);  // F(2x2,3x3) oc block: 0 auto, 32 or 64
 // image resize, NHWC. mode: 0 legacy (src = dst*scale), 1 align_corners, 2 half_pixel_centers
 struct ResizeArgs {
   int64_t N, H, W, C, OH, OW;

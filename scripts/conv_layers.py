@@ -96,10 +96,8 @@ def main():
              "tile": tile, "tile_dims": None if dims is None else f"{dims[0]}x{dims[1]}",
              "core": None if dims is None else ("g2" if dims[2] == 2 else "round4")}
         # the algorithm that ran: the plan carries a Winograd filter for 3x3 /
-        # 1x7 / 7x1 stride-1 convs; the kernel layer declines OC <= 32 unless
-        # a Winograd variant is forced (conv_wino.hip conv_wino_eligible)
-        wino = "+winograd" in prog.describe([xin[:1].cpu()], True) and _C.conv_wino_enabled() and (
-            oc > 32 or os.environ.get("TFA_WINO_TILE") not in (None, "", "-1"))
+        # 1x7 / 7x1 stride-1 convs (conv_wino.hip conv_wino_eligible)
+        wino = "+winograd" in prog.describe([xin[:1].cpu()], True) and _C.conv_wino_enabled()
         r["algo"] = ("wino_f23" if kh == 3 else "wino_f27") if wino else (
             "direct" if dims is None else f"gemm {r['core']} {r['tile_dims']}")
         if a.vendor:

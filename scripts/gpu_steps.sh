@@ -91,6 +91,7 @@ for s in ${STEPS:-tests}; do
     wsweep) run wsweep 300 python scripts/wino_sweep.py ;;
     wsweep3) TFA_WINO_TILE=3 run wsweep3 300 python scripts/wino_sweep.py ;;
     layers_v2) TFA_WINO_TILE=2 run layers_wino_v2 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v2.json ;;
+    layers_bn32) TFA_WINO_BN=32 run layers_bn32 700 python scripts/conv_layers.py --json gpurun_out/layers_bn32.json ;;
     layers_v0) TFA_WINO_TILE=0 run layers_wino_v0 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v0.json ;;
     steptest) run steptest 300 python -u -m pytest tests/test_gpu_step_timing.py -x -v --timeout 120 --timeout-method thread ;;
     slim) run read_image4k_slim 400 python examples/read_image.py --images 4096 --prep slim ;;

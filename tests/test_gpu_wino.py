@@ -40,10 +40,12 @@ def ref_conv(x, f, pad):
 
 @pytest.fixture
 def variant():
-    def force(v):
+    def force(v, bn=0):
         _C.set_wino_tile(v)
+        _C.set_wino_bn(bn)
     yield force
     _C.set_wino_tile(-1)
+    _C.set_wino_bn(0)
     _C.set_conv_wino(True)
 
 
@@ -90,13 +92,14 @@ def test_wino_matches_fp64_and_gate(variant, geom):
     _, (yd,) = run(g, ["y"], {"x": x})
     _C.set_conv_wino(True)
     err_direct = np.max(np.abs(yd - want) / scale)
-    for v in (0, 3):  # forced (also OC <= 32): persistent blocks, one item per block
-        variant(v)
+    # persistent blocks / one item per block; F(2x2,3x3) with 64- and 32-wide oc blocks
+    for v, bn in ([(0, 64), (3, 64), (0, 32), (3, 32)] if kh == 3 else [(0, 0), (3, 0)]):
+        variant(v, bn)
         _, (y,) = run(g, ["y"], {"x": x})
         assert y.shape == want.shape
         err = np.max(np.abs(y - want) / scale)
-        assert err <= 1e-5, f"variant {v}: {err}"
-        assert err <= 4 * max(err_direct, 1e-7), f"variant {v}: {err} vs direct {err_direct}"
+        assert err <= 1e-5, f"variant {v}/{bn}: {err}"
+        assert err <= 4 * max(err_direct, 1e-7), f"variant {v}/{bn}: {err} vs direct {err_direct}"
         # Winograd really ran (it does not give the direct path's bits)
         assert not np.array_equal(y, yd)
         # deterministic: the same conv gives the same bits
