@@ -683,6 +683,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       d["op"] = r.op;
       d["label"] = r.label;
       d["flops"] = r.flops;
+      d["bytes"] = r.bytes;
       d["ms"] = r.ms;
       out.append(d);
     }

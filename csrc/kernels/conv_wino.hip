@@ -374,17 +374,22 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
 // tiles x 64 oc; 8-channel stages of 48 KB (input [8 pos][4 tq][2 quads][32
 // tiles][16 B], filter [8 xi][2 quads][64 oc][16 B]) in a ring of 3, DMA two
 // stages ahead; persistent blocks prefetch the next item's first stage under
-// the epilogue (as wino23_kernel).
+// the epilogue (as wino23_kernel). BN = 32 (OC = 160 layers: 5 blocks of 32
+// instead of 3 of 64 with the last half empty): 8 waves = 8 tile groups x one
+// 32-oc half = 256 tiles x 32 oc, 72 KB stages in a ring of 2, DMA one stage
+// ahead (as the F(2x2,3x3) kernel).
+template <int BN>
 __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, int nbn, int nwork) {
-  constexpr int T = 128, BN = 64;
+  constexpr int T = 8192 / BN, NQ = T / 32;   // tiles per item, 32-tile groups
   constexpr int IN_BYTES = 8 * 2 * T * 16, U_BYTES = 8 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
-  constexpr int S = 3;
-  constexpr int GI = 4, GU = 2, G = GI + GU;  // DMA pieces per wave per stage (32 + 16 per block)
+  constexpr int S = BN == 64 ? 3 : 2;         // ring depth (DMA S - 1 stages ahead)
+  constexpr int GI = NQ, GU = BN / 32, G = GI + GU;  // DMA pieces per wave per stage
   constexpr int NST = 32;                     // stores per lane per item (unconditional)
+  static_assert(S * STAGE <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int tq = wave & 3, nh = wave >> 2;
+  const int tq = BN == 64 ? (wave & 3) : wave, nh = BN == 64 ? (wave >> 2) : 0;
   const int h = lane >> 5, r32 = lane & 31;
   const int Gd = gridDim.x;
   const int KT = q.KT;
@@ -392,10 +397,11 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
   const float* x = static_cast<const float*>(g.A);
   const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
   const __amdgpu_buffer_rsrc_t rnil = wrsrc(g.B, 0u);
-  // filter piece p = wave * GU + i: (xi, quad) = (p >> 1, p & 1), oc n0 + lane
+  // filter piece p = wave * GU + i covers (xi, quad) rows p * (64 / BN) + lane / BN, oc n0 + lane % BN
   uint32_t uoff[GU];
 #pragma unroll
-  for (int i = 0; i < GU; ++i) uoff[i] = (uint32_t)(((wave * GU + i) * q.OCP + lane) * 16);
+  for (int i = 0; i < GU; ++i)
+    uoff[i] = (uint32_t)((((wave * GU + i) * (64 / BN) + lane / BN) * q.OCP + lane % BN) * 16);
   const uint32_t ustep = (uint32_t)(16 * q.OCP * 16);  // filter bytes per 8-channel stage
 
   auto tile_of = [&](uint32_t tc, uint32_t& n, int& o_h, int& o_w) __attribute__((always_inline)) {
@@ -405,8 +411,8 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
     o_h = dh ? 2 * (int)i0 : (int)i0;   // the tile's first output pixel
     o_w = dh ? (int)i1 : 2 * (int)i1;
   };
-  // input piece p = wave * GI + i: patch position p >> 2, tile quarter p & 3;
-  // lane L: tile 32 (p & 3) + (L & 31), channel quad L >> 5
+  // input piece p = wave * GI + i: patch position p / NQ, tile group p % NQ;
+  // lane L: tile 32 (p % NQ) + (L & 31), channel quad L >> 5
   struct Item {
     int64_t t0;
     int n0;
@@ -423,8 +429,8 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
     it.rf = live ? ru : rnil;
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int p = wave * GI + i, pos = p >> 2;
-      const int64_t t = it.t0 + (p & 3) * 32 + r32;
+      const int p = wave * GI + i, pos = p / NQ;
+      const int64_t t = it.t0 + (p % NQ) * 32 + r32;
       const bool tl = t < q.ntiles;
       uint32_t n;
       int oh, ow;
@@ -451,7 +457,7 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
     f32x4 d[8];
 #pragma unroll
     for (int p = 0; p < 8; ++p)
-      d[p] = *reinterpret_cast<const f32x4*>(st + (((p * 4 + tq) * 2 + h) * 512) + r32 * 16);
+      d[p] = *reinterpret_cast<const f32x4*>(st + (((p * NQ + tq) * 2 + h) * 512) + r32 * 16);
 #pragma unroll
     for (int xi = 0; xi < 8; ++xi)
       bv[xi] = *reinterpret_cast<const f32x4*>(st + IN_BYTES + ((xi * 2 + h) * BN + nh * 32 + r32) * 16);
@@ -485,12 +491,12 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
   for (bool first = true;; first = false) {
 #pragma unroll
     for (int xi = 0; xi < 8; ++xi) acc[xi] = (f32x16){};
-    if (KT > 1) issue(cur, 1);
+    if (S == 3 && KT > 1) issue(cur, 1);
     for (int kt = 0; kt < KT; ++kt) {
-      // stage kt landed: newer ops that may fly are stage kt+1's DMA and, in
-      // an item's first stage, the previous item's epilogue stores (older
-      // than stage 1's DMA, newer than stage 0's)
-      const bool more = kt + 1 < KT;
+      // stage kt landed: newer ops that may fly are (ring of 3) stage kt+1's
+      // DMA and, in an item's first stage, the previous item's epilogue
+      // stores (older than stage 1's DMA, newer than stage 0's)
+      const bool more = S == 3 && kt + 1 < KT;
       if (kt == 0 && !first) {
         if (more) wwait_vm<NST + G>();
         else wwait_vm<NST>();
@@ -500,7 +506,8 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
         wwait_vm<0>();
       }
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < KT) issue(cur, kt + 2);  // into the slot of stage kt-1, read before this barrier
+      // into the slot of stage kt-1 (ring of 3: kt+2; ring of 2: kt+1), read before this barrier
+      if (kt + S - 1 < KT) issue(cur, kt + S - 1);
       // the last two transform points' MFMAs of stage kt-1 run here, in the
       // shadow of this stage's fragment reads and input transform
       if (kt > 0) mfma_pts(6, 8, pa, pb);
@@ -661,7 +668,7 @@ bool conv_wino_eligible(const ConvArgs& a) {
   if (!al16p(a.x) || !al16p(a.wino) || (a.bias && !al16p(a.bias))) return false;
   const int64_t tpi = kind == 1 ? ((a.OH + 1) / 2) * ((a.OW + 1) / 2)
                                 : (kind == 2 ? a.OH * ((a.OW + 1) / 2) : ((a.OH + 1) / 2) * a.OW);
-  const int64_t T = kind == 1 ? 4096 / wino23_bn(a.OC) : 128, ntiles = a.N * tpi;
+  const int64_t T = (kind == 1 ? 4096 : 8192) / wino23_bn(a.OC), ntiles = a.N * tpi;
   if (ntiles >= (int64_t(1) << 31)) return false;
   // a block's taps lie within (images a block spans + 1) images of its first
   // image: under 2^31 bytes for the input descriptor's 32-bit offsets
@@ -715,8 +722,8 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   g.act = a.act;
   g.batch = 1;
   g.seg = a.seg;
-  const int bn = kind == 1 ? wino23_bn(a.OC) : 64;
-  const int64_t TB = kind == 1 ? 4096 / bn : 128;
+  const int bn = wino23_bn(a.OC);
+  const int64_t TB = kind == 1 ? 4096 / bn : 8192 / bn;
   const int64_t nbt = (q.ntiles + TB - 1) / TB, nbn = (a.OC + bn - 1) / bn;
   TFA_CHECK(nbt * nbn < (int64_t(1) << 31), "conv_wino: grid too large");
   const int nwork = (int)(nbt * nbn);
@@ -733,8 +740,10 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(wino23_kernel<32>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   else if (kind == 1)
     hipLaunchKernelGGL(wino23_kernel<64>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  else if (bn == 32)
+    hipLaunchKernelGGL(wino27_kernel<32>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   else
-    hipLaunchKernelGGL(wino27_kernel, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+    hipLaunchKernelGGL(wino27_kernel<64>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   TFA_LAUNCH_CHECK("conv_wino");
 }
 

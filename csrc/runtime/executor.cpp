@@ -64,7 +64,7 @@ struct RangeGuard {
 std::atomic<bool> g_step_timing{false};
 struct StepRec {
   std::string node, op, label;
-  double flops = 0;
+  double flops = 0, bytes = 0;
   hipEvent_t a = nullptr, b = nullptr;
 };
 std::mutex g_step_mu;
@@ -1625,6 +1625,11 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
       TFA_CHECK(hipEventRecord(rec.b, static_cast<hipStream_t>(stream)) == hipSuccess, "hipEventRecord failed");
       rec.node = g_->node(st.out_node >= 0 ? st.out_node : st.node).name;
       rec.op = nd.op;
+      // the least HBM traffic the step can do: its operands once in, its outputs once out
+      for (auto& t : c.in)
+        if (t.defined()) rec.bytes += static_cast<double>(t.numel()) * t.element_size();
+      for (auto& t : c.out)
+        if (t.defined()) rec.bytes += static_cast<double>(t.numel()) * t.element_size();
       if (st.kind == Step::CONV || st.kind == Step::GEMM) {
         // 2 * output elements * reduction length, summed over sibling outputs
         int64_t outs_n = 0;
@@ -1708,7 +1713,7 @@ std::vector<StepTiming> read_step_timing() {
     TFA_CHECK(hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess, "hipEventElapsedTime failed");
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
-    out.push_back({r.node, r.op, r.label, r.flops, ms});
+    out.push_back({r.node, r.op, r.label, r.flops, r.bytes, ms});
   }
   return out;
 }

@@ -185,7 +185,7 @@ class Program {
 // of the plan that ran); read_step_timing waits for and drains the records
 struct StepTiming {
   std::string node, op, label;
-  double flops;
+  double flops, bytes;  // bytes: operands in + outputs out, once each
   float ms;
 };
 void set_step_timing(bool on);

@@ -92,8 +92,8 @@ def test_wino_matches_fp64_and_gate(variant, geom):
     _, (yd,) = run(g, ["y"], {"x": x})
     _C.set_conv_wino(True)
     err_direct = np.max(np.abs(yd - want) / scale)
-    # persistent blocks / one item per block; F(2x2,3x3) with 64- and 32-wide oc blocks
-    for v, bn in ([(0, 64), (3, 64), (0, 32), (3, 32)] if kh == 3 else [(0, 0), (3, 0)]):
+    # persistent blocks / one item per block; 64- and 32-wide oc blocks
+    for v, bn in [(0, 64), (3, 64), (0, 32), (3, 32)]:
         variant(v, bn)
         _, (y,) = run(g, ["y"], {"x": x})
         assert y.shape == want.shape
