@@ -93,6 +93,8 @@ for s in ${STEPS:-tests}; do
     layers_v2) TFA_WINO_TILE=2 run layers_wino_v2 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v2.json ;;
     layers_bn32) TFA_WINO_BN=32 run layers_bn32 700 python scripts/conv_layers.py --json gpurun_out/layers_bn32.json ;;
     layers_v0) TFA_WINO_TILE=0 run layers_wino_v0 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v0.json ;;
+    kmeans_cfg) run kmeans_cfg 300 python bench/configs.py kmeans ;;
+    gemm_bench) run gemm_bench 600 python scripts/gemm_bench.py --json gpurun_out/gemm_bench.json ;;
     steptest) run steptest 300 python -u -m pytest tests/test_gpu_step_timing.py -x -v --timeout 120 --timeout-method thread ;;
     slim) run read_image4k_slim 400 python examples/read_image.py --images 4096 --prep slim ;;
     # ---- round 6: the executed plan (per-step device time) and one timed window's kernel trace
