@@ -92,9 +92,12 @@ void run_gemm(ExecCtx& c, const at::Tensor& a0, const at::Tensor& b0, bool ta, b
 void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,
                          std::vector<at::Tensor>& outs, const std::vector<int>& acts,
                          const at::Tensor* wino = nullptr);
+// pool2: `out` is the 2x2 / stride-2 VALID max pool of the conv's activated
+// output (planner-fused); the Winograd epilogue pools its own output tiles,
+// any other kernel path runs the conv into a temporary and the pool after it
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
                 int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr,
-                const at::Tensor* wino = nullptr);
+                const at::Tensor* wino = nullptr, bool pool2 = false);
 // MaxPool/AvgPool with a fused bias + activation, into `out` (GPU; `out` may
 // be a channel slice of a concat output)
 void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Tensor* bias, int act,

@@ -126,8 +126,9 @@ void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Ten
 
 // shared with the planner's fused conv epilogue
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
-                int act, at::Tensor& out, const std::vector<EpiStep>* epi, const at::Tensor* wino) {
+                int act, at::Tensor& out, const std::vector<EpiStep>* epi, const at::Tensor* wino, bool pool2) {
   Conv2DGeom g = conv_geom(c.node, x0.sizes().vec(), w0.sizes().vec());
+  TFA_CHECK(!pool2 || (c.gpu && !epi && g.OH % 2 == 0 && g.OW % 2 == 0), "internal: pooled conv step");
   if (!c.gpu) {
     at::Tensor x = x0.permute({0, 3, 1, 2});
     x = at::constant_pad_nd(x, {g.pl, g.pr, g.pt, g.pb}, 0);
@@ -145,6 +146,11 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
   require_gpu_dtype(x0, {at::kFloat}, "Conv2D");
   at::Tensor x = materialize(c, x0), w = materialize(c, w0);
   if (out.numel() == 0) return;
+  if (pool2) {
+    TFA_CHECK(out.dim() == 4 && out.size(0) == g.N && out.size(1) == g.OH / 2 && out.size(2) == g.OW / 2 &&
+                  out.size(3) == g.OC,
+              "internal: pooled conv output shape");
+  }
   k::ConvArgs a;
   a.N = g.N; a.H = g.H; a.W = g.W; a.C = g.C;
   a.KH = g.KH; a.KW = g.KW; a.OC = g.OC; a.OH = g.OH; a.OW = g.OW;
@@ -159,12 +165,31 @@ void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at
             "Conv2D: output must be NHWC-contiguous up to the channel stride");
   a.ldc = out.stride(2);
   if (wino) a.wino = wino_filter_ptr(*wino, g.KH, g.KW, g.C, g.OC);
+  at::Tensor conv_out;  // pool2 without a pooled epilogue: the conv's own output, pooled after
+  if (pool2) {
+    a.pool2 = k::conv2d_pool2_direct(a);
+    if (!a.pool2) {
+      conv_out = c.alloc({g.N, g.OH, g.OW, g.OC}, x.options());
+      a.y = conv_out.data_ptr();
+      a.ldc = g.OC;
+    }
+  }
   at::Tensor work;
   if (size_t ws = k::conv2d_workspace_bytes(DType::F32, a)) {
     work = c.alloc({static_cast<int64_t>(ws)}, x.options().dtype(at::kByte));
     a.workspace = work.data_ptr();
   }
   k::conv2d_nhwc(DType::F32, a, stream_of(c));
+  if (conv_out.defined()) {
+    k::PoolArgs pa;
+    pa.N = g.N; pa.H = g.OH; pa.W = g.OW; pa.C = g.OC; pa.OH = g.OH / 2; pa.OW = g.OW / 2;
+    pa.KH = 2; pa.KW = 2; pa.sh = 2; pa.sw = 2; pa.pad_t = 0; pa.pad_l = 0;
+    pa.is_max = true;
+    pa.x = conv_out.data_ptr();
+    pa.y = out.data_ptr();
+    pa.ldc = out.stride(2) == g.OC ? 0 : out.stride(2);
+    k::pool2d_nhwc(DType::F32, pa, stream_of(c));
+  }
 }
 
 void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias, int act,

@@ -111,7 +111,7 @@ __device__ __attribute__((aligned(16))) float4 kWinoTrash[64];
 // [32 (w >> 2), +32) x 64 oc. BN = 32 (T = 128, OC <= 32 layers such as
 // Inception's Conv2d_2a: no padded oc half): tiles [64 (w >> 2), +64) x 32 oc.
 // Either way acc[xi_x][2] = 4 x 2 32x32 accumulators = 128 registers per lane.
-template <int BN>
+template <int BN, bool POOL>
 __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, int nbn, int nwork) {
   constexpr int T = 4096 / BN, TWV = 32;
   constexpr int NG = T / 32;                   // 32-tile groups per block
@@ -124,7 +124,9 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
   constexpr int SMEM = (2 * STAGE > STAGE + EH_BYTES) ? 2 * STAGE : STAGE + EH_BYTES;  // slot 0 | slot 1 (+ exchange)
   constexpr int LPT = BN / 4, TPP = 64 / LPT;  // epilogue: lanes per tile (float4 of oc), tiles per pass
   constexpr int NPASS = T / 8 / TPP;           // passes over the wave's T/8 tiles
-  constexpr int NST = NPASS * 2 * 2;           // stores per lane per item (unconditional)
+  // stores per lane per item (unconditional): one per (pass, px, py), or with
+  // the fused 2x2 max pool one per pass (the pooled pixel of the 2x2 tile)
+  constexpr int NST = POOL ? NPASS : NPASS * 2 * 2;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -300,7 +302,9 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
     // ---- epilogue, one output column px at a time. A^T along x in
     // registers: m'[xr][px] (C/D layout of 32x32x2: oc = 32 nh + (l & 31),
     // tile = (r & 3) + 8 (r >> 2) + 4 h of a 32-tile group); the 4 xi rows
-    // through LDS; A^T along y; bias + activation; float4 stores.
+    // through LDS; A^T along y; bias + activation; float4 stores (POOL: the
+    // max of the tile's 4 activated outputs, one store at the pooled pixel).
+    float4 pmax[NPASS];
 #pragma unroll
     for (int px = 0; px < 2; ++px) {
 #pragma unroll
@@ -330,19 +334,37 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
         const f32x4 y0 = (e[0] + e[1]) + e[2];
         const f32x4 y1 = (e[1] - e[2]) - e[3];
         const int ow = 2 * (int)tx + px;
+        float4 ov[2];
 #pragma unroll
         for (int py = 0; py < 2; ++py) {
-          const int oh = 2 * (int)ty + py;
           const f32x4 v = py ? y1 : y0;
-          float4 o;
-          o.x = act3(v[0] + bvv.x, cact);
-          o.y = act3(v[1] + bvv.y, cact);
-          o.z = act3(v[2] + bvv.z, cact);
-          o.w = act3(v[3] + bvv.w, cact);
-          const bool ok = tl && colok && ow < q.OW && oh < q.OH && !(q.dbg & 4);
-          const int64_t row = ((int64_t)n * q.OH + oh) * q.OW + ow;
-          float4* dst = ok ? reinterpret_cast<float4*>(cbase + (ok ? row : 0) * cld) : &kWinoTrash[lane];
-          *dst = o;
+          ov[py].x = act3(v[0] + bvv.x, cact);
+          ov[py].y = act3(v[1] + bvv.y, cact);
+          ov[py].z = act3(v[2] + bvv.z, cact);
+          ov[py].w = act3(v[3] + bvv.w, cact);
+        }
+        if constexpr (POOL) {  // OH, OW even: a tile is one whole pooling window
+          const float4 m = make_float4(fmaxf(ov[0].x, ov[1].x), fmaxf(ov[0].y, ov[1].y), fmaxf(ov[0].z, ov[1].z),
+                                       fmaxf(ov[0].w, ov[1].w));
+          if (px == 0) {
+            pmax[ps] = m;
+          } else {
+            const float4 o = make_float4(fmaxf(pmax[ps].x, m.x), fmaxf(pmax[ps].y, m.y), fmaxf(pmax[ps].z, m.z),
+                                         fmaxf(pmax[ps].w, m.w));
+            const bool ok = tl && colok && !(q.dbg & 4);
+            const int64_t row = ((int64_t)n * (q.OH / 2) + ty) * (q.OW / 2) + tx;
+            float4* dst = ok ? reinterpret_cast<float4*>(cbase + (ok ? row : 0) * cld) : &kWinoTrash[lane];
+            *dst = o;
+          }
+        } else {
+#pragma unroll
+          for (int py = 0; py < 2; ++py) {
+            const int oh = 2 * (int)ty + py;
+            const bool ok = tl && colok && ow < q.OW && oh < q.OH && !(q.dbg & 4);
+            const int64_t row = ((int64_t)n * q.OH + oh) * q.OW + ow;
+            float4* dst = ok ? reinterpret_cast<float4*>(cbase + (ok ? row : 0) * cld) : &kWinoTrash[lane];
+            *dst = ov[py];
+          }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -736,10 +758,13 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   }();
   const int per_cu = wino_variant().load() == 3 ? 0 : 1;  // 3: one item per block (no persistence), for A/B
   const int grid = per_cu ? std::min(nwork, ncu) : nwork;
-  if (kind == 1 && bn == 32)
-    hipLaunchKernelGGL(wino23_kernel<32>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
-  else if (kind == 1)
-    hipLaunchKernelGGL(wino23_kernel<64>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  TFA_CHECK(!a.pool2 || kind == 1, "conv_wino: pooled epilogue on F(2x2,3x3) only");
+  if (kind == 1) {
+    TFA_CHECK(!a.pool2 || (a.OH % 2 == 0 && a.OW % 2 == 0 && a.seg.n == 0), "conv_wino: pooled epilogue geometry");
+    auto k23 = bn == 32 ? (a.pool2 ? wino23_kernel<32, true> : wino23_kernel<32, false>)
+                        : (a.pool2 ? wino23_kernel<64, true> : wino23_kernel<64, false>);
+    hipLaunchKernelGGL(k23, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  }
   else if (bn == 32)
     hipLaunchKernelGGL(wino27_kernel<32>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   else

@@ -454,12 +454,27 @@ thread_local const char* t_conv_algo = "";
 }
 const char* last_conv_algo() { return t_conv_algo; }
 
+bool conv2d_pool2_direct(const ConvArgs& a) {
+  if (a.seg.n != 0 || a.OH % 2 != 0 || a.OW % 2 != 0 || a.KH != 3 || a.KW != 3) return false;
+  ConvArgs b = a;
+  b.pool2 = false;
+  if (bf16_candidate(conv_as_gemm(b))) return false;  // the bf16 modes have no pooled epilogue
+  return conv_wino_eligible(b);
+}
+
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
   TFA_CHECK(dt == DType::F32, "conv2d: f32 only");
   TFA_CHECK(a.N > 0 && a.OH > 0 && a.OW > 0 && a.OC > 0, "conv2d: empty output");
   TFA_CHECK(a.H < (1 << 30) && a.W < (1 << 30) && a.C < (1 << 30), "conv2d: dims too large");
   TFA_CHECK(a.H * a.W * a.C < (int64_t(1) << 31), "conv2d: one input image must hold < 2^31 elements");
   GemmArgs g = conv_as_gemm(a);
+  if (a.pool2) {  // conv + 2x2 max pool in the Winograd epilogue
+    TFA_CHECK(conv2d_pool2_direct(a), "conv2d: pooled output without a pooling kernel path");
+    t_conv_algo = "wino_f23+pool2x2";
+    conv_wino_launch(a, s);
+    TFA_LAUNCH_CHECK("conv2d");
+    return;
+  }
   // the bf16 modes have no segmented epilogue: fused sibling convs stay exact f32
   if (a.seg.n == 0 && bf16_candidate(g) && bf16_gemm_eligible(g, true, a.C)) {
     Im2colGeom cg;

@@ -255,9 +255,15 @@ struct ConvArgs {
   // Winograd filter (conv_wino_filter layout) when the planner made one:
   // 3x3 / 1x7 / 7x1 stride-1 convs then run conv_wino.hip unless TFA_CONV_ALGO=direct
   const void* wino = nullptr;
+  // planner-fused 2x2 / stride 2 VALID MaxPool after the conv (and its bias /
+  // activation): y is the pooled [N, OH/2, OW/2] output (ldc as above). Only
+  // where conv2d_pool2_direct says so (the F(2x2,3x3) epilogue pools its own
+  // 2x2 output tiles); run_conv2d falls back to conv + pool otherwise.
+  bool pool2 = false;
 };
 size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a);
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s);
+bool conv2d_pool2_direct(const ConvArgs& a);
 // the kernel family the calling thread's last conv2d_nhwc ran ("wino_f23",
 // "implicit_gemm", "gemm_1x1", "direct", ...): step-timing labels
 const char* last_conv_algo();

@@ -121,6 +121,16 @@ bool pool_fusion_enabled() {
   return on;
 }
 
+// TFA_CONV_POOL_FUSION=0: a 2x2 / stride-2 MaxPool after a Winograd conv
+// stays its own step (A/B of the pooled Winograd epilogue)
+bool conv_pool_fusion_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TFA_CONV_POOL_FUSION");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // transposition flags of MatMul (transpose_a/b) and BatchMatMul (adj_x/y)
 bool gemm_ta(const Node& nd) {
   return nd.op == "MatMul" ? nd.attr_b("transpose_a", false) : nd.attr_b("adj_x", false);
@@ -203,6 +213,7 @@ struct Program::Step {
   // Winograd F(2x2,3x3) filter of this CONV step (plan-made constant slot, or
   // -1): 3x3 stride-1 convs whose filter is a constant (conv_wino.hip)
   int wino_slot = -1;
+  bool pool2 = false;  // CONV: writes the 2x2 / stride-2 max pool of its output (planner-fused MaxPool)
 };
 
 struct Program::Plan {
@@ -1107,6 +1118,76 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
   }
   phase("winograd");
 
+  // ---- 2x2 / stride-2 VALID MaxPool after a Winograd 3x3 conv (VGG's
+  // conv -> bias -> relu -> pool): the F(2x2,3x3) epilogue pools its own 2x2
+  // output tiles and writes only the pooled tensor (the full-size activation
+  // and the pool's read of it never reach HBM). The pool step goes away.
+  if (gpu_plan && k::conv_wino_enabled() && conv_pool_fusion_enabled()) {
+    std::map<int, size_t> reader;  // slot -> the only step reading it (or SIZE_MAX when several)
+    for (size_t i = 0; i < p->steps.size(); ++i) {
+      const Step& st = p->steps[i];
+      std::vector<int> rd = st.in_slots;
+      if (st.bias_slot >= 0) rd.push_back(st.bias_slot);
+      for (auto& e : st.epi)
+        if (e.slot >= 0) rd.push_back(e.slot);
+      for (int sl : rd) {
+        auto it = reader.find(sl);
+        if (it == reader.end()) reader[sl] = i;
+        else if (it->second != i) it->second = SIZE_MAX;
+      }
+    }
+    std::set<int> fetch_set(p->fetch_slots.begin(), p->fetch_slots.end());
+    std::set<size_t> gone;
+    for (size_t i = 0; i < p->steps.size(); ++i) {
+      Step& st = p->steps[i];
+      if (st.kind != Step::CONV || st.wino_slot < 0 || !st.sibs.empty() || !st.epi.empty() || st.alias_slot >= 0 ||
+          st.out_slots.size() != 1 || !(st.out_info[0].shape == st.gemm_shape))
+        continue;
+      const Shape& cs = st.out_info[0].shape;
+      if (cs.rank() != 4 || !cs.fully_known() || cs.dims[1] % 2 || cs.dims[2] % 2) continue;
+      const int oslot = st.out_slots[0];
+      auto rit = reader.find(oslot);
+      if (fetch_set.count(oslot) || rit == reader.end() || rit->second == SIZE_MAX || gone.count(rit->second)) continue;
+      Step& ps = p->steps[rit->second];
+      const Node& pn = g_->node(ps.node);
+      const std::vector<int64_t> two{1, 2, 2, 1};
+      if (ps.kind != Step::OP || pn.op != "MaxPool" || ps.in_slots.size() != 1 || ps.in_slots[0] != oslot ||
+          ps.bias_slot >= 0 || ps.act != 0 || !ps.epi.empty() || ps.out_slots.size() != 1 ||
+          pn.attr_ilist("ksize") != two || pn.attr_ilist("strides") != two ||
+          pn.attr_s("padding", std::string("VALID")) != "VALID" ||
+          pn.attr_s("data_format", std::string("NHWC")) != "NHWC")
+        continue;
+      const at::Tensor* w = nullptr;
+      {
+        auto sc = p->synth_consts.find(st.in_slots[1]);
+        if (sc != p->synth_consts.end()) w = &sc->second;
+        for (auto& cs2 : p->const_slots)
+          if (!w && cs2.first == st.in_slots[1]) {
+            const auto& v = infos[cs2.second.node][cs2.second.index].value;
+            if (v) w = &*v;
+          }
+      }
+      if (!w || w->dim() != 4 || w->size(0) != 3 || w->size(1) != 3) continue;
+      st.pool2 = true;
+      st.out_slots = ps.out_slots;
+      st.out_info = ps.out_info;
+      st.out_node = ps.out_node;
+      st.gemm_shape = ps.out_info[0].shape;
+      st.alias_slot = ps.alias_slot;
+      st.alias_offset = ps.alias_offset;
+      st.alias_info = ps.alias_info;
+      gone.insert(rit->second);
+      ++p->fused;
+    }
+    if (!gone.empty()) {
+      std::vector<Step> steps;
+      for (size_t i = 0; i < p->steps.size(); ++i)
+        if (!gone.count(i)) steps.push_back(std::move(p->steps[i]));
+      p->steps = std::move(steps);
+    }
+  }
+  phase("conv_pool");
+
   // liveness: release each slot after its last reading step (fetches/consts are kept)
   std::vector<int> last(p->nslots, -1);
   for (size_t i = 0; i < p->steps.size(); ++i) {
@@ -1577,7 +1658,8 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
             run_gemm(c, c.in[0], c.in[1], gemm_ta(nd), gemm_tb(nd), bp, st.act, out,
                      epp);
           else
-            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr);
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, out, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr,
+                       st.pool2);
           c.out[0] = out;
         } else {
           at::Tensor out = gpu ? c.alloc_out(0) : at::Tensor();
@@ -1594,7 +1676,8 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
             run_gemm(c, c.in[0], c.in[1], gemm_ta(nd), gemm_tb(nd), bp, st.act,
                      kout, epp);
           else
-            run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr);
+            run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr,
+                       st.pool2);
           c.out[0] = viewed ? kout.reshape(st.out_info[0].shape.dims) : kout;
         }
       } catch (const GraphError& e) {
@@ -1634,6 +1717,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
         // 2 * output elements * reduction length, summed over sibling outputs
         int64_t outs_n = 0;
         for (auto& o : c.out) outs_n += o.numel();
+        if (st.pool2) outs_n *= 4;  // the conv's own outputs, before the fused pool
         int64_t red = 0;
         if (st.kind == Step::CONV) {
           const at::Tensor& f = c.in[1];
@@ -2504,6 +2588,7 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
     }
     if (st.alias_slot >= 0) os << " ->concat-slice@" << st.alias_offset;
     if (st.wino_slot >= 0) os << " +winograd";
+    if (st.pool2) os << " +maxpool2x2";
     if (!st.sibs.empty()) {
       os << " siblings[";
       for (size_t k = 0; k < st.sibs.size(); ++k) {

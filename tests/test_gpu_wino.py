@@ -182,3 +182,45 @@ def test_full_models_top5_identical(model):
         _C.set_conv_wino(True)
     np.testing.assert_array_equal(iw, idd)
     np.testing.assert_allclose(pw, pd, rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("bn", [64, 32])
+@pytest.mark.parametrize("geom", [(4, 28, 28, 64, 128, "SAME"), (3, 14, 18, 32, 96, "SAME"), (2, 16, 12, 16, 32, "VALID")])
+def test_conv_relu_maxpool_fused(variant, geom, bn):
+    """VGG's conv -> bias -> relu -> 2x2/2 max pool: one Winograd step whose
+    epilogue pools its own 2x2 output tiles (`+maxpool2x2` in the plan). Equal
+    bit for bit to the same Winograd conv followed by the pool kernel
+    (TFA-level switch: set_conv_wino(False) gives the exact path + pool, the
+    gate against fp64 as above)."""
+    nb, h, w, c, oc, pad = geom
+    rng = np.random.default_rng(h + w + c)
+    x = rng.uniform(-1, 1, (nb, h, w, c)).astype(np.float32)
+    f = rng.uniform(-1, 1, (3, 3, c, oc)).astype(np.float32)
+    bias = rng.uniform(-1, 1, oc).astype(np.float32)
+
+    def graph(pool):
+        g = tf.Graph()
+        with g.as_default():
+            xi = tf.placeholder(tf.float32, [None, h, w, c], name="x")
+            y = tf.nn.relu(tf.nn.bias_add(tf.nn.conv2d(xi, tf.constant(f), [1, 1, 1, 1], pad), tf.constant(bias)))
+            if pool:
+                y = tf.nn.max_pool(y, [1, 2, 2, 1], [1, 2, 2, 1], "VALID")
+            tf.identity(y, name="y")
+        return g
+    variant(0, bn)
+    prog, (yp,) = run(graph(True), ["y"], {"x": x})
+    assert "+maxpool2x2" in prog.describe([torch.from_numpy(x)], True)
+    _, (yc,) = run(graph(False), ["y"], {"x": x})  # the same Winograd conv, unpooled
+    want = yc.reshape(nb, yc.shape[1] // 2, 2, yc.shape[2] // 2, 2, oc).max(axis=(2, 4))
+    assert yp.shape == want.shape
+    assert np.array_equal(yp, want)
+    ref, scale = ref_conv(x, f, pad)
+    r = np.maximum(ref + bias, 0)
+    r = r.reshape(want.shape[0], want.shape[1], 2, want.shape[2], 2, oc).max(axis=(2, 4))
+    s = (scale + np.abs(bias)).reshape(r.shape[0], r.shape[1], 2, r.shape[2], 2, oc).max(axis=(2, 4))
+    assert np.max(np.abs(yp - r) / s) <= 1e-5
+    # Winograd off: the exact conv, then the pool kernel (run_conv2d's fallback)
+    _C.set_conv_wino(False)
+    _, (yd,) = run(graph(True), ["y"], {"x": x})
+    _C.set_conv_wino(True)
+    assert np.max(np.abs(yd - r) / s) <= 1e-5
