@@ -138,6 +138,7 @@ for s in ${STEPS:-tests}; do
         timeout -s KILL 90 rocprofv3 --pmc $PA --output-format csv -d "$PWD/gpurun_out/lab_pmc/a" -o run -- /tmp/g2_lab 4096 4096 4096 one > gpurun_out/lab_pmc_a.log 2>&1 &&
         timeout -s KILL 90 rocprofv3 --pmc $PB --output-format csv -d "$PWD/gpurun_out/lab_pmc/b" -o run -- /tmp/g2_lab 4096 4096 4096 one > gpurun_out/lab_pmc_b.log 2>&1 || exit 1
       fi ;;
+    tile_table_vgg) run tile_table_vgg 600 python scripts/tile_table.py --add-read-image --out gpurun_out/gfx950.json ;;
     tile_table) run tile_table 1000 python scripts/tile_table.py --out gpurun_out/gfx950.json ;;
     layers_time) run layers_time 700 python scripts/conv_layers.py --json gpurun_out/layers.json ;;
     layers_pmc) run layers_pmc 1150 python scripts/layers_pmc.py --layers scripts/data/inception_layers.json --out gpurun_out/layers_pmc --first ${FIRST:-0} --last ${LAST:-21} ;;

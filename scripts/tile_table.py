@@ -6,6 +6,8 @@ with TFA_GEMM_TUNE_DUMP, which merges that process's autotuner picks into the
 table at exit; run it on the GPU box, then commit the JSON.
 
     python scripts/tile_table.py [--out tensorframes_amd/tiles/gfx950.json]
+    python scripts/tile_table.py --add-read-image   # keep every entry, add the VGG-16
+                                                    # read_image shapes (FC GEMMs)
 """
 import argparse
 import json
@@ -19,8 +21,28 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tensorframes_amd", "tiles", "gfx950.json"))
+    ap.add_argument("--add-read-image", action="store_true",
+                    help="merge the shapes of examples/read_image.py (VGG-16 scoring) into the existing table, "
+                         "tuned with the table's defaults in force (a default moves only on a 2%% win, twice)")
     a = ap.parse_args()
     a.out = os.path.abspath(a.out)
+    if a.add_read_image:
+        import shutil
+        tmp = a.out + ".new"
+        shutil.copyfile(os.path.join(REPO, "tensorframes_amd", "tiles", "gfx950.json"), tmp)  # the shipped table
+        before = len(json.load(open(tmp))["entries"])
+        env = dict(os.environ, TFA_GEMM_TUNE_DUMP=tmp)
+        r = subprocess.run([sys.executable, "examples/read_image.py", "--images", "2048"], cwd=REPO, env=env,
+                           timeout=900)
+        if r.returncode != 0:
+            sys.exit(r.returncode)
+        table = json.load(open(tmp))
+        table["note"] = table.get("note", "") + "; plus the autotuner picks of examples/read_image.py (VGG-16)"
+        with open(a.out, "w") as f:
+            json.dump(table, f, indent=1)
+        os.remove(tmp)
+        print(f"{before} -> {len(table['entries'])} entries -> {a.out}")
+        return
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     tmp = a.out + ".new"
     if os.path.exists(tmp):
