@@ -26,7 +26,9 @@
 #include <map>
 #include <mutex>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <string>
 #include <type_traits>
 
 #include "gemm_f32_core.h"
@@ -96,10 +98,10 @@ constexpr int kTiles[kNumTiles][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}
                                       {256, 256}, {256, 256},
                                       // g2
                                       {256, 256}, {256, 192}, {256, 128}, {256, 64}, {128, 128}, {128, 64},
-                                      {128, 192}, {256, 96}, {128, 160}, {192, 192}};
+                                      {128, 192}, {256, 96}, {128, 160}, {192, 192}, {128, 224}};
 static_assert(g2::kG2Tiles[0][0] == 256 && g2::kG2Tiles[0][1] == 256 && g2::kG2Tiles[5][1] == 64 &&
                   g2::kG2Tiles[6][1] == 192 && g2::kG2Tiles[7][1] == 96 && g2::kG2Tiles[8][1] == 160 &&
-                  g2::kG2Tiles[9][0] == 192,
+                  g2::kG2Tiles[9][0] == 192 && g2::kG2Tiles[10][1] == 224,
               "kTiles' g2 rows mirror kG2Tiles");
 
 // the g2 core's loaders: k-contiguous A (or the vec conv loader), 16-byte
@@ -308,6 +310,10 @@ F32Plan tuned_plan(const F32Plan& heur, const GemmArgs& g0, int al, bool vec, co
   return plan_for(best, g.M, g.N, g.K, g.batch);
 }
 
+namespace {
+thread_local char t_tile_label[48] = "";  // the tile the calling thread's last run_f32 launched
+}
+
 void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream_t s) {
   F32Plan p = plan_f32(g0.M, g0.N, g0.K, g0.batch);
   if (p.cfg >= kFirstG2 && !g2_ok(g0, al, vec))  // a forced g2 tile on a layout it does not load
@@ -320,6 +326,8 @@ void run_f32(const GemmArgs& g0, int al, bool vec, const ConvGeom& cg, hipStream
     g.workspace = nullptr;
   }
   launch_plan(p, g, al, vec, cg, s);
+  std::snprintf(t_tile_label, sizeof(t_tile_label), " %s %dx%d%s", p.cfg >= kFirstG2 ? "g2" : "r4", kTiles[p.cfg][0],
+                kTiles[p.cfg][1], p.splits > 1 ? " split-K" : "");
   if (p.splits > 1) {
     int64_t total = g.batch * g.M * g.N;
     hipLaunchKernelGGL(splitk_reduce, dim3(ew_grid(total)), dim3(256), 0, s, static_cast<const float*>(g.workspace), g,
@@ -425,7 +433,10 @@ size_t conv2d_workspace_bytes(DType dt, const ConvArgs& a) {
   return f32_ws_bytes(g.M, g.N, g.K, 1);
 }
 
+const char* last_f32_tile() { return t_tile_label; }
+
 void gemm(DType dt, const GemmArgs& g, hipStream_t s) {
+  t_tile_label[0] = 0;
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
   TFA_CHECK(g.K > 0, "gemm: K must be > 0");
   TFA_CHECK(g.A && g.B && g.C, "gemm: null operand");
@@ -451,8 +462,14 @@ void gemm(DType dt, const GemmArgs& g, hipStream_t s) {
 
 namespace {
 thread_local const char* t_conv_algo = "";
+thread_local std::string t_conv_label;
 }
-const char* last_conv_algo() { return t_conv_algo; }
+// the family, plus the tile for the implicit-GEMM / 1x1 paths
+const char* last_conv_algo() {
+  t_conv_label = t_conv_algo;
+  if (!std::strcmp(t_conv_algo, "implicit_gemm") || !std::strcmp(t_conv_algo, "gemm_1x1")) t_conv_label += t_tile_label;
+  return t_conv_label.c_str();
+}
 
 bool conv2d_pool2_direct(const ConvArgs& a) {
   if (a.seg.n != 0 || a.OH % 2 != 0 || a.OW % 2 != 0 || a.KH != 3 || a.KW != 3) return false;
@@ -463,6 +480,7 @@ bool conv2d_pool2_direct(const ConvArgs& a) {
 }
 
 void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
+  t_tile_label[0] = 0;
   TFA_CHECK(dt == DType::F32, "conv2d: f32 only");
   TFA_CHECK(a.N > 0 && a.OH > 0 && a.OW > 0 && a.OC > 0, "conv2d: empty output");
   TFA_CHECK(a.H < (1 << 30) && a.W < (1 << 30) && a.C < (1 << 30), "conv2d: dims too large");

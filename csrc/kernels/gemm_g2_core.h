@@ -65,11 +65,15 @@ void launch_conv(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStr
 // accumulators per lane and one block per CU; the smaller ones are sized
 // (<= 256 registers, <= 80 KB of LDS) for two, so one block's prologue and
 // epilogue overlap the other's main loop (K = 512 GEMMs, the convs)
-constexpr int kNumG2Tiles = 10;
+// 128x224 (7 column tiles per wave, two blocks per CU): the fused sibling 1x1
+// convs whose OC sum is 208-224 (Inception Mixed_5b: 64 + 48 + 64 + 32) or 448
+// (= 2 x 224), which 64- / 96- / 128-wide tiles pad by 14-23 %. (A 256x224
+// one-block tile needs 472 bytes of scratch per lane: not shipped.)
+constexpr int kNumG2Tiles = 11;
 constexpr int kG2Tiles[kNumG2Tiles][6] = {
     {256, 256, 2, 2, 4, 1}, {256, 192, 2, 2, 4, 1}, {256, 128, 2, 2, 3, 2}, {256, 64, 4, 1, 4, 2},
     {128, 128, 2, 2, 4, 2}, {128, 64, 2, 2, 5, 2},  {128, 192, 2, 2, 4, 2}, {256, 96, 4, 1, 3, 2},
-    {128, 160, 4, 1, 4, 2}, {192, 192, 2, 2, 3, 2}};
+    {128, 160, 4, 1, 4, 2}, {192, 192, 2, 2, 3, 2}, {128, 224, 4, 1, 3, 2}};
 
 namespace {
 
@@ -493,7 +497,8 @@ void launch_cfg(const F32Plan& p, const GemmArgs& g, const ConvGeom& cg, hipStre
     case 6: TFA_G2(6); break;
     case 7: TFA_G2(7); break;
     case 8: TFA_G2(8); break;
-    default: TFA_G2(9); break;
+    case 9: TFA_G2(9); break;
+    default: TFA_G2(10); break;
   }
 #undef TFA_G2
 }

@@ -267,6 +267,7 @@ bool conv2d_pool2_direct(const ConvArgs& a);
 // the kernel family the calling thread's last conv2d_nhwc ran ("wino_f23",
 // "implicit_gemm", "gemm_1x1", "direct", ...): step-timing labels
 const char* last_conv_algo();
+const char* last_f32_tile();  // " g2 256x64" etc.: the tile of the calling thread's last f32 GEMM / conv ("" if none)
 struct PoolArgs {
   int64_t N, H, W, C, OH, OW, KH, KW, sh, sw, pad_t, pad_l;
   bool is_max;

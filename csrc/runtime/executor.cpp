@@ -1727,7 +1727,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
           red = a.dim() >= 2 ? (gemm_ta(nd) ? a.size(a.dim() - 2) : a.size(a.dim() - 1)) : 0;
         }
         rec.flops = 2.0 * static_cast<double>(outs_n) * static_cast<double>(red);
-        rec.label = st.kind == Step::GEMM ? "gemm" : k::last_conv_algo();
+        rec.label = st.kind == Step::GEMM ? std::string("gemm") + k::last_f32_tile() : std::string(k::last_conv_algo());
         if (!st.sibs.empty()) rec.label += str_cat("+siblings", st.sibs.size());
       } else {
         rec.label = st.kind == Step::FUSED ? "fused" : "op";

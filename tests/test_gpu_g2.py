@@ -42,7 +42,8 @@ def forced():
 
 
 def test_g2_tiles_exist():
-    assert len(G2_TILES) == 10
+    assert len(G2_TILES) == 11
+    assert tuple(_C.gemm_tile_dims(G2_TILES[-1])[:2]) == (128, 224)
 
 
 @pytest.mark.parametrize("tb", [False, True])
