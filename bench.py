@@ -105,6 +105,7 @@ def rank_main(args):
     from tensorframes_amd.frame.block import Block
     from tensorframes_amd.frame.types import ArrayType, FloatType, StructField, StructType
     from tensorframes_amd.parallel import dist
+    from tensorframes_amd.utils.sysinfo import box_id
 
     use_gpu = args.device == "cuda"
     dist.init(backend=None if use_gpu else "gloo")
@@ -242,6 +243,7 @@ def rank_main(args):
             "max_abs_err": err,
             "rank0_numa_bound_cpus": len(numa_cpus),
             "gemm_tiles": _chosen_tiles() if use_gpu else None,
+            "box": box_id(),
         }
         print(json.dumps(out))
     dist.shutdown()

@@ -78,6 +78,8 @@ def emit(d):
         d.setdefault("steps", _ARGS.get("steps"))
         d.setdefault("warmup", _ARGS.get("warmup"))
         d.setdefault("higher_is_better", True)
+        from tensorframes_amd.utils.sysinfo import box_id
+        d.setdefault("box", box_id())
         print(json.dumps(d))
 
 

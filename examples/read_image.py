@@ -69,6 +69,8 @@ def main():
         print(r.image_uri, list(r["index"]), [round(v, 4) for v in r["value"]])
     m = tfs.metrics.snapshot()
     print({k: round(v, 1) for k, v in m.items() if k.startswith("map_rows")})
+    from tensorframes_amd.utils.sysinfo import box_id
+    print("box:", box_id())
 
 
 if __name__ == "__main__":
