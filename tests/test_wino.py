@@ -169,3 +169,35 @@ def test_gpu_plan_carries_winograd_filters_only_for_3x3_stride1():
         assert "+winograd" not in prog.describe([torch.zeros(2, 9, 9, 8)], True)
     finally:
         _C.set_conv_wino(True)
+
+
+def _vgg_block(pool_k=2, extra_reader=False, h=8):
+    rng = np.random.default_rng(1)
+    g = tf.Graph()
+    with g.as_default():
+        x = tf.placeholder(tf.float32, [None, h, h, 8], name="x")
+        y = tf.nn.relu(tf.nn.bias_add(tf.nn.conv2d(x, tf.constant(rng.standard_normal((3, 3, 8, 16)).astype(np.float32)),
+                                                   [1, 1, 1, 1], "SAME"), tf.constant(np.ones(16, np.float32))))
+        p = tf.nn.max_pool(y, [1, pool_k, pool_k, 1], [1, 2, 2, 1], "VALID")
+        out = tf.reduce_sum(p, [1, 2, 3])
+        if extra_reader:
+            out = out + tf.reduce_sum(y, [1, 2, 3])
+        tf.identity(out, name="s")
+    return g
+
+
+def test_plan_fuses_2x2_maxpool_into_the_winograd_conv():
+    """VGG's conv -> bias -> relu -> 2x2/2 max pool becomes one step whose
+    Winograd epilogue pools (the GPU plan, built from host tensors); a 3x3
+    pool, a second reader of the conv output or odd output sizes keep the
+    pool step."""
+    import torch
+
+    def desc(g, h=8):
+        prog = engine.program(g.serialize(), ["s"], ["x"])
+        return prog.describe([torch.zeros(2, h, h, 8)], True)
+    d = desc(_vgg_block())
+    assert "+winograd +maxpool2x2" in d and "MaxPool" not in d.split("+maxpool2x2")[1].split("\n")[0], d
+    assert "+maxpool2x2" not in desc(_vgg_block(pool_k=3))
+    assert "+maxpool2x2" not in desc(_vgg_block(extra_reader=True))
+    assert "+maxpool2x2" not in desc(_vgg_block(h=9), h=9)
