@@ -95,6 +95,7 @@ for s in ${STEPS:-tests}; do
     layers_v0) TFA_WINO_TILE=0 run layers_wino_v0 700 python scripts/conv_layers.py --json gpurun_out/layers_wino_v0.json ;;
     kmeans_cfg) run kmeans_cfg 300 python bench/configs.py kmeans ;;
     gemm_bench) run gemm_bench 600 python scripts/gemm_bench.py --json gpurun_out/gemm_bench.json ;;
+    tune_log) TFA_GEMM_TUNE_LOG=1 run tune_log 600 python bench/configs.py inception --source device --rows 4096 --steps 1 --warmup 1 ;;
     steptest) run steptest 300 python -u -m pytest tests/test_gpu_step_timing.py -x -v --timeout 120 --timeout-method thread ;;
     slim) run read_image4k_slim 400 python examples/read_image.py --images 4096 --prep slim ;;
     # ---- round 6: the executed plan (per-step device time) and one timed window's kernel trace
