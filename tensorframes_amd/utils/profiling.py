@@ -52,17 +52,22 @@ def aggregate(recs: List[dict]) -> List[dict]:
         key = (r["node"], r["op"], r["label"])
         e = by.get(key)
         if e is None:
-            e = by[key] = {"node": r["node"], "op": r["op"], "algo": r["label"], "calls": 0, "ms": 0.0, "flops": 0.0}
+            e = by[key] = {"node": r["node"], "op": r["op"], "algo": r["label"], "calls": 0, "ms": 0.0, "flops": 0.0,
+                           "bytes": 0.0}
             order.append(key)
         e["calls"] += 1
         e["ms"] += float(r["ms"])
         e["flops"] += float(r["flops"])
+        e["bytes"] += float(r.get("bytes", 0.0))
     total = sum(e["ms"] for e in by.values()) or 1.0
     rows = []
     for k in order:
         e = by[k]
         e["share"] = e["ms"] / total
         e["tflops"] = e["flops"] / (e["ms"] * 1e-3) / 1e12 if e["ms"] > 0 and e["flops"] else None
+        # operands + outputs once each over the step's time: a step near the
+        # HBM rate (~5-6 TB/s achievable) is memory-bound, whatever its TF/s
+        e["min_GBps"] = e["bytes"] / (e["ms"] * 1e-3) / 1e9 if e["ms"] > 0 and e["bytes"] else None
         rows.append(e)
     rows.sort(key=lambda e: -e["ms"])
     return rows
@@ -74,9 +79,11 @@ def markdown(rows: List[dict], title: str = "") -> str:
     out = [f"# {title}\n" if title else "",
            f"Sum of step device times: {total:.2f} ms; conv/GEMM FLOPs {flops / 1e12:.2f} T "
            f"({flops / (total * 1e-3) / 1e12 if total else 0:.1f} TFLOP/s over all steps).\n",
-           "| node | op | algorithm | calls | ms | share | TFLOP/s |", "|---|---|---|---:|---:|---:|---:|"]
+           "| node | op | algorithm | calls | ms | share | TFLOP/s | min GB/s |",
+           "|---|---|---|---:|---:|---:|---:|---:|"]
     for e in rows:
         tf = f"{e['tflops']:.1f}" if e["tflops"] else ""
+        bw = f"{e['min_GBps']:.0f}" if e.get("min_GBps") else ""
         out.append(f"| {e['node']} | {e['op']} | {e['algo']} | {e['calls']} | {e['ms']:.3f} | "
-                   f"{100 * e['share']:.1f}% | {tf} |")
+                   f"{100 * e['share']:.1f}% | {tf} | {bw} |")
     return "\n".join(out) + "\n"
