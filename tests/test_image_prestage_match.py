@@ -147,3 +147,59 @@ def test_split_branches_with_different_steps_are_refused():
         r, gc, b = tf.split(x, 3, axis=2)
         x = tf.expand_dims(tf.concat([r - 1.0, gc * 2.0, b - 3.0], 2), 0, name="prepped")
     assert core._match_image_prep(g.serialize(), ["DecodeJpeg"], "prepped", [1, 32, 32, 3]) is None
+
+
+def _shape_graph(variant):
+    """decoded image -> a resize size / crop offset computed with the ops the
+    host evaluator models (half-to-even Round, truncating and flooring
+    integer division, Minimum / Maximum, Select, float64 arithmetic)"""
+    g = tf.Graph()
+    with g.as_default():
+        data = tf.placeholder(tf.string, [], name="data")
+        im = tf.image.decode_jpeg(data, channels=3, name="DecodeJpeg")
+        s = tf.shape(im)
+        h, w = s[0], s[1]
+        if variant == "round_half_even":
+            # x.5 cases: 0.5 * odd sizes
+            nh = tf.cast(tf.round(tf.cast(h, tf.float32) * 0.5 + 40.0), tf.int32)
+            nw = tf.cast(tf.round(tf.cast(w, tf.float32) * 0.5 + 40.0), tf.int32)
+        elif variant == "float64_div":
+            hd, wd = tf.cast(h, tf.float64), tf.cast(w, tf.float64)
+            sc = 97.0 / tf.minimum(hd, wd)
+            nh = tf.cast(hd * sc, tf.int32)
+            nw = tf.cast(wd * sc, tf.int32)
+        else:  # integer arithmetic with Maximum and FloorDiv / truncating Div
+            nh = tf.maximum(h // 2, 64) + tf.floordiv(w - h, 7)
+            nw = tf.maximum(w // 2, 64) + tf.div(h - w, 7)  # Div on int32: truncates toward zero
+        nh = tf.identity(tf.maximum(nh, 64), name="new_h")
+        nw = tf.identity(tf.maximum(nw, 64), name="new_w")
+        x = tf.image.resize_bilinear(tf.expand_dims(im, 0), tf.stack([nh, nw]), align_corners=True)
+        x = tf.squeeze(x, [0])
+        oy = tf.identity((nh - 48) // 2, name="off_h")
+        ox = tf.identity((nw - 48) // 2, name="off_w")
+        x = tf.slice(x, tf.stack([oy, ox, 0]), [48, 48, 3])
+        tf.expand_dims(x * (1.0 / 255.0), 0, name="prepped")
+    return g
+
+
+@pytest.mark.parametrize("variant", ["round_half_even", "float64_div", "int_ops"])
+def test_shape_evaluator_matches_cpu_executor(variant):
+    import torch
+
+    from tensorframes_amd import engine
+    g = _shape_graph(variant)
+    p = core._match_image_prep(g.serialize(), ["DecodeJpeg"], "prepped", [1, 48, 48, 3])
+    assert p is not None and p.dyn is not None and p.mode == 1
+    rng = np.random.default_rng(3)
+    hw = np.concatenate([rng.integers(60, 700, (30, 2)), [[61, 61], [63, 701], [99, 100], [301, 77]]]).astype(np.int32)
+    try:
+        got = p.row_params(hw)
+    except image_prep.Unsupported:
+        got = None
+    prog = engine.program(g.serialize(), ["new_h:0", "new_w:0", "off_h:0", "off_w:0"], ["DecodeJpeg"])
+    want = np.array([[int(t.item()) for t in engine.run_program(prog, [torch.zeros((int(H), int(W), 3), dtype=torch.uint8)],
+                                                                  torch.device("cpu"))] for H, W in hw])
+    if got is None:  # a row's crop falls outside its resize: the chunk runs per row
+        assert np.any(want[:, 2] < 0) or np.any(want[:, 3] < 0) or np.any(want[:, 0] - want[:, 2] < 48)
+    else:
+        assert np.array_equal(got, want), (got[:4], want[:4])
