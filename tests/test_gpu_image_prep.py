@@ -197,3 +197,28 @@ def test_slim_scoring_batched_equals_per_row(native):
     for a, b in zip(res[False], res[True]):
         assert a.uri == b.uri
         assert np.array_equal(np.asarray(a["s"]), np.asarray(b["s"]))
+
+
+@pytest.mark.parametrize("variant", ["round_half_even", "float64_div", "int_ops"])
+def test_per_row_align_corners_and_shape_ops_equal_cpu_executor(variant):
+    """Per-row sizes from the host shape evaluator, align_corners resize,
+    a scale step: the ragged kernel against the CPU executor, bit for bit."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_image_prestage_match import _shape_graph
+
+    from tensorframes_amd import core
+    g = _shape_graph(variant)
+    prep = core._match_image_prep(g.serialize(), ["DecodeJpeg"], "prepped", [1, 48, 48, 3])
+    assert prep is not None and prep.dyn is not None
+    rng = np.random.default_rng(11)
+    shapes = [(120, 160), (97, 301), (250, 99), (64, 64), (333, 222)]
+    imgs = [rng.integers(0, 255, (h, w, 3), dtype=np.uint8) for h, w in shapes]
+    got = prep.run(imgs, DEV)
+    assert got is not None
+    got = got.cpu()
+    prog = engine.program(g.serialize(), ["prepped:0"], ["DecodeJpeg"])
+    for i, a in enumerate(imgs):
+        want = engine.run_program(prog, [torch.from_numpy(a)], torch.device("cpu"))[0]
+        assert torch.equal(got[i:i + 1], want), f"{shapes[i]}: max diff {(got[i] - want[0]).abs().max().item()}"
