@@ -113,6 +113,15 @@ class Config:
     # cost more host time than the overlap saves (0.92 -> 1.12 ms/iteration,
     # profiles/r4_validation/kmeans_concurrency.md)
     concurrent_partitions: bool = dataclasses.field(default_factory=lambda: _env("TFA_CONCURRENT_PARTITIONS", False, bool))
+    # large device-resident partitions (each >= concurrent_large_bytes of
+    # input: GPU-bound plans) of one map_blocks run two at a time on two
+    # streams: one partition's kernels fill the CUs the other's kernel tails
+    # leave idle (Inception-v3, 8 x 2048 images: 24.47 -> 25.19 k img/s on one box,
+    # profiles/r6_final/incep_dev_2streams_run*.log vs incep_dev_serial_same_box.log). Peak memory: two plans' activations.
+    concurrent_large_partitions: bool = dataclasses.field(
+        default_factory=lambda: _env("TFA_CONCURRENT_LARGE", True, bool))
+    concurrent_large_bytes: int = dataclasses.field(
+        default_factory=lambda: _env("TFA_CONCURRENT_LARGE_BYTES", 64 << 20, int))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 

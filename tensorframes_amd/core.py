@@ -391,6 +391,7 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
         res: Dict[int, Block] = {}
         host_jobs = []
         dev_jobs = []  # small device-resident partitions: run side by side
+        big_jobs = []  # large device-resident partitions: two at a time
         for pid in sorted(blocks):
             b = blocks[pid]
             if b.nrows == 0:
@@ -401,10 +402,14 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
                 continue
             ins = _dense_inputs(b, feed_cols, "map_blocks")
             on_device = bool(ins) and all(t.is_cuda for t in ins)
-            if on_device and config.concurrent_partitions and \
-                    sum(t.numel() * t.element_size() for t in ins) <= _CONCURRENT_MAX_BYTES and \
+            nbytes = sum(t.numel() * t.element_size() for t in ins)
+            if on_device and config.concurrent_partitions and nbytes <= _CONCURRENT_MAX_BYTES and \
                     len({t.device for t in ins}) == 1:
                 dev_jobs.append((pid, b, ins))
+                continue
+            if on_device and config.concurrent_large_partitions and nbytes >= config.concurrent_large_bytes and \
+                    len({t.device for t in ins}) == 1:
+                big_jobs.append((pid, b, ins))
                 continue
             if on_device or not engine.gpu_available() or not ins:
                 outs = engine.run_program(prog, ins, ins[0].device if on_device else None)
@@ -413,6 +418,18 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
                 res[pid] = _assemble(b, outs, out_meta, trim)
             else:
                 host_jobs.append((pid, b, ins))
+        # large GPU-bound partitions, two at a time (per device)
+        by_dev: Dict[Any, list] = {}
+        for j in big_jobs:
+            by_dev.setdefault(j[2][0].device, []).append(j)
+        for dv, jobs in by_dev.items():
+            if len(jobs) == 1:
+                pid, b, ins = jobs[0]
+                res[pid] = _assemble(b, engine.run_program(prog, ins, dv), out_meta, trim)
+                continue
+            outs_all = engine.run_programs_concurrent(prog, [j[2] for j in jobs], dv, max_streams=2)
+            for (pid, b, _), outs in zip(jobs, outs_all):
+                res[pid] = _assemble(b, outs, out_meta, trim)
         if len(dev_jobs) > 1 and len({j[2][0].device for j in dev_jobs}) == 1:
             outs_all = engine.run_programs_concurrent(prog, [j[2] for j in dev_jobs], dev_jobs[0][2][0].device)
             for (pid, b, _), outs in zip(dev_jobs, outs_all):

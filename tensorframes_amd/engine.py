@@ -375,7 +375,8 @@ def run_program(prog, inputs: List[torch.Tensor], dev: Optional[torch.device] = 
 _side_streams: Dict[int, List[torch.cuda.Stream]] = {}
 
 
-def run_programs_concurrent(prog, inputs_list: List[List[torch.Tensor]], dev: torch.device) -> List[List[torch.Tensor]]:
+def run_programs_concurrent(prog, inputs_list: List[List[torch.Tensor]], dev: torch.device,
+                            max_streams: int = 4) -> List[List[torch.Tensor]]:
     """Several independent runs of one program (the device-resident partitions
     of a map_blocks) issued on up to 4 streams at once, so a GPU that one small
     partition cannot fill runs them side by side (K-Means: 4 partitions of
@@ -388,15 +389,15 @@ def run_programs_concurrent(prog, inputs_list: List[List[torch.Tensor]], dev: to
         # events and pool-block bookkeeping in C++, GIL released
         ins_list = [[t.contiguous() for t in ins] for ins in inputs_list]
         if dev.index is None or dev.index == torch.cuda.current_device():
-            outs = [list(o) for o in prog.run_concurrent(ins_list)]
+            outs = [list(o) for o in prog.run_concurrent(ins_list, max_streams)]
         else:
             with torch.cuda.device(dev):
-                outs = [list(o) for o in prog.run_concurrent(ins_list)]
+                outs = [list(o) for o in prog.run_concurrent(ins_list, max_streams)]
         metrics.add("concurrent_partition_runs", len(inputs_list))
         return outs
     main = torch.cuda.current_stream(dev)
     pool = _side_streams.setdefault(dev.index, [])
-    k = min(len(inputs_list), 4)
+    k = min(len(inputs_list), max_streams)
     while len(pool) < k:
         pool.append(torch.cuda.Stream(dev))
     ready = main.record_event()
