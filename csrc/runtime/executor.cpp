@@ -121,6 +121,15 @@ bool pool_fusion_enabled() {
   return on;
 }
 
+// TFA_PIPE_COMPUTE_STREAMS: compute streams of the chunk pipeline (1 or 2)
+int pipe_compute_streams() {
+  static const int n = [] {
+    const char* e = std::getenv("TFA_PIPE_COMPUTE_STREAMS");
+    return e && e[0] == '1' ? 1 : 2;
+  }();
+  return n;
+}
+
 // TFA_CONV_POOL_FUSION=0: a 2x2 / stride-2 MaxPool after a Winograd conv
 // stays its own step (A/B of the pooled Winograd epilogue)
 bool conv_pool_fusion_enabled() {
@@ -2350,7 +2359,20 @@ int64_t Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inp
     HIP_OK(hipEventRecord(tev[ci][k], s));
   };
   if (timed) tev.assign(chunks.size(), std::array<hipEvent_t, 6>{});
+  // chunks alternate between the caller's compute stream and a second,
+  // persistent one (TFA_PIPE_COMPUTE_STREAMS=1: one): a GPU-bound chunk's
+  // kernel tails are filled by the next chunk's kernels. The second stream
+  // forks from the caller's stream here and joins it at the end.
+  const int ncomp = (pipe_compute_streams() > 1 && chunks.size() > 1) ? 2 : 1;
+  hipStream_t cstr[2] = {compute.stream(), ncomp > 1 ? copy_stream(device, 2) : compute.stream()};
+  hipEvent_t fork_ev = nullptr;
+  if (ncomp > 1) {
+    HIP_OK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(fork_ev, compute.stream()));
+    HIP_OK(hipStreamWaitEvent(cstr[1], fork_ev, 0));
+  }
   for (size_t ci = 0; ci < chunks.size(); ++ci) {
+    const hipStream_t cs = cstr[ci % ncomp];
     const Chunk& ch = chunks[ci];
     const int slot = static_cast<int>(P.next++ % depth);
     // H2D: wait until the compute (and any D2H of outputs aliasing the ring)
@@ -2374,16 +2396,16 @@ int64_t Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inp
     stamp(ci, 1, h2d.stream());
     HIP_OK(hipEventRecord(ev_h2d[slot], h2d.stream()));
     // compute
-    HIP_OK(hipStreamWaitEvent(compute.stream(), ev_h2d[slot], 0));
+    HIP_OK(hipStreamWaitEvent(cs, ev_h2d[slot], 0));
     std::vector<at::Tensor> outs;
-    stamp(ci, 2, compute.stream());
+    stamp(ci, 2, cs);
     {
       RangeGuard rg("chunk_compute");
       auto p = plan_for(dev_in);
-      outs = execute(*p, dev_in, compute.stream());
+      outs = execute(*p, dev_in, cs);
     }
-    stamp(ci, 3, compute.stream());
-    HIP_OK(hipEventRecord(P.ev_comp[slot], compute.stream()));
+    stamp(ci, 3, cs);
+    HIP_OK(hipEventRecord(P.ev_comp[slot], cs));
     // D2H
     HIP_OK(hipStreamWaitEvent(d2h.stream(), P.ev_comp[slot], 0));
     stamp(ci, 4, d2h.stream());
@@ -2404,6 +2426,11 @@ int64_t Program::run_chunked(const std::vector<std::vector<at::Tensor>>& seg_inp
     HIP_OK(hipEventRecord(P.ev_d2h[slot], d2h.stream()));
     P.used[slot] = true;
     stats_.chunks++;
+  }
+  if (ncomp > 1) {  // join: later work on the caller's stream follows every chunk
+    HIP_OK(hipEventRecord(fork_ev, cstr[1]));
+    HIP_OK(hipStreamWaitEvent(compute.stream(), fork_ev, 0));
+    HIP_OK(hipEventDestroy(fork_ev));
   }
   int64_t handle = 0;
   if (wait) {
