@@ -11,6 +11,7 @@ as RCCL collectives.
 """
 from __future__ import annotations
 
+import contextlib
 import functools
 from collections import OrderedDict
 import os
@@ -691,6 +692,7 @@ class _BatchCut:
         self.modes: List[str] = []
         self.image_prep: Optional[_ImagePrep] = None
         self._side: Dict[int, Any] = {}
+        self._alt: Dict[int, Any] = {}
         try:
             self._find()
         except ValueError:
@@ -839,6 +841,11 @@ class _BatchCut:
             if side is None:
                 side = self._side[dev.index] = torch.cuda.Stream(dev)
         step = max(1, int(config.map_rows_batch_rows))
+        alt = None
+        if main is not None and config.concurrent_large_partitions and nrows > step:
+            alt = self._alt.get(dev.index)
+            if alt is None:
+                alt = self._alt[dev.index] = torch.cuda.Stream(dev)
         prep = self.image_prep if (dev.type == "cuda" and config.map_rows_batched_prestage) else None
         native = _native_jpeg(prep, raw)
         nxt = native(0, step) if native is not None else None
@@ -901,14 +908,28 @@ class _BatchCut:
                 t_in += t1 - t0
                 t_pre += time.perf_counter() - t1
             t0 = time.perf_counter()
+            # the batched part of chunk k runs on main (even k) or on a second
+            # stream (odd k): one chunk's kernels fill the CUs the other's
+            # kernel tails leave idle (joined into main after the loop)
+            ps = main
+            if alt is not None and (a // step) % 2 == 1:
+                ps = alt
+                for c in cut:
+                    engine.record_stream(c, alt)
             if side is not None:
-                main.wait_stream(side)
-            outs = engine.run_program(self.post, [engine.cat_rows(cut)], dev)
+                ps.wait_stream(side)
+            with torch.cuda.stream(ps) if ps is not None else contextlib.nullcontext():
+                outs = engine.run_program(self.post, [engine.cat_rows(cut)], dev)
+            if ps is alt and alt is not None:
+                for o in outs:
+                    engine.record_stream(o, main)
             for j, (o, mode) in enumerate(zip(outs, self.modes)):
                 chunks[j].append(o)
                 for k, i in enumerate(rows):
                     per_out[j][i] = o[k] if mode == "index" else o[k:k + 1]
             t_post += time.perf_counter() - t0
+        if alt is not None:
+            main.wait_stream(alt)
         metrics.add("map_rows_batch_cut_rows", nrows)
         # host-side times (launches are asynchronous): row inputs (decode), per-row part, batched part
         metrics.add("map_rows_batch_cut_inputs_ms", t_in * 1e3)
