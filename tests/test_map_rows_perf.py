@@ -43,7 +43,7 @@ def test_map_rows_scalar_rows_close_to_map_blocks_cpu():
         tb, tr = _best(blocks), _best(rows)
     finally:
         tfs.set_config(device="auto")
-    assert tr <= 2.0 * tb + 0.002, (tr, tb)
+    assert tr <= 2.0 * tb + 0.01, (tr, tb)  # (10 ms of slack for a loaded host)
 
 
 def test_row_matmul_lifts_to_one_fused_gemm():
