@@ -97,6 +97,9 @@ for s in ${STEPS:-tests}; do
     gemm_bench) run gemm_bench 600 python scripts/gemm_bench.py --json gpurun_out/gemm_bench.json ;;
     tune_log) TFA_GEMM_TUNE_LOG=1 run tune_log 600 python bench/configs.py inception --source device --rows 4096 --steps 1 --warmup 1 ;;
     incep_serial) TFA_CONCURRENT_LARGE=0 run incep_serial 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
+    bench_ab) for i in 1 2; do
+        run bench_s2_$i 600 python bench.py --steps 5 --warmup 2 &&
+        TFA_PIPE_COMPUTE_STREAMS=1 run bench_s1_$i 600 python bench.py --steps 5 --warmup 2 || exit 1; done ;;
     steptest) run steptest 300 python -u -m pytest tests/test_gpu_step_timing.py -x -v --timeout 120 --timeout-method thread ;;
     slim) run read_image4k_slim 400 python examples/read_image.py --images 4096 --prep slim ;;
     # ---- round 6: the executed plan (per-step device time) and one timed window's kernel trace
