@@ -100,7 +100,7 @@ for s in ${STEPS:-tests}; do
     bench_ab) for i in 1 2; do
         run bench_s2_$i 600 python bench.py --steps 5 --warmup 2 &&
         TFA_PIPE_COMPUTE_STREAMS=1 run bench_s1_$i 600 python bench.py --steps 5 --warmup 2 || exit 1; done ;;
-    steptest) run steptest 300 python -u -m pytest tests/test_gpu_step_timing.py -x -v --timeout 120 --timeout-method thread ;;
+    steptest) run steptest 300 python -u -m pytest tests/test_gpu_step_timing.py tests/test_gpu_overlap.py -x -v --timeout 120 --timeout-method thread ;;
     slim) run read_image4k_slim 400 python examples/read_image.py --images 4096 --prep slim ;;
     # ---- round 6: the executed plan (per-step device time) and one timed window's kernel trace
     layers_exec)
