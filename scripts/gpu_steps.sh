@@ -96,6 +96,7 @@ for s in ${STEPS:-tests}; do
     kmeans_cfg) run kmeans_cfg 300 python bench/configs.py kmeans ;;
     gemm_bench) run gemm_bench 600 python scripts/gemm_bench.py --json gpurun_out/gemm_bench.json ;;
     tune_log) TFA_GEMM_TUNE_LOG=1 run tune_log 600 python bench/configs.py inception --source device --rows 4096 --steps 1 --warmup 1 ;;
+    incep_s3) TFA_CONCURRENT_LARGE_STREAMS=3 run incep_s3 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
     incep_serial) TFA_CONCURRENT_LARGE=0 run incep_serial 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
     bench_ab) for i in 1 2; do
         run bench_s2_$i 600 python bench.py --steps 5 --warmup 2 &&

@@ -122,6 +122,8 @@ class Config:
         default_factory=lambda: _env("TFA_CONCURRENT_LARGE", True, bool))
     concurrent_large_bytes: int = dataclasses.field(
         default_factory=lambda: _env("TFA_CONCURRENT_LARGE_BYTES", 64 << 20, int))
+    concurrent_large_streams: int = dataclasses.field(
+        default_factory=lambda: _env("TFA_CONCURRENT_LARGE_STREAMS", 2, int))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 

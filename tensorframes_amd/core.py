@@ -428,7 +428,8 @@ def _map_blocks_frame(dframe: DataFrame, spec: "GraphSpec", prog, out_schema: St
                 pid, b, ins = jobs[0]
                 res[pid] = _assemble(b, engine.run_program(prog, ins, dv), out_meta, trim)
                 continue
-            outs_all = engine.run_programs_concurrent(prog, [j[2] for j in jobs], dv, max_streams=2)
+            outs_all = engine.run_programs_concurrent(prog, [j[2] for j in jobs], dv,
+                                                      max_streams=max(1, config.concurrent_large_streams))
             for (pid, b, _), outs in zip(jobs, outs_all):
                 res[pid] = _assemble(b, outs, out_meta, trim)
         if len(dev_jobs) > 1 and len({j[2][0].device for j in dev_jobs}) == 1:
