@@ -41,7 +41,7 @@ struct SmallConv {
   FastDivU32 fOW, fOH;
 };
 
-template <int KS, int TN, bool FAST>
+template <int KS, int TN, bool FAST, bool PAD = false>
 __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5, col = lane & 31;
@@ -108,11 +108,26 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
           const uint32_t ow = mm - t * (uint32_t)p.OW;
           const uint32_t n = fdiv(t, p.fOH);
           const uint32_t oh = t - n * (uint32_t)p.OH;
-          const uint32_t ob = (n * HWC + oh * rs + ow * cs) * 4u;
+          if constexpr (PAD) {
+            // padded (SAME) convs: a tap outside the image reads the base
+            // (any valid address) and contributes 0; 32-bit signed offsets
+            const int ih0 = (int)(oh * (uint32_t)p.sh) - p.pt, iw0 = (int)(ow * (uint32_t)p.sw) - p.pl;
+            const int ob = (int)(n * HWC) + (ih0 * p.W + iw0) * p.C;
 #pragma unroll
-          for (int s = 0; s < KS; ++s) {
-            const float v = *reinterpret_cast<const float*>(xb + (ob + tb[s]));
-            a[q][s] = kv[s] ? v : 0.f;
+            for (int s = 0; s < KS; ++s) {
+              const int ih = ih0 + tdy[s], iw = iw0 + tdx[s];
+              const bool inb = kv[s] & ((unsigned)ih < (unsigned)p.H) & ((unsigned)iw < (unsigned)p.W);
+              const uint32_t off = inb ? (uint32_t)(ob * 4 + (int)tb[s]) : 0u;
+              const float v = *reinterpret_cast<const float*>(xb + off);
+              a[q][s] = inb ? v : 0.f;
+            }
+          } else {
+            const uint32_t ob = (n * HWC + oh * rs + ow * cs) * 4u;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+              const float v = *reinterpret_cast<const float*>(xb + (ob + tb[s]));
+              a[q][s] = kv[s] ? v : 0.f;
+            }
           }
         }
         f32x16 acc[2][TN];
@@ -220,13 +235,16 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
 }
 
 template <int KS>
-void launch_ks(const SmallConv& p, int tn, bool fast, hipStream_t s) {
+void launch_ks(const SmallConv& p, int tn, int fast, hipStream_t s) {
   const int64_t groups = (p.M + 31) / 32;
   const int64_t waves = (groups + 1) / 2;
   // enough waves to fill 256 CUs x 8 waves a few times over; grid-stride beyond
   const int64_t blocks = std::min<int64_t>((waves + 3) / 4, 256 * 16);
   const dim3 g((unsigned)blocks), b(256);
-  if (fast) {
+  if (fast == 2) {  // 32-bit offsets, padding taps checked
+    if (tn == 1) hipLaunchKernelGGL((conv_smallc_kernel<KS, 1, true, true>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((conv_smallc_kernel<KS, 2, true, true>), g, b, 0, s, p);
+  } else if (fast) {
     if (tn == 1) hipLaunchKernelGGL((conv_smallc_kernel<KS, 1, true>), g, b, 0, s, p);
     else hipLaunchKernelGGL((conv_smallc_kernel<KS, 2, true>), g, b, 0, s, p);
   } else {
@@ -280,11 +298,15 @@ void conv_smallc_launch(const ConvArgs& a, hipStream_t s) {
     const char* e = std::getenv("TFA_SMALLC_GENERIC");
     return e && e[0] == '1';
   }();
-  // all taps in bounds (VALID-style, no padding) and 32-bit byte offsets
-  const bool fast = !generic && a.pad_t == 0 && a.pad_l == 0 &&
-                    (a.OH - 1) * a.sh + (a.KH - 1) * a.dh <= a.H - 1 &&
-                    (a.OW - 1) * a.sw + (a.KW - 1) * a.dw <= a.W - 1 &&
-                    a.N * a.H * a.W * a.C * 4 < (int64_t(1) << 32) && p.M * p.ldc * 4 < (int64_t(1) << 32);
+  // 32-bit byte offsets (signed: the padded variant's window origins may
+  // be negative); 1 = all taps in bounds (VALID-style), 2 = padding checked
+  const int64_t xbytes = a.N * a.H * a.W * a.C * 4;
+  const bool ysmall = p.M * p.ldc * 4 < (int64_t(1) << 32);
+  const bool inside = a.pad_t == 0 && a.pad_l == 0 && (a.OH - 1) * a.sh + (a.KH - 1) * a.dh <= a.H - 1 &&
+                      (a.OW - 1) * a.sw + (a.KW - 1) * a.dw <= a.W - 1;
+  const int fast = (generic || !ysmall) ? 0
+                   : inside                          ? (xbytes < (int64_t(1) << 32) ? 1 : 0)
+                                                     : (xbytes < (int64_t(1) << 31) ? 2 : 0);
   if (ks <= 4) launch_ks<4>(p, tn, fast, s);
   else if (ks <= 8) launch_ks<8>(p, tn, fast, s);
   else if (ks <= 12) launch_ks<12>(p, tn, fast, s);

@@ -161,6 +161,9 @@ for s in ${STEPS:-tests}; do
     stemx) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run stem_gen_l0 300 python scripts/conv_layers.py --only 0 &&
       run stem_fast_l0 300 python scripts/conv_layers.py --only 0 ;;
+    vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
+      TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
+      run vgg_stem_padfast 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_padfast.json ;;
     headab) for i in 1 2; do
         run head_default_$i 600 python bench.py --steps 3 --warmup 2 &&
         TFA_GEMM_DEFAULTS=scripts/data/gfx950_t19.json run head_t19_$i 600 python bench.py --steps 3 --warmup 2 || exit 1; done ;;

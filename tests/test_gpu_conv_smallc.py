@@ -1,6 +1,7 @@
 """Direct small-reduction conv (csrc/kernels/conv_smallc.hip, KH*KW*C <= 32:
 RGB stems) against the implicit-GEMM core (bitwise: same k order) and an fp64
-host reference of the same op."""
+host reference of the same op. The SAME cases run the padded fast path (32-bit
+offsets, per-tap bounds test), the in-bounds VALID ones the unpadded one."""
 import numpy as np
 import pytest
 import torch
@@ -42,7 +43,7 @@ def conv_ref(x, w, b, stride, pad, dil, relu):
 
 CASES = [  # n, h, w, c, kh, kw, oc, stride, pad, dil, relu
     (8, 37, 41, 3, 3, 3, 32, 2, "VALID", 1, True),    # Inception Conv2d_1a
-    (4, 30, 30, 3, 3, 3, 64, 1, "SAME", 1, True),     # VGG conv1_1
+    (4, 30, 30, 3, 3, 3, 64, 1, "SAME", 1, True),     # VGG conv1_1 (padded fast path)
     (3, 17, 19, 1, 5, 5, 20, 1, "SAME", 1, False),    # odd OC, one channel
     (2, 23, 23, 2, 3, 3, 48, 1, "SAME", 2, True),     # dilation
     (5, 9, 9, 4, 2, 2, 7, 3, "SAME", 1, False),       # stride 3, tiny OC
