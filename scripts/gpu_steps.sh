@@ -161,6 +161,7 @@ for s in ${STEPS:-tests}; do
     stemx) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run stem_gen_l0 300 python scripts/conv_layers.py --only 0 &&
       run stem_fast_l0 300 python scripts/conv_layers.py --only 0 ;;
+    groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
       run vgg_stem_padfast 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_padfast.json ;;
