@@ -813,13 +813,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "Winograd F(2x2,3x3) / F(2,7) for 3x3 / 1x7 / 7x1 stride-1 convs with constant filters (default on; TFA_CONV_ALGO=direct "
         "turns it off). Plans built while it is off carry no Winograd filters.");
   m.def("conv_wino_enabled", [] { return k::conv_wino_enabled(); });
+  m.def("set_wino_5x5", [](bool on) { k::set_wino_5x5(on ? 1 : 0); }, py::arg("on"),
+        "Winograd F(4,5) for 5x5 stride-1 convs in plans made after the call (opt-in)");
   m.def("set_wino_bn", &tfa::k::set_wino_bn, py::arg("bn"), "F(2x2,3x3) oc block: 0 auto (32 for OC <= 32), 32 or 64");
   m.def("set_wino_tile", [](int v) { k::set_wino_tile(v); },
         "force the Winograd kernel variant: -1 auto, 0 = 64 tiles x 64 oc, 1 = 128 tiles x 32 oc");
   m.def("conv_wino_filter", [](const at::Tensor& w) {
           TFA_CHECK(w.dim() == 4 && w.scalar_type() == at::kFloat, "conv_wino_filter: HWIO float32 filter");
           const int kind = k::conv_wino_kind(w.size(0), w.size(1), 1, 1, 1, 1, w.size(2), w.size(3));
-          TFA_CHECK(kind != 0, "conv_wino_filter: 3x3, 1x7 or 7x1 with C % 8 == 0 and OC % 4 == 0");
+          TFA_CHECK(kind != 0, "conv_wino_filter: 3x3, 1x7, 7x1 or 5x5 with C % 8 == 0 and OC % 4 == 0");
           at::Tensor wc = w.cpu().contiguous();
           at::Tensor u = at::empty({k::conv_wino_filter_elems(kind, wc.size(2), wc.size(3))}, wc.options());
           k::conv_wino_filter(kind, wc.data_ptr<float>(), wc.size(2), wc.size(3), u.data_ptr<float>());

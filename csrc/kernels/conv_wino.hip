@@ -65,6 +65,9 @@ struct WinoGeom {
   // is W (axis 0: tile = 2 outputs along W) or H (axis 1)
   int axis, D0, D1;
   FastDivU32 fD0, fD1;
+  // F(4,5) x 5 rows (5x5): k-stage kt = kh * KTC + (8-channel block)
+  int KTC;
+  FastDivU32 fKTC;
   FastDivU32 fTW, fTH;
 };
 
@@ -400,13 +403,27 @@ __global__ __launch_bounds__(512, 1) void wino23_kernel(GemmArgs g, WinoGeom q, 
 // instead of 3 of 64 with the last half empty): 8 waves = 8 tile groups x one
 // 32-oc half = 256 tiles x 32 oc, 72 KB stages in a ring of 2, DMA one stage
 // ahead (as the F(2x2,3x3) kernel).
-template <int BN>
+// ---------------------------------------------------------------- F(4,5)
+// 5x5 convs (Inception-v3 Mixed_5b/c/d branch 1): the same 8 transform points
+// (so the same input transform B^T) give F(4,5) along W: a tile is 4 outputs,
+// its patch 8 inputs, U = G5 g with G5[i][k] = c_i p_i^k (G7's row scales)
+// and A^T = [p_i^j] (j < 4, the inf point in row 3):
+//   Y0 = M0 + ... + M6,  Y1 = (M1 - M2) + 2 (M3 - M4) + (M5 - M6) / 2,
+//   Y2 = (M1 + M2) + 4 (M3 + M4) + (M5 + M6) / 4,
+//   Y3 = (M1 - M2) + 8 (M3 - M4) + (M5 - M6) / 8 + M7.
+// The 5 filter rows are 5 more k blocks of the same accumulation (stage kt =
+// kh * C/8 + channel block reads input row oh - pt + kh): 8 products per 4
+// outputs per filter row instead of 20 (2.5x fewer MFMA FLOPs). tests/test_wino.py
+// checks the matrices exactly; the f32 error gate is tests/test_gpu_wino.py's.
+template <int BN, bool F45 = false>
 __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, int nbn, int nwork) {
   constexpr int T = 8192 / BN, NQ = T / 32;   // tiles per item, 32-tile groups
   constexpr int IN_BYTES = 8 * 2 * T * 16, U_BYTES = 8 * 2 * BN * 16, STAGE = IN_BYTES + U_BYTES;
   constexpr int S = BN == 64 ? 3 : 2;         // ring depth (DMA S - 1 stages ahead)
   constexpr int GI = NQ, GU = BN / 32, G = GI + GU;  // DMA pieces per wave per stage
-  constexpr int NST = 32;                     // stores per lane per item (unconditional)
+  constexpr int NST = F45 ? 64 : 32;          // stores per lane per item (unconditional)
+  // vmcnt saturates at 63: a smaller count only waits longer (in-order counter)
+  constexpr int WFIRST = NST + G < 63 ? NST + G : 63, WST = NST < 63 ? NST : 63;
   static_assert(S * STAGE <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
@@ -415,7 +432,8 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
   const int h = lane >> 5, r32 = lane & 31;
   const int Gd = gridDim.x;
   const int KT = q.KT;
-  const int dh = q.axis, dw = 1 - q.axis;  // the conv axis: H (7x1) or W (1x7)
+  const int dh = F45 ? 0 : q.axis, dw = 1 - dh;  // the conv axis: H (7x1) or W (1x7, 5x5)
+  const uint32_t rowb = (uint32_t)(q.W * q.C * 4);  // F(4,5): bytes per input row
   const float* x = static_cast<const float*>(g.A);
   const __amdgpu_buffer_rsrc_t ru = wrsrc(g.B, (q.dbg & 1) ? 0u : (uint32_t)q.u_bytes);
   const __amdgpu_buffer_rsrc_t rnil = wrsrc(g.B, 0u);
@@ -431,7 +449,7 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
     n = fdiv(qa, q.fD0);
     const uint32_t i0 = qa - n * (uint32_t)q.D0;
     o_h = dh ? 2 * (int)i0 : (int)i0;   // the tile's first output pixel
-    o_w = dh ? (int)i1 : 2 * (int)i1;
+    o_w = dh ? (int)i1 : (F45 ? 4 : 2) * (int)i1;
   };
   // input piece p = wave * GI + i: patch position p / NQ, tile group p % NQ;
   // lane L: tile 32 (p % NQ) + (L & 31), channel quad L >> 5
@@ -440,6 +458,7 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
     int n0;
     __amdgpu_buffer_rsrc_t rin, rf;
     uint32_t ioff[GI];
+    int ihw[F45 ? GI : 1];  // F(4,5): the patch's row at kh = 0 (tile / column out of range: far negative)
   };
   auto setup = [&](int item, bool live, Item& it) __attribute__((always_inline)) {
     const int itc = live ? item : 0;
@@ -458,15 +477,33 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
       int oh, ow;
       tile_of(tl ? (uint32_t)t : 0u, n, oh, ow);
       const int ih = oh - q.pt + pos * dh, iw = ow - q.pl + pos * dw;
-      const bool ok = tl & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
-      it.ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
+      if constexpr (F45) {
+        // row kh is in range iff 0 <= ih + kh < H; the offset at kh = 0 may be
+        // negative (top padding): kept as its 32-bit pattern, + kh rows at issue
+        const bool okw = tl & ((unsigned)iw < (unsigned)q.W);
+        it.ihw[i] = okw ? ih : -(1 << 20);
+        it.ioff[i] = (uint32_t)(int)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16);
+      } else {
+        const bool ok = tl & ((unsigned)ih < (unsigned)q.H) & ((unsigned)iw < (unsigned)q.W);
+        it.ioff[i] = ok ? (uint32_t)((((int64_t)(n - nb0) * q.H + ih) * q.W + iw) * q.C * 4 + h * 16) : kOOB;
+      }
     }
   };
   auto issue = [&](const Item& it, int kt) __attribute__((always_inline)) {
     char* base = smem + (kt % S) * STAGE;
-    const uint32_t is = (uint32_t)kt * 32u, us = (uint32_t)(it.n0 * 16) + (uint32_t)kt * ustep;
+    const uint32_t us = (uint32_t)(it.n0 * 16) + (uint32_t)kt * ustep;
+    if constexpr (F45) {
+      const uint32_t kh = fdiv((uint32_t)kt, q.fKTC), is = ((uint32_t)kt - kh * (uint32_t)q.KTC) * 32u;
 #pragma unroll
-    for (int i = 0; i < GI; ++i) bdma16(it.rin, it.ioff[i], is, base + (wave * GI + i) * 1024);
+      for (int i = 0; i < GI; ++i) {
+        const uint32_t off = (unsigned)(it.ihw[i] + (int)kh) < (unsigned)q.H ? it.ioff[i] + kh * rowb : kOOB;
+        bdma16(it.rin, off, is, base + (wave * GI + i) * 1024);
+      }
+    } else {
+      const uint32_t is = (uint32_t)kt * 32u;
+#pragma unroll
+      for (int i = 0; i < GI; ++i) bdma16(it.rin, it.ioff[i], is, base + (wave * GI + i) * 1024);
+    }
 #pragma unroll
     for (int i = 0; i < GU; ++i) bdma16(it.rf, uoff[i], us, base + IN_BYTES + (wave * GU + i) * 1024);
   };
@@ -520,8 +557,8 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
       // stores (older than stage 1's DMA, newer than stage 0's)
       const bool more = S == 3 && kt + 1 < KT;
       if (kt == 0 && !first) {
-        if (more) wwait_vm<NST + G>();
-        else wwait_vm<NST>();
+        if (more) wwait_vm<WFIRST>();
+        else wwait_vm<WST>();
       } else if (more) {
         wwait_vm<G>();
       } else {
@@ -557,7 +594,30 @@ __global__ __launch_bounds__(512, 1) void wino27_kernel(GemmArgs g, WinoGeom q, 
     issue(nx, 0);
     // ---- epilogue in registers: C/D row r -> tile 32 tq + (r & 3) + 8 (r >> 2) + 4 h
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < 16 && F45; ++r) {
+      const float s12 = acc[1][r] - acc[2][r], s34 = acc[3][r] - acc[4][r], s56 = acc[5][r] - acc[6][r];
+      const float a12 = acc[1][r] + acc[2][r], a34 = acc[3][r] + acc[4][r], a56 = acc[5][r] + acc[6][r];
+      float y[4];
+      y[0] = ((acc[0][r] + a12) + a34) + a56;
+      y[1] = (s12 + 2.f * s34) + 0.5f * s56;
+      y[2] = (a12 + 4.f * a34) + 0.25f * a56;
+      y[3] = ((s12 + 8.f * s34) + 0.125f * s56) + acc[7][r];
+      const int64_t t = cur.t0 + tq * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const bool tl = t < q.ntiles;
+      uint32_t n;
+      int oh, ow;
+      tile_of(tl ? (uint32_t)t : 0u, n, oh, ow);
+      const int64_t row0 = ((int64_t)n * q.OH + oh) * q.OW + ow;
+      const bool ok0 = tl && colok && !(q.dbg & 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool okj = ok0 && ow + j < q.OW;
+        float* pj = okj ? cbase + (okj ? row0 + j : 0) * cld : reinterpret_cast<float*>(&kWinoTrash[lane]) + j;
+        *pj = act3(y[j] + bias, cact);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16 && !F45; ++r) {
       const float y0 = ((((acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r])) + (acc[4][r] + acc[5][r])) + acc[6][r]);
       const float y1 = (((acc[1][r] - acc[2][r]) + 2.f * (acc[3][r] - acc[4][r])) + 0.5f * (acc[5][r] - acc[6][r])) +
                        acc[7][r];
@@ -630,20 +690,36 @@ void set_wino_bn(int bn) {
 
 int64_t conv_wino_ocp(int64_t OC) { return (OC + 63) / 64 * 64; }
 
+// F(4,5) for 5x5 convs: opt-in (TFA_WINO_5X5=1, config.wino_5x5). Its f32
+// error is 5.6e-7 of sum|a*b| on Inception's Mixed_5x b1_5x5, 5.0x the
+// implicit-GEMM path's, above the 4x gate the default-on kernels pass
+// (tests/test_gpu_wino.py). Read by the planner when it makes the filters.
+std::atomic<int>& wino_5x5_state() {
+  static std::atomic<int> v([] {
+    const char* e = std::getenv("TFA_WINO_5X5");
+    return (e && e[0] == '1') ? 1 : 0;
+  }());
+  return v;
+}
+static bool wino_5x5_enabled() { return wino_5x5_state().load() != 0; }
+void set_wino_5x5(int on) { wino_5x5_state().store(on ? 1 : 0); }
+
 int conv_wino_kind(int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t C, int64_t OC) {
   if (sh != 1 || sw != 1 || dh != 1 || dw != 1 || C <= 0 || OC <= 0 || C % 8 != 0 || OC % 4 != 0) return 0;
   if (KH == 3 && KW == 3) return 1;
   if (KH == 1 && KW == 7) return 2;
   if (KH == 7 && KW == 1) return 3;
+  if (KH == 5 && KW == 5 && wino_5x5_enabled()) return 4;
   return 0;
 }
 
 int64_t conv_wino_filter_elems(int kind, int64_t C, int64_t OC) {
-  return (kind == 1 ? 16 : 8) * C * conv_wino_ocp(OC);
+  return (kind == 1 ? 16 : kind == 4 ? 40 : 8) * C * conv_wino_ocp(OC);
 }
 
 // kind 1: U = G g G^T per (c, oc) into [C/8][16 xi][2][OCP][4 c];
-// kinds 2/3: U = G7 g into [C/8][8 xi][2][OCP][4 c]. fp64, rounded once to f32.
+// kinds 2/3: U = G7 g into [C/8][8 xi][2][OCP][4 c]; kind 4 (5x5): U = G5 g
+// per filter row into [5 kh][C/8][8 xi][2][OCP][4 c]. fp64, rounded once to f32.
 void conv_wino_filter(int kind, const float* w, int64_t C, int64_t OC, float* u) {
   static const double G[4][3] = {{1, 0, 0}, {.5, .5, .5}, {.5, -.5, .5}, {0, 0, 1}};
   // F(2,7), points {0, 1, -1, 2, -2, 1/2, -1/2, inf} (rows of G7: tests/test_wino.py)
@@ -671,6 +747,18 @@ void conv_wino_filter(int kind, const float* w, int64_t C, int64_t OC, float* u)
             const double v = t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2];
             u[((((c / 8) * 16 + i * 4 + j) * 2 + (c / 4) % 2) * OCP + o) * 4 + c % 4] = static_cast<float>(v);
           }
+      } else if (kind == 4) {
+        // G5[i][k] = c_i p_i^k = G7[i][k] for the finite points (k < 5); the
+        // inf point takes the last tap
+        for (int kh = 0; kh < 5; ++kh)
+          for (int i = 0; i < 8; ++i) {
+            double v = 0;
+            for (int k = 0; k < 5; ++k) {
+              const double g5 = i == 7 ? (k == 4 ? 1.0 : 0.0) : G7[i][k];
+              v += g5 * w[((kh * 5 + k) * C + c) * OC + o];
+            }
+            u[(((((int64_t)kh * (C / 8) + c / 8) * 8 + i) * 2 + (c / 4) % 2) * OCP + o) * 4 + c % 4] = static_cast<float>(v);
+          }
       } else {
         // HWIO [1][7] or [7][1]: tap k at w[(k * C + c) * OC + o] either way
         for (int i = 0; i < 8; ++i) {
@@ -688,8 +776,10 @@ bool conv_wino_eligible(const ConvArgs& a) {
   if (kind == 0) return false;
   if (a.epi.n != 0 || a.act > ACT_RELU6) return false;
   if (!al16p(a.x) || !al16p(a.wino) || (a.bias && !al16p(a.bias))) return false;
-  const int64_t tpi = kind == 1 ? ((a.OH + 1) / 2) * ((a.OW + 1) / 2)
-                                : (kind == 2 ? a.OH * ((a.OW + 1) / 2) : ((a.OH + 1) / 2) * a.OW);
+  const int64_t tpi = kind == 1   ? ((a.OH + 1) / 2) * ((a.OW + 1) / 2)
+                      : kind == 2 ? a.OH * ((a.OW + 1) / 2)
+                      : kind == 4 ? a.OH * ((a.OW + 3) / 4)
+                                  : ((a.OH + 1) / 2) * a.OW;
   const int64_t T = (kind == 1 ? 4096 : 8192) / wino23_bn(a.OC), ntiles = a.N * tpi;
   if (ntiles >= (int64_t(1) << 31)) return false;
   // a block's taps lie within (images a block spans + 1) images of its first
@@ -715,11 +805,14 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
   q.pt = (int)a.pad_t; q.pl = (int)a.pad_l;
   q.TH = (int)((a.OH + 1) / 2); q.TW = (int)((a.OW + 1) / 2);
   q.OCP = (int)conv_wino_ocp(a.OC);
-  q.KT = (int)(a.C / 8);
   const int kind = conv_wino_kind(a.KH, a.KW, a.sh, a.sw, a.dh, a.dw, a.C, a.OC);
+  q.KTC = (int)(a.C / 8);
+  q.KT = kind == 4 ? 5 * q.KTC : q.KTC;
+  q.fKTC = make_fastdiv((uint32_t)q.KTC);
   q.axis = kind == 3 ? 1 : 0;
-  q.D0 = kind == 2 ? (int)a.OH : q.TH;       // F(2,7): tiles (n, i0, i1) over (D0, D1)
-  q.D1 = kind == 3 ? (int)a.OW : q.TW;
+  // F(2,7) / F(4,5): tiles (n, i0, i1) over (D0, D1)
+  q.D0 = (kind == 2 || kind == 4) ? (int)a.OH : q.TH;
+  q.D1 = kind == 3 ? (int)a.OW : kind == 4 ? (int)((a.OW + 3) / 4) : q.TW;
   q.fD0 = make_fastdiv((uint32_t)q.D0);
   q.fD1 = make_fastdiv((uint32_t)q.D1);
   q.ntiles = kind == 1 ? a.N * q.TH * q.TW : a.N * (int64_t)q.D0 * q.D1;
@@ -765,6 +858,10 @@ void conv_wino_launch(const ConvArgs& a, hipStream_t s) {
                         : (a.pool2 ? wino23_kernel<64, true> : wino23_kernel<64, false>);
     hipLaunchKernelGGL(k23, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   }
+  else if (kind == 4 && bn == 32)
+    hipLaunchKernelGGL((wino27_kernel<32, true>), dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
+  else if (kind == 4)
+    hipLaunchKernelGGL((wino27_kernel<64, true>), dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   else if (bn == 32)
     hipLaunchKernelGGL(wino27_kernel<32>, dim3((unsigned)grid), dim3(512), 0, s, g, q, (int)nbn, nwork);
   else

@@ -505,7 +505,7 @@ void conv2d_nhwc(DType dt, const ConvArgs& a, hipStream_t s) {
     return;
   }
   if (conv_wino_eligible(a)) {  // 3x3 stride 1 with a planner-made Winograd filter
-    t_conv_algo = a.KH == 3 ? "wino_f23" : "wino_f27";
+    t_conv_algo = a.KH == 3 ? "wino_f23" : a.KH == 5 ? "wino_f45" : "wino_f27";
     conv_wino_launch(a, s);
     return;
   }

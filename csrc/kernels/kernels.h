@@ -292,6 +292,7 @@ void set_conv_wino(int on);
 bool conv_wino_enabled();
 void set_wino_tile(int v);
 void set_wino_bn(int bn);  // F(2x2,3x3) oc block: 0 auto, 32 or 64
+void set_wino_5x5(int on);  // F(4,5) for 5x5 convs (opt-in; plans made after the call)
 // image resize, NHWC. mode: 0 legacy (src = dst*scale), 1 align_corners, 2 half_pixel_centers
 struct ResizeArgs {
   int64_t N, H, W, C, OH, OW;

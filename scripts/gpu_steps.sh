@@ -161,6 +161,11 @@ for s in ${STEPS:-tests}; do
     stemx) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run stem_gen_l0 300 python scripts/conv_layers.py --only 0 &&
       run stem_fast_l0 300 python scripts/conv_layers.py --only 0 ;;
+    f45) run f45_tests 400 python -u -m pytest tests/test_gpu_wino.py tests/test_wino.py -x -v --timeout 200 --timeout-method thread &&
+      run incep_dev_no5x5 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_no5x5.json &&
+      TFA_WINO_5X5=1 run incep_dev_f45 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_f45.json &&
+      run incep_dev_no5x5_2 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
+      TFA_WINO_5X5=1 run incep_dev_f45_2 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&

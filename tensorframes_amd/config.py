@@ -124,6 +124,11 @@ class Config:
         default_factory=lambda: _env("TFA_CONCURRENT_LARGE_BYTES", 64 << 20, int))
     concurrent_large_streams: int = dataclasses.field(
         default_factory=lambda: _env("TFA_CONCURRENT_LARGE_STREAMS", 2, int))
+    # Winograd F(4,5) for the 5x5 stride-1 convs (Inception-v3 Mixed_5x b1_5x5:
+    # 2.1x faster per layer, device-resident Inception 25.28 -> 25.88 k img/s,
+    # profiles/r6_f45/). Opt-in: its f32 error (5.6e-7 of sum|a*b|) is 5.0x the
+    # exact path's, above the 4x gate of the default-on Winograd kernels
+    wino_5x5: bool = dataclasses.field(default_factory=lambda: _env("TFA_WINO_5X5", False, bool))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 
@@ -146,6 +151,11 @@ def set_config(**kw):
         _C.set_debug_sync(bool(kw["debug_sync"]))  # read by the executor on every launch
     if "precision" in kw:
         apply_precision()
+    if "wino_5x5" in kw:
+        from ._native import _C
+        from . import engine
+        _C.set_wino_5x5(bool(kw["wino_5x5"]))
+        engine.clear_program_cache()  # plans hold (or lack) the F(4,5) filters
 
 
 PRECISION_MODES = {"f32": 0, "bf16": 1, "bf16x3": 2}

@@ -141,6 +141,84 @@ def test_f27_matrices_from_toom_cook():
                 assert v == (1 if l == j + k else 0), (j, k, l, v)
 
 
+def emulate45(x, u_flat, oc, pad):
+    """The F(4,5) x 5-row kernel's algorithm (the F(2,7) input transform, the
+    4-output A^T, rows accumulated in the transform domain) on a 5x5 conv."""
+    n, h, w, c = x.shape
+    ocp = -(-oc // 64) * 64
+    u = (u_flat.astype(np.float64).reshape(5, c // 8, 8, 2, ocp, 4).transpose(0, 2, 1, 3, 5, 4)
+         .reshape(5, 8, c, ocp)[..., :oc])
+    p = 2 if pad == "SAME" else 0
+    oh, ow = h + 2 * p - 4, w + 2 * p - 4
+    nt = -(-ow // 4)
+    xp = np.zeros((n, h + 2 * p, 4 * nt + 4, c))
+    xp[:, p:p + h, p:p + w] = x
+    y = np.zeros((n, oh, 4 * nt, oc))
+    for t in range(nt):
+        m = [0.0] * 8
+        for kh in range(5):
+            d = [xp[:, kh:kh + oh, 4 * t + q, :] for q in range(8)]
+            v = [None] * 8
+            v[0] = (d[6] - d[0]) + 5.25 * (d[2] - d[4])
+            v[7] = (d[7] - d[1]) + 5.25 * (d[3] - d[5])
+            e1, o1 = (d[2] + d[6]) - 4.25 * d[4], (d[1] + d[5]) - 4.25 * d[3]
+            v[1], v[2] = e1 + o1, e1 - o1
+            e3, o3 = (0.25 * d[2] + d[6]) - 1.25 * d[4], (0.5 * d[1] + 2 * d[5]) - 2.5 * d[3]
+            v[3], v[4] = e3 + o3, e3 - o3
+            e5, o5 = (4 * d[2] + d[6]) - 5 * d[4], (2 * d[1] + 0.5 * d[5]) - 2.5 * d[3]
+            v[5], v[6] = e5 + o5, e5 - o5
+            m = [m[i] + np.einsum("nhc,co->nho", v[i], u[kh, i]) for i in range(8)]
+        s12, s34, s56 = m[1] - m[2], m[3] - m[4], m[5] - m[6]
+        a12, a34, a56 = m[1] + m[2], m[3] + m[4], m[5] + m[6]
+        y[:, :, 4 * t] = m[0] + a12 + a34 + a56
+        y[:, :, 4 * t + 1] = s12 + 2 * s34 + 0.5 * s56
+        y[:, :, 4 * t + 2] = a12 + 4 * a34 + 0.25 * a56
+        y[:, :, 4 * t + 3] = s12 + 8 * s34 + 0.125 * s56 + m[7]
+    return y[:, :, :ow]
+
+
+@pytest.mark.parametrize("pad", ["SAME", "VALID"])
+def test_f45_transform_and_algorithm_match_direct(pad):
+    import torch
+    rng = np.random.default_rng(11)
+    x = rng.uniform(-1, 1, (2, 9, 11, 16))
+    f = rng.uniform(-1, 1, (5, 5, 16, 12)).astype(np.float32)
+    _C.set_wino_5x5(True)  # opt-in kernel (config.wino_5x5)
+    try:
+        u = _C.conv_wino_filter(torch.from_numpy(f)).numpy()
+    finally:
+        _C.set_wino_5x5(False)
+    assert u.shape == (5 * 8 * 16 * 64,)
+    xt = torch.from_numpy(x).permute(0, 3, 1, 2)
+    ft = torch.from_numpy(f.astype(np.float64)).permute(3, 2, 0, 1)
+    p = 2 if pad == "SAME" else 0
+    want = torch.nn.functional.conv2d(xt, ft, padding=p).permute(0, 2, 3, 1).numpy()
+    scale = torch.nn.functional.conv2d(xt.abs(), ft.abs(), padding=p).permute(0, 2, 3, 1).numpy()
+    got = emulate45(x, u, 12, pad)
+    assert got.shape == want.shape
+    assert np.max(np.abs(got - want) / (scale + 1)) < 1e-6
+
+
+def test_f45_matrices_from_toom_cook():
+    """F(4,5) on the F(2,7) points: the kernel's B^T, its 4-row A^T and the
+    host's G5 (G7's first 5 columns, inf row on the last tap) reproduce 1-D
+    correlation exactly."""
+    from fractions import Fraction as F
+    pts = [0, 1, -1, 2, -2, F(1, 2), F(-1, 2)]
+    scale = [-1, F(-2, 9), F(-2, 9), F(1, 90), F(1, 90), F(32, 45), F(32, 45)]
+    G5 = [[scale[i] * F(pts[i]) ** k for k in range(5)] for i in range(7)] + [[0, 0, 0, 0, 1]]
+    BT = [[-1, 0, F(21, 4), 0, F(-21, 4), 0, 1, 0], [0, 1, 1, F(-17, 4), F(-17, 4), 1, 1, 0],
+          [0, -1, 1, F(17, 4), F(-17, 4), -1, 1, 0], [0, F(1, 2), F(1, 4), F(-5, 2), F(-5, 4), 2, 1, 0],
+          [0, F(-1, 2), F(1, 4), F(5, 2), F(-5, 4), -2, 1, 0], [0, 2, 4, F(-5, 2), -5, F(1, 2), 1, 0],
+          [0, -2, 4, F(5, 2), -5, F(-1, 2), 1, 0], [0, -1, 0, F(21, 4), 0, F(-21, 4), 0, 1]]
+    AT = [[F(pts[i]) ** j for i in range(7)] + [1 if j == 3 else 0] for j in range(4)]
+    for j in range(4):
+        for k in range(5):
+            for l in range(8):
+                v = sum(F(AT[j][i]) * F(G5[i][k]) * F(BT[i][l]) for i in range(8))
+                assert v == (1 if l == j + k else 0), (j, k, l, v)
+
+
 def _inception_like_graph():
     rng = np.random.default_rng(0)
     g = tf.Graph()
@@ -201,3 +279,19 @@ def test_plan_fuses_2x2_maxpool_into_the_winograd_conv():
     assert "+maxpool2x2" not in desc(_vgg_block(pool_k=3))
     assert "+maxpool2x2" not in desc(_vgg_block(extra_reader=True))
     assert "+maxpool2x2" not in desc(_vgg_block(h=9), h=9)
+
+
+def test_config_wino_5x5_switch():
+    """config.wino_5x5 (opt-in) turns the 5x5 kind on for plans made after it."""
+    import torch
+    import tensorframes_amd as tfs
+    f = torch.zeros((5, 5, 8, 8))
+    with pytest.raises(Exception):
+        _C.conv_wino_filter(f)
+    tfs.set_config(wino_5x5=True)
+    try:
+        assert _C.conv_wino_filter(f).numel() == 5 * 8 * 8 * 64
+    finally:
+        tfs.set_config(wino_5x5=False)
+    with pytest.raises(Exception):
+        _C.conv_wino_filter(f)
