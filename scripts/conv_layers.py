@@ -98,7 +98,7 @@ def main():
         # the algorithm that ran: the plan carries a Winograd filter for 3x3 /
         # 1x7 / 7x1 stride-1 convs (conv_wino.hip conv_wino_eligible)
         wino = "+winograd" in prog.describe([xin[:1].cpu()], True) and _C.conv_wino_enabled()
-        r["algo"] = ("wino_f23" if kh == 3 else "wino_f27") if wino else (
+        r["algo"] = ("wino_f23" if kh == 3 else "wino_f45" if kh == 5 else "wino_f27") if wino else (
             "direct" if dims is None else f"gemm {r['core']} {r['tile_dims']}")
         if a.vendor:
             import torch.nn.functional as F
