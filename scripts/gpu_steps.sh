@@ -167,6 +167,11 @@ for s in ${STEPS:-tests}; do
       run incep_dev_no5x5_2 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
       TFA_WINO_5X5=1 run incep_dev_f45_2 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
     vgg_serial) TFA_CONCURRENT_LARGE=0 run vgg_serial 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_serial.json ;;
+    prio_ab) for i in 1 2; do for pr in 0 1; do
+        TFA_WINO_PRIO=$pr run prio${pr}_l4_$i 200 python scripts/conv_layers.py --only 4 --iters 20 &&
+        TFA_WINO_PRIO=$pr run prio${pr}_l2_$i 200 python scripts/conv_layers.py --only 2 --iters 20 &&
+        TFA_WINO_PRIO=$pr run prio${pr}_l9_$i 200 python scripts/conv_layers.py --only 9 --iters 20 || exit 1; done; done
+      grep -h '"layer"' gpurun_out/prio*_l*.log | cut -c1-200 ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
