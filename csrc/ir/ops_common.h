@@ -95,9 +95,13 @@ void run_conv2d_siblings(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0,
 // pool2: `out` is the 2x2 / stride-2 VALID max pool of the conv's activated
 // output (planner-fused); the Winograd epilogue pools its own output tiles,
 // any other kernel path runs the conv into a temporary and the pool after it
+// pool_in (planner-fused MaxPool -> 1x1 conv): x0 is the pool's input and
+// pool_in = {kh, kw, sh, sw} its VALID window; the conv reads the pooled values
+// without the pooled tensor reaching HBM (kernels/conv_smallc.hip), or, where
+// that kernel does not apply, pools into a temporary first
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
                 int act, at::Tensor& out, const std::vector<EpiStep>* epi = nullptr,
-                const at::Tensor* wino = nullptr, bool pool2 = false);
+                const at::Tensor* wino = nullptr, bool pool2 = false, const int* pool_in = nullptr);
 // MaxPool/AvgPool with a fused bias + activation, into `out` (GPU; `out` may
 // be a channel slice of a concat output)
 void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Tensor* bias, int act,

@@ -126,7 +126,46 @@ void run_pool_fused(ExecCtx& c, bool is_max, const at::Tensor& x0, const at::Ten
 
 // shared with the planner's fused conv epilogue
 void run_conv2d(ExecCtx& c, const at::Tensor& x0, const at::Tensor& w0, const at::Tensor* bias,
-                int act, at::Tensor& out, const std::vector<EpiStep>* epi, const at::Tensor* wino, bool pool2) {
+                int act, at::Tensor& out, const std::vector<EpiStep>* epi, const at::Tensor* wino, bool pool2,
+                const int* pool_in) {
+  if (pool_in) {
+    TFA_CHECK(c.gpu && !epi && !wino && !pool2 && x0.dim() == 4 && w0.dim() == 4 && w0.size(0) == 1 &&
+                  w0.size(1) == 1,
+              "internal: pooled-input conv step");
+    require_gpu_dtype(x0, {at::kFloat}, "Conv2D");
+    at::Tensor x = materialize(c, x0), w = materialize(c, w0);
+    const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), OC = w.size(3);
+    const int64_t PH = (H - pool_in[0]) / pool_in[2] + 1, PW = (W - pool_in[1]) / pool_in[3] + 1;
+    TFA_CHECK(H >= pool_in[0] && W >= pool_in[1] && w.size(2) == C, "internal: pooled-input conv geometry");
+    TFA_CHECK(out.dim() == 4 && out.size(0) == N && out.size(1) == PH && out.size(2) == PW && out.size(3) == OC &&
+                  out.stride(3) == 1 && out.stride(1) == PW * out.stride(2) && out.stride(0) == PH * out.stride(1),
+              "internal: pooled-input conv output");
+    if (out.numel() == 0) return;
+    const int64_t ldc = out.stride(2);
+    if (pool_in[0] == 3 && pool_in[1] == 3 && k::pool_conv1x1_eligible(N, H, W, C, PH, PW, OC, ldc, act) &&
+        (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0) {
+      k::PoolConvArgs a;
+      a.N = N; a.H = H; a.W = W; a.C = C; a.PH = PH; a.PW = PW;
+      a.pkh = pool_in[0]; a.pkw = pool_in[1]; a.psh = pool_in[2]; a.psw = pool_in[3];
+      a.OC = OC; a.ldc = ldc;
+      a.x = x.data_ptr(); a.w = w.data_ptr(); a.y = out.data_ptr();
+      a.bias = bias ? bias->data_ptr() : nullptr;
+      a.act = act;
+      k::set_last_conv_algo("maxpool3x3+conv1x1");
+      k::pool_conv1x1(a, stream_of(c));
+      return;
+    }
+    at::Tensor pooled = c.alloc({N, PH, PW, C}, x.options());
+    k::PoolArgs pa;
+    pa.N = N; pa.H = H; pa.W = W; pa.C = C; pa.OH = PH; pa.OW = PW;
+    pa.KH = pool_in[0]; pa.KW = pool_in[1]; pa.sh = pool_in[2]; pa.sw = pool_in[3]; pa.pad_t = 0; pa.pad_l = 0;
+    pa.is_max = true;
+    pa.x = x.data_ptr();
+    pa.y = pooled.data_ptr();
+    k::pool2d_nhwc(DType::F32, pa, stream_of(c));
+    run_conv2d(c, pooled, w, bias, act, out);
+    return;
+  }
   Conv2DGeom g = conv_geom(c.node, x0.sizes().vec(), w0.sizes().vec());
   TFA_CHECK(!pool2 || (c.gpu && !epi && g.OH % 2 == 0 && g.OW % 2 == 0), "internal: pooled conv step");
   if (!c.gpu) {

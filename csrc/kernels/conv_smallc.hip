@@ -264,7 +264,187 @@ std::atomic<int>& smallc_state() {
 }
 bool smallc_enabled() { return smallc_state().load() != 0; }
 
+// ---- VALID 3x3 max pool -> 1x1 conv (+ bias + act), one kernel. The 1x1 conv's
+// A element (pixel m, channel k) is the max of the pool window, computed from
+// float4 loads of 4 channels (a lane's k-steps 4j..4j+3 take channels
+// 8j + 4h + 0..3: the same k order as above, so the conv part matches the
+// GEMM cores bitwise); the filter (C x OC, C <= 64) lives in registers.
+struct PoolConv {
+  uint32_t M;  // N * PH * PW output pixels
+  int H, W, C, PH, PW, pkh, pkw, psh, psw, OC;
+  uint32_t ldc;
+  const float* x;
+  const float* w;
+  const float* bias;
+  float* y;
+  int act;
+  FastDivU32 fPW, fPH;
+};
+
+template <int KS, int TN>
+__global__ __launch_bounds__(256) void pool_conv1x1_kernel(PoolConv p) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5, col = lane & 31;
+  float b[KS][TN];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 8 * (s >> 2) + (s & 3) + 4 * h;  // < C = 2 KS
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = 32 * j + col;
+      b[s][j] = n < p.OC ? p.w[k * p.OC + n] : 0.f;
+    }
+  }
+  float bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = 32 * j + col;
+    bv[j] = (p.bias && n < p.OC) ? p.bias[n] : 0.f;
+  }
+  const uint32_t groups = (p.M + 31) / 32;
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t wave0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const char* xb = reinterpret_cast<const char*>(p.x);
+  char* yb = reinterpret_cast<char*>(p.y);
+  const uint32_t rowb = (uint32_t)(p.W * p.C) * 4u, pixb = (uint32_t)p.C * 4u;
+  const uint64_t imgb = (uint64_t)rowb * (uint32_t)p.H;
+  // the group's pooled A tile goes through this wave's LDS rows: the window
+  // loads are coalesced (16 lanes x 16 B cover a 64-channel pixel), the
+  // fragment reads then take a lane's channels 8j + 4h + 0..3 of its pixel
+  constexpr int C = 2 * KS, QPP = C / 4, PPI = 64 / QPP, NIT = 32 / PPI, TP = C + 4;  // TP: row pitch (floats)
+  __shared__ __attribute__((aligned(16))) float tile_all[4][32 * TP];
+  float* tile = tile_all[threadIdx.x >> 6];
+  const int cq = lane % QPP, pr = lane / QPP;
+  auto run = [&](auto act_c) __attribute__((always_inline)) {
+    constexpr int ACT = decltype(act_c)::value;
+    for (uint32_t g0 = wave0; g0 < groups; g0 += nwaves) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int pi = it * PPI + pr;
+        const uint32_t m = g0 * 32 + (uint32_t)pi;
+        const uint32_t mm = m < p.M ? m : 0u;  // pixels past M re-read pixel 0 (never stored)
+        const uint32_t t = fdiv(mm, p.fPW);
+        const uint32_t pw = mm - t * (uint32_t)p.PW;
+        const uint32_t n = fdiv(t, p.fPH);
+        const uint32_t ph = t - n * (uint32_t)p.PH;
+        // VALID pool: every window tap is inside the image; 64-bit image
+        // base, 32-bit offsets inside one image (< 4 GiB: eligible)
+        const char* ib = xb + (uint64_t)n * imgb;
+        const uint32_t ob = ((ph * (uint32_t)p.psh) * (uint32_t)p.W + pw * (uint32_t)p.psw) * pixb + (uint32_t)(16 * cq);
+        float4 v = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) {
+            const float4 u = *reinterpret_cast<const float4*>(ib + (ob + (uint32_t)dy * rowb + (uint32_t)dx * pixb));
+            v.x = fmaxf(v.x, u.x);
+            v.y = fmaxf(v.y, u.y);
+            v.z = fmaxf(v.z, u.z);
+            v.w = fmaxf(v.w, u.w);
+          }
+        *reinterpret_cast<float4*>(&tile[pi * TP + 4 * cq]) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float a[KS];
+#pragma unroll
+      for (int j = 0; j < KS / 4; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(&tile[col * TP + 8 * j + 4 * h]);
+        a[4 * j] = v.x;
+        a[4 * j + 1] = v.y;
+        a[4 * j + 2] = v.z;
+        a[4 * j + 3] = v.w;
+      }
+      // the next group's tile writes wait for these reads (they feed the MFMAs below)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      f32x16 acc[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s][j], acc[j], 0, 0, 0);
+      const uint32_t m0 = g0 * 32 + 4 * h;
+      const bool full = (g0 + 1) * 32 <= p.M;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint32_t nn = 32 * j + col;
+        if (nn >= (uint32_t)p.OC) continue;
+        const uint32_t base = m0 * p.ldc + nn;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          v[r] = acc[j][r] + bv[j];
+          if (ACT == ACT_RELU) v[r] = v[r] > 0.f ? v[r] : 0.f;
+          if (ACT == ACT_RELU6) v[r] = v[r] > 0.f ? (v[r] < 6.f ? v[r] : 6.f) : 0.f;
+        }
+        if (full) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            *reinterpret_cast<float*>(yb + (base + (uint32_t)((r & 3) + 8 * (r >> 2)) * p.ldc) * 4u) = v[r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
+            if (m0 + ro < p.M) *reinterpret_cast<float*>(yb + (base + ro * p.ldc) * 4u) = v[r];
+          }
+        }
+      }
+    }
+  };
+  if (p.act == ACT_RELU) run(std::integral_constant<int, ACT_RELU>{});
+  else if (p.act == ACT_RELU6) run(std::integral_constant<int, ACT_RELU6>{});
+  else run(std::integral_constant<int, ACT_NONE>{});
+}
+
+template <int KS>
+void launch_pool_conv(const PoolConv& p, int tn, hipStream_t s) {
+  const uint32_t groups = (p.M + 31) / 32;
+  const unsigned blocks = std::min<uint32_t>((groups + 3) / 4, 256 * 8);
+  if (tn == 1) hipLaunchKernelGGL((pool_conv1x1_kernel<KS, 1>), dim3(blocks), dim3(256), 0, s, p);
+  else if (tn == 2) hipLaunchKernelGGL((pool_conv1x1_kernel<KS, 2>), dim3(blocks), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((pool_conv1x1_kernel<KS, 3>), dim3(blocks), dim3(256), 0, s, p);
+}
+
 }  // namespace
+
+bool pool_conv1x1_eligible(int64_t N, int64_t H, int64_t W, int64_t C, int64_t PH, int64_t PW, int64_t OC,
+                           int64_t ldc, int act) {
+  return (C == 16 || C == 32 || C == 64) && OC >= 1 && OC <= 96 && ldc >= OC &&
+         (act == ACT_NONE || act == ACT_RELU || act == ACT_RELU6) && H * W * C * 4 < (int64_t(1) << 32) &&
+         N * PH * PW * ldc * 4 < (int64_t(1) << 32) && N * PH * PW > 0;
+}
+
+void pool_conv1x1(const PoolConvArgs& a, hipStream_t s) {
+  TFA_CHECK(pool_conv1x1_eligible(a.N, a.H, a.W, a.C, a.PH, a.PW, a.OC, a.ldc, a.act), "pool_conv1x1: not eligible");
+  TFA_CHECK(a.pkh == 3 && a.pkw == 3 && a.psh >= 1 && a.psw >= 1 && (a.PH - 1) * a.psh + a.pkh <= a.H &&
+                (a.PW - 1) * a.psw + a.pkw <= a.W,
+            "pool_conv1x1: VALID pool geometry");
+  TFA_CHECK((reinterpret_cast<uintptr_t>(a.x) & 15) == 0, "pool_conv1x1: input must be 16-byte aligned");
+  PoolConv p;
+  p.M = (uint32_t)(a.N * a.PH * a.PW);
+  p.H = (int)a.H; p.W = (int)a.W; p.C = (int)a.C; p.PH = (int)a.PH; p.PW = (int)a.PW;
+  p.pkh = (int)a.pkh; p.pkw = (int)a.pkw; p.psh = (int)a.psh; p.psw = (int)a.psw;
+  p.OC = (int)a.OC;
+  p.ldc = (uint32_t)a.ldc;
+  p.x = static_cast<const float*>(a.x);
+  p.w = static_cast<const float*>(a.w);
+  p.bias = static_cast<const float*>(a.bias);
+  p.y = static_cast<float*>(a.y);
+  p.act = a.act;
+  p.fPW = make_fastdiv((uint32_t)a.PW);
+  p.fPH = make_fastdiv((uint32_t)a.PH);
+  const int tn = (int)((a.OC + 31) / 32);
+  if (a.C == 16) launch_pool_conv<8>(p, tn, s);
+  else if (a.C == 32) launch_pool_conv<16>(p, tn, s);
+  else launch_pool_conv<32>(p, tn, s);
+  TFA_LAUNCH_CHECK("maxpool -> conv 1x1");
+}
 
 void set_conv_smallc(int on) { smallc_state().store(on ? 1 : 0); }
 

@@ -464,6 +464,7 @@ namespace {
 thread_local const char* t_conv_algo = "";
 thread_local std::string t_conv_label;
 }
+void set_last_conv_algo(const char* label) { t_conv_algo = label; }  // kernels outside conv2d_nhwc
 // the family, plus the tile for the implicit-GEMM / 1x1 paths
 const char* last_conv_algo() {
   t_conv_label = t_conv_algo;

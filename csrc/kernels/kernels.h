@@ -267,6 +267,7 @@ bool conv2d_pool2_direct(const ConvArgs& a);
 // the kernel family the calling thread's last conv2d_nhwc ran ("wino_f23",
 // "implicit_gemm", "gemm_1x1", "direct", ...): step-timing labels
 const char* last_conv_algo();
+void set_last_conv_algo(const char* label);  // a static string
 const char* last_f32_tile();  // " g2 256x64" etc.: the tile of the calling thread's last f32 GEMM / conv ("" if none)
 struct PoolArgs {
   int64_t N, H, W, C, OH, OW, KH, KW, sh, sw, pad_t, pad_l;
@@ -279,6 +280,17 @@ struct PoolArgs {
   int64_t ldc = 0;             // 0 = C
 };
 void pool2d_nhwc(DType dt, const PoolArgs& a, hipStream_t s);
+// VALID 3x3 max pool (any stride) feeding a 1x1 / stride-1 conv (+ bias + act) in one kernel
+// (conv_smallc.hip): Inception-v3 MaxPool_3a -> Conv2d_3b. The pooled tensor
+// never reaches HBM. x: the pool's NHWC input; w: [C][OC]; y: [N*PH*PW][ldc].
+struct PoolConvArgs {
+  int64_t N, H, W, C, PH, PW, pkh, pkw, psh, psw, OC, ldc;
+  const void* x; const void* w; const void* bias; void* y;
+  int act = 0;
+};
+bool pool_conv1x1_eligible(int64_t N, int64_t H, int64_t W, int64_t C, int64_t PH, int64_t PW, int64_t OC,
+                           int64_t ldc, int act);
+void pool_conv1x1(const PoolConvArgs& a, hipStream_t s);
 // Winograd paths (conv_wino.hip): the planner's shape test (0 none, 1
 // F(2x2,3x3), 2 F(2,7) along W (1x7), 3 F(2,7) along H (7x1)), padded filter
 // width, runtime switch (TFA_CONV_ALGO=direct turns it off) and forced

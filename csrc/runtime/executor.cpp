@@ -130,6 +130,25 @@ int pipe_compute_streams() {
   return n;
 }
 
+// TFA_POOL_CONV_FUSION=1 (or set_pool_conv_fusion(true), for plans made
+// after it): a 3x3 VALID MaxPool feeding only a 1x1 conv runs inside the
+// conv's step. Off by default: on Inception-v3 (MaxPool_3a -> Conv2d_3b,
+// batch 2048) the fused kernel takes 22.0 ms per 8 calls against 18.7 ms for
+// the pool kernel + the 1x1 GEMM (profiles/r6_poolconv/)
+std::atomic<int>& pool_conv_fusion_state() {
+  static std::atomic<int> v([] {
+    const char* e = std::getenv("TFA_POOL_CONV_FUSION");
+    return (e && e[0] == '1') ? 1 : 0;
+  }());
+  return v;
+}
+
+}  // namespace
+
+void set_pool_conv_fusion(bool on) { pool_conv_fusion_state().store(on ? 1 : 0); }
+
+namespace {
+
 // TFA_CONV_POOL_FUSION=0: a 2x2 / stride-2 MaxPool after a Winograd conv
 // stays its own step (A/B of the pooled Winograd epilogue)
 bool conv_pool_fusion_enabled() {
@@ -223,6 +242,8 @@ struct Program::Step {
   // -1): 3x3 stride-1 convs whose filter is a constant (conv_wino.hip)
   int wino_slot = -1;
   bool pool2 = false;  // CONV: writes the 2x2 / stride-2 max pool of its output (planner-fused MaxPool)
+  // CONV 1x1: reads the VALID max pool {kh, kw, sh, sw} of in_slots[0] (planner-fused MaxPool before it)
+  int pool_in[4] = {0, 0, 0, 0};
 };
 
 struct Program::Plan {
@@ -1197,6 +1218,80 @@ std::shared_ptr<Program::Plan> Program::build_plan(const std::vector<at::Tensor>
   }
   phase("conv_pool");
 
+  // ---- 3x3 VALID MaxPool feeding only a 1x1 stride-1 conv (Inception-v3
+  // MaxPool_3a -> Conv2d_3b): the conv reads the pool window maxima straight
+  // from the pool's input (kernels/conv_smallc.hip pool_conv1x1), the pooled
+  // tensor is never written. The pool step goes away.
+  if (gpu_plan && pool_conv_fusion_state().load()) {
+    std::map<int, size_t> reader, producer;
+    for (size_t i = 0; i < p->steps.size(); ++i) {
+      const Step& st = p->steps[i];
+      std::vector<int> rd = st.in_slots;
+      if (st.bias_slot >= 0) rd.push_back(st.bias_slot);
+      for (auto& e : st.epi)
+        if (e.slot >= 0) rd.push_back(e.slot);
+      for (int sl : rd) {
+        auto it = reader.find(sl);
+        if (it == reader.end()) reader[sl] = i;
+        else if (it->second != i) it->second = SIZE_MAX;
+      }
+      for (int sl : st.out_slots) producer[sl] = i;
+    }
+    std::set<int> fetch_set(p->fetch_slots.begin(), p->fetch_slots.end());
+    std::set<size_t> gone;
+    const std::vector<int64_t> one{1, 1, 1, 1};
+    for (size_t i = 0; i < p->steps.size(); ++i) {
+      Step& st = p->steps[i];
+      if (st.kind != Step::CONV || st.wino_slot >= 0 || st.pool2 || !st.sibs.empty() || !st.epi.empty() ||
+          st.in_slots.size() != 2 || st.out_slots.size() != 1 || st.act > k::ACT_RELU6)
+        continue;
+      const Node& nd = g_->node(st.node);
+      if (nd.op != "Conv2D" || nd.attr_s("data_format", std::string("NHWC")) != "NHWC") continue;
+      const auto dil = nd.attr_ilist("dilations", one);
+      if (nd.attr_ilist("strides", one) != one || !(dil == one || dil.empty())) continue;
+      const int xs = st.in_slots[0];
+      auto pit = producer.find(xs);
+      auto rit = reader.find(xs);
+      if (pit == producer.end() || rit == reader.end() || rit->second != i || fetch_set.count(xs) ||
+          gone.count(pit->second))
+        continue;
+      const at::Tensor* w = nullptr;
+      for (auto& cs2 : p->const_slots)
+        if (!w && cs2.first == st.in_slots[1]) {
+          const auto& v = infos[cs2.second.node][cs2.second.index].value;
+          if (v) w = &*v;
+        }
+      if (!w || w->dim() != 4 || w->size(0) != 1 || w->size(1) != 1 || w->scalar_type() != at::kFloat) continue;
+      const int64_t C = w->size(2), OC = w->size(3);
+      if (!(C == 16 || C == 32 || C == 64) || OC > 96) continue;
+      Step& ps = p->steps[pit->second];
+      const Node& pn = g_->node(ps.node);
+      if (ps.kind != Step::OP || pn.op != "MaxPool" || ps.in_slots.size() != 1 || ps.bias_slot >= 0 ||
+          ps.act != 0 || !ps.epi.empty() || ps.out_slots.size() != 1 || ps.alias_slot >= 0 ||
+          pn.attr_s("padding", std::string("VALID")) != "VALID" ||
+          pn.attr_s("data_format", std::string("NHWC")) != "NHWC")
+        continue;
+      const auto ks = pn.attr_ilist("ksize", one), ss = pn.attr_ilist("strides", one);
+      if (ks.size() != 4 || ss.size() != 4 || ks[0] != 1 || ks[3] != 1 || ss[0] != 1 || ss[3] != 1 || ks[1] != 3 ||
+          ks[2] != 3)
+        continue;
+      st.in_slots[0] = ps.in_slots[0];
+      st.pool_in[0] = (int)ks[1];
+      st.pool_in[1] = (int)ks[2];
+      st.pool_in[2] = (int)ss[1];
+      st.pool_in[3] = (int)ss[2];
+      gone.insert(pit->second);
+      ++p->fused;
+    }
+    if (!gone.empty()) {
+      std::vector<Step> steps;
+      for (size_t i = 0; i < p->steps.size(); ++i)
+        if (!gone.count(i)) steps.push_back(std::move(p->steps[i]));
+      p->steps = std::move(steps);
+    }
+  }
+  phase("pool_conv");
+
   // liveness: release each slot after its last reading step (fetches/consts are kept)
   std::vector<int> last(p->nslots, -1);
   for (size_t i = 0; i < p->steps.size(); ++i) {
@@ -1668,7 +1763,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
                      epp);
           else
             run_conv2d(c, c.in[0], c.in[1], bp, st.act, out, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr,
-                       st.pool2);
+                       st.pool2, st.pool_in[0] ? st.pool_in : nullptr);
           c.out[0] = out;
         } else {
           at::Tensor out = gpu ? c.alloc_out(0) : at::Tensor();
@@ -1686,7 +1781,7 @@ std::vector<at::Tensor> Program::execute(Plan& p, const std::vector<at::Tensor>&
                      kout, epp);
           else
             run_conv2d(c, c.in[0], c.in[1], bp, st.act, kout, epp, st.wino_slot >= 0 ? &slots[st.wino_slot] : nullptr,
-                       st.pool2);
+                       st.pool2, st.pool_in[0] ? st.pool_in : nullptr);
           c.out[0] = viewed ? kout.reshape(st.out_info[0].shape.dims) : kout;
         }
       } catch (const GraphError& e) {
@@ -2616,6 +2711,7 @@ std::string Program::describe_plan(const std::vector<at::Tensor>& inputs, bool a
     if (st.alias_slot >= 0) os << " ->concat-slice@" << st.alias_offset;
     if (st.wino_slot >= 0) os << " +winograd";
     if (st.pool2) os << " +maxpool2x2";
+    if (st.pool_in[0]) os << " +maxpool" << st.pool_in[0] << "x" << st.pool_in[1] << "/" << st.pool_in[2] << "-in";
     if (!st.sibs.empty()) {
       os << " siblings[";
       for (size_t k = 0; k < st.sibs.size(); ++k) {

@@ -172,6 +172,11 @@ for s in ${STEPS:-tests}; do
         TFA_WINO_PRIO=$pr run prio${pr}_l2_$i 200 python scripts/conv_layers.py --only 2 --iters 20 &&
         TFA_WINO_PRIO=$pr run prio${pr}_l9_$i 200 python scripts/conv_layers.py --only 9 --iters 20 || exit 1; done; done
       grep -h '"layer"' gpurun_out/prio*_l*.log | cut -c1-200 ;;
+    poolconv) run poolconv_tests 300 python -u -m pytest tests/test_gpu_pool_conv.py tests/test_pool_conv_plan.py tests/test_gpu_conv_smallc.py -x -v --timeout 120 --timeout-method thread &&
+      TFA_POOL_CONV_FUSION=0 TFA_CONCURRENT_LARGE=0 run incep_serial_nopc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_nopc.json &&
+      TFA_CONCURRENT_LARGE=0 run incep_serial_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_pc.json &&
+      TFA_POOL_CONV_FUSION=0 run incep_dev_nopc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
+      run incep_dev_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
