@@ -177,6 +177,11 @@ for s in ${STEPS:-tests}; do
       TFA_CONCURRENT_LARGE=0 run incep_serial_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_pc.json &&
       TFA_POOL_CONV_FUSION=0 run incep_dev_nopc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
       run incep_dev_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
+    smallc_tr) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_smallc.py tests/test_gpu_conv_direct.py -x -q --timeout 120 --timeout-method thread &&
+      for i in 1 2; do for tr in 0 1; do
+        TFA_SMALLC_TR=$tr run tr${tr}_l0_$i 200 python scripts/conv_layers.py --only 0 --iters 20 || exit 1; done; done &&
+      TFA_SMALLC_TR=0 TFA_CONCURRENT_LARGE=0 run vgg_tr0 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_tr0.json &&
+      TFA_CONCURRENT_LARGE=0 run vgg_tr1 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_tr1.json ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
