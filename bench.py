@@ -115,7 +115,10 @@ def rank_main(args):
     # for: N ranks over RCCL. A silent fallback (gloo, or fewer ranks) fails here.
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)")
-    if use_gpu and world > 1 and backend != "nccl":
+    # TFA_BENCH_REHEARSAL=1 (with TFA_DIST_BACKEND=gloo): N ranks sharing one
+    # GPU, where RCCL refuses duplicate devices; the JSON line says so
+    rehearsal = os.environ.get("TFA_BENCH_REHEARSAL") == "1"
+    if use_gpu and world > 1 and backend != "nccl" and not rehearsal:
         raise SystemExit(f"bench.py: GPU job with backend {backend!r}; expected 'nccl' (RCCL over xGMI)")
     if use_gpu:
         assert torch.cuda.is_available(), "bench.py needs a GPU (or --device cpu)"
@@ -245,6 +248,8 @@ def rank_main(args):
             "gemm_tiles": _chosen_tiles() if use_gpu else None,
             "box": box_id(),
         }
+        if rehearsal:
+            out["rehearsal"] = f"{world} ranks sharing one GPU over {backend} (not a multi-GPU number)"
         print(json.dumps(out))
     dist.shutdown()
 
