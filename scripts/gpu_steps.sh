@@ -153,7 +153,6 @@ for s in ${STEPS:-tests}; do
       TFA_PRECISION=bf16x3 run read_image4k_bf16x3 400 python examples/read_image.py --images 4096 ;;
     decode_bench) run decode_bench 300 python scripts/decode_bench.py --images 1024 ;;
     pool) run pool 400 python -u -m pytest tests/test_gpu_pool_accounting.py tests/test_multirank_gpu.py tests/test_gpu_engine.py -x -v --timeout 200 --timeout-method thread ;;
-    lab_g2) run lab_g2 600 bash scripts/lab_g2.sh ;;
     poolb)
       TFA_POOL_GENERIC=1 run pool_generic 300 python scripts/pool_bench.py &&
       TFA_POOL_XCD=0 run pool_3x3 300 python scripts/pool_bench.py &&
