@@ -1,9 +1,11 @@
 """Per-layer f32 conv throughput of Inception-v3 (the BASELINE config-5 model)
-on device-resident tensors: every Conv2D+BiasAdd+Relu of the network, timed
-on its own through the engine (autotuned tile), with its share of the total.
-Shows which layers hold the network below the f32 MFMA peak.
+or VGG-16 (the reference's read_image network) on device-resident tensors:
+every Conv2D+BiasAdd+Relu of the network, timed on its own through the engine
+(autotuned tile), with its share of the total. Shows which layers hold the
+network below the f32 MFMA peak. (The plan that really runs, with its fusions,
+is timed per step by `--step-profile` of bench/configs.py and read_image.py.)
 
-    python scripts/conv_layers.py [--batch 2048] [--image 224] [--json out.json] [--vendor]
+    python scripts/conv_layers.py [--model inception_v3|vgg16] [--batch 2048] [--image 224] [--json out.json] [--vendor]
 """
 import argparse
 import json
@@ -22,7 +24,7 @@ from tensorframes_amd.models import cnn  # noqa: E402
 F32_PEAK_TF = 157.3
 
 
-def inception_convs(image):
+def model_convs(image, model="inception_v3"):
     """(H, W, C, KH, KW, OC, stride, padding) of every conv, in network order."""
     seen = []
     orig = cnn._Builder.conv
@@ -35,7 +37,7 @@ def inception_convs(image):
 
     cnn._Builder.conv = rec
     try:
-        cnn.inception_v3(image_size=image)
+        getattr(cnn, model)(image_size=image)
     finally:
         cnn._Builder.conv = orig
     return seen
@@ -43,7 +45,8 @@ def inception_convs(image):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--model", default="inception_v3", choices=["inception_v3", "vgg16"])
+    ap.add_argument("--batch", type=int, default=None, help="default: 2048 (Inception), 256 (VGG-16)")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
@@ -54,7 +57,9 @@ def main():
     torch.backends.cudnn.allow_tf32 = False
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
-    layers = inception_convs(a.image)
+    if a.batch is None:
+        a.batch = 2048 if a.model == "inception_v3" else 256
+    layers = model_convs(a.image, a.model)
     uniq = {}
     for l in layers:
         uniq.setdefault(l[:8], []).append(l[8])
@@ -127,7 +132,7 @@ def main():
         del xin
     for r in res:
         r["share"] = r["ms"] * r["count"] / tot_ms
-    summ = {"batch": a.batch, "image": a.image, "conv_ms_total": tot_ms, "conv_tflops": tot_fl / tot_ms / 1e9,
+    summ = {"model": a.model, "batch": a.batch, "image": a.image, "conv_ms_total": tot_ms, "conv_tflops": tot_fl / tot_ms / 1e9,
             "fraction_of_f32_peak": tot_fl / tot_ms / 1e9 / F32_PEAK_TF,
             "images_per_s_conv_only": a.batch / tot_ms * 1e3}
     print(json.dumps(summ), flush=True)
