@@ -183,6 +183,8 @@ for s in ${STEPS:-tests}; do
       TFA_CONCURRENT_LARGE=0 run vgg_tr1 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_tr1.json ;;
     bench2r) TFA_DIST_BACKEND=gloo TFA_BENCH_REHEARSAL=1 run bench_2ranks_1gpu 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 3 --warmup 1 ;;
     layers_vgg) run layers_vgg 600 python scripts/conv_layers.py --model vgg16 --json gpurun_out/layers_vgg.json ;;
+    add_chunks) for c in 16 8 4 32; do TFA_MIN_PIPELINE_CHUNKS=$c run cfg_add_c$c 300 python bench/configs.py add --steps 10 --warmup 3 || exit 1; done
+      grep -ho '"value": [0-9.]*' gpurun_out/cfg_add_c*.log ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&

@@ -129,6 +129,11 @@ class Config:
     # profiles/r6_f45/). Opt-in: its f32 error (5.6e-7 of sum|a*b|) is 5.0x the
     # exact path's, above the 4x gate of the default-on Winograd kernels
     wino_5x5: bool = dataclasses.field(default_factory=lambda: _env("TFA_WINO_5X5", False, bool))
+    # a 3x3 VALID MaxPool read only by a 1x1 conv runs inside the conv's kernel
+    # (the pooled tensor never reaches HBM). Opt-in: on Inception-v3's
+    # MaxPool_3a -> Conv2d_3b it is slower than the two kernels (22.0 vs
+    # 18.7 ms per 8 x 2048 images, profiles/r6_poolconv/)
+    pool_conv_fusion: bool = dataclasses.field(default_factory=lambda: _env("TFA_POOL_CONV_FUSION", False, bool))
     # synchronise + check after every kernel (debugging)
     debug_sync: bool = dataclasses.field(default_factory=lambda: _env("TFA_DEBUG_SYNC", False, bool))
 
@@ -151,6 +156,11 @@ def set_config(**kw):
         _C.set_debug_sync(bool(kw["debug_sync"]))  # read by the executor on every launch
     if "precision" in kw:
         apply_precision()
+    if "pool_conv_fusion" in kw:
+        from ._native import _C
+        from . import engine
+        _C.set_pool_conv_fusion(bool(kw["pool_conv_fusion"]))
+        engine.clear_program_cache()
     if "wino_5x5" in kw:
         from ._native import _C
         from . import engine

@@ -59,3 +59,15 @@ def test_switch_and_non_matching_shapes_keep_the_pool():
         p = pool(x)
         tf.identity(_conv(p) + tf.reduce_mean(p), name="y")
     assert "-in" not in _desc(two_readers)
+
+
+def test_config_switch():
+    import tensorframes_amd as tfs
+    build = lambda x: tf.identity(_conv(tf.nn.max_pool(x, [1, 3, 3, 1], [1, 2, 2, 1], "VALID")), name="y")  # noqa: E731
+    tfs.set_config(pool_conv_fusion=False)
+    try:
+        assert "-in" not in _desc(build)
+        tfs.set_config(pool_conv_fusion=True)
+        assert "+maxpool3x3/2-in" in _desc(build)
+    finally:
+        tfs.set_config(pool_conv_fusion=False)
