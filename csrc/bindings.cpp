@@ -809,7 +809,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_smallc", [](bool on) { k::set_conv_smallc(on ? 1 : 0); },
         "route tiny-reduction convs (KH*KW*C <= 32) to the direct kernel (default on)");
   m.def("set_pool_conv_fusion", [](bool on) { tfa::set_pool_conv_fusion(on); }, py::arg("on"),
-        "fuse a 3x3 VALID MaxPool into the 1x1 conv that alone reads it (GPU plans made after the call; default off)");
+        "fuse a 3x3 VALID MaxPool into the 1x1 conv that alone reads it (GPU plans made after the call; default on)");
   m.def("set_conv_direct", [](bool on) { k::set_conv_direct(on ? 1 : 0); },
         "route narrow wide-image convs (C in {32, 64}, OC <= 64) to the direct LDS-filter kernel (default on)");
   m.def("set_conv_wino", [](bool on) { k::set_conv_wino(on ? 1 : 0); },

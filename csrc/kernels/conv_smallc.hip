@@ -402,9 +402,154 @@ __global__ __launch_bounds__(256) void pool_conv1x1_kernel(PoolConv p) {
   else run(std::integral_constant<int, ACT_NONE>{});
 }
 
+// Wave-specialised variant: waves 0-1 of a block only pool (coalesced window
+// loads, many in flight) into a two-set LDS ring, waves 2-3 only run the
+// MFMAs and stores of the set the producers filled one step earlier; one
+// block barrier per step. Step i of block b covers groups 2 (i B + b) + {0, 1}
+// (consumer c takes the + c one), B = gridDim.x.
+template <int KS, int TN>
+__global__ __launch_bounds__(256) void pool_conv1x1_ws_kernel(PoolConv p) {
+  constexpr int C = 2 * KS, QPP = C / 4, TP = C + 4, PER = QPP / 2;  // PER: float4 outputs per producer lane per step
+  __shared__ __attribute__((aligned(16))) float ring[2][2][32 * TP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = lane >> 5, col = lane & 31;
+  const uint32_t groups = (p.M + 31) / 32;
+  const uint32_t B = gridDim.x, b0 = blockIdx.x;
+  const uint32_t nsteps = groups > 2 * b0 ? (groups - 2 * b0 + 2 * B - 1) / (2 * B) : 0;  // block-uniform
+  const char* xb = reinterpret_cast<const char*>(p.x);
+  char* yb = reinterpret_cast<char*>(p.y);
+  const uint32_t rowb = (uint32_t)(p.W * p.C) * 4u, pixb = (uint32_t)p.C * 4u;
+  const uint64_t imgb = (uint64_t)rowb * (uint32_t)p.H;
+  auto produce = [&](uint32_t i) __attribute__((always_inline)) {
+    const int pl = threadIdx.x;  // 0..127
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int el = e * 128 + pl, tt = el / (32 * QPP), px = (el / QPP) % 32, cq = el % QPP;
+      const uint32_t g = 2 * (i * B + b0) + (uint32_t)tt;
+      const uint32_t m = g * 32 + (uint32_t)px;
+      const uint32_t mm = (g < groups && m < p.M) ? m : 0u;  // never stored
+      const uint32_t t = fdiv(mm, p.fPW);
+      const uint32_t pw = mm - t * (uint32_t)p.PW;
+      const uint32_t n = fdiv(t, p.fPH);
+      const uint32_t ph = t - n * (uint32_t)p.PH;
+      const char* ib = xb + (uint64_t)n * imgb;
+      const uint32_t ob = ((ph * (uint32_t)p.psh) * (uint32_t)p.W + pw * (uint32_t)p.psw) * pixb + (uint32_t)(16 * cq);
+      float4 v = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const float4 u = *reinterpret_cast<const float4*>(ib + (ob + (uint32_t)dy * rowb + (uint32_t)dx * pixb));
+          v.x = fmaxf(v.x, u.x);
+          v.y = fmaxf(v.y, u.y);
+          v.z = fmaxf(v.z, u.z);
+          v.w = fmaxf(v.w, u.w);
+        }
+      *reinterpret_cast<float4*>(&ring[i & 1][tt][px * TP + 4 * cq]) = v;
+    }
+  };
+  if (nsteps == 0) return;  // block-uniform: no barrier is skipped by part of the block
+  if (wave < 2) {
+    produce(0);
+    __syncthreads();
+    for (uint32_t i = 0; i < nsteps; ++i) {
+      if (i + 1 < nsteps) produce(i + 1);
+      __syncthreads();
+    }
+    return;
+  }
+  // consumers: the filter (B operand) and bias in registers
+  const int c = wave - 2;
+  float bw[KS][TN];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 8 * (s >> 2) + (s & 3) + 4 * h;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = 32 * j + col;
+      bw[s][j] = n < p.OC ? p.w[k * p.OC + n] : 0.f;
+    }
+  }
+  float bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = 32 * j + col;
+    bv[j] = (p.bias && n < p.OC) ? p.bias[n] : 0.f;
+  }
+  __syncthreads();  // the producers' step-0 set
+  auto run = [&](auto act_c) __attribute__((always_inline)) {
+    constexpr int ACT = decltype(act_c)::value;
+    for (uint32_t i = 0; i < nsteps; ++i) {
+      const uint32_t g0 = 2 * (i * B + b0) + (uint32_t)c;
+      if (g0 < groups) {
+        const float* tile = ring[i & 1][c];
+        float a[KS];
+#pragma unroll
+        for (int j = 0; j < KS / 4; ++j) {
+          const float4 v = *reinterpret_cast<const float4*>(&tile[col * TP + 8 * j + 4 * h]);
+          a[4 * j] = v.x;
+          a[4 * j + 1] = v.y;
+          a[4 * j + 2] = v.z;
+          a[4 * j + 3] = v.w;
+        }
+        f32x16 acc[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bw[s][j], acc[j], 0, 0, 0);
+        const uint32_t m0 = g0 * 32 + 4 * h;
+        const bool full = (g0 + 1) * 32 <= p.M;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const uint32_t nn = 32 * j + col;
+          if (nn >= (uint32_t)p.OC) continue;
+          const uint32_t base = m0 * p.ldc + nn;
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            v[r] = acc[j][r] + bv[j];
+            if (ACT == ACT_RELU) v[r] = v[r] > 0.f ? v[r] : 0.f;
+            if (ACT == ACT_RELU6) v[r] = v[r] > 0.f ? (v[r] < 6.f ? v[r] : 6.f) : 0.f;
+          }
+          if (full) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              *reinterpret_cast<float*>(yb + (base + (uint32_t)((r & 3) + 8 * (r >> 2)) * p.ldc) * 4u) = v[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
+              if (m0 + ro < p.M) *reinterpret_cast<float*>(yb + (base + ro * p.ldc) * 4u) = v[r];
+            }
+          }
+        }
+      }
+      __syncthreads();  // set i & 1 is read: the producers refill it next step
+    }
+  };
+  if (p.act == ACT_RELU) run(std::integral_constant<int, ACT_RELU>{});
+  else if (p.act == ACT_RELU6) run(std::integral_constant<int, ACT_RELU6>{});
+  else run(std::integral_constant<int, ACT_NONE>{});
+}
+
 template <int KS>
 void launch_pool_conv(const PoolConv& p, int tn, hipStream_t s) {
   const uint32_t groups = (p.M + 31) / 32;
+  static const bool ws = [] {
+    const char* e = std::getenv("TFA_POOLCONV_WS");
+    return !(e && e[0] == '0');
+  }();
+  if (ws) {  // two 32-pixel groups per block step
+    const unsigned blocks = std::min<uint32_t>((groups + 1) / 2, 256 * 3);
+    if (tn == 1) hipLaunchKernelGGL((pool_conv1x1_ws_kernel<KS, 1>), dim3(blocks), dim3(256), 0, s, p);
+    else if (tn == 2) hipLaunchKernelGGL((pool_conv1x1_ws_kernel<KS, 2>), dim3(blocks), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((pool_conv1x1_ws_kernel<KS, 3>), dim3(blocks), dim3(256), 0, s, p);
+    return;
+  }
   const unsigned blocks = std::min<uint32_t>((groups + 3) / 4, 256 * 8);
   if (tn == 1) hipLaunchKernelGGL((pool_conv1x1_kernel<KS, 1>), dim3(blocks), dim3(256), 0, s, p);
   else if (tn == 2) hipLaunchKernelGGL((pool_conv1x1_kernel<KS, 2>), dim3(blocks), dim3(256), 0, s, p);

@@ -130,15 +130,15 @@ int pipe_compute_streams() {
   return n;
 }
 
-// TFA_POOL_CONV_FUSION=1 (or set_pool_conv_fusion(true), for plans made
-// after it): a 3x3 VALID MaxPool feeding only a 1x1 conv runs inside the
-// conv's step. Off by default: on Inception-v3 (MaxPool_3a -> Conv2d_3b,
-// batch 2048) the fused kernel takes 22.0 ms per 8 calls against 18.7 ms for
-// the pool kernel + the 1x1 GEMM (profiles/r6_poolconv/)
+// TFA_POOL_CONV_FUSION=0 (or set_pool_conv_fusion(false), for plans made
+// after it): a 3x3 VALID MaxPool feeding only a 1x1 conv stays its own step.
+// Fused (default), Inception-v3's MaxPool_3a -> Conv2d_3b takes 13.9 ms per
+// 8 x 2048 images against 18.8 ms for the pool kernel + the 1x1 GEMM
+// (the wave-specialised kernel, profiles/r6_poolconv/)
 std::atomic<int>& pool_conv_fusion_state() {
   static std::atomic<int> v([] {
     const char* e = std::getenv("TFA_POOL_CONV_FUSION");
-    return (e && e[0] == '1') ? 1 : 0;
+    return (e && e[0] == '0') ? 0 : 1;
   }());
   return v;
 }

@@ -173,9 +173,10 @@ for s in ${STEPS:-tests}; do
       grep -h '"layer"' gpurun_out/prio*_l*.log | cut -c1-200 ;;
     poolconv) run poolconv_tests 300 python -u -m pytest tests/test_gpu_pool_conv.py tests/test_pool_conv_plan.py tests/test_gpu_conv_smallc.py -x -v --timeout 120 --timeout-method thread &&
       TFA_POOL_CONV_FUSION=0 TFA_CONCURRENT_LARGE=0 run incep_serial_nopc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_nopc.json &&
-      TFA_CONCURRENT_LARGE=0 run incep_serial_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_pc.json &&
+      TFA_POOL_CONV_FUSION=1 TFA_CONCURRENT_LARGE=0 run incep_serial_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_pc.json &&
+      TFA_POOL_CONV_FUSION=1 TFA_POOLCONV_WS=0 TFA_CONCURRENT_LARGE=0 run incep_serial_pc_nows 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 --step-profile gpurun_out/layers_pc_nows.json &&
       TFA_POOL_CONV_FUSION=0 run incep_dev_nopc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
-      run incep_dev_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
+      TFA_POOL_CONV_FUSION=1 run incep_dev_pc 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 ;;
     smallc_tr) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_smallc.py tests/test_gpu_conv_direct.py -x -q --timeout 120 --timeout-method thread &&
       for i in 1 2; do for tr in 0 1; do
         TFA_SMALLC_TR=$tr run tr${tr}_l0_$i 200 python scripts/conv_layers.py --only 0 --iters 20 || exit 1; done; done &&

@@ -1,6 +1,6 @@
 """3x3 VALID MaxPool -> 1x1 conv (+ bias + ReLU) fused into one kernel
 (csrc/kernels/conv_smallc.hip pool_conv1x1, planner pass "pool_conv" in
-csrc/runtime/executor.cpp; opt-in): Inception-v3 MaxPool_3a -> Conv2d_3b. The fused
+csrc/runtime/executor.cpp): Inception-v3 MaxPool_3a -> Conv2d_3b. The fused
 step must give the unfused plan's bits (same k order as the GEMM cores) and
 match a float64 host reference of the same ops."""
 import numpy as np
@@ -43,7 +43,7 @@ def _run(g, x, fused):
         desc = prog.describe([torch.from_numpy(x[:1])], True)
         y = engine.run_program(prog, [torch.from_numpy(x)], DEV)[0].cpu().numpy()
     finally:
-        _C.set_pool_conv_fusion(False)
+        _C.set_pool_conv_fusion(True)
         engine.clear_program_cache()
     return desc, y
 
@@ -86,7 +86,7 @@ def test_fused_kernel_runs(tmp_path):
         torch.cuda.synchronize()
         rows = step_profile(lambda: engine.run_program(prog, [xin], DEV), str(tmp_path / "p.json"), "t")
     finally:
-        _C.set_pool_conv_fusion(False)
+        _C.set_pool_conv_fusion(True)
         engine.clear_program_cache()
     conv = [r for r in rows if r["op"] == "Conv2D"]
     assert len(conv) == 1 and conv[0]["algo"] == "maxpool3x3+conv1x1", rows
@@ -103,6 +103,6 @@ def test_inception_plan_fuses_maxpool_3a():
         prog = engine.program(g.serialize(), [oname], [iname])
         desc = prog.describe([torch.zeros((1, 224, 224, 3))], True)
     finally:
-        _C.set_pool_conv_fusion(False)
+        _C.set_pool_conv_fusion(True)
         engine.clear_program_cache()
     assert "+maxpool3x3/2-in" in desc

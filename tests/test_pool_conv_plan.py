@@ -30,9 +30,9 @@ import pytest  # noqa: E402
 
 @pytest.fixture(autouse=True)
 def fusion_on():
-    _C.set_pool_conv_fusion(True)  # opt-in (TFA_POOL_CONV_FUSION=1)
+    _C.set_pool_conv_fusion(True)  # the default (TFA_POOL_CONV_FUSION=0 turns it off)
     yield
-    _C.set_pool_conv_fusion(False)
+    _C.set_pool_conv_fusion(True)
 
 
 def test_fuses_3x3_pool_into_1x1_conv():
@@ -70,4 +70,4 @@ def test_config_switch():
         tfs.set_config(pool_conv_fusion=True)
         assert "+maxpool3x3/2-in" in _desc(build)
     finally:
-        tfs.set_config(pool_conv_fusion=False)
+        tfs.set_config(pool_conv_fusion=True)
