@@ -186,6 +186,11 @@ for s in ${STEPS:-tests}; do
     layers_vgg) run layers_vgg 600 python scripts/conv_layers.py --model vgg16 --json gpurun_out/layers_vgg.json ;;
     add_chunks) for c in 16 8 4 32; do TFA_MIN_PIPELINE_CHUNKS=$c run cfg_add_c$c 300 python bench/configs.py add --steps 10 --warmup 3 || exit 1; done
       grep -ho '"value": [0-9.]*' gpurun_out/cfg_add_c*.log ;;
+    smallc_ws) TFA_SMALLC_WS=1 run stem_tests_ws 300 python -u -m pytest tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
+      for i in 1 2; do for w in 0 1; do
+        TFA_SMALLC_WS=$w run ws${w}_l0_$i 200 python scripts/conv_layers.py --only 0 --iters 20 || exit 1; done; done &&
+      TFA_CONCURRENT_LARGE=0 run vgg_ws0 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_ws0.json &&
+      TFA_SMALLC_WS=1 TFA_CONCURRENT_LARGE=0 run vgg_ws1 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_ws1.json ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
