@@ -191,6 +191,8 @@ for s in ${STEPS:-tests}; do
         TFA_SMALLC_WS=$w run ws${w}_l0_$i 200 python scripts/conv_layers.py --only 0 --iters 20 || exit 1; done; done &&
       TFA_CONCURRENT_LARGE=0 run vgg_ws0 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_ws0.json &&
       TFA_SMALLC_WS=1 TFA_CONCURRENT_LARGE=0 run vgg_ws1 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_ws1.json ;;
+    optin_tests) TFA_WINO_5X5=1 run tests_wino5x5 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
+      TFA_POOL_CONV_FUSION=0 run tests_nopoolconv 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
