@@ -247,8 +247,8 @@ def cfg_inception(a):
     size = a.image_size
     world = max(1, dist.world_size())
     host = a.source == "host"
-    images = a.rows or (1_000_000 if host else 4096 * world)
-    batch = a.batch
+    images = a.rows or (1_000_000 if host else 16384 * world)
+    batch = a.batch or (2048 if host else 4096)
     nparts = max(1, -(-images // batch))
     u8 = a.input_dtype == "uint8"
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -379,14 +379,16 @@ def main():
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--parts-per-gpu", type=int, default=1)
     ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--batch", type=int, default=2048,
-                    help="rows per partition (inception: 2048 fills the chip; measured 17.7k vs 16.6k img/s at 512)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="rows per partition (inception: default 4096 device-resident, 2048 host-resident; "
+                         "device 25.46k / 25.20k / 24.80k img/s at 4096 / 2048 / 1024, profiles/r6_validate/sweep/)")
     ap.add_argument("--source", choices=["host", "device"], default="host", help="inception: where the column lives")
     ap.add_argument("--step-profile", default="", help="inception: after the timed steps, one more step with "
                     "per-step device timing, written to this JSON (+ .md)")
     ap.add_argument("--input-dtype", choices=["float32", "uint8"], default="float32", help="inception image dtype")
-    ap.add_argument("--chunk-images", type=int, default=1024,
-                    help="inception (host): images per pipelined chunk (1024: 16.8k vs 15.2k img/s at 256)")
+    ap.add_argument("--chunk-images", type=int, default=2048,
+                    help="inception (host): images per pipelined chunk (1M rows: 25.28k vs 24.94k img/s at 1024, "
+                         "profiles/r6_validate/sweep/)")
     ap.add_argument("--ring", type=int, default=3, help="inception (host): distinct synthetic partitions")
     ap.add_argument("--precision", choices=["f32", "bf16x3", "bf16"], default="f32",
                     help="float32 MatMul/Conv2D compute mode (Config.precision); f32 = exact")

@@ -193,6 +193,11 @@ for s in ${STEPS:-tests}; do
       TFA_SMALLC_WS=1 TFA_CONCURRENT_LARGE=0 run vgg_ws1 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_ws1.json ;;
     optin_tests) TFA_WINO_5X5=1 run tests_wino5x5 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
       TFA_POOL_CONV_FUSION=0 run tests_nopoolconv 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    incep_sweep3) for b in 1024 2048 4096; do run incep3_b$b 600 python bench/configs.py inception --source device --rows 16384 --batch $b --steps 2 --warmup 1 || exit 1; done
+      for c in 512 1024 2048; do run incep3_host_c$c 900 python bench/configs.py inception --rows 65536 --chunk-images $c --steps 1 --warmup 1 || exit 1; done ;;
+    incep_sweep4) for b in 4096 2048; do run incep4_b$b 600 python bench/configs.py inception --source device --rows 16384 --batch $b --steps 2 --warmup 1 || exit 1; done
+      run incep4_1m_c2048 900 python bench/configs.py inception --rows 1000000 --chunk-images 2048 --steps 1 --warmup 1 &&
+      run incep4_1m_c1024 900 python bench/configs.py inception --rows 1000000 --chunk-images 1024 --steps 1 --warmup 1 ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
