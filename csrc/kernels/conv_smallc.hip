@@ -81,7 +81,8 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
   const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if constexpr (FAST) {
     // every tap of every output pixel is inside the image (no padding, checked
-    // on the host) and input and output are < 4 GiB: a tap is one 32-bit add
+    // on the host) and the input is < 4 GiB (the output is addressed from a
+    // 64-bit base per 32-pixel group): a tap is one 32-bit add
     // and one load off the uniform base, pixels past M re-read pixel 0 (never
     // stored), and the epilogue is specialised per activation with one bounds
     // test per group. Same k order and MFMA sequence: bitwise the generic path.
@@ -153,7 +154,8 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
           for (int j = 0; j < TN; ++j) {
             const uint32_t n = 32 * j + col;
             if (n >= (uint32_t)p.OC) continue;
-            const uint32_t base = m0 * ldc + n;
+            // 64-bit group base (the output may exceed 4 GiB), 32-bit row offsets
+            char* yg = yb + ((uint64_t)m0 * ldc + n) * 4u;
             float v[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -164,12 +166,12 @@ __global__ __launch_bounds__(256) void conv_smallc_kernel(SmallConv p) {
             if (full) {  // straight-line stores; only the last group is partial
 #pragma unroll
               for (int r = 0; r < 16; ++r)
-                *reinterpret_cast<float*>(yb + (base + (uint32_t)((r & 3) + 8 * (r >> 2)) * ldc) * 4u) = v[r];
+                *reinterpret_cast<float*>(yg + (uint32_t)((r & 3) + 8 * (r >> 2)) * ldc * 4u) = v[r];
             } else {
 #pragma unroll
               for (int r = 0; r < 16; ++r) {
                 const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
-                if (m0 + ro < M) *reinterpret_cast<float*>(yb + (base + ro * ldc) * 4u) = v[r];
+                if (m0 + ro < M) *reinterpret_cast<float*>(yg + ro * ldc * 4u) = v[r];
               }
             }
           }
@@ -626,7 +628,7 @@ void conv_smallc_launch(const ConvArgs& a, hipStream_t s) {
   // 32-bit byte offsets (signed: the padded variant's window origins may
   // be negative); 1 = all taps in bounds (VALID-style), 2 = padding checked
   const int64_t xbytes = a.N * a.H * a.W * a.C * 4;
-  const bool ysmall = p.M * p.ldc * 4 < (int64_t(1) << 32);
+  const bool ysmall = p.ldc * 4 * 32 < (int64_t(1) << 32);  // per-group row offsets (64-bit group base)
   const bool inside = a.pad_t == 0 && a.pad_l == 0 && (a.OH - 1) * a.sh + (a.KH - 1) * a.dh <= a.H - 1 &&
                       (a.OW - 1) * a.sw + (a.KW - 1) * a.dw <= a.W - 1;
   const int fast = (generic || !ysmall) ? 0

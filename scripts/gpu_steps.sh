@@ -198,6 +198,11 @@ for s in ${STEPS:-tests}; do
     incep_sweep4) for b in 4096 2048; do run incep4_b$b 600 python bench/configs.py inception --source device --rows 16384 --batch $b --steps 2 --warmup 1 || exit 1; done
       run incep4_1m_c2048 900 python bench/configs.py inception --rows 1000000 --chunk-images 2048 --steps 1 --warmup 1 &&
       run incep4_1m_c1024 900 python bench/configs.py inception --rows 1000000 --chunk-images 1024 --steps 1 --warmup 1 ;;
+    stem64) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_smallc.py tests/test_gpu_conv_direct.py -x -q --timeout 120 --timeout-method thread &&
+      run stem64_l0_b4096 200 python scripts/conv_layers.py --only 0 --batch 4096 --iters 10 &&
+      run stem64_incep_dev 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
+      run stem64_read_image 400 python examples/read_image.py --images 4096 &&
+      TFA_MAP_ROWS_BATCH=512 run stem64_read_image_b512 400 python examples/read_image.py --images 4096 ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
