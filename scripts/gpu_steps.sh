@@ -203,6 +203,10 @@ for s in ${STEPS:-tests}; do
       run stem64_incep_dev 900 python bench/configs.py inception --source device --rows 16384 --steps 2 --warmup 1 &&
       run stem64_read_image 400 python examples/read_image.py --images 4096 &&
       TFA_MAP_ROWS_BATCH=512 run stem64_read_image_b512 400 python examples/read_image.py --images 4096 ;;
+    incep_sweep5) run incep5_b8192 600 python bench/configs.py inception --source device --rows 16384 --batch 8192 --steps 2 --warmup 1 &&
+      run incep5_b4096 600 python bench/configs.py inception --source device --rows 16384 --batch 4096 --steps 2 --warmup 1 &&
+      run incep5_1m_b4096_c4096 900 python bench/configs.py inception --rows 1000000 --batch 4096 --chunk-images 4096 --steps 1 --warmup 1 &&
+      run incep5_1m_b4096_c2048 900 python bench/configs.py inception --rows 1000000 --batch 4096 --chunk-images 2048 --steps 1 --warmup 1 ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
