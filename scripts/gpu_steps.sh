@@ -207,6 +207,8 @@ for s in ${STEPS:-tests}; do
       run incep5_b4096 600 python bench/configs.py inception --source device --rows 16384 --batch 4096 --steps 2 --warmup 1 &&
       run incep5_1m_b4096_c4096 900 python bench/configs.py inception --rows 1000000 --batch 4096 --chunk-images 4096 --steps 1 --warmup 1 &&
       run incep5_1m_b4096_c2048 900 python bench/configs.py inception --rows 1000000 --batch 4096 --chunk-images 2048 --steps 1 --warmup 1 ;;
+    img_batch) for b in 128 192 256 384; do TFA_MAP_ROWS_BATCH=$b run img_b$b 400 python examples/read_image.py --images 4096 || exit 1; done
+      grep -h steady gpurun_out/img_b*.log ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&
