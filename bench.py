@@ -161,11 +161,14 @@ def rank_main(args):
         out = tfs.map_blocks(y, base, trim=True)
         return out.local_blocks()
 
-    def timed(fn, steps, warmup):
+    def timed(fn, steps, warmup, marker="tfa.timed_steps"):
+        from tensorframes_amd._native import _C
         for _ in range(warmup):
             fn()
         sync()
         dist.barrier()
+        if use_gpu:
+            _C.roctx_push(marker)  # rocprofv3 --marker-trace: the timed window (scripts/trace_window.py)
         t0 = time.perf_counter()
         res = None
         for _ in range(steps):
@@ -174,6 +177,8 @@ def rank_main(args):
         sync()
         dist.barrier()
         dt = time.perf_counter() - t0
+        if use_gpu:
+            _C.roctx_pop()
         own_dt = dt
         if dist.is_distributed():
             t = torch.tensor([dt], dtype=torch.float64)
@@ -197,7 +202,7 @@ def rank_main(args):
 
         def step_dev():
             return tfs.map_blocks(y, base_dev, trim=True).local_blocks()
-        ddt, own["device"], _ = timed(step_dev, args.steps, args.warmup)
+        ddt, own["device"], _ = timed(step_dev, args.steps, args.warmup, "tfa.timed_steps_device")
         dev_rows_per_s = args.rows * args.steps / ddt
         results["device"] = ddt
         del base_dev

@@ -209,6 +209,9 @@ for s in ${STEPS:-tests}; do
       run incep5_1m_b4096_c2048 900 python bench/configs.py inception --rows 1000000 --batch 4096 --chunk-images 2048 --steps 1 --warmup 1 ;;
     img_batch) for b in 128 192 256 384; do TFA_MAP_ROWS_BATCH=$b run img_b$b 400 python examples/read_image.py --images 4096 || exit 1; done
       grep -h steady gpurun_out/img_b*.log ;;
+    trace_bench) export TMPDIR=/tmp
+      run trace_bench 900 rocprofv3 --kernel-trace --marker-trace --output-format csv -d "$PWD/gpurun_out/trace_bench" -o run -- python bench.py --steps 3 --warmup 2 &&
+      run trace_bench_window 120 python scripts/trace_window.py gpurun_out/trace_bench --out gpurun_out/trace_bench_step.md --title "Headline bench.py (config 3, host-resident), 3 timed steps" ;;
     groupby) run groupby 300 python scripts/groupby_profile.py ;;
     vggstem) run stem_tests 300 python -u -m pytest tests/test_gpu_conv_direct.py tests/test_gpu_conv_smallc.py -x -q --timeout 120 --timeout-method thread &&
       TFA_SMALLC_GENERIC=1 run vgg_stem_generic 400 python examples/read_image.py --images 4096 --step-profile gpurun_out/vgg_stem_generic.json &&

@@ -35,7 +35,7 @@ def _col(row, *keys):
 def window(marker_csv, marker):
     rows = _rows(marker_csv)
     for r in rows:
-        if any(marker in str(v) for v in r.values()):
+        if any(str(v).strip() == marker for v in r.values()):
             s, e = _col(r, "start_timestamp", "start"), _col(r, "end_timestamp", "end")
             return int(r[s]), int(r[e])
     raise SystemExit(f"no '{marker}' range in {marker_csv}")
